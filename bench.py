@@ -1,0 +1,218 @@
+#!/usr/bin/env python
+"""Headline benchmark: MOPO model-rollout transitions/s on halfcheetah-mixed (BASELINE.json).
+
+Workload (BASELINE.json configs[1]; examples/config/d4rl/halfcheetah_mixed.py + base.py + base_mopo.py):
+  obs 17, act 6, ensemble 7 (5 elites), hidden 200, separate mean/var heads, learned-var penalty
+  coeff 1.0, rollout_batch 50,000 per GPU, horizon 5, fp32, policy 256-256, model pool 1.25M rows
+  (mopo.py:693-695).  One step = one ``MOPO._rollout_model`` (mopo.py:723-765): start-state gather
+  from a 101,000-row env pool, 5 x (actor -> ensemble -> FakeEnv post -> pool append).
+  Synthetic data / random-init weights (D4RL and pretrained .mat weights are not available offline).
+
+Multi-GPU (torchrun, one rank per GPU, RCCL): weak scaling -- every rank rolls out its own 50,000
+rows (disjoint Philox sub-streams) into a staging buffer; an all-gather over xGMI then appends all
+ranks' transitions, in global row order, to every rank's replicated device pool; the timed region
+includes the all-gather.  value = all ranks' transitions / max-over-ranks time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+O, A, E, ELITES, H, HP = 17, 6, 7, 5, 200, 256
+ENV_ROWS = 101000
+FLOP_BNN_ROW = 2 * E * ((O + A) * H + 3 * H * H + 2 * H * (O + 1))       # 1,845,200
+FLOP_ACTOR_ROW = 2 * (O * HP + HP * HP + HP * 2 * A)                      # 145,920
+MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=10)
+    p.add_argument('--warmup', type=int, default=2)
+    p.add_argument('--batch', type=int, default=50000)
+    p.add_argument('--horizon', type=int, default=5)
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--cpu-batch', type=int, default=30000)
+    return p.parse_args()
+
+
+def dist_setup(args):
+    import torch
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    return rank, world, torch.device('cuda', local if world > 1 else 0)
+
+
+def build(args, dev, rank):
+    import torch
+    from mopo_amd.bnn import construct_model
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout, init_sac_params
+    rs = np.random.RandomState(0)  # identical synthetic env pool on every rank (replicated D4RL data)
+    env_obs = rs.normal(size=(ENV_ROWS, O)).astype(np.float32)
+    env_act = rs.uniform(-1, 1, size=(ENV_ROWS, A)).astype(np.float32)
+    model = construct_model(obs_dim=O, act_dim=A, hidden_dim=H, num_networks=E, num_elites=ELITES,
+                            separate_mean_var=True, seed=1)
+    mats = model.get_params()
+    x = np.concatenate([env_obs, env_act], 1)
+    mats[0] = x.mean(0, keepdims=True).astype(np.float32)                 # scaler.fit (utils.py:79-81)
+    mats[1] = x.std(0, keepdims=True).astype(np.float32)
+    model.set_params(mats)
+    model.set_elites([0, 1, 2, 3, 4])
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    pool_rows = 5 * args.horizon * args.batch * world                       # mopo.py:693-695 (x ranks)
+    pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=pool_rows)
+    ro = ModelRollout(model, args.batch, args.horizon)
+    pi = torch.from_numpy(init_sac_params(O, A, HP, seed=2)).to(dev)
+    env = torch.from_numpy(env_obs).to(dev)
+    staging = None
+    if world > 1:
+        staging = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=args.horizon * args.batch)
+    return model, pool, ro, pi, env, staging
+
+
+def rollout_step(args, ro, pool, pi, env, staging, epoch, rank, world):
+    """One MOPO._rollout_model; returns transitions added (device tensor)."""
+    import torch
+    if world == 1:
+        return ro.run(env, pi, pool, args.batch, args.horizon, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=epoch)
+    import torch.distributed as dist
+    steps = ro.run(env, pi, staging, args.batch, args.horizon, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=epoch,
+                   staged=True, uid_offset=rank * args.batch)
+    # RCCL all-gather of the staged transitions (+ per-step counts) into every rank's pool
+    n = args.horizon * args.batch
+    f = staging.fields
+    packed = torch.cat([f['observations'][:n], f['actions'][:n], f['rewards'][:n],
+                        f['terminals'][:n].float(), f['next_observations'][:n]], 1)
+    gathered = torch.empty((world,) + tuple(packed.shape), dtype=packed.dtype, device=packed.device)
+    dist.all_gather_into_tensor(gathered, packed)
+    counts = torch.empty((world, args.horizon), dtype=torch.int64, device=steps.device)
+    dist.all_gather_into_tensor(counts, steps.contiguous())
+    cnt = counts.cpu().numpy()
+    g = gathered.view(world, args.horizon, args.batch, -1)
+    parts = []
+    for i in range(args.horizon):          # global order: step-major, then rank-major row shards
+        for r in range(world):
+            parts.append(g[r, i, :int(cnt[r, i])])
+    rows = torch.cat(parts, 0)
+    pool.add_samples({'observations': rows[:, :O], 'actions': rows[:, O:O + A], 'rewards': rows[:, O + A:O + A + 1],
+                      'terminals': rows[:, O + A + 1:O + A + 2] > 0.5, 'next_observations': rows[:, O + A + 2:]})
+    return counts.sum(0)
+
+
+def cpu_baseline(args):
+    """Oracle (numpy port of the reference rollout) on a bounded sample, BLAS threads as configured."""
+    from oracle import bnn as obnn
+    from oracle import fake_env as ofe
+    from oracle import replay_pool as opool
+    from oracle import rollout as orollout
+    from oracle import sac as osac
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get('num_threads', 1) for i in threadpool_info() if i.get('user_api') == 'blas'] or [1])
+    except Exception:
+        threads = 1
+    rs = np.random.RandomState(0)
+    n_env = 20000
+    env_obs = rs.normal(size=(n_env, O)).astype(np.float32)
+    p = obnn.init_params(E, O, A, hidden=H, seed=1, inputs=np.concatenate([env_obs, rs.uniform(-1, 1, (n_env, A))], 1))
+    P = osac.init_params(O, A, HP, seed=2)[:8]
+    envp = opool.Pool(O, A, n_env)
+    envp.add_samples({'observations': env_obs, 'actions': np.zeros((n_env, A)), 'rewards': np.zeros((n_env, 1)),
+                      'terminals': np.zeros((n_env, 1), bool), 'next_observations': env_obs})
+    B = args.cpu_batch
+    mp = opool.Pool(O, A, B * args.horizon)
+    np.random.seed(88)
+    t0 = time.perf_counter()
+    out = orollout.rollout(envp, mp, p, [0, 1, 2, 3, 4], P, B, args.horizon, ofe.term_halfcheetah, 1.0,
+                           eps_act=lambda n: np.random.normal(size=(n, A)))
+    dt = time.perf_counter() - t0
+    trans = sum(out['steps_added'])
+    return {'value': trans / dt, 'unit': 'transitions/s', 'cores': int(threads), 'kind': 'port',
+            'sample': 'oracle numpy rollout (mopo.py:723-765 restated), B=%d, horizon=%d, E=%d, H=%d: '
+                      '%d transitions in %.2f s' % (B, args.horizon, E, H, trans, dt)}
+
+
+def main():
+    args = parse()
+    import torch
+    rank, world, dev = dist_setup(args)
+    from mopo_amd import _lib as L
+    model, pool, ro, pi, env, staging = build(args, dev, rank)
+    for w in range(args.warmup):
+        rollout_step(args, ro, pool, pi, env, staging, w, rank, world)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    L.check(L.lib().mopo_rollout_profile(ro._h, 1))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    total = 0
+    steps_t = []
+    for s in range(args.steps):
+        steps_t.append(rollout_step(args, ro, pool, pi, env, staging, args.warmup + s, rank, world))
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    total = int(sum(int(x.sum().item()) for x in steps_t))
+    ms = (C_double * 6)()
+    nl = (C_int64 * 6)()
+    L.check(L.lib().mopo_rollout_profile_read(ro._h, ms, nl, 6))
+    L.check(L.lib().mopo_rollout_profile(ro._h, 0))
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+        if staging is not None:
+            total = total  # counts are already global (gathered)
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    bnn_ms = ms[2] / max(nl[2], 1)
+    rows_per_launch = args.batch  # halfcheetah: no terminations, every step runs all rows
+    achieved = rows_per_launch * FLOP_BNN_ROW / (bnn_ms * 1e-3) / 1e12
+    kernel_ms = {k: ms[i] / max(nl[i], 1) for i, k in enumerate(['start', 'actor', 'ensemble_fwd', 'fakeenv_post',
+                                                                  'compact', 'advance'])}
+    value = total / dt
+    out = {
+        'metric': 'model-rollout transitions/s (halfcheetah-mixed)',
+        'value': value, 'unit': 'transitions/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'fp32', 'data': 'synthetic (random-init weights, N(0,1) env pool; D4RL/.mat unavailable offline)',
+        'config': {'workload': 'halfcheetah_mixed rollout: E=7 (5 elites), H=200 smv, obs=17, act=6, '
+                               'rollout_batch=%d per GPU, horizon=%d, penalty_coeff=1.0, learned-var penalty'
+                               % (args.batch, args.horizon),
+                   'rollout_batch_per_gpu': args.batch, 'horizon': args.horizon, 'parallelism': 'dp%d' % world},
+        'roofline': {'bound': 'mfma', 'kernel': 'bnn_fwd_kernel (ensemble forward, f32 MFMA 16x16x4)',
+                     'achieved': achieved, 'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': achieved / MFMA_F32_PEAK_TFLOPS, 'traffic': None,
+                     'flop_per_launch': rows_per_launch * FLOP_BNN_ROW, 'avg_launch_ms': bnn_ms},
+        'kernel_ms_avg': kernel_ms,
+    }
+    if not args.no_cpu_baseline and world == 1:
+        out['cpu_baseline'] = cpu_baseline(args)
+    print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+from ctypes import c_double as C_double, c_int64 as C_int64  # noqa: E402
+
+if __name__ == '__main__':
+    main()

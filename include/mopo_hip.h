@@ -1,0 +1,186 @@
+/*
+ * libmopo_hip — MI355X (gfx950) C ABI for the MOPO model-rollout + SAC-update hot path.
+ *
+ * Plain C types only (pointers, sizes); no torch types.  All array pointers named d_* are
+ * DEVICE pointers owned by the caller (the library borrows them for the duration of the call);
+ * h_* are host pointers.  `stream` is a hipStream_t passed as void* (NULL = default stream).
+ * Every entry point returns 0 on success and -1 on error; mopo_last_error() returns a
+ * thread-local message.  One handle = one stream at a time (not re-entrant), matching the
+ * reference's single Python thread driving one tf.Session.
+ *
+ * Reference interfaces replaced (xionghuichen/mopo @ v0):
+ *   mopo_bnn_*        construct_model / BNN.finalize / BNN.load_params / BNN.predict
+ *                     (mopo/models/constructor.py:7-43, mopo/models/bnn.py:166-281, 508-546)
+ *   mopo_fakeenv_step FakeEnv.step (mopo/models/fake_env.py:37-131) + termination_fn
+ *                     (mopo/static/{halfcheetah,walker2d,hopper}.py)
+ *   mopo_actor_forward MOPO.get_action_meta (mopo/algorithms/mopo.py:468-485, 298-308)
+ *   mopo_rollout_*    MOPO._rollout_model (mopo/algorithms/mopo.py:723-765) writing into
+ *                     SimpleReplayPool.add_samples (softlearning/replay_pools/flexible_replay_pool.py:57-83)
+ *   mopo_pool_gather  FlexibleReplayPool.random_batch / batch_by_indices (flexible_replay_pool.py:85-135)
+ *   mopo_sac_*        MOPO._do_training / _update_target (mopo/algorithms/mopo.py:834-853,
+ *                     graph mopo.py:204-466); SAC API sac.py:26-47
+ *   mopo_mt_*         numpy legacy RandomState (MT19937) as used by fake_env.py:72,
+ *                     bnn.py:343, flexible_replay_pool.py:87
+ */
+#ifndef MOPO_HIP_H
+#define MOPO_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- errors / info ------------------------------------------------------------------ */
+const char* mopo_last_error(void);
+int mopo_version(void);
+
+/* ---- probabilistic ensemble (BNN) ---------------------------------------------------- */
+typedef struct mopo_bnn_s* mopo_bnn_t;
+
+/* E members, obs_dim O, act_dim A, hidden H (4 swish layers), D = O+1 outputs.
+ * smv=1: separate mean / var heads (bnn.py:656-675); smv=0: joint 2D head (bnn.py:644-655).
+ * dtype: 0 = fp32 (exact-f32 MFMA), 1 = bf16 weights/activations with fp32 accumulate. */
+int mopo_bnn_create(mopo_bnn_t* out, int E, int obs_dim, int act_dim, int hidden, int smv, int dtype);
+int mopo_bnn_destroy(mopo_bnn_t h);
+/* The reference .mat layout, keys '0'..'15' (bnn.py:224-225, 588-592): mu[1,IN], sigma[1,IN],
+ * (W[E,in,out], b[E,1,out]) x 5 mean layers, (Wv[E,H,D], bv[E,1,D]) if smv, maxlv[1,D], minlv[1,D].
+ * n_arrays = 16 (smv) or 14; all host float32, C order. */
+int mopo_bnn_set_params(mopo_bnn_t h, const float* const* h_arrays, int n_arrays);
+/* BNN.predict(inputs, factored=True): d_inputs [B, O+A] (f32 if inputs_f64==0 else f64)
+ * -> d_mean, d_var [E, B, D] f32. */
+int mopo_bnn_predict(mopo_bnn_t h, const void* d_inputs, int inputs_f64, int64_t B,
+                     float* d_mean, float* d_var, void* stream);
+
+/* ---- FakeEnv.step ------------------------------------------------------------------- */
+enum { MOPO_TERM_NONE = 0, MOPO_TERM_HALFCHEETAH = 0, MOPO_TERM_WALKER2D = 1, MOPO_TERM_HOPPER = 2 };
+
+typedef struct {
+  const void* d_obs;        /* [B, O], f64 if obs_f64 else f32 */
+  int obs_f64;
+  const float* d_act;       /* [B, A] f32 */
+  int64_t B;
+  const double* d_noise_sel; /* [B, D] f64: the standard normals of fake_env.py:72 for the SELECTED
+                               member of each row, noise[model_inds[b], b]; unused if deterministic */
+  const int64_t* d_model_inds; /* [B] member index per row (bnn.py:343); unused if deterministic */
+  int deterministic;        /* fake_env.py:69-70,84-86 */
+  float penalty_coeff;      /* fake_env.py:97,115 */
+  int penalty_learned_var;  /* 1: max_e ||std_e||  0: max_e ||mean_e - mean|| (fake_env.py:98-110) */
+  int term_kind;            /* MOPO_TERM_* */
+  /* outputs (device) */
+  double* d_next_obs;       /* [B, O] f64 */
+  double* d_rewards;        /* [B] penalized rewards f64 */
+  uint8_t* d_terminals;     /* [B] */
+  float* d_penalty;         /* [B] f32, may be NULL */
+  double* d_unpenalized;    /* [B] f64, may be NULL */
+  float* d_info_mean;       /* [B, D+1] f32 (model mean with terminal column), may be NULL */
+  float* d_info_std;        /* [B, D+1] f32, may be NULL */
+  double* d_log_prob;       /* [B] f64, may be NULL */
+  float* d_dev;             /* [B] f32, may be NULL */
+  float* d_ens_mean;        /* workspace / output [E, B, D] f32 (required) */
+  float* d_ens_var;         /* workspace / output [E, B, D] f32 (required) */
+} mopo_fakeenv_args;
+
+int mopo_fakeenv_step(mopo_bnn_t h, const mopo_fakeenv_args* a, void* stream);
+
+/* ---- policy (actor) --------------------------------------------------------------------
+ * SAC parameters are one flat f32 buffer in reference creation order (mopo.py:32-33, 298-324):
+ *   pi: W1[O,Hp] b1[Hp] W2[Hp,Hp] b2[Hp] Wmu[Hp,A] bmu[A] Wls[Hp,A] bls[A]
+ *   q1: W1[O+A,Hp] b1 W2[Hp,Hp] b2 W3[Hp,1] b3[1]      q2: same
+ * mopo_sac_param_count() gives the total; the pi block starts at offset 0. */
+int64_t mopo_sac_param_count(int obs_dim, int act_dim, int hidden);
+
+/* get_action_meta(obs): act = tanh(mu + eps*exp(clip(log_std))) (mopo.py:298-308, 286-296).
+ * d_eps [B, A] f32 injected normals, or NULL to draw Philox normals from (seed, step). */
+int mopo_actor_forward(const float* d_pi_params, int obs_dim, int act_dim, int hidden,
+                       const void* d_obs, int obs_f64, int64_t B, const float* d_eps,
+                       uint64_t seed, uint32_t step, float* d_act, float* d_mu, void* stream);
+
+/* ---- device-resident SimpleReplayPool ---------------------------------------------------
+ * SoA fields (simple_replay_pool.py:48-70), all caller-owned device arrays of max_size rows:
+ * observations f32[O], actions f32[A], rewards f32[1], terminals u8[1], next_observations f32[O].
+ * d_state = int64[2] {pointer, size} on the device. */
+typedef struct {
+  float* d_obs;
+  float* d_act;
+  float* d_rew;
+  uint8_t* d_term;
+  float* d_next_obs;
+  int64_t* d_state;
+  int64_t max_size;
+} mopo_pool_desc;
+
+/* add_samples with device arrays of n rows (flexible_replay_pool.py:57-83). */
+int mopo_pool_add(const mopo_pool_desc* pool, int obs_dim, int act_dim, const float* d_obs,
+                  const float* d_act, const float* d_rew, const uint8_t* d_term,
+                  const float* d_next_obs, int64_t n, void* stream);
+/* batch_by_indices: d_idx int64[n] -> dst rows (dst_* arrays of n rows, any may be NULL).
+ * dst_row_offset lets two gathers (env + model pool, mopo.py:809-816) fill one batch. */
+int mopo_pool_gather(const mopo_pool_desc* pool, int obs_dim, int act_dim, const int64_t* d_idx,
+                     int64_t n, float* dst_obs, float* dst_act, float* dst_rew, float* dst_term,
+                     float* dst_next_obs, int64_t dst_row_offset, void* stream);
+/* uniform random indices in [0, size) from Philox (perf mode of random_indices). */
+int mopo_pool_random_indices(const mopo_pool_desc* pool, int64_t n, uint64_t seed, uint32_t step,
+                             int64_t* d_idx, void* stream);
+
+/* ---- fused model rollout (MOPO._rollout_model) ----------------------------------------- */
+typedef struct mopo_rollout_s* mopo_rollout_t;
+
+typedef struct {
+  /* env pool observations (start states) */
+  const float* d_env_obs;   /* [env_size, O] f32 */
+  int64_t env_size;
+  const int64_t* d_start_idx; /* [B] injected start rows (flexible_replay_pool.py:87) or NULL */
+  const float* d_pi_params; /* flat SAC params (pi block used) */
+  int pi_hidden;
+  const int32_t* d_elites;  /* [n_elites] member ids (bnn.py:337-339) */
+  int n_elites;
+  int64_t B;                /* rollout_batch_size */
+  int horizon;              /* rollout_length */
+  float penalty_coeff;
+  int term_kind;
+  uint64_t seed;            /* Philox key (perf mode) */
+  uint32_t epoch;           /* mixed into the Philox counter */
+  int64_t uid_offset;       /* global id of this rank's first row (Philox counter; multi-GPU shards) */
+  /* parity mode (all NULL in perf mode): per-step injected streams, step i uses rows [0, B_i) */
+  const float* d_eps_act;   /* [horizon, B, A] f32 */
+  const double* d_eps_obs;  /* [horizon, B, D] f64: the noise of the SELECTED member per row */
+  const int32_t* d_model_inds; /* [horizon, B] member per row */
+  /* outputs */
+  int64_t* d_steps;         /* [horizon] rows added per step (mopo.py:748) */
+} mopo_rollout_args;
+
+int mopo_rollout_create(mopo_rollout_t* out, mopo_bnn_t bnn, int64_t max_batch, int max_horizon);
+int mopo_rollout_destroy(mopo_rollout_t h);
+/* Runs the whole horizon on `stream` without host synchronisation; transitions are appended
+ * to `pool` in the reference's order (step-major, order-preserving non-terminal compaction). */
+int mopo_rollout_run(mopo_rollout_t h, const mopo_rollout_args* a, const mopo_pool_desc* pool,
+                     void* stream);
+/* Rollout that writes its transitions to a caller staging buffer instead of a pool:
+ * staging rows [horizon][B] (step i rows [0, steps[i]) valid) - the per-rank leg of the
+ * multi-GPU all-gather path. */
+int mopo_rollout_run_staged(mopo_rollout_t h, const mopo_rollout_args* a,
+                            const mopo_pool_desc* staging, void* stream);
+
+/* Live kernel timing (hipEvents on the launch stream around every launch, per kernel class:
+ * 0 start-gather, 1 actor, 2 ensemble forward, 3 FakeEnv post, 4 compaction, 5 pointer advance).
+ * profile_read synchronises the recorded events, returns summed ms and launch counts for the
+ * runs since the last read, and clears them. */
+int mopo_rollout_profile(mopo_rollout_t h, int enable);
+int mopo_rollout_profile_read(mopo_rollout_t h, double* ms, int64_t* launches, int n);
+
+/* ---- numpy legacy RandomState replica (host) ------------------------------------------ */
+typedef struct mopo_mt_s* mopo_mt_t;
+int mopo_mt_create(mopo_mt_t* out, uint32_t seed);
+int mopo_mt_destroy(mopo_mt_t h);
+int mopo_mt_seed(mopo_mt_t h, uint32_t seed);
+/* state exchange with numpy.random.get_state()/set_state() */
+int mopo_mt_set_state(mopo_mt_t h, const uint32_t* key624, int pos, int has_gauss, double gauss);
+int mopo_mt_get_state(mopo_mt_t h, uint32_t* key624, int* pos, int* has_gauss, double* gauss);
+int mopo_mt_normal(mopo_mt_t h, double* h_out, int64_t n);                  /* legacy_gauss */
+int mopo_mt_randint(mopo_mt_t h, int64_t* h_out, int64_t n, int64_t low, int64_t high); /* randint(low, high, n) */
+int mopo_mt_random_sample(mopo_mt_t h, double* h_out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,28 @@
+#pragma once
+#include "internal.h"
+
+namespace mopo {
+
+struct ActorArgs {
+  const float* P;  // flat SAC params; pi block at offset 0 (TF [in,out] layout)
+  int O, A, Hp;
+  const void* obs; int obs_f64;
+  int64_t B;               // grid rows
+  const int* d_count;      // optional device row count
+  const float* eps;        // [B, A] injected normals or NULL (Philox)
+  uint64_t seed; uint32_t step;
+  const int64_t* d_uid;    // optional per-row global id (Philox counter)
+  int64_t uid_offset;
+  float* act;              // [B, A]
+  float* mu;               // [B, A] tanh(mu) or NULL
+  // rollout: write the obs/act half of the pool row and clear the penalty accumulator
+  float* pool_obs; float* pool_act; const int64_t* pool_state; int64_t pool_max;
+  int64_t stage_base;      // >= 0: staged layout, row goes to stage_base + row
+  uint32_t* pen_zero;
+  // rollout: member selection per row (bnn.py:343): injected sel_in or Philox choice over elites
+  int32_t* sel_out; const int32_t* sel_in; const int32_t* elites; int n_elites;
+};
+
+int launch_actor(const ActorArgs& a, hipStream_t s);
+
+}  // namespace mopo

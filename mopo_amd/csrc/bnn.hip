@@ -1,0 +1,344 @@
+// Probabilistic ensemble (BNN) forward on CDNA4 MFMA.
+//
+// Replaces BNN._compile_outputs / BNN.predict (mopo/models/bnn.py:508-546, 631-675),
+// TensorStandardScaler.transform (mopo/models/utils.py:96) and FC.compute_output_tensor
+// (mopo/models/fc.py:84-106).
+//
+// Work decomposition: one wave (= one 64-thread workgroup) owns one (member e, tile of 16*R
+// rows) item and runs all five layers for it with the activations held entirely in VGPRs:
+// every layer is the transposed product Out^T[n][m] = W^T[n][k] X^T[k][m] on
+// v_mfma_f32_16x16x4_f32, whose accumulator layout (feature on the register axis, row on the
+// lane axis) is exactly the B operand of the next layer, so no LDS round trip and no barrier
+// is needed.  Weights stream from L2 as 1 KiB fragments (one dwordx4 per lane per 4 MFMAs),
+// double-buffered in registers across k-groups.  Items are member-major so the waves resident
+// on one XCD share one member's weights in L2.
+#include "internal.h"
+
+#include <vector>
+#include <cstring>
+
+namespace mopo {
+
+// ---------------------------------------------------------------------------------------
+// weight packing:  src W[E][K][N] (TF layout, x @ W)  ->  fragment-major (see internal.h)
+__global__ void pack_frags_kernel(const float* __restrict__ src, float* __restrict__ dst, int E, int K,
+                                  int N, int KG, int NB) {
+  int64_t total = (int64_t)E * KG * NB * 256;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int t = i & 3, lane = (i >> 2) & 63;
+    int64_t f = i >> 8;
+    int nb = f % NB;
+    int kg = (f / NB) % KG;
+    int e = f / ((int64_t)NB * KG);
+    int k = kg * 16 + 4 * (lane >> 4) + t, n = nb * 16 + (lane & 15);
+    dst[i] = (k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f;
+  }
+}
+
+__global__ void pack_bias_kernel(const float* __restrict__ src, float* __restrict__ dst, int E, int N,
+                                 int NP) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E * NP) return;
+  int e = i / NP, n = i % NP;
+  dst[i] = n < N ? src[e * N + n] : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float load_feat(const void* p, int f64, int64_t idx) {
+  return f64 ? (float)reinterpret_cast<const double*>(p)[idx] : reinterpret_cast<const float*>(p)[idx];
+}
+
+// acc[r][nb] += sum over KG k-groups:  W(frag kg,nb) x in[r][kg]
+template <int KG, int NB, int R>
+__device__ __forceinline__ void layer_mfma(const float* __restrict__ wf, const f32x4 (&in)[R][KG],
+                                           f32x4 (&acc)[R][NB], int lane) {
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[r][nb] = zero4();
+  f32x4 wc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) wc[nb] = ld4(wf + (nb * 64 + lane) * 4);
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) {
+    f32x4 wn[NB];
+    if (kg + 1 < KG) {
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) wn[nb] = ld4(wf + (((kg + 1) * NB + nb) * 64 + lane) * 4);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r][nb] = mfma4(wc[nb][t], in[r][kg][t], acc[r][nb]);
+    if (kg + 1 < KG) {
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) wc[nb] = wn[nb];
+    }
+  }
+}
+
+// bias + swish, acc -> next-layer input (fc.py:21,99-106)
+template <int NB, int R>
+__device__ __forceinline__ void bias_swish(const float* __restrict__ b, const f32x4 (&acc)[R][NB],
+                                           f32x4 (&out)[R][NB], int g) {
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    f32x4 bb = ld4(b + nb * 16 + 4 * g);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) out[r][nb][t] = swishf(acc[r][nb][t] + bb[t]);
+  }
+}
+
+template <int KG0, int NBH, int NBO, int R, int MODE>
+__global__ __launch_bounds__(64) void bnn_fwd_kernel(const BnnDev w, const FwdArgs a) {
+  const int lane = threadIdx.x, m = lane & 15, g = lane >> 4;
+  const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
+  const int e = blockIdx.x / a.ntiles, tile = blockIdx.x % a.ntiles;
+  const int64_t row0 = (int64_t)tile * 16 * R;
+  if (row0 >= count) return;
+  const int IN = w.IN, O = w.O, H = w.H, D = w.D;
+
+  // ---- layer-0 input: scaler transform (utils.py:96), f64 inputs cast to f32 as TF's feed does
+  f32x4 x0[R][KG0];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + r * 16 + m;
+    const bool ok = row < count;
+#pragma unroll
+    for (int kg = 0; kg < KG0; ++kg)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int k = kg * 16 + 4 * g + t;
+        float v = 0.f;
+        if (ok && k < IN) {
+          float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
+                            : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
+          v = (raw - w.mu[k]) / w.sigma[k];
+        }
+        x0[r][kg][t] = v;
+      }
+  }
+  f32x4 acc[R][NBH], hcur[R][NBH];
+  const int64_t hp = (int64_t)NBH * 16;
+  layer_mfma<KG0, NBH, R>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lane);
+  bias_swish<NBH, R>(w.b0 + e * hp, acc, hcur, g);
+  for (int l = 0; l < 3; ++l) {  // hidden layers 1..3 (constructor.py:31-33)
+    layer_mfma<NBH, NBH, R>(w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lane);
+    bias_swish<NBH, R>(w.bh + ((int64_t)l * w.E + e) * hp, acc, hcur, g);
+  }
+  // ---- heads on the 4th hidden output (bnn.py:661-667): n < D mean, D <= n < 2D log-var
+  f32x4 hd[R][NBO];
+  layer_mfma<NBH, NBO, R>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lane);
+  (void)H;
+
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + r * 16 + m;
+    const bool ok = row < count;
+    float ss = 0.f;  // sum of std^2 over D (learned-var penalty, fake_env.py:110)
+    const bool selected = (MODE == FWD_ROLLOUT) && ok && a.sel[row] == e;
+#pragma unroll
+    for (int nb = 0; nb < NBO; ++nb) {
+      f32x4 bb = ld4(w.bhd + e * NBO * 16 + nb * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int n = nb * 16 + 4 * g + t;
+        float v = hd[r][nb][t] + bb[t];
+        if (n < D) {
+          if (MODE == FWD_PREDICT) {
+            if (ok) a.mean[((int64_t)e * a.B + row) * D + n] = v;
+          } else if (selected) {
+            a.mean_sel[row * D + n] = v;
+          }
+        } else if (n < 2 * D) {
+          const int d = n - D;
+          const float mx = w.maxlv[d], mn = w.minlv[d];
+          float lv = mx - softplusf(mx - v);  // bnn.py:669
+          lv = mn + softplusf(lv - mn);       // bnn.py:670
+          const float var = expf(lv);         // bnn.py:675
+          if (MODE == FWD_PREDICT) {
+            if (ok) a.var[((int64_t)e * a.B + row) * D + d] = var;
+          } else {
+            const float sd = sqrtf(var);      // fake_env.py:67
+            ss += sd * sd;
+            if (selected) a.std_sel[row * D + d] = sd;
+          }
+        }
+      }
+    }
+    if (MODE == FWD_ROLLOUT) {
+      ss += __shfl_xor(ss, 16);
+      ss += __shfl_xor(ss, 32);
+      if (g == 0 && ok) atomicMax(a.pen_bits + row, __float_as_uint(sqrtf(ss)));  // >= 0: uint order
+    }
+  }
+}
+
+template <int KG0, int NBH, int NBO, int R>
+static int launch_fwd_t(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
+  a.ntiles = (int)ceil_div((int)a.B, 16 * R);
+  dim3 grid(a.ntiles * h->E), block(64);
+  if (a.ntiles == 0) return 0;
+  if (mode == FWD_PREDICT)
+    hipLaunchKernelGGL((bnn_fwd_kernel<KG0, NBH, NBO, R, FWD_PREDICT>), grid, block, 0, s, h->dev, a);
+  else
+    hipLaunchKernelGGL((bnn_fwd_kernel<KG0, NBH, NBO, R, FWD_ROLLOUT>), grid, block, 0, s, h->dev, a);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+template <int KG0, int NBO>
+static int launch_fwd_h(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) {
+  switch (h->dev.NBH) {
+    case 2: return launch_fwd_t<KG0, 2, NBO, 2>(h, mode, a, s);
+    case 4: return launch_fwd_t<KG0, 4, NBO, 2>(h, mode, a, s);
+    case 13: return launch_fwd_t<KG0, 13, NBO, 2>(h, mode, a, s);
+    case 25: return launch_fwd_t<KG0, 25, NBO, 1>(h, mode, a, s);
+  }
+  return fail("bnn: unsupported hidden size (supported: 32, 64, 200, 400; got H=" +
+              std::to_string(h->H) + ")");
+}
+
+int launch_bnn_fwd(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) {
+  if (!h->has_params) return fail("bnn: parameters not set (mopo_bnn_set_params)");
+  if (h->dev.KG0 != 2) return fail("bnn: obs_dim + act_dim must be in (16, 32]");
+  switch (h->dev.NBO) {
+    case 3: return launch_fwd_h<2, 3>(h, mode, a, s);
+    case 2: return launch_fwd_h<2, 2>(h, mode, a, s);
+  }
+  return fail("bnn: unsupported output dim");
+}
+
+}  // namespace mopo
+
+using namespace mopo;
+
+// ---------------------------------------------------------------------------------------- C ABI
+extern "C" int mopo_bnn_create(mopo_bnn_t* out, int E, int obs_dim, int act_dim, int hidden, int smv,
+                               int dtype) {
+  MOPO_REQUIRE(out != nullptr, "mopo_bnn_create: out is NULL");
+  MOPO_REQUIRE(E >= 1 && E <= 256, "mopo_bnn_create: num_networks must be in [1, 256]");
+  MOPO_REQUIRE(obs_dim >= 1 && act_dim >= 1, "mopo_bnn_create: bad obs/act dims");
+  MOPO_REQUIRE(dtype == 0 || dtype == 1, "mopo_bnn_create: dtype must be 0 (fp32) or 1 (bf16)");
+  Bnn* h = new Bnn();
+  h->E = E; h->O = obs_dim; h->A = act_dim; h->H = hidden; h->smv = smv; h->dtype = dtype;
+  BnnDev& d = h->dev;
+  d.E = E; d.O = obs_dim; d.A = act_dim; d.IN = obs_dim + act_dim; d.H = hidden; d.D = obs_dim + 1;
+  d.KG0 = ceil_div(d.IN, 16);
+  d.NBH = ceil_div(hidden, 16);
+  d.NBO = ceil_div(2 * d.D, 16);
+  *out = reinterpret_cast<mopo_bnn_t>(h);
+  return 0;
+}
+
+extern "C" int mopo_bnn_destroy(mopo_bnn_t hh) {
+  Bnn* h = reinterpret_cast<Bnn*>(hh);
+  if (!h) return 0;
+  if (h->buf) (void)hipFree(h->buf);
+  if (h->bbuf) (void)hipFree(h->bbuf);
+  delete h;
+  return 0;
+}
+
+extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int n) {
+  Bnn* h = reinterpret_cast<Bnn*>(hh);
+  MOPO_REQUIRE(h != nullptr, "mopo_bnn_set_params: NULL handle");
+  MOPO_REQUIRE(n == (h->smv ? 16 : 14), "mopo_bnn_set_params: expected 16 (smv) or 14 arrays (.mat keys)");
+  BnnDev& d = h->dev;
+  const int E = h->E, IN = d.IN, H = h->H, D = d.D;
+  const int KG0 = d.KG0, NBH = d.NBH, NBO = d.NBO;
+  const int64_t hp = NBH * 16;
+  // sizes (floats) of the packed regions
+  const int64_t s_w0 = (int64_t)E * KG0 * NBH * 256, s_wh = 3LL * E * NBH * NBH * 256,
+                s_whd = (int64_t)E * NBH * NBO * 256, s_b0 = E * hp, s_bh = 3 * E * hp,
+                s_bhd = (int64_t)E * NBO * 16;
+  const int64_t total = s_w0 + s_wh + s_whd + s_b0 + s_bh + s_bhd + 2 * 64 + 2 * 64;
+  if (!h->buf) MOPO_HIP(hipMalloc(&h->buf, total * sizeof(float)));
+  float* base = h->buf;
+  float* w0 = base; float* wh = w0 + s_w0; float* whd = wh + s_wh;
+  float* b0 = whd + s_whd; float* bh = b0 + s_b0; float* bhd = bh + s_bh;
+  float* mu = bhd + s_bhd; float* sg = mu + 64; float* mx = sg + 64; float* mn = mx + 64;
+
+  // stage raw arrays on the device, then pack there (same code path as on-device repacking)
+  const int n_layers = 5;
+  std::vector<const float*> W(n_layers), Bv(n_layers);
+  for (int i = 0; i < n_layers; ++i) { W[i] = arrs[2 + 2 * i]; Bv[i] = arrs[3 + 2 * i]; }
+  // combined head raw [E][H][2D] : mean columns then log-var columns
+  std::vector<float> head((size_t)E * H * 2 * D), headb((size_t)E * 2 * D);
+  for (int e = 0; e < E; ++e)
+    for (int k = 0; k < H; ++k)
+      for (int j = 0; j < 2 * D; ++j) {
+        float v;
+        if (h->smv) v = j < D ? W[4][((size_t)e * H + k) * D + j] : arrs[12][((size_t)e * H + k) * D + (j - D)];
+        else v = W[4][((size_t)e * H + k) * 2 * D + j];
+        head[((size_t)e * H + k) * 2 * D + j] = v;
+      }
+  for (int e = 0; e < E; ++e)
+    for (int j = 0; j < 2 * D; ++j)
+      headb[(size_t)e * 2 * D + j] = h->smv ? (j < D ? Bv[4][e * D + j] : arrs[13][e * D + (j - D)])
+                                            : Bv[4][e * 2 * D + j];
+  const float* maxlv = arrs[h->smv ? 14 : 12];
+  const float* minlv = arrs[h->smv ? 15 : 13];
+
+  size_t stage_n = std::max((size_t)E * H * H, head.size());
+  stage_n = std::max(stage_n, (size_t)E * IN * H);
+  float* stage = nullptr;
+  MOPO_HIP(hipMalloc(&stage, stage_n * sizeof(float)));
+  auto pack = [&](const float* src, size_t nsrc, float* dst, int K, int N, int KG, int NB) -> int {
+    MOPO_HIP(hipMemcpy(stage, src, nsrc * sizeof(float), hipMemcpyHostToDevice));
+    int64_t tot = (int64_t)E * KG * NB * 256;
+    int blocks = (int)std::min<int64_t>((tot + 255) / 256, 4096);
+    hipLaunchKernelGGL(pack_frags_kernel, dim3(blocks), dim3(256), 0, 0, stage, dst, E, K, N, KG, NB);
+    MOPO_HIP(hipGetLastError());
+    MOPO_HIP(hipDeviceSynchronize());
+    return 0;
+  };
+  auto packb = [&](const float* src, float* dst, int N, int NP) -> int {
+    MOPO_HIP(hipMemcpy(stage, src, (size_t)E * N * sizeof(float), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(pack_bias_kernel, dim3(ceil_div(E * NP, 256)), dim3(256), 0, 0, stage, dst, E, N, NP);
+    MOPO_HIP(hipGetLastError());
+    MOPO_HIP(hipDeviceSynchronize());
+    return 0;
+  };
+  int rc = 0;
+  rc |= pack(W[0], (size_t)E * IN * H, w0, IN, H, KG0, NBH);
+  rc |= packb(Bv[0], b0, H, (int)hp);
+  for (int l = 0; l < 3; ++l) {
+    rc |= pack(W[1 + l], (size_t)E * H * H, wh + (int64_t)l * E * NBH * NBH * 256, H, H, NBH, NBH);
+    rc |= packb(Bv[1 + l], bh + l * E * hp, H, (int)hp);
+  }
+  rc |= pack(head.data(), head.size(), whd, H, 2 * D, NBH, NBO);
+  rc |= packb(headb.data(), bhd, 2 * D, NBO * 16);
+  (void)hipFree(stage);
+  if (rc) return -1;
+  MOPO_HIP(hipMemcpy(mu, arrs[0], IN * sizeof(float), hipMemcpyHostToDevice));
+  MOPO_HIP(hipMemcpy(sg, arrs[1], IN * sizeof(float), hipMemcpyHostToDevice));
+  MOPO_HIP(hipMemcpy(mx, maxlv, D * sizeof(float), hipMemcpyHostToDevice));
+  MOPO_HIP(hipMemcpy(mn, minlv, D * sizeof(float), hipMemcpyHostToDevice));
+  d.w0 = w0; d.wh = wh; d.whd = whd; d.b0 = b0; d.bh = bh; d.bhd = bhd;
+  d.mu = mu; d.sigma = sg; d.maxlv = mx; d.minlv = mn;
+  h->has_params = true;
+  return 0;
+}
+
+extern "C" int mopo_bnn_predict(mopo_bnn_t hh, const void* x, int x_f64, int64_t B, float* mean,
+                                float* var, void* stream) {
+  Bnn* h = reinterpret_cast<Bnn*>(hh);
+  MOPO_REQUIRE(h != nullptr, "mopo_bnn_predict: NULL handle");
+  MOPO_REQUIRE(B >= 0 && B < (1LL << 31) / 32, "mopo_bnn_predict: batch too large");
+  if (B == 0) return 0;
+  MOPO_REQUIRE(x && mean && var, "mopo_bnn_predict: NULL pointer");
+  FwdArgs a{};
+  const int IN = h->dev.IN;
+  const size_t es = x_f64 ? 8 : 4;
+  a.in = FwdIn{x, x_f64, IN, (const char*)x + es * h->O, x_f64, IN};
+  a.B = B;
+  a.mean = mean;
+  a.var = var;
+  return launch_bnn_fwd(h, FWD_PREDICT, a, (hipStream_t)stream);
+}

@@ -1,0 +1,88 @@
+// Internal declarations shared by the libmopo_hip translation units.
+#pragma once
+#include "common.h"
+#include "../../include/mopo_hip.h"
+
+namespace mopo {
+
+constexpr int MAX_IN_KG = 4;  // layer-0 input features <= 64
+
+// Device view of a packed ensemble.  Weight matrices are stored "fragment-major": for
+// layer input K (KG = ceil(K/16) k-groups) and output N (NB = ceil(N/16) blocks), member e,
+// fragment (kg, nb) is 64 lanes x 4 floats contiguous (1 KiB):
+//   frag[((e*KG + kg)*NB + nb)*256 + lane*4 + t] = W[e][kg*16 + 4*(lane>>4) + t][nb*16 + (lane&15)]
+// i.e. exactly the per-lane A operand of 4 consecutive v_mfma_f32_16x16x4_f32 steps.
+struct BnnDev {
+  int E, O, A, IN, H, D;
+  int KG0, NBH, NBO;  // layer-0 k-groups, hidden blocks (= hidden k-groups), head blocks
+  const float* w0;    // [E][KG0][NBH] frags
+  const float* wh;    // [3][E][NBH][NBH] frags
+  const float* whd;   // [E][NBH][NBO] frags (head: n < D mean, D <= n < 2D log-var)
+  const float* b0;    // [E][NBH*16]
+  const float* bh;    // [3][E][NBH*16]
+  const float* bhd;   // [E][NBO*16]
+  const float* mu;    // [IN]
+  const float* sigma; // [IN]
+  const float* maxlv; // [D]
+  const float* minlv; // [D]
+  // bf16 copies (dtype 1); same fragment order with 8 bf16 per lane per 32-deep k-group
+  const uint16_t* w0b;
+  const uint16_t* whb;
+  const uint16_t* whdb;
+};
+
+struct Bnn {
+  int E, O, A, H, smv, dtype;
+  bool has_params = false;
+  float* buf = nullptr;      // one device allocation for all packed params
+  uint16_t* bbuf = nullptr;  // bf16 packed weights
+  BnnDev dev{};
+};
+
+// Input view: features [0, O) from xa (row stride sa), [O, IN) from xb (row stride sb).
+struct FwdIn {
+  const void* xa; int xa_f64; int64_t sa;
+  const void* xb; int xb_f64; int64_t sb;
+};
+
+enum { FWD_PREDICT = 0, FWD_ROLLOUT = 1 };
+
+struct FwdArgs {
+  FwdIn in;
+  int64_t B;              // launch rows (grid sized for this)
+  const int* d_count;     // optional device row count (<= B)
+  int ntiles;             // tiles per member in the grid
+  // predict outputs
+  float* mean;            // [E][B][D]
+  float* var;
+  // rollout outputs
+  uint32_t* pen_bits;     // [B] max_e ||std_e|| (as ordered uint bits)
+  const int32_t* sel;     // [B] selected member per row
+  float* mean_sel;        // [B][D]
+  float* std_sel;         // [B][D]
+};
+
+int launch_bnn_fwd(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s);
+
+// termination kinds (mopo/static)
+__device__ __forceinline__ bool term_fn(int kind, const double* nobs, int O) {
+  if (kind == MOPO_TERM_WALKER2D) {  // walker2d.py:10-16
+    double hh = nobs[0], an = nobs[1];
+    bool not_done = (hh > 0.8) && (hh < 2.0) && (an > -1.0) && (an < 1.0);
+    return !not_done;
+  }
+  if (kind == MOPO_TERM_HOPPER) {  // hopper.py:10-17 (np.abs(bool) == bool)
+    bool fin = true, small = true;
+    for (int d = 0; d < O; ++d) {
+      double v = nobs[d];
+      fin = fin && isfinite(v);
+      if (d >= 1) small = small && (v < 100.0);
+    }
+    double hh = nobs[0], an = nobs[1];
+    bool not_done = fin && small && (hh > 0.7) && (fabs(an) < 0.2);
+    return !not_done;
+  }
+  return false;  // halfcheetah.py:9-10
+}
+
+}  // namespace mopo

@@ -1,0 +1,355 @@
+// Fused model rollout: MOPO._rollout_model (mopo/algorithms/mopo.py:723-765) on the device.
+//
+// Per horizon step (all launched back-to-back on one stream, no host synchronisation; the live
+// row count, pool pointer and size stay on the device):
+//   actor_kernel      get_action_meta (mopo.py:734) + obs/act half of the pool row + member pick
+//   bnn_fwd ROLLOUT   ensemble forward; per row keeps only the selected member's mean/std and the
+//                     max-over-members aleatoric norm (fake_env.py:66-81, 110) -> no [E,B,D] in HBM
+//   rollout_post      sample, reward penalty, termination, next_obs/rew/term half of the pool row
+//                     (fake_env.py:72, 90-115; mopo.py:750-751)
+//   rollout_compact   order-preserving non-terminal compaction  obs = next_obs[~term] (mopo.py:753-758)
+//   step_advance      steps_added / pool pointer & size (mopo.py:748; flexible_replay_pool.py:45-48)
+#include "actor.h"
+
+#include <vector>
+
+namespace mopo {
+
+enum { KC_START = 0, KC_ACTOR, KC_BNN, KC_POST, KC_COMPACT, KC_ADVANCE, KC_N };
+
+struct Rollout {
+  // optional live kernel timing: hipEvents recorded around every launch, per kernel class
+  bool profile = false;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev;
+  std::vector<hipEvent_t> pool_ev;
+  size_t ev_used = 0;
+  Bnn* bnn = nullptr;
+  int64_t Bmax = 0;
+  int Hmax = 0;
+  void* mem = nullptr;
+  double* obs[2];
+  int64_t* uid[2];
+  float* act;
+  uint32_t* pen;
+  int32_t* sel;
+  float* mean_sel;
+  float* std_sel;
+  uint8_t* keep;
+  int* blockcnt;
+  int* cnt;  // [0] live rows this step, [1] survivors
+};
+
+constexpr int PB = 256;  // rows per block in post / compact
+
+// scoped hipEvent pair on the launch stream (only when profiling is enabled)
+struct KTimer {
+  Rollout* h; hipStream_t s; size_t idx = (size_t)-1;
+  KTimer(Rollout* h_, int cls, hipStream_t s_) : h(h_), s(s_) {
+    if (!h->profile) return;
+    if (h->ev_used == h->ev.size()) {
+      hipEvent_t a, b;
+      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+      h->ev.push_back({cls, {a, b}});
+    }
+    idx = h->ev_used++;
+    h->ev[idx].first = cls;
+    (void)hipEventRecord(h->ev[idx].second.first, s);
+  }
+  ~KTimer() {
+    if (idx != (size_t)-1) (void)hipEventRecord(h->ev[idx].second.second, s);
+  }
+};
+
+__global__ void rollout_start_kernel(const float* env_obs, int64_t env_size, const int64_t* idx_in, int O,
+                                     int64_t B, uint64_t seed, uint32_t step, int64_t uid_offset, double* obs,
+                                     int64_t* uid, int* cnt) {
+  const int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (row == 0) cnt[0] = (int)B;
+  if (row >= B) return;
+  int64_t src;
+  const int64_t u = uid_offset + row;
+  if (idx_in) {
+    src = idx_in[row];
+  } else {  // perf mode of np.random.randint(0, size, B) (flexible_replay_pool.py:87)
+    u32x4 c{(uint32_t)u, (uint32_t)((uint64_t)u >> 32), step, RNG_START};
+    u32x4 r = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    src = (int64_t)(((uint64_t)r.x * (uint64_t)env_size) >> 32);
+  }
+  for (int k = 0; k < O; ++k) obs[row * O + k] = (double)env_obs[src * O + k];
+  uid[row] = u;
+}
+
+struct PostArgs {
+  int O;
+  const int* cnt;
+  const double* obs;        // current obs f64 [B][O]
+  const int64_t* uid;
+  const float* mean_sel;    // [B][D]
+  const float* std_sel;
+  const uint32_t* pen;
+  const double* eps;        // injected [B][D] or NULL
+  uint64_t seed; uint32_t step;
+  float coeff;
+  int term_kind;
+  double* obs_next;         // [B][O]
+  uint8_t* keep;
+  int* blockcnt;
+  mopo_pool_desc pool;
+  int64_t stage_base;       // >= 0: staged layout
+};
+
+__global__ __launch_bounds__(PB) void rollout_post_kernel(const PostArgs a) {
+  __shared__ int wcnt[PB / 64];
+  const int64_t row = blockIdx.x * (int64_t)PB + threadIdx.x;
+  const int O = a.O, D = O + 1;
+  const int64_t count = *a.cnt;
+  bool keep = false;
+  if (row < count) {
+    double s[33];
+    float z[36];
+    if (!a.eps) {  // Philox normals for the selected member (perf mode of fake_env.py:72)
+      const int64_t u = a.uid[row];
+      for (int blk = 0; blk * 4 < D; ++blk) {
+        u32x4 c{(uint32_t)u, (uint32_t)((uint64_t)u >> 32) ^ ((uint32_t)blk << 20), a.step, RNG_OBS_NOISE};
+        u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+        box_muller(r.x, r.y, z[blk * 4 + 0], z[blk * 4 + 1]);
+        box_muller(r.z, r.w, z[blk * 4 + 2], z[blk * 4 + 3]);
+      }
+    }
+    for (int d = 0; d < D; ++d) {
+      float m = a.mean_sel[row * D + d];
+      if (d >= 1) m = (float)((double)m + a.obs[row * O + d - 1]);  // fake_env.py:66
+      const double e = a.eps ? a.eps[row * D + d] : (double)z[d];
+      s[d] = (double)m + e * (double)a.std_sel[row * D + d];       // fake_env.py:72
+    }
+    const bool term = term_fn(a.term_kind, s + 1, O);               // fake_env.py:91
+    const double rew = s[0];
+    const double pr = a.coeff != 0.f ? rew - (double)a.coeff * (double)__uint_as_float(a.pen[row]) : rew;
+    const int64_t pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool.d_state[0] + row) % a.pool.max_size;
+    for (int k = 0; k < O; ++k) {
+      a.obs_next[row * O + k] = s[k + 1];
+      a.pool.d_next_obs[pos * O + k] = (float)s[k + 1];
+    }
+    a.pool.d_rew[pos] = (float)pr;
+    a.pool.d_term[pos] = term ? 1 : 0;
+    keep = !term;
+    a.keep[row] = keep ? 1 : 0;
+  }
+  const unsigned long long bal = __ballot(keep);
+  if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = __popcll(bal);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < PB / 64; ++w) t += wcnt[w];
+    a.blockcnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(PB) void rollout_compact_kernel(int O, const int* blockcnt, const uint8_t* keepf,
+                                                             const int* cnt, const double* obs_src,
+                                                             double* obs_dst, const int64_t* uid_src,
+                                                             int64_t* uid_dst, int* survivors) {
+  __shared__ int red[PB];
+  __shared__ int woff[PB / 64 + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int part = 0;
+  for (int j = tid; j < (int)blockIdx.x; j += PB) part += blockcnt[j];
+  red[tid] = part;
+  __syncthreads();
+  for (int st = PB / 2; st > 0; st >>= 1) {
+    if (tid < st) red[tid] += red[tid + st];
+    __syncthreads();
+  }
+  const int base = red[0];
+  const int64_t row = blockIdx.x * (int64_t)PB + tid;
+  const int64_t count = *cnt;
+  const bool keep = row < count && keepf[row];
+  const unsigned long long bal = __ballot(keep);
+  const int pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+  if (lane == 0) woff[wid] = __popcll(bal);
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int w = 0; w < PB / 64; ++w) { int c = woff[w]; woff[w] = acc; acc += c; }
+    woff[PB / 64] = acc;
+  }
+  __syncthreads();
+  if (keep) {
+    const int64_t pos = base + woff[wid] + pre;
+    for (int k = 0; k < O; ++k) obs_dst[pos * O + k] = obs_src[row * O + k];
+    uid_dst[pos] = uid_src[row];
+  }
+  if (blockIdx.x == gridDim.x - 1 && tid == 0) *survivors = base + woff[PB / 64];
+}
+
+__global__ void step_advance_kernel(int* cnt, int64_t* steps, int i, int compacted, int64_t* pool_state,
+                                    int64_t max_size) {
+  const int64_t n = cnt[0];
+  steps[i] = n;
+  if (pool_state) {
+    pool_state[0] = (pool_state[0] + n) % max_size;
+    pool_state[1] = min(pool_state[1] + n, max_size);
+  }
+  if (compacted) cnt[0] = cnt[1];
+}
+
+static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc* p, bool staged,
+                    hipStream_t s) {
+  MOPO_REQUIRE(a && p, "rollout: NULL argument");
+  MOPO_REQUIRE(a->B >= 0 && a->B <= h->Bmax, "rollout: B exceeds the handle's max_batch");
+  MOPO_REQUIRE(a->horizon >= 0 && a->horizon <= h->Hmax, "rollout: horizon exceeds max_horizon");
+  MOPO_REQUIRE(a->d_env_obs && a->env_size > 0, "rollout: empty env pool");
+  MOPO_REQUIRE(a->d_pi_params, "rollout: NULL policy params");
+  MOPO_REQUIRE(a->d_model_inds || (a->d_elites && a->n_elites > 0), "rollout: elites required");
+  MOPO_REQUIRE(p->d_obs && p->d_act && p->d_rew && p->d_term && p->d_next_obs, "rollout: NULL pool field");
+  MOPO_REQUIRE(staged || p->d_state, "rollout: pool state required");
+  MOPO_REQUIRE(!staged || p->max_size >= (int64_t)a->horizon * a->B, "rollout: staging buffer too small");
+  MOPO_REQUIRE(a->d_steps, "rollout: d_steps output required");
+  if (a->B == 0 || a->horizon == 0) return 0;
+  Bnn* bnn = h->bnn;
+  const int O = bnn->O, A = bnn->A, D = O + 1;
+  const int64_t B = a->B;
+  const int nblk = ceil_div((int)B, PB);
+  const uint32_t step0 = a->epoch * 4096u;
+  {
+    KTimer t(h, KC_START, s);
+    hipLaunchKernelGGL(rollout_start_kernel, dim3(nblk), dim3(PB), 0, s, a->d_env_obs, a->env_size,
+                       a->d_start_idx, O, B, a->seed, step0, a->uid_offset, h->obs[0], h->uid[0], h->cnt);
+  }
+  MOPO_HIP(hipGetLastError());
+  const bool compact = a->term_kind != MOPO_TERM_HALFCHEETAH;
+  int oc = 0, uc = 0;
+  for (int i = 0; i < a->horizon; ++i) {
+    const uint32_t st = step0 + 1 + i;
+    ActorArgs aa{};
+    aa.P = a->d_pi_params; aa.O = O; aa.A = A; aa.Hp = a->pi_hidden;
+    aa.obs = h->obs[oc]; aa.obs_f64 = 1; aa.B = B; aa.d_count = h->cnt;
+    aa.eps = a->d_eps_act ? a->d_eps_act + (int64_t)i * B * A : nullptr;
+    aa.seed = a->seed; aa.step = st; aa.d_uid = h->uid[uc];
+    aa.act = h->act;
+    aa.pool_obs = p->d_obs; aa.pool_act = p->d_act; aa.pool_state = p->d_state; aa.pool_max = p->max_size;
+    aa.stage_base = staged ? (int64_t)i * B : -1;
+    aa.pen_zero = h->pen;
+    aa.sel_out = h->sel;
+    aa.sel_in = a->d_model_inds ? a->d_model_inds + (int64_t)i * B : nullptr;
+    aa.elites = a->d_elites; aa.n_elites = a->n_elites;
+    {
+      KTimer t(h, KC_ACTOR, s);
+      if (launch_actor(aa, s)) return -1;
+    }
+
+    FwdArgs f{};
+    f.in = FwdIn{h->obs[oc], 1, O, h->act, 0, A};
+    f.B = B; f.d_count = h->cnt;
+    f.pen_bits = h->pen; f.sel = h->sel; f.mean_sel = h->mean_sel; f.std_sel = h->std_sel;
+    {
+      KTimer t(h, KC_BNN, s);
+      if (launch_bnn_fwd(bnn, FWD_ROLLOUT, f, s)) return -1;
+    }
+
+    PostArgs pa{};
+    pa.O = O; pa.cnt = h->cnt; pa.obs = h->obs[oc]; pa.uid = h->uid[uc];
+    pa.mean_sel = h->mean_sel; pa.std_sel = h->std_sel; pa.pen = h->pen;
+    pa.eps = a->d_eps_obs ? a->d_eps_obs + (int64_t)i * B * D : nullptr;
+    pa.seed = a->seed; pa.step = st; pa.coeff = a->penalty_coeff; pa.term_kind = a->term_kind;
+    pa.obs_next = h->obs[oc ^ 1]; pa.keep = h->keep; pa.blockcnt = h->blockcnt;
+    pa.pool = *p; pa.stage_base = staged ? (int64_t)i * B : -1;
+    {
+      KTimer t(h, KC_POST, s);
+      hipLaunchKernelGGL(rollout_post_kernel, dim3(nblk), dim3(PB), 0, s, pa);
+    }
+    MOPO_HIP(hipGetLastError());
+    if (compact) {
+      KTimer t(h, KC_COMPACT, s);
+      hipLaunchKernelGGL(rollout_compact_kernel, dim3(nblk), dim3(PB), 0, s, O, h->blockcnt, h->keep, h->cnt,
+                         h->obs[oc ^ 1], h->obs[oc], h->uid[uc], h->uid[uc ^ 1], h->cnt + 1);
+      MOPO_HIP(hipGetLastError());
+      uc ^= 1;
+    } else {
+      oc ^= 1;
+    }
+    {
+      KTimer t(h, KC_ADVANCE, s);
+      hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, s, h->cnt, a->d_steps, i, compact ? 1 : 0,
+                         staged ? nullptr : p->d_state, p->max_size);
+    }
+    MOPO_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+}  // namespace mopo
+
+using namespace mopo;
+
+extern "C" int mopo_rollout_create(mopo_rollout_t* out, mopo_bnn_t bnn, int64_t max_batch, int max_horizon) {
+  MOPO_REQUIRE(out && bnn, "mopo_rollout_create: NULL argument");
+  MOPO_REQUIRE(max_batch > 0 && max_batch < (1LL << 30), "mopo_rollout_create: bad max_batch");
+  Bnn* b = reinterpret_cast<Bnn*>(bnn);
+  MOPO_REQUIRE(b->O + 1 <= 32, "mopo_rollout_create: obs_dim must be < 32");
+  Rollout* h = new Rollout();
+  h->bnn = b; h->Bmax = max_batch; h->Hmax = max_horizon;
+  const int O = b->O, A = b->A, D = O + 1;
+  const int64_t B = max_batch;
+  const int nblk = ceil_div((int)B, PB);
+  size_t sz[] = {(size_t)B * O * 8, (size_t)B * O * 8, (size_t)B * 8, (size_t)B * 8, (size_t)B * A * 4,
+                 (size_t)B * 4,     (size_t)B * 4,     (size_t)B * D * 4, (size_t)B * D * 4, (size_t)B,
+                 (size_t)nblk * 4,  16};
+  size_t off[12], tot = 0;
+  for (int i = 0; i < 12; ++i) { off[i] = tot; tot += (sz[i] + 255) & ~(size_t)255; }
+  if (hipMalloc(&h->mem, tot) != hipSuccess) { delete h; return fail("mopo_rollout_create: out of device memory"); }
+  char* m = (char*)h->mem;
+  h->obs[0] = (double*)(m + off[0]); h->obs[1] = (double*)(m + off[1]);
+  h->uid[0] = (int64_t*)(m + off[2]); h->uid[1] = (int64_t*)(m + off[3]);
+  h->act = (float*)(m + off[4]); h->pen = (uint32_t*)(m + off[5]); h->sel = (int32_t*)(m + off[6]);
+  h->mean_sel = (float*)(m + off[7]); h->std_sel = (float*)(m + off[8]); h->keep = (uint8_t*)(m + off[9]);
+  h->blockcnt = (int*)(m + off[10]); h->cnt = (int*)(m + off[11]);
+  *out = reinterpret_cast<mopo_rollout_t>(h);
+  return 0;
+}
+
+extern "C" int mopo_rollout_profile(mopo_rollout_t hh, int enable) {
+  Rollout* h = reinterpret_cast<Rollout*>(hh);
+  MOPO_REQUIRE(h, "mopo_rollout_profile: NULL handle");
+  h->profile = enable != 0;
+  h->ev_used = 0;
+  return 0;
+}
+
+extern "C" int mopo_rollout_profile_read(mopo_rollout_t hh, double* ms, int64_t* launches, int n) {
+  Rollout* h = reinterpret_cast<Rollout*>(hh);
+  MOPO_REQUIRE(h && ms && launches, "mopo_rollout_profile_read: NULL argument");
+  for (int i = 0; i < n; ++i) { ms[i] = 0.0; launches[i] = 0; }
+  for (size_t i = 0; i < h->ev_used; ++i) {
+    auto& e = h->ev[i];
+    MOPO_HIP(hipEventSynchronize(e.second.second));
+    float t = 0.f;
+    MOPO_HIP(hipEventElapsedTime(&t, e.second.first, e.second.second));
+    if (e.first < n) { ms[e.first] += t; launches[e.first] += 1; }
+  }
+  h->ev_used = 0;
+  return 0;
+}
+
+extern "C" int mopo_rollout_destroy(mopo_rollout_t hh) {
+  Rollout* h = reinterpret_cast<Rollout*>(hh);
+  if (!h) return 0;
+  for (auto& e : h->ev) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
+  if (h->mem) (void)hipFree(h->mem);
+  delete h;
+  return 0;
+}
+
+extern "C" int mopo_rollout_run(mopo_rollout_t hh, const mopo_rollout_args* a, const mopo_pool_desc* p,
+                                void* stream) {
+  Rollout* h = reinterpret_cast<Rollout*>(hh);
+  MOPO_REQUIRE(h, "mopo_rollout_run: NULL handle");
+  return run_impl(h, a, p, false, (hipStream_t)stream);
+}
+
+extern "C" int mopo_rollout_run_staged(mopo_rollout_t hh, const mopo_rollout_args* a, const mopo_pool_desc* p,
+                                       void* stream) {
+  Rollout* h = reinterpret_cast<Rollout*>(hh);
+  MOPO_REQUIRE(h, "mopo_rollout_run_staged: NULL handle");
+  return run_impl(h, a, p, true, (hipStream_t)stream);
+}

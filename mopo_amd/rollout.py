@@ -1,0 +1,95 @@
+"""Fused model rollout: ``MOPO._rollout_model`` (mopo/algorithms/mopo.py:723-765) on one GPU.
+
+``ModelRollout.run`` launches the whole horizon (actor -> ensemble -> FakeEnv post -> compaction
+-> pool append, csrc/rollout.hip) on the current stream with no host synchronisation; the
+transitions land in a device ``SimpleReplayPool`` in the reference's order.  Two RNG modes:
+
+* ``perf`` (default): Philox on the device (start rows, policy noise, member choice, obs noise).
+* ``parity``: every stream injected -- start rows, TF policy noise ``eps_act`` and the numpy
+  FakeEnv draws (the selected member's noise and the member index per row), so the result can be
+  compared to the reference for identical inputs.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+def sac_param_shapes(O, A, H=256):
+    """Creation order of get_vars('main') (mopo.py:32-33, 298-324): pi, q1, q2 in TF [in,out] layout."""
+    pi = [(O, H), (H,), (H, H), (H,), (H, A), (A,), (H, A), (A,)]
+    q = [(O + A, H), (H,), (H, H), (H,), (H, 1), (1,)]
+    return pi + q + q
+
+
+def init_sac_params(O, A, H=256, seed=2):
+    """tf.layers.dense defaults: glorot_uniform kernels, zero biases; returns a flat float32 array."""
+    rng = np.random.RandomState(seed)
+    parts = []
+    for shp in sac_param_shapes(O, A, H):
+        if len(shp) == 2:
+            lim = np.sqrt(6.0 / (shp[0] + shp[1]))
+            parts.append(rng.uniform(-lim, lim, size=shp).astype(np.float32).ravel())
+        else:
+            parts.append(np.zeros(shp, np.float32))
+    flat = np.concatenate(parts)
+    assert flat.size == L.lib().mopo_sac_param_count(O, A, H)
+    return flat
+
+
+def split_params(flat, O, A, H=256):
+    out, off = [], 0
+    for shp in sac_param_shapes(O, A, H):
+        n = int(np.prod(shp))
+        out.append(flat[off:off + n].reshape(shp))
+        off += n
+    return out
+
+
+class ModelRollout:
+    """Owns the rollout workspace for up to ``max_batch`` rows x ``max_horizon`` steps."""
+
+    def __init__(self, model, max_batch, max_horizon=32):
+        self.model = model
+        self.max_batch, self.max_horizon = int(max_batch), int(max_horizon)
+        h = C.c_void_p()
+        L.check(L.lib().mopo_rollout_create(C.byref(h), model.handle, self.max_batch, self.max_horizon))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, '_h', None)
+        if h is not None and h.value:
+            L.lib().mopo_rollout_destroy(h)
+            self._h = None
+
+    def run(self, env_obs, pi_params, pool, batch_size, horizon, term_kind, penalty_coeff, elites,
+            seed=0, epoch=0, pi_hidden=256, start_idx=None, eps_act=None, eps_obs=None, model_inds=None,
+            staged=False, uid_offset=0, stream=None):
+        """Returns the device int64[horizon] tensor of rows added per step (steps_added)."""
+        import torch
+        dev = env_obs.device
+        B = int(batch_size)
+        steps = torch.zeros(max(horizon, 1), dtype=torch.int64, device=dev)
+        el = torch.as_tensor(np.asarray(elites, np.int32)).to(dev)
+        keep = [steps, el]
+
+        def dptr(x, dt):
+            if x is None:
+                return None
+            t = torch.as_tensor(x).to(dev, dt).contiguous()
+            keep.append(t)
+            return L.ptr(t)
+
+        args = L.RolloutArgs(
+            d_env_obs=L.ptr(env_obs), env_size=int(env_obs.shape[0]), d_start_idx=dptr(start_idx, torch.int64),
+            d_pi_params=L.ptr(pi_params), pi_hidden=int(pi_hidden), d_elites=L.ptr(el), n_elites=int(el.numel()),
+            B=B, horizon=int(horizon), penalty_coeff=float(penalty_coeff), term_kind=int(term_kind),
+            seed=int(seed) & (2 ** 64 - 1), epoch=int(epoch), uid_offset=int(uid_offset),
+            d_eps_act=dptr(eps_act, torch.float32), d_eps_obs=dptr(eps_obs, torch.float64),
+            d_model_inds=dptr(model_inds, torch.int32), d_steps=L.ptr(steps))
+        desc = pool.desc() if not isinstance(pool, L.PoolDesc) else pool
+        fn = L.lib().mopo_rollout_run_staged if staged else L.lib().mopo_rollout_run
+        L.check(fn(self._h, args, desc, L.stream_ptr(stream)))
+        self._keepalive = keep
+        return steps[:horizon]

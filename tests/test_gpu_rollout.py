@@ -1,0 +1,257 @@
+"""GPU parity: HIP ensemble forward, FakeEnv.step, actor, pool and fused rollout vs the oracle.
+
+Tolerances (fp32 device vs reference dtypes; the reference mixes f32 GEMMs with f64 sampling):
+  * ensemble mean/var (f32 GEMM order differs from TF/BLAS):   |d| <= 2e-5 * (1 + |ref|)
+  * next_obs / rewards / penalized rewards:                      |d| <= 5e-5 * (1 + |ref|)
+  * penalty:                                                     rel 1e-5
+  * log_prob (where finite):                                     |d| <= 1e-4 * (1 + |ref|)
+  * integer work (model_inds consumed, terminals, pool pointer/size, compaction order): bit-exact
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import bnn as obnn
+from oracle import fake_env as ofe
+from oracle import replay_pool as opool
+from oracle import sac as osac
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+CASES = sorted(glob.glob(os.path.join(GOLD, 'fakeenv_*.npz')))
+
+
+def close(a, b, tol):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    err = np.abs(a - b) / (1 + np.abs(b))
+    assert np.all(np.isfinite(a) == np.isfinite(b))
+    m = np.isfinite(b)
+    assert err[m].max(initial=0) <= tol, 'max scaled err %.3g > %.3g' % (err[m].max(), tol)
+
+
+def golden_params(E, H):
+    z = np.load(os.path.join(GOLD, 'bnn_E%d_H%d.npz' % (E, H)))
+    return [z['w%d' % i] for i in range(16)]
+
+
+def make_model(mats, E, H, O=17, A=6):
+    from mopo_amd.bnn import BNN
+    m = BNN({'name': 't', 'num_networks': E, 'num_elites': 5, 'separate_mean_var': True, 'obs_dim': O,
+             'act_dim': A, 'hidden_dim': H})
+    return m.set_params(mats)
+
+
+@pytest.mark.parametrize('E,H,B,f64', [(7, 64, 257, False), (32, 32, 100, True), (7, 200, 4099, False),
+                                       (7, 200, 33, True), (3, 400, 500, False), (7, 200, 1, False)])
+def test_bnn_predict_vs_oracle(E, H, B, f64):
+    rs = np.random.RandomState(E * 1000 + H)
+    if (E, H) in ((7, 64), (32, 32)):
+        mats = golden_params(E, H)
+    else:
+        mats = obnn.to_mat_list(obnn.init_params(E, 17, 6, hidden=H, seed=3, inputs=rs.normal(size=(300, 23)) * 3))
+    p = obnn.from_mat_list(mats)
+    x = rs.normal(size=(B, 23)) * 2
+    x = x if f64 else x.astype(np.float32)
+    model = make_model(mats, E, H)
+    mean, var = model.predict(x, factored=True)
+    rm, rv = obnn.forward(p, x, dtype=np.float64)
+    close(mean, rm, 2e-5)
+    close(var, rv, 2e-5)
+
+
+@pytest.mark.parametrize('path', CASES, ids=[os.path.basename(c) for c in CASES])
+def test_fakeenv_step_vs_reference_golden(path):
+    from mopo_amd.fake_env import FakeEnv
+    from mopo_amd.static import static_fns
+    c = dict(np.load(path))
+    E, H = int(c['E']), int(c['H'])
+    model = make_model(golden_params(E, H), E, H)
+    model.set_elites(list(c['elites']))
+    env = FakeEnv(model, static_fns[str(c['domain'])], penalty_coeff=float(c['penalty_coeff']),
+                  penalty_learned_var=bool(c['learned_var']))
+    det = bool(c['deterministic'])
+    np.random.seed(int(c['seed']))
+    nobs, rew, term, info = env.step(c['obs'], c['act'], deterministic=det)
+    # numpy's global stream consumed exactly like the reference (normal then choice)
+    np.random.seed(int(c['seed']))
+    if not det:
+        np.random.normal(size=(E, int(c['B']), 18))
+        np.testing.assert_array_equal(np.random.choice(list(c['elites']), size=int(c['B'])), c['model_inds'])
+    close(nobs, c['next_obs'], 5e-5)
+    close(rew, c['rew'], 5e-5)
+    close(info['unpenalized_rewards'], c['unpenalized'], 5e-5)
+    close(info['penalty'], c['penalty'], 1e-5)
+    close(info['mean'], c['info_mean'], 5e-5)
+    close(info['std'], c['info_std'], 5e-5)
+    close(info['dev'], c['dev'], 1e-4)
+    lp = c['log_prob']
+    fin = np.isfinite(lp)
+    close(info['log_prob'][fin], lp[fin], 1e-4)
+    # terminals bit-exact except where the f32-vs-f64 threshold operand is within 1e-4 of a bound
+    bad = term[:, 0] != c['term'][:, 0]
+    if bad.any():
+        h, a = c['next_obs'][bad, 0], c['next_obs'][bad, 1]
+        bounds = np.array([0.7, 0.8, 2.0])
+        near = (np.abs(h[:, None] - bounds).min(1) < 1e-4) | (np.abs(np.abs(a)[:, None] - np.array([0.2, 1.0])).min(1) < 1e-4)
+        assert near.all()
+
+
+def test_actor_forward_vs_oracle():
+    import torch
+    from mopo_amd import _lib as L
+    from mopo_amd.rollout import init_sac_params, split_params
+    O, A, H, B = 17, 6, 256, 1000
+    flat = init_sac_params(O, A, H, seed=4)
+    rs = np.random.RandomState(0)
+    flat = flat + (rs.normal(size=flat.shape) * 0.01).astype(np.float32)   # non-zero biases
+    P = [p.astype(np.float64) for p in split_params(flat, O, A, H)[:8]]
+    obs = rs.normal(size=(B, O))
+    eps = rs.normal(size=(B, A)).astype(np.float32)
+    dev = torch.device('cuda')
+    tp, to, te = (torch.from_numpy(x).to(dev) for x in (flat, obs, eps))
+    act = torch.empty((B, A), device=dev)
+    mu = torch.empty((B, A), device=dev)
+    L.check(L.lib().mopo_actor_forward(L.ptr(tp), O, A, H, L.ptr(to), 1, B, L.ptr(te), 0, 0, L.ptr(act),
+                                       L.ptr(mu), L.stream_ptr()))
+    ra, rmu = osac.actor_act(P, obs.astype(np.float32).astype(np.float64), eps.astype(np.float64))
+    close(act.cpu().numpy(), ra, 2e-5)
+    close(mu.cpu().numpy(), rmu, 2e-5)
+
+
+def test_pool_vs_reference_trace():
+    import torch
+    from mopo_amd.replay_pool import SimpleReplayPool
+    z = np.load(os.path.join(GOLD, 'pool_trace.npz'))
+    pool = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=int(z['max_size']))
+    for i, n in enumerate(z['adds']):
+        if n == 0:
+            continue
+        pool.add_samples({k: z['add%d_%s' % (i, k)] for k in opool.FIELDS})
+        assert pool._pointer == int(z['add%d_ptr' % i]) and pool.size == int(z['add%d_size' % i])
+        np.random.seed(50 + i)
+        b = pool.random_batch(33, as_numpy=True)
+        for k in opool.FIELDS:
+            np.testing.assert_array_equal(b[k], z['add%d_batch_%s' % (i, k)].astype(b[k].dtype))
+    for k, v in pool.return_all_samples(as_numpy=True).items():
+        np.testing.assert_array_equal(v, z['final_' + k].astype(v.dtype))
+    # a single add larger than the pool keeps only the last max_size rows, like the reference ring
+    p2 = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=10)
+    o2 = opool.Pool(17, 6, 10)
+    s = {'observations': np.arange(25 * 17, dtype=np.float32).reshape(25, 17), 'actions': np.zeros((25, 6)),
+         'next_observations': np.zeros((25, 17)), 'rewards': np.arange(25.).reshape(25, 1),
+         'terminals': np.zeros((25, 1), bool)}
+    p2.add_samples(s); o2.add_samples(s)
+    assert p2._pointer == o2._pointer and p2.size == o2.size
+    np.testing.assert_array_equal(p2.fields['rewards'].cpu().numpy(), o2.fields['rewards'])
+    torch.cuda.synchronize()
+
+
+def _rollout_case(domain, E, H, B, horizon, seed, coeff=1.0, O=17, A=6):
+    """Oracle rollout with every random stream drawn in the reference order; returns inputs,
+    injected streams and the oracle pool."""
+    rs = np.random.RandomState(seed)
+    env_n = 3000
+    env_obs = rs.normal(size=(env_n, O)).astype(np.float32)
+    if domain == 'walker2d':
+        env_obs[:, 0] = rs.uniform(0.9, 1.9, env_n)
+        env_obs[:, 1] = rs.uniform(-0.9, 0.9, env_n)
+    mats = obnn.to_mat_list(obnn.init_params(E, O, A, hidden=H, seed=seed + 1,
+                                             inputs=np.concatenate([env_obs, rs.uniform(-1, 1, (env_n, A))], 1)))
+    p = obnn.from_mat_list(mats)
+    # keep the model's predicted change small so walker rows terminate at a moderate rate
+    flat = __import__('mopo_amd.rollout', fromlist=['x']).init_sac_params(O, A, 256, seed=seed + 2)
+    P = [q.astype(np.float64) for q in __import__('mopo_amd.rollout', fromlist=['x']).split_params(flat, O, A)[:8]]
+    elites = [4, 1, 0, 6, 2][:min(5, E)]
+    env_pool = opool.Pool(O, A, env_n)
+    env_pool.add_samples({'observations': env_obs, 'actions': np.zeros((env_n, A)), 'rewards': np.zeros((env_n, 1)),
+                          'terminals': np.zeros((env_n, 1), bool), 'next_observations': env_obs})
+    model_pool = opool.Pool(O, A, B * horizon + 7)
+    np.random.seed(seed)
+    start = env_pool.random_indices(B)
+    obs = env_obs[start]
+    act_rs = np.random.RandomState(seed + 99)    # stands in for TF's policy noise stream
+    eps_act = np.zeros((horizon, B, A), np.float32)
+    eps_obs = np.zeros((horizon, B, O + 1))
+    inds_all = np.zeros((horizon, B), np.int32)
+    steps = []
+    for i in range(horizon):
+        Bi = len(obs)
+        ea = act_rs.normal(size=(Bi, A)).astype(np.float32)
+        act, _ = osac.actor_act(P, obs.astype(np.float32).astype(np.float64), ea.astype(np.float64))
+        act = act.astype(np.float32)
+        noise = np.random.normal(size=(E, Bi, O + 1))
+        inds = np.random.choice(elites, size=Bi)
+        nobs, rew, term, info = ofe.step(p, elites, obs, act, ofe.TERMINATION[domain], penalty_coeff=coeff,
+                                         penalty_learned_var=True, noise=noise, model_inds=inds)
+        eps_act[i, :Bi] = ea
+        eps_obs[i, :Bi] = noise[inds, np.arange(Bi)]
+        inds_all[i, :Bi] = inds
+        steps.append(Bi)
+        model_pool.add_samples({'observations': obs, 'actions': act, 'next_observations': nobs,
+                                'rewards': rew, 'terminals': term})
+        nt = ~term[:, 0]
+        if nt.sum() == 0:
+            break
+        obs = nobs[nt]
+    return dict(env_obs=env_obs, mats=mats, flat=flat, elites=elites, start=start, eps_act=eps_act,
+                eps_obs=eps_obs, inds=inds_all, steps=steps, pool=model_pool, coeff=coeff)
+
+
+@pytest.mark.parametrize('domain,E,H,B,horizon', [('halfcheetah', 7, 200, 1000, 5), ('walker2d', 7, 200, 777, 5),
+                                                  ('hopper', 7, 64, 300, 4), ('halfcheetah', 32, 32, 64, 3)])
+def test_fused_rollout_parity(domain, E, H, B, horizon):
+    import torch
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout
+    from mopo_amd.static import static_fns
+    c = _rollout_case(domain, E, H, B, horizon, seed=11)
+    model = make_model(c['mats'], E, H)
+    dev = torch.device('cuda')
+    pool = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=B * horizon + 7)
+    ro = ModelRollout(model, B, horizon)
+    env = torch.from_numpy(c['env_obs']).to(dev)
+    pi = torch.from_numpy(c['flat']).to(dev)
+    steps = ro.run(env, pi, pool, B, horizon, static_fns[domain].term_kind, c['coeff'], c['elites'],
+                   start_idx=c['start'], eps_act=c['eps_act'], eps_obs=c['eps_obs'], model_inds=c['inds'])
+    st = steps.cpu().numpy()
+    exp = np.zeros(horizon, np.int64)
+    exp[:len(c['steps'])] = c['steps']
+    np.testing.assert_array_equal(st, exp)                         # compaction counts bit-exact
+    op = c['pool']
+    assert pool.size == op.size and pool._pointer == op._pointer
+    got = pool.return_all_samples(as_numpy=True)
+    ref = op.return_all_samples()
+    np.testing.assert_array_equal(got['terminals'], ref['terminals'])
+    close(got['observations'], ref['observations'], 5e-5)
+    close(got['actions'], ref['actions'], 5e-5)
+    close(got['next_observations'], ref['next_observations'], 5e-5)
+    close(got['rewards'], ref['rewards'], 5e-5)
+
+
+def test_fused_rollout_perf_mode_runs():
+    import torch
+    from mopo_amd.bnn import construct_model
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout, init_sac_params
+    dev = torch.device('cuda')
+    model = construct_model(obs_dim=17, act_dim=6, hidden_dim=200, num_networks=7, num_elites=5,
+                            separate_mean_var=True, seed=0)
+    B, h = 5000, 5
+    pool = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=3 * B * h)
+    ro = ModelRollout(model, B, h)
+    env = torch.randn(20000, 17, device=dev)
+    pi = torch.from_numpy(init_sac_params(17, 6)).to(dev)
+    for ep in range(3):
+        steps = ro.run(env, pi, pool, B, h, 0, 1.0, [0, 1, 2, 3, 4], seed=7, epoch=ep)
+        assert steps.cpu().tolist() == [B] * h
+    assert pool.size == min(3 * B * h, pool._max_size)
+    f = pool.return_all_samples(as_numpy=True)
+    assert np.isfinite(f['next_observations']).all() and np.isfinite(f['rewards']).all()
+    # Philox noise is standard normal: next_obs - mean has unit-ish spread (sanity, not parity)
+    assert 0.1 < np.std(f['next_observations'] - f['observations']) < 100
+    # determinism: same seed/epoch -> identical transitions
+    p2 = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=B * h)
+    ro.run(env, pi, p2, B, h, 0, 1.0, [0, 1, 2, 3, 4], seed=7, epoch=0)
+    np.testing.assert_array_equal(p2.fields['next_observations'].cpu().numpy(), f['next_observations'][:B * h])
