@@ -81,6 +81,9 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError('libmopo_hip.so not built at %s (run make -C mopo_amd/csrc)' % LIB_PATH)
+        # torch ships its own libamdhip64.so.7; load it first so the library binds to that one HIP
+        # runtime (same soname) instead of pulling /opt/rocm's copy into the process beside it.
+        import torch  # noqa: F401
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)
