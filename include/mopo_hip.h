@@ -168,6 +168,35 @@ int mopo_rollout_run_staged(mopo_rollout_t h, const mopo_rollout_args* a,
 int mopo_rollout_profile(mopo_rollout_t h, int enable);
 int mopo_rollout_profile_read(mopo_rollout_t h, double* ms, int64_t* launches, int n);
 
+/* ---- SAC update (MOPO._do_training + _update_target) ------------------------------------
+ * h_params: initial flat parameters (mopo_sac_param_count floats, layout above); target = copy
+ * (target_init, mopo.py:449-450); log_alpha initial value (mopo.py:357-360); Adam lr / gamma / tau /
+ * reward_scale / target_entropy as MOPO.__init__ (mopo.py:56-61, 171-174).  batch = 256 in the
+ * reference (sampler batch_size), of which n_env rows come from the env pool (int(256*real_ratio),
+ * mopo.py:801-816). */
+typedef struct mopo_sac_s* mopo_sac_t;
+int mopo_sac_create(mopo_sac_t* out, int obs_dim, int act_dim, int hidden, int batch, int n_env,
+                    const float* h_params, float log_alpha, float lr, float gamma, float tau,
+                    float reward_scale, float target_entropy);
+int mopo_sac_destroy(mopo_sac_t h);
+/* device buffers owned by the handle: params [n_params + 1] (last = log_alpha), target, Adam m/v,
+ * grads (same layout; grads[n_params] = d alpha_loss / d log_alpha), logs[16]:
+ * 0 q1_loss 1 q2_loss 2 mean q1 3 mean q2 4 alpha 5 pi_entropy 6 logp_pi 7 pi_global_norm
+ * 8 q_global_norm 9 policy_loss  (the fetches of mopo.py:453-463; values of the last step) */
+int mopo_sac_buffers(mopo_sac_t h, float** d_params, float** d_target, float** d_adam_m, float** d_adam_v,
+                     float** d_grads, float** d_logs, int64_t* n_params);
+/* Run n_steps grad steps (batch gather from env_pool/model_pool + update + Polyak) on `stream`.
+ * Perf mode (all injected pointers NULL): Philox batch indices / policy noise; the step sequence is
+ * captured once into a hipGraph and replayed.  Parity mode (n_steps = 1): d_idx[batch] int64 rows
+ * (first n_env from the env pool), d_eps_s / d_eps_n [batch, act_dim] policy noise for pi(s), pi(s'). */
+int mopo_sac_step(mopo_sac_t h, const mopo_pool_desc* env_pool, const mopo_pool_desc* model_pool,
+                  int n_steps, uint64_t seed, const int64_t* d_idx, const float* d_eps_s,
+                  const float* d_eps_n, void* stream);
+int mopo_sac_set_graph(mopo_sac_t h, int enable);
+/* device<->device copy of a handle buffer (which: 0 params, 1 target, 2 adam_m, 3 adam_v, 4 grads,
+ * 5 logs); to_handle=1 writes the handle's buffer from d_buf (e.g. loading a checkpoint). */
+int mopo_sac_copy(mopo_sac_t h, int which, int to_handle, void* d_buf, int64_t count, void* stream);
+
 /* ---- numpy legacy RandomState replica (host) ------------------------------------------ */
 typedef struct mopo_mt_s* mopo_mt_t;
 int mopo_mt_create(mopo_mt_t* out, uint32_t seed);

@@ -61,6 +61,14 @@ SIGNATURES = {
     'mopo_rollout_run_staged': (c_int, [c_void_p, C.POINTER(RolloutArgs), C.POINTER(PoolDesc), c_void_p]),
     'mopo_rollout_profile': (c_int, [c_void_p, c_int]),
     'mopo_rollout_profile_read': (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+    'mopo_sac_create': (c_int, [C.POINTER(c_void_p), c_int, c_int, c_int, c_int, c_int, c_void_p, c_float,
+                                c_float, c_float, c_float, c_float, c_float]),
+    'mopo_sac_destroy': (c_int, [c_void_p]),
+    'mopo_sac_buffers': (c_int, [c_void_p] + [C.POINTER(c_void_p)] * 6 + [C.POINTER(c_i64)]),
+    'mopo_sac_step': (c_int, [c_void_p, C.POINTER(PoolDesc), C.POINTER(PoolDesc), c_int, c_u64, c_void_p,
+                              c_void_p, c_void_p, c_void_p]),
+    'mopo_sac_set_graph': (c_int, [c_void_p, c_int]),
+    'mopo_sac_copy': (c_int, [c_void_p, c_int, c_int, c_void_p, c_i64, c_void_p]),
     'mopo_mt_create': (c_int, [C.POINTER(c_void_p), c_u32]),
     'mopo_mt_destroy': (c_int, [c_void_p]),
     'mopo_mt_seed': (c_int, [c_void_p, c_u32]),

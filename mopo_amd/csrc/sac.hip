@@ -1,0 +1,683 @@
+// MOPO's in-graph SAC update (K6/K7): forward, hand-derived backward, four TF1 Adams, Polyak.
+//
+// Replaces MOPO._build's training graph and MOPO._do_training / _update_target
+// (mopo/algorithms/mopo.py:275-466, 834-853); batch assembly MOPO._training_batch (mopo.py:801-821).
+// Semantics: every forward and gradient uses the pre-step parameters; then pi, q1, q2
+// and alpha are updated by their own Adam (identical step counts -> one shared lr_t); then Polyak.
+//
+// Structure: ~17 launches per step on one stream (batch gather, 3 grouped-GEMM forward stages for
+// pi(s), pi(s'), Q1/Q2(s,a), the squashed-Gaussian head, 3 for Q1/Q2(s,pi) and the targets, a
+// single-block loss kernel, 4 grouped-GEMM backward stages with fused relu masks and bias-gradient
+// column sums, the policy-head backward, one fused Adam+Polyak pass).  The sequence has fixed
+// pointers, so it is captured once into a hipGraph and replayed (no host work per step).
+// GEMMs are f32-in/f32-acc MFMA (v_mfma_f32_16x16x4_f32): a 16x16 output tile per 256-thread
+// block, K split across the four waves and reduced through LDS -- the shapes are tiny (batch 256,
+// width 256), so the kernel is built for latency (many small independent tiles), not throughput.
+#include <vector>
+#include <cstring>
+
+#include "internal.h"
+
+namespace mopo {
+
+constexpr int MAXP = 8;
+
+struct GemmProb {
+  int M, N, K;
+  const float* A; int lda; int ta;   // ta=0: A(i,k)=A[i*lda+k]; ta=1: A(i,k)=A[k*lda+i]
+  const float* B; int ldb; int tb;   // tb=0: B(k,j)=B[k*ldb+j]; tb=1: B(k,j)=B[j*ldb+k]
+  float* C; int ldc;
+  const float* bias;                 // C += bias[j]
+  int relu;                          // C = max(C, 0)
+  const float* mask; int ldm;        // C *= (mask(i,j) > 0)   (relu' from the saved activation)
+  float* colsum;                     // colsum[j] = sum_k B(k,j)   (bias gradient), by tile-row 0
+};
+
+struct GemmGroup {
+  int n;
+  int prefix[MAXP + 1];
+  GemmProb p[MAXP];
+};
+
+__global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
+  __shared__ float part[4][256];
+  __shared__ float csum[16][17];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int pi = 0;
+  while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
+  const GemmProb& p = g.p[pi];
+  const int t = blockIdx.x - g.prefix[pi];
+  const int tn_cnt = ceil_div(p.N, 16);
+  const int tm = t / tn_cnt, tn = t % tn_cnt;
+  const int i0 = tm * 16, j0 = tn * 16;
+  const int li = lane & 15, lk = lane >> 4;
+  // K split over the 4 waves in chunks of 4
+  const int ksteps = ceil_div(p.K, 4);
+  const int per = ceil_div(ksteps, 4);
+  const int kb = w * per * 4, ke = min(p.K, (w + 1) * per * 4);
+  f32x4 acc0 = zero4(), acc1 = zero4();
+  const int ai = i0 + li, bj = j0 + li;
+  int s = 0;
+  for (int k0 = kb; k0 < ke; k0 += 4, ++s) {
+    const int k = k0 + lk;
+    float a = 0.f, b = 0.f;
+    if (ai < p.M && k < ke) a = p.ta ? p.A[(int64_t)k * p.lda + ai] : p.A[(int64_t)ai * p.lda + k];
+    if (bj < p.N && k < ke) b = p.tb ? p.B[(int64_t)bj * p.ldb + k] : p.B[(int64_t)k * p.ldb + bj];
+    if (s & 1) acc1 = mfma4(a, b, acc1);
+    else acc0 = mfma4(a, b, acc0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[w][(lk * 4 + r) * 16 + li] = acc0[r] + acc1[r];  // D: col li, row 4*lk+r
+  // bias-gradient column sums of B over all K (tile row 0 only)
+  if (p.colsum && tm == 0) {
+    const int j = tid & 15, q = tid >> 4;
+    float cs = 0.f;
+    if (j0 + j < p.N)
+      for (int k = q; k < p.K; k += 16) cs += p.tb ? p.B[(int64_t)(j0 + j) * p.ldb + k] : p.B[(int64_t)k * p.ldb + j0 + j];
+    csum[q][j] = cs;
+  }
+  __syncthreads();
+  {
+    const int i = tid >> 4, j = tid & 15;
+    float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+    const int gi = i0 + i, gj = j0 + j;
+    if (gi < p.M && gj < p.N) {
+      if (p.bias) v += p.bias[gj];
+      if (p.relu) v = fmaxf(v, 0.f);
+      if (p.mask && !(p.mask[(int64_t)gi * p.ldm + gj] > 0.f)) v = 0.f;
+      p.C[(int64_t)gi * p.ldc + gj] = v;
+    }
+  }
+  if (p.colsum && tm == 0 && tid < 16) {
+    float cs = 0.f;
+    for (int q = 0; q < 16; ++q) cs += csum[q][tid];
+    if (j0 + tid < p.N) p.colsum[j0 + tid] = cs;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+struct SacDims { int O, A, H, n, n_env; int64_t P; };
+
+// parameter offsets (flat, TF creation order; mopo.py:32-33)
+struct Offs {
+  int64_t pW1, pb1, pW2, pb2, pWm, pbm, pWl, pbl;
+  int64_t q[2][6];  // W1 b1 W2 b2 W3 b3 for q1, q2
+  int64_t n_pi, n_q, total;
+};
+
+static Offs make_offs(int O, int A, int H) {
+  Offs o{};
+  int64_t c = 0;
+  auto take = [&](int64_t n) { int64_t r = c; c += n; return r; };
+  o.pW1 = take((int64_t)O * H); o.pb1 = take(H); o.pW2 = take((int64_t)H * H); o.pb2 = take(H);
+  o.pWm = take((int64_t)H * A); o.pbm = take(A); o.pWl = take((int64_t)H * A); o.pbl = take(A);
+  o.n_pi = c;
+  for (int qi = 0; qi < 2; ++qi) {
+    o.q[qi][0] = take((int64_t)(O + A) * H); o.q[qi][1] = take(H); o.q[qi][2] = take((int64_t)H * H);
+    o.q[qi][3] = take(H); o.q[qi][4] = take(H); o.q[qi][5] = take(1);
+  }
+  o.n_q = o.q[1][0] - o.q[0][0];
+  o.total = c;
+  return o;
+}
+
+enum {
+  LOG_Q1_LOSS = 0, LOG_Q2_LOSS, LOG_Q1, LOG_Q2, LOG_ALPHA, LOG_ENTROPY, LOG_LOGP, LOG_PI_GNORM, LOG_Q_GNORM,
+  LOG_PI_LOSS, LOG_N = 16
+};
+
+struct Sac {
+  SacDims d{};
+  Offs o{};
+  float lr, gamma, tau, rscale, tent;
+  void* mem = nullptr;
+  float *P, *G, *M, *V, *T;       // [total + 1]: last element = log_alpha
+  float* beta_pow;                // [2] f32 beta1_power, beta2_power (TF1 non-slot vars)
+  int64_t* iter;                  // device step counter (Philox)
+  float* logs;                    // [LOG_N]
+  float* norm_part;               // [nblk][2]
+  int adam_blocks = 0;
+  // activations
+  float *sa, *xpi, *xn, *rew, *term;
+  float *h1[8], *h2[8], *out[8];  // 0 pi(s) 1 pi(s') 2 Q1(s,a) 3 Q2(s,a) 4 Q1(s,pi) 5 Q2(s,pi) 6 Qt1 7 Qt2
+  float *logp_s, *logp_n, *eps_s, *eps_n;
+  float *dq[4];                   // dq for instances 2,3,4,5
+  float *dh2[4], *dh1[4];
+  float *dx1, *dx2, *dhead, *dh2p, *dh1p;
+  int64_t* idx;                   // [n] sampled rows
+  // device arrays of pointers for the multi-instance element-wise kernels
+  float** outp_dev;               // [8] out[]
+  float** dq_dev;                 // [4]
+  float** w3_dev;                 // [4] main W3 of Q1, Q2, Q1, Q2
+  float** h2q_dev;                // [4] h2[2..5]
+  float** dh2_dev;                // [4]
+  // graph
+  bool use_graph = true;
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  mopo_pool_desc genv{}, gmod{};
+  hipStream_t gstream = nullptr;
+  uint64_t gseed = 0;
+};
+
+// ---- batch gather (_training_batch, mopo.py:801-821): rows [0, n_env) from the env pool, rest
+// from the model pool; each index uniform over the pool's live size (Philox) unless injected
+__global__ void sac_gather_kernel(const mopo_pool_desc env, const mopo_pool_desc mod, int n, int n_env, int O, int A,
+                                  const int64_t* idx_in, int64_t* idx_out, uint64_t seed, const int64_t* iter,
+                                  float* sa, float* xpi, float* xn, float* rew, float* term) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const bool from_env = r < n_env;
+  const mopo_pool_desc& p = from_env ? env : mod;
+  int64_t src;
+  if (idx_in) {
+    src = idx_in[r];
+  } else {
+    const uint64_t size = (uint64_t)p.d_state[1];
+    u32x4 c{(uint32_t)r, (uint32_t)(*iter), (uint32_t)((uint64_t)(*iter) >> 32), RNG_SAC};
+    u32x4 q = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    src = (int64_t)(((uint64_t)q.x * size) >> 32);
+  }
+  idx_out[r] = src;
+  const int W = O + A;
+  for (int k = 0; k < O; ++k) {
+    const float v = p.d_obs[src * O + k];
+    sa[r * W + k] = v;
+    xpi[r * W + k] = v;
+    xn[r * W + k] = p.d_next_obs[src * O + k];
+  }
+  for (int k = 0; k < A; ++k) sa[r * W + O + k] = p.d_act[src * A + k];
+  rew[r] = p.d_rew[src];
+  term[r] = (float)p.d_term[src];
+}
+
+__device__ __forceinline__ float softplus_f(float x) { return softplusf(x); }
+
+// ---- squashed Gaussian head, forward (mopo.py:282-308, 286-296) for pi(s) and pi(s')
+__global__ void pi_head_fwd_kernel(int n, int O, int A, const float* head_s, const float* head_n, const float* eps_in_s,
+                                   const float* eps_in_n, float* eps_s, float* eps_n, uint64_t seed,
+                                   const int64_t* iter, float* xpi, float* xn, float* logp_s, float* logp_n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * n) return;
+  const bool nxt = t >= n;
+  const int r = nxt ? t - n : t;
+  const float* hd = (nxt ? head_n : head_s) + r * 2 * A;
+  const float* ein = nxt ? eps_in_n : eps_in_s;
+  float* eo = (nxt ? eps_n : eps_s) + r * A;
+  float z[8];
+  if (ein) {
+    for (int j = 0; j < A; ++j) z[j] = ein[r * A + j];
+  } else {
+    for (int blk = 0; blk * 4 < A; ++blk) {
+      u32x4 c{(uint32_t)r | ((uint32_t)nxt << 31), (uint32_t)(*iter) ^ ((uint32_t)blk << 24),
+              (uint32_t)((uint64_t)(*iter) >> 32), RNG_SAC + 16};
+      u32x4 q = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+      float zz[4];
+      box_muller(q.x, q.y, zz[0], zz[1]);
+      box_muller(q.z, q.w, zz[2], zz[3]);
+      for (int i = 0; i < 4 && blk * 4 + i < A; ++i) z[blk * 4 + i] = zz[i];
+    }
+  }
+  float logp = 0.f, corr = 0.f;
+  float* x = (nxt ? xn : xpi) + r * (O + A) + O;
+  for (int j = 0; j < A; ++j) {
+    const float mu = hd[j];
+    const float ls = fminf(fmaxf(hd[A + j], -20.f), 2.f);
+    const float sd = expf(ls);
+    const float u = mu + z[j] * sd;
+    const float zz = (u - mu) / (sd + 1e-8f);
+    logp += -0.5f * (zz * zz + 2.f * ls + 1.8378770664093453f);
+    corr += 2.f * (0.6931471805599453f - u - softplus_f(-2.f * u));
+    x[j] = tanhf(u);
+    eo[j] = z[j];
+  }
+  (nxt ? logp_n : logp_s)[r] = logp - corr;
+}
+
+__device__ float block_sum(float v, float* sh) {
+  // deterministic tree reduction over blockDim.x (power of two <= 1024)
+  const int tid = threadIdx.x;
+  sh[tid] = v;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (tid < s) sh[tid] += sh[tid + s];
+    __syncthreads();
+  }
+  float r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+// ---- losses, output gradients, alpha gradient, logs (single block, one thread per row)
+__global__ __launch_bounds__(1024) void sac_loss_kernel(int n, int A, float gamma, float rscale, float tent,
+                                                        float* const* outs, const float* logp_s, const float* logp_n,
+                                                        const float* rew, const float* term, const float* head_s,
+                                                        const float* log_alpha, float* dq1, float* dq2, float* dq1p,
+                                                        float* dq2p, float* g_alpha, float* logs) {
+  __shared__ float sh[1024];
+  const int r = threadIdx.x;
+  const bool ok = r < n;
+  const float alpha = expf(*log_alpha);                             // mopo.py:361
+  float q1 = 0, q2 = 0, q1p = 0, q2p = 0, lps = 0, ent = 0, y = 0;
+  if (ok) {
+    q1 = outs[2][r]; q2 = outs[3][r]; q1p = outs[4][r]; q2p = outs[5][r];
+    const float qt = fminf(outs[6][r], outs[7][r]);                 // mopo.py:368
+    y = rscale * rew[r] + gamma * ((1.f - term[r]) * (qt - alpha * logp_n[r]));  // mopo.py:380-386
+    lps = logp_s[r];
+    const float inv_n = 1.f / (float)n;
+    dq1[r] = (q1 - y) * inv_n;                                      // d(0.5 mean (q-y)^2)
+    dq2[r] = (q2 - y) * inv_n;
+    const bool sel1 = q1p <= q2p;                                   // tf.minimum grad -> x where x <= y
+    dq1p[r] = sel1 ? -inv_n : 0.f;
+    dq2p[r] = sel1 ? 0.f : -inv_n;
+    for (int j = 0; j < A; ++j) {                                   // pi_entropy (mopo.py:341)
+      const float ls = fminf(fmaxf(head_s[r * 2 * A + A + j], -20.f), 2.f);
+      ent += logf(expf(ls) + 1e-8f) + 0.5f * logf(2.f * 3.14159265358979f * 2.718281828459045f);
+    }
+  }
+  const float fn = (float)n;
+  const float l1 = block_sum(ok ? (q1 - y) * (q1 - y) : 0.f, sh) / fn * 0.5f;   // mopo.py:403
+  const float l2 = block_sum(ok ? (q2 - y) * (q2 - y) : 0.f, sh) / fn * 0.5f;
+  const float m1 = block_sum(q1, sh) / fn, m2 = block_sum(q2, sh) / fn;
+  const float mlp = block_sum(lps, sh) / fn;
+  const float ment = block_sum(ent, sh) / fn;
+  const float pil = block_sum(ok ? alpha * lps - fminf(q1p, q2p) : 0.f, sh) / fn;  // mopo.py:371-377
+  if (r == 0) {
+    *g_alpha = -(mlp + tent);                                       // d/dlog_alpha of -mean(la*(logp+H))
+    logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;
+    logs[LOG_ALPHA] = alpha; logs[LOG_ENTROPY] = ment; logs[LOG_LOGP] = mlp; logs[LOG_PI_LOSS] = pil;
+  }
+}
+
+// ---- dh2 = dq (x) W3 * (h2 > 0) for the 4 critic instances (rank-1 output layer backward)
+__global__ void q_out_bwd_kernel(int n, int H, const float* const* dq, const float* const* W3, const float* const* h2,
+                                 float* const* dh2) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int inst = blockIdx.y;
+  if (t >= (int64_t)n * H) return;
+  const int r = t / H, j = t % H;
+  const float h = h2[inst][t];
+  dh2[inst][t] = h > 0.f ? dq[inst][r] * W3[inst][j] : 0.f;
+}
+
+// ---- squashed Gaussian head backward + dh2 of the policy trunk (one block per batch row)
+__global__ __launch_bounds__(256) void pi_head_bwd_kernel(int n, int O, int A, int H, const float* head_s,
+                                                          const float* eps_s, const float* dx1, const float* dx2,
+                                                          const float* log_alpha, const float* Wm, const float* Wl,
+                                                          const float* h2p, float* dhead, float* dh2p) {
+  __shared__ float dmu_s[8], dls_s[8];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  if (tid < A) {
+    const int j = tid;
+    const float g = expf(*log_alpha) / (float)n;                    // d L_pi / d logp (stop_gradient(alpha))
+    const float mu = head_s[r * 2 * A + j], raw = head_s[r * 2 * A + A + j];
+    const float ls = fminf(fmaxf(raw, -20.f), 2.f);
+    const float sd = expf(ls);
+    const float e = eps_s[r * A + j];
+    const float u = mu + e * sd;
+    const float a = tanhf(u);
+    const float inv = 1.f / (sd + 1e-8f);
+    const float zz = (u - mu) * inv;
+    const float da = dx1[r * (O + A) + O + j] + dx2[r * (O + A) + O + j];  // -dmin q / da through Q1/Q2
+    float du = da * (1.f - a * a);                                  // tanh grad (y-based)
+    du += g * (-zz * inv);                                          // gaussian_likelihood wrt x
+    du += g * (2.f - 4.f / (1.f + expf(2.f * u)));                  // squash correction: 2 - 4 sigmoid(-2u)
+    const float dmu = g * zz * inv + du;
+    const float dstd = g * zz * zz * inv + du * e;
+    float dls = -g + dstd * sd;
+    if (!(raw >= -20.f && raw <= 2.f)) dls = 0.f;                   // clip_by_value grad
+    dhead[r * 2 * A + j] = dmu;
+    dhead[r * 2 * A + A + j] = dls;
+    dmu_s[j] = dmu;
+    dls_s[j] = dls;
+  }
+  __syncthreads();
+  for (int j = tid; j < H; j += blockDim.x) {
+    float v = 0.f;
+    for (int k = 0; k < A; ++k) v += dmu_s[k] * Wm[j * A + k] + dls_s[k] * Wl[j * A + k];
+    dh2p[(int64_t)r * H + j] = h2p[(int64_t)r * H + j] > 0.f ? v : 0.f;
+  }
+}
+
+// ---- four TF1 Adams (identical step counts -> one lr_t) + Polyak, and grad-norm partials
+__global__ __launch_bounds__(256) void sac_adam_kernel(int64_t total, int64_t n_pi, int64_t n_q, float* P, const float* G,
+                                                       float* Mm, float* Vv, float* T, const float* beta_pow, float lr,
+                                                       float tau, float* norm_part) {
+  __shared__ float sh[256];
+  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
+  const float lr_t = lr * sqrtf(1.f - beta_pow[1]) / (1.f - beta_pow[0]);
+  float npi = 0.f, nq = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= total; i += (int64_t)gridDim.x * blockDim.x) {
+    const float g = G[i];
+    if (i < n_pi) npi += g * g;
+    else if (i < n_pi + n_q) nq += g * g;
+    float m = Mm[i], v = Vv[i];
+    m += (g - m) * (1.f - b1);
+    v += (g * g - v) * (1.f - b2);
+    Mm[i] = m;
+    Vv[i] = v;
+    const float p = P[i] - (m * lr_t) / (sqrtf(v) + eps);
+    P[i] = p;
+    if (i < total) T[i] = (1.f - tau) * T[i] + tau * p;             // mopo.py:446-447 (after the updates)
+  }
+  npi = block_sum(npi, sh);
+  nq = block_sum(nq, sh);
+  if (threadIdx.x == 0) {
+    norm_part[blockIdx.x * 2] = npi;
+    norm_part[blockIdx.x * 2 + 1] = nq;
+  }
+}
+
+__global__ void sac_finalize_kernel(int nblk, const float* norm_part, float* logs, float* beta_pow, int64_t* iter) {
+  float a = 0.f, b = 0.f;
+  for (int i = 0; i < nblk; ++i) { a += norm_part[2 * i]; b += norm_part[2 * i + 1]; }
+  logs[LOG_PI_GNORM] = sqrtf(a);
+  logs[LOG_Q_GNORM] = 0.5f * sqrtf(b);                                // grads of Q_loss = (l1+l2)/2 wrt q1
+  beta_pow[0] *= 0.9f;
+  beta_pow[1] *= 0.999f;
+  *iter += 1;
+}
+
+// ---------------------------------------------------------------------------------------------
+static GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C,
+                   int ldc) {
+  GemmProb p{};
+  p.M = M; p.N = N; p.K = K; p.A = A; p.lda = lda; p.ta = ta; p.B = B; p.ldb = ldb; p.tb = tb; p.C = C; p.ldc = ldc;
+  return p;
+}
+
+static int launch_group(std::vector<GemmProb> ps, hipStream_t s) {
+  GemmGroup g{};
+  g.n = (int)ps.size();
+  if (g.n > MAXP) return fail("sac: gemm group too large");
+  int tot = 0;
+  for (int i = 0; i < g.n; ++i) {
+    g.p[i] = ps[i];
+    g.prefix[i] = tot;
+    tot += ceil_div(ps[i].M, 16) * ceil_div(ps[i].N, 16);
+  }
+  g.prefix[g.n] = tot;
+  hipLaunchKernelGGL(gemm_group_kernel, dim3(tot), dim3(256), 0, s, g);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+static int sac_step_impl(Sac* h, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
+                         const int64_t* idx_in, const float* eps_in_s, const float* eps_in_n, hipStream_t s) {
+  const SacDims& d = h->d;
+  const Offs& o = h->o;
+  const int n = d.n, O = d.O, A = d.A, H = d.H, W = O + A;
+  const float* P = h->P;
+  const float* T = h->T;
+  float* G = h->G;
+  hipLaunchKernelGGL(sac_gather_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, *env, *mod, n, d.n_env, O, A, idx_in,
+                     h->idx, seed, h->iter, h->sa, h->xpi, h->xn, h->rew, h->term);
+  MOPO_HIP(hipGetLastError());
+  auto Wq = [&](int qi, int k) { return P + o.q[qi][k]; };
+  auto Tq = [&](int qi, int k) { return T + o.q[qi][k]; };
+  // ---- forward stage 1-3: pi(s), pi(s'), Q1(s,a), Q2(s,a)
+  {
+    std::vector<GemmProb> g;
+    auto a = mk(n, H, O, h->sa, W, 0, P + o.pW1, H, 0, h->h1[0], H); a.bias = P + o.pb1; a.relu = 1; g.push_back(a);
+    auto b = mk(n, H, O, h->xn, W, 0, P + o.pW1, H, 0, h->h1[1], H); b.bias = P + o.pb1; b.relu = 1; g.push_back(b);
+    for (int qi = 0; qi < 2; ++qi) {
+      auto c = mk(n, H, W, h->sa, W, 0, Wq(qi, 0), H, 0, h->h1[2 + qi], H); c.bias = Wq(qi, 1); c.relu = 1; g.push_back(c);
+    }
+    if (launch_group(g, s)) return -1;
+  }
+  {
+    std::vector<GemmProb> g;
+    for (int i = 0; i < 4; ++i) {
+      const float* w2 = i < 2 ? P + o.pW2 : Wq(i - 2, 2);
+      const float* b2 = i < 2 ? P + o.pb2 : Wq(i - 2, 3);
+      auto a = mk(n, H, H, h->h1[i], H, 0, w2, H, 0, h->h2[i], H); a.bias = b2; a.relu = 1; g.push_back(a);
+    }
+    if (launch_group(g, s)) return -1;
+  }
+  {
+    std::vector<GemmProb> g;
+    for (int i = 0; i < 2; ++i) {
+      auto m = mk(n, A, H, h->h2[i], H, 0, P + o.pWm, A, 0, h->out[i], 2 * A); m.bias = P + o.pbm; g.push_back(m);
+      auto l = mk(n, A, H, h->h2[i], H, 0, P + o.pWl, A, 0, h->out[i] + A, 2 * A); l.bias = P + o.pbl; g.push_back(l);
+    }
+    for (int qi = 0; qi < 2; ++qi) {
+      auto q = mk(n, 1, H, h->h2[2 + qi], H, 0, Wq(qi, 4), 1, 0, h->out[2 + qi], 1); q.bias = Wq(qi, 5); g.push_back(q);
+    }
+    if (launch_group(g, s)) return -1;
+  }
+  hipLaunchKernelGGL(pi_head_fwd_kernel, dim3(ceil_div(2 * n, 256)), dim3(256), 0, s, n, O, A, h->out[0], h->out[1],
+                     eps_in_s, eps_in_n, h->eps_s, h->eps_n, seed, h->iter, h->xpi, h->xn, h->logp_s, h->logp_n);
+  MOPO_HIP(hipGetLastError());
+  // ---- forward stage 4-6: Q1/Q2(s, pi(s)) with main params, Qt1/Qt2(s', pi(s')) with target params
+  {
+    std::vector<GemmProb> g;
+    for (int i = 0; i < 4; ++i) {
+      const int qi = i & 1;
+      const bool tgt = i >= 2;
+      const float* x = tgt ? h->xn : h->xpi;
+      auto a = mk(n, H, W, x, W, 0, tgt ? Tq(qi, 0) : Wq(qi, 0), H, 0, h->h1[4 + i], H);
+      a.bias = tgt ? Tq(qi, 1) : Wq(qi, 1); a.relu = 1; g.push_back(a);
+    }
+    if (launch_group(g, s)) return -1;
+  }
+  {
+    std::vector<GemmProb> g;
+    for (int i = 0; i < 4; ++i) {
+      const int qi = i & 1;
+      const bool tgt = i >= 2;
+      auto a = mk(n, H, H, h->h1[4 + i], H, 0, tgt ? Tq(qi, 2) : Wq(qi, 2), H, 0, h->h2[4 + i], H);
+      a.bias = tgt ? Tq(qi, 3) : Wq(qi, 3); a.relu = 1; g.push_back(a);
+    }
+    if (launch_group(g, s)) return -1;
+  }
+  {
+    std::vector<GemmProb> g;
+    for (int i = 0; i < 4; ++i) {
+      const int qi = i & 1;
+      const bool tgt = i >= 2;
+      auto a = mk(n, 1, H, h->h2[4 + i], H, 0, tgt ? Tq(qi, 4) : Wq(qi, 4), 1, 0, h->out[4 + i], 1);
+      a.bias = tgt ? Tq(qi, 5) : Wq(qi, 5); g.push_back(a);
+    }
+    if (launch_group(g, s)) return -1;
+  }
+  // ---- losses
+  hipLaunchKernelGGL(sac_loss_kernel, dim3(1), dim3(1024), 0, s, n, A, h->gamma, h->rscale, h->tent, h->outp_dev,
+                     h->logp_s, h->logp_n, h->rew, h->term, h->out[0], P + o.total, h->dq[0], h->dq[1], h->dq[2],
+                     h->dq[3], G + o.total, h->logs);
+  MOPO_HIP(hipGetLastError());
+  // ---- critic backward: output layer (rank-1), then hidden layers
+  hipLaunchKernelGGL(q_out_bwd_kernel, dim3(ceil_div(n * H, 256), 4), dim3(256), 0, s, n, H, h->dq_dev, h->w3_dev,
+                     h->h2q_dev, h->dh2_dev);
+  MOPO_HIP(hipGetLastError());
+  {
+    std::vector<GemmProb> g;
+    for (int i = 0; i < 4; ++i) {  // dh1 = dh2 W2^T * (h1 > 0); instances Q1(sa) Q2(sa) Q1(pi) Q2(pi)
+      const int qi = i & 1;
+      auto a = mk(n, H, H, h->dh2[i], H, 0, Wq(qi, 2), H, 1, h->dh1[i], H); a.mask = h->h1[2 + i]; a.ldm = H;
+      g.push_back(a);
+    }
+    for (int qi = 0; qi < 2; ++qi) {  // dW2 = h1^T dh2 (+db2), dW3 = h2^T dq (+db3)
+      auto w2 = mk(H, H, n, h->h1[2 + qi], H, 1, h->dh2[qi], H, 0, G + o.q[qi][2], H); w2.colsum = G + o.q[qi][3];
+      g.push_back(w2);
+      auto w3 = mk(H, 1, n, h->h2[2 + qi], H, 1, h->dq[qi], 1, 0, G + o.q[qi][4], 1); w3.colsum = G + o.q[qi][5];
+      g.push_back(w3);
+    }
+    if (launch_group(g, s)) return -1;
+  }
+  {
+    std::vector<GemmProb> g;
+    g.push_back(mk(n, W, H, h->dh1[2], H, 0, Wq(0, 0), H, 1, h->dx1, W));   // d/dx of Q1(s, pi)
+    g.push_back(mk(n, W, H, h->dh1[3], H, 0, Wq(1, 0), H, 1, h->dx2, W));   // d/dx of Q2(s, pi)
+    for (int qi = 0; qi < 2; ++qi) {  // dW1 = [s,a]^T dh1 (+db1)
+      auto w1 = mk(W, H, n, h->sa, W, 1, h->dh1[qi], H, 0, G + o.q[qi][0], H); w1.colsum = G + o.q[qi][1];
+      g.push_back(w1);
+    }
+    if (launch_group(g, s)) return -1;
+  }
+  // ---- policy backward
+  hipLaunchKernelGGL(pi_head_bwd_kernel, dim3(n), dim3(256), 0, s, n, O, A, H, h->out[0], h->eps_s, h->dx1, h->dx2,
+                     P + o.total, P + o.pWm, P + o.pWl, h->h2[0], h->dhead, h->dh2p);
+  MOPO_HIP(hipGetLastError());
+  {
+    std::vector<GemmProb> g;
+    auto a = mk(n, H, H, h->dh2p, H, 0, P + o.pW2, H, 1, h->dh1p, H); a.mask = h->h1[0]; a.ldm = H; g.push_back(a);
+    auto w2 = mk(H, H, n, h->h1[0], H, 1, h->dh2p, H, 0, G + o.pW2, H); w2.colsum = G + o.pb2; g.push_back(w2);
+    auto wm = mk(H, A, n, h->h2[0], H, 1, h->dhead, 2 * A, 0, G + o.pWm, A); wm.colsum = G + o.pbm; g.push_back(wm);
+    auto wl = mk(H, A, n, h->h2[0], H, 1, h->dhead + A, 2 * A, 0, G + o.pWl, A); wl.colsum = G + o.pbl; g.push_back(wl);
+    if (launch_group(g, s)) return -1;
+  }
+  {
+    std::vector<GemmProb> g;
+    auto w1 = mk(O, H, n, h->sa, W, 1, h->dh1p, H, 0, G + o.pW1, H); w1.colsum = G + o.pb1; g.push_back(w1);
+    if (launch_group(g, s)) return -1;
+  }
+  // ---- Adam x4 + Polyak, norms, counters
+  hipLaunchKernelGGL(sac_adam_kernel, dim3(h->adam_blocks), dim3(256), 0, s, o.total, o.n_pi, o.n_q, h->P, h->G, h->M,
+                     h->V, h->T, h->beta_pow, h->lr, h->tau, h->norm_part);
+  MOPO_HIP(hipGetLastError());
+  hipLaunchKernelGGL(sac_finalize_kernel, dim3(1), dim3(1), 0, s, h->adam_blocks, h->norm_part, h->logs, h->beta_pow,
+                     h->iter);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace mopo
+
+using namespace mopo;
+
+extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, int n_env, const float* h_params,
+                               float log_alpha, float lr, float gamma, float tau, float reward_scale,
+                               float target_entropy) {
+  MOPO_REQUIRE(out && h_params, "mopo_sac_create: NULL argument");
+  MOPO_REQUIRE(O >= 1 && A >= 1 && A <= 8 && H >= 1, "mopo_sac_create: bad dims (act_dim <= 8)");
+  MOPO_REQUIRE(batch >= 1 && batch <= 1024, "mopo_sac_create: batch must be in [1, 1024]");
+  MOPO_REQUIRE(n_env >= 0 && n_env <= batch, "mopo_sac_create: n_env must be in [0, batch]");
+  Sac* h = new Sac();
+  h->d = SacDims{O, A, H, batch, n_env, 0};
+  h->o = make_offs(O, A, H);
+  h->d.P = h->o.total;
+  h->lr = lr; h->gamma = gamma; h->tau = tau; h->rscale = reward_scale; h->tent = target_entropy;
+  const int64_t tot = h->o.total + 1, n = batch, W = O + A;
+  h->adam_blocks = (int)std::min<int64_t>(512, (tot + 255) / 256);
+  std::vector<std::pair<void**, size_t>> reg;
+  auto f = [&](float** p, size_t cnt) { reg.push_back({(void**)p, cnt * 4}); };
+  f(&h->P, tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->T, tot);
+  f(&h->beta_pow, 2); f(&h->logs, LOG_N); f(&h->norm_part, 2 * h->adam_blocks);
+  reg.push_back({(void**)&h->iter, 8});
+  f(&h->sa, n * W); f(&h->xpi, n * W); f(&h->xn, n * W); f(&h->rew, n); f(&h->term, n);
+  for (int i = 0; i < 8; ++i) { f(&h->h1[i], n * H); f(&h->h2[i], n * H); f(&h->out[i], n * 2 * A); }
+  f(&h->logp_s, n); f(&h->logp_n, n); f(&h->eps_s, n * A); f(&h->eps_n, n * A);
+  for (int i = 0; i < 4; ++i) { f(&h->dq[i], n); f(&h->dh2[i], n * H); f(&h->dh1[i], n * H); }
+  f(&h->dx1, n * W); f(&h->dx2, n * W); f(&h->dhead, n * 2 * A); f(&h->dh2p, n * H); f(&h->dh1p, n * H);
+  reg.push_back({(void**)&h->idx, (size_t)n * 8});
+  reg.push_back({(void**)&h->outp_dev, 8 * sizeof(float*)});
+  reg.push_back({(void**)&h->dq_dev, 4 * sizeof(float*)});
+  reg.push_back({(void**)&h->w3_dev, 4 * sizeof(float*)});
+  reg.push_back({(void**)&h->h2q_dev, 4 * sizeof(float*)});
+  reg.push_back({(void**)&h->dh2_dev, 4 * sizeof(float*)});
+  size_t total = 0;
+  for (auto& r : reg) total += (r.second + 255) & ~(size_t)255;
+  if (hipMalloc(&h->mem, total) != hipSuccess) { delete h; return fail("mopo_sac_create: out of device memory"); }
+  if (hipMemset(h->mem, 0, total) != hipSuccess) { (void)hipFree(h->mem); delete h; return fail("mopo_sac_create: memset"); }
+  char* m = (char*)h->mem;
+  for (auto& r : reg) { *r.first = m; m += (r.second + 255) & ~(size_t)255; }
+  // parameters, target = main (target_init, mopo.py:449-450), log_alpha, beta powers
+  std::vector<float> pv(h_params, h_params + h->o.total);
+  pv.push_back(log_alpha);
+  MOPO_HIP(hipMemcpy(h->P, pv.data(), tot * 4, hipMemcpyHostToDevice));
+  MOPO_HIP(hipMemcpy(h->T, pv.data(), tot * 4, hipMemcpyHostToDevice));
+  float bp[2] = {0.9f, 0.999f};
+  MOPO_HIP(hipMemcpy(h->beta_pow, bp, 8, hipMemcpyHostToDevice));
+  float* outs[8];
+  for (int i = 0; i < 8; ++i) outs[i] = h->out[i];
+  MOPO_HIP(hipMemcpy(h->outp_dev, outs, sizeof(outs), hipMemcpyHostToDevice));
+  MOPO_HIP(hipMemcpy(h->dq_dev, h->dq, 4 * sizeof(float*), hipMemcpyHostToDevice));
+  float* w3[4] = {h->P + h->o.q[0][4], h->P + h->o.q[1][4], h->P + h->o.q[0][4], h->P + h->o.q[1][4]};
+  MOPO_HIP(hipMemcpy(h->w3_dev, w3, sizeof(w3), hipMemcpyHostToDevice));
+  float* h2q[4] = {h->h2[2], h->h2[3], h->h2[4], h->h2[5]};
+  MOPO_HIP(hipMemcpy(h->h2q_dev, h2q, sizeof(h2q), hipMemcpyHostToDevice));
+  MOPO_HIP(hipMemcpy(h->dh2_dev, h->dh2, 4 * sizeof(float*), hipMemcpyHostToDevice));
+  *out = reinterpret_cast<mopo_sac_t>(h);
+  return 0;
+}
+
+extern "C" int mopo_sac_destroy(mopo_sac_t hh) {
+  Sac* h = reinterpret_cast<Sac*>(hh);
+  if (!h) return 0;
+  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+  if (h->graph) (void)hipGraphDestroy(h->graph);
+  if (h->mem) (void)hipFree(h->mem);
+  delete h;
+  return 0;
+}
+
+extern "C" int mopo_sac_buffers(mopo_sac_t hh, float** params, float** target, float** adam_m, float** adam_v,
+                                float** grads, float** logs, int64_t* n_params) {
+  Sac* h = reinterpret_cast<Sac*>(hh);
+  MOPO_REQUIRE(h, "mopo_sac_buffers: NULL handle");
+  if (params) *params = h->P;
+  if (target) *target = h->T;
+  if (adam_m) *adam_m = h->M;
+  if (adam_v) *adam_v = h->V;
+  if (grads) *grads = h->G;
+  if (logs) *logs = h->logs;
+  if (n_params) *n_params = h->o.total;
+  return 0;
+}
+
+extern "C" int mopo_sac_copy(mopo_sac_t hh, int which, int to_handle, void* d_buf, int64_t count, void* stream) {
+  Sac* h = reinterpret_cast<Sac*>(hh);
+  MOPO_REQUIRE(h && d_buf, "mopo_sac_copy: NULL argument");
+  float* bufs[6] = {h->P, h->T, h->M, h->V, h->G, h->logs};
+  MOPO_REQUIRE(which >= 0 && which < 6, "mopo_sac_copy: which must be in [0, 6)");
+  const int64_t cap = which == 5 ? LOG_N : h->o.total + 1;
+  MOPO_REQUIRE(count >= 0 && count <= cap, "mopo_sac_copy: count exceeds the buffer");
+  if (to_handle)
+    MOPO_HIP(hipMemcpyAsync(bufs[which], d_buf, count * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  else
+    MOPO_HIP(hipMemcpyAsync(d_buf, bufs[which], count * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+extern "C" int mopo_sac_set_graph(mopo_sac_t hh, int enable) {
+  Sac* h = reinterpret_cast<Sac*>(hh);
+  MOPO_REQUIRE(h, "mopo_sac_set_graph: NULL handle");
+  h->use_graph = enable != 0;
+  return 0;
+}
+
+static bool same_desc(const mopo_pool_desc& a, const mopo_pool_desc& b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
+
+extern "C" int mopo_sac_step(mopo_sac_t hh, const mopo_pool_desc* env, const mopo_pool_desc* mod, int n_steps,
+                             uint64_t seed, const int64_t* d_idx, const float* d_eps_s, const float* d_eps_n,
+                             void* stream) {
+  Sac* h = reinterpret_cast<Sac*>(hh);
+  MOPO_REQUIRE(h && env && mod, "mopo_sac_step: NULL argument");
+  MOPO_REQUIRE(env->d_state && mod->d_state, "mopo_sac_step: pool state required");
+  hipStream_t s = (hipStream_t)stream;
+  const bool injected = d_idx || d_eps_s || d_eps_n;
+  if (injected) {
+    MOPO_REQUIRE(n_steps == 1, "mopo_sac_step: injected streams drive exactly one step");
+    return sac_step_impl(h, env, mod, seed, d_idx, d_eps_s, d_eps_n, s);
+  }
+  if (!h->use_graph) {
+    for (int i = 0; i < n_steps; ++i)
+      if (sac_step_impl(h, env, mod, seed, nullptr, nullptr, nullptr, s)) return -1;
+    return 0;
+  }
+  if (!h->gexec || !same_desc(h->genv, *env) || !same_desc(h->gmod, *mod) || h->gseed != seed || h->gstream != s) {
+    if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+    if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
+    MOPO_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    const int rc = sac_step_impl(h, env, mod, seed, nullptr, nullptr, nullptr, s);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(s, &g);
+    if (rc) { if (g) (void)hipGraphDestroy(g); return -1; }
+    if (e != hipSuccess) return fail(std::string("mopo_sac_step: capture failed: ") + hipGetErrorString(e));
+    h->graph = g;
+    MOPO_HIP(hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0));
+    h->genv = *env; h->gmod = *mod; h->gseed = seed; h->gstream = s;
+  }
+  for (int i = 0; i < n_steps; ++i) MOPO_HIP(hipGraphLaunch(h->gexec, s));
+  return 0;
+}

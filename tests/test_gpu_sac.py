@@ -1,0 +1,159 @@
+"""GPU parity: the SAC update (K6/K7) vs the fp64 oracle restatement of mopo.py's graph.
+
+Tolerances (fp32 device vs fp64 oracle, identical batch rows and policy noise):
+  * losses / logged means / alpha / grad norms:      rel 2e-4
+  * gradients (every parameter):                      |d| <= 1e-4 * max|g| of that tensor + 1e-7
+  * Adam m, v after one step: follow from the gradient tolerance (checked the same way)
+  * params after one step: |d| <= 1e-6 + 2*lr_t where a gradient is ~0 (Adam's first step is
+    lr_t*sign(g), so a sign flip of a vanishing gradient moves a param by <= 2 lr_t); all others 1e-6
+  * 20 steps: losses within 1e-3 relative (chaotic divergence afterwards is expected)
+"""
+import numpy as np
+import pytest
+
+from oracle import replay_pool as opool
+from oracle import sac as osac
+
+pytestmark = pytest.mark.gpu
+O, A, H = 17, 6, 256
+
+
+def pools(rs, n_env_rows=500, n_model_rows=3000):
+    import torch
+    from mopo_amd.replay_pool import SimpleReplayPool
+    out = []
+    for n in (n_env_rows, n_model_rows):
+        s = {'observations': rs.normal(size=(n, O)).astype(np.float32),
+             'actions': rs.uniform(-1, 1, (n, A)).astype(np.float32),
+             'next_observations': rs.normal(size=(n, O)).astype(np.float32),
+             'rewards': rs.normal(size=(n, 1)).astype(np.float32),
+             'terminals': rs.uniform(size=(n, 1)) < 0.1}
+        p = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=n + 10)
+        p.add_samples(s)
+        op = opool.Pool(O, A, n + 10)
+        op.add_samples(s)
+        out.append((p, op))
+    torch.cuda.synchronize()
+    return out
+
+
+def draw(rs, env_size, model_size, n=256, n_env=12):
+    idx = np.concatenate([rs.randint(0, env_size, n_env), rs.randint(0, model_size, n - n_env)])
+    return idx, rs.normal(size=(n, A)).astype(np.float32), rs.normal(size=(n, A)).astype(np.float32)
+
+
+def host_batch(env_op, mod_op, idx, n_env=12):
+    b1 = env_op.batch_by_indices(idx[:n_env])
+    b2 = mod_op.batch_by_indices(idx[n_env:])
+    return {k: np.concatenate([b1[k], b2[k]]).astype(np.float64) for k in b1}   # mopo.py:815-816
+
+
+def oracle_grads(st, batch, e1, e2, gamma=0.99, tent=-3.0):
+    """Gradients of one step (pre-update params), same math as osac.sac_step."""
+    s, a, s2 = batch['observations'], batch['actions'], batch['next_observations']
+    r, d = batch['rewards'][:, 0], batch['terminals'][:, 0]
+    n = s.shape[0]
+    P, Q1, Q2 = osac.split(st.params)
+    T = osac.split(st.target)
+    alpha = np.exp(st.log_alpha)
+    _, a_pi, logp_pi, _, cpi = osac.pi_forward(P, s, e1)
+    q1_pi, c1p = osac.q_forward(Q1, s, a_pi)
+    q2_pi, c2p = osac.q_forward(Q2, s, a_pi)
+    _, a_n, logp_n, _, _ = osac.pi_forward(P, s2, e2)
+    y = r + gamma * (1 - d) * (np.minimum(osac.q_forward(T[1], s2, a_n)[0], osac.q_forward(T[2], s2, a_n)[0])
+                               - alpha * logp_n)
+    q1, c1 = osac.q_forward(Q1, s, a)
+    q2, c2 = osac.q_forward(Q2, s, a)
+    g1, _ = osac.q_backward(Q1, c1, (q1 - y) / n)
+    g2, _ = osac.q_backward(Q2, c2, (q2 - y) / n)
+    sel = q1_pi <= q2_pi
+    _, dx1 = osac.q_backward(Q1, c1p, np.where(sel, -1.0 / n, 0.0), need_params=False)
+    _, dx2 = osac.q_backward(Q2, c2p, np.where(sel, 0.0, -1.0 / n), need_params=False)
+    gp = osac.pi_backward(P, cpi, np.full(n, alpha / n), dx1[:, O:] + dx2[:, O:])
+    return gp + g1 + g2, -np.mean(logp_pi + tent)
+
+
+def flat(ts):
+    return np.concatenate([np.asarray(t).ravel() for t in ts])
+
+
+def test_sac_one_step_parity():
+    from mopo_amd.sac import SAC
+    rs = np.random.RandomState(0)
+    (env_p, env_op), (mod_p, mod_op) = pools(rs)
+    params = osac.init_params(O, A, H, seed=5)
+    params = [p + rs.normal(size=p.shape) * 0.02 for p in params]        # non-zero biases
+    fl = flat(params).astype(np.float32)
+    sac = SAC(O, A, H, batch_size=256, real_ratio=0.05, target_entropy=-3, params=fl, log_alpha=0.1)
+    assert sac.n_env == 12
+    idx, e1, e2 = draw(rs, env_p.size, mod_p.size)
+    st = osac.SACState([p.astype(np.float32).astype(np.float64) for p in params], log_alpha=np.float32(0.1))
+    batch = host_batch(env_op, mod_op, idx)
+    gref, garef = oracle_grads(st, batch, e1.astype(np.float64), e2.astype(np.float64))
+    logs_ref = osac.sac_step(st, batch, e1.astype(np.float64), e2.astype(np.float64))
+    sac._do_training(0, env_p, mod_p, idx=idx, eps_s=e1, eps_n=e2)
+    lg = sac.logs()
+    for k in ['Q/q1_loss', 'sac_Q/q2_loss', 'sac_Q/q1', 'sac_Q/q2', 'sac_pi/alpha', 'sac_pi/pi_entropy',
+              'sac_pi/logp_pi', 'sac_pi/pi_global_norm', 'sac_Q/q_global_norm']:
+        np.testing.assert_allclose(lg[k], logs_ref[k], rtol=2e-4, atol=1e-6, err_msg=k)
+    np.testing.assert_allclose(lg['policy_loss'], logs_ref['pi_loss'], rtol=2e-4, atol=1e-6)
+    g, ga = sac.get_grads()
+    g = g.cpu().numpy()
+    off = 0
+    for i, gr in enumerate(gref):
+        n = gr.size
+        scale = np.abs(gr).max() + 1e-12
+        err = np.abs(g[off:off + n] - gr.ravel()).max()
+        assert err <= 1e-4 * scale + 1e-7, 'grad tensor %d: err %.3g scale %.3g' % (i, err, scale)
+        off += n
+    np.testing.assert_allclose(float(ga.item()), garef, rtol=1e-4, atol=1e-6)
+    # updated params: Adam's first step is ~lr_t*sign(g)
+    lr_t = 3e-4 * np.sqrt(1 - 0.999) / (1 - 0.9)
+    p_new, la_new = sac.get_params()
+    p_new = p_new.cpu().numpy()
+    p_ref = flat(st.params)
+    gr = flat(gref)
+    d = np.abs(p_new - p_ref)
+    tiny = np.abs(gr) < 1e-3 * np.abs(gr).max()
+    assert d[~tiny].max() <= 1e-6 + 1e-6 * np.abs(p_ref[~tiny]).max()
+    assert d[tiny].max() <= 1e-6 + 2 * lr_t
+    np.testing.assert_allclose(float(la_new.item()), float(st.log_alpha), atol=1e-6)
+    # Polyak target after the update
+    tgt = sac.get_target().cpu().numpy()
+    np.testing.assert_allclose(tgt, flat(st.target), atol=2e-6 + 5e-3 * 2 * lr_t)
+
+
+def test_sac_twenty_steps_track_oracle():
+    from mopo_amd.sac import SAC
+    rs = np.random.RandomState(1)
+    (env_p, env_op), (mod_p, mod_op) = pools(rs)
+    params = osac.init_params(O, A, H, seed=6)
+    sac = SAC(O, A, H, batch_size=256, real_ratio=0.05, target_entropy=-3, params=flat(params).astype(np.float32))
+    st = osac.SACState([p.astype(np.float64) for p in params])
+    for it in range(20):
+        idx, e1, e2 = draw(rs, env_p.size, mod_p.size)
+        ref = osac.sac_step(st, host_batch(env_op, mod_op, idx), e1.astype(np.float64), e2.astype(np.float64))
+        sac._do_training(it, env_p, mod_p, idx=idx, eps_s=e1, eps_n=e2)
+        lg = sac.logs()
+        for k in ['Q/q1_loss', 'sac_Q/q2_loss', 'sac_pi/alpha', 'sac_pi/logp_pi']:
+            np.testing.assert_allclose(lg[k], ref[k], rtol=1e-3, atol=1e-5, err_msg='%s @ step %d' % (k, it))
+
+
+def test_sac_graph_replay_matches_eager():
+    import torch
+    from mopo_amd.sac import SAC
+    rs = np.random.RandomState(2)
+    (env_p, _), (mod_p, _) = pools(rs)
+    fl = init = None
+    from mopo_amd.rollout import init_sac_params
+    init = init_sac_params(O, A, H, seed=9)
+    a = SAC(O, A, H, params=init, use_graph=True, target_entropy=-3)
+    b = SAC(O, A, H, params=init, use_graph=False, target_entropy=-3)
+    a._do_training(0, env_p, mod_p, n_steps=50, seed=123)
+    b._do_training(0, env_p, mod_p, n_steps=50, seed=123)
+    torch.cuda.synchronize()
+    pa, pb = a.get_params()[0], b.get_params()[0]
+    assert torch.equal(pa, pb)
+    assert torch.isfinite(pa).all()
+    lg = a.logs()
+    assert all(np.isfinite(v) for v in lg.values())
