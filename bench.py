@@ -40,6 +40,8 @@ def parse():
     p.add_argument('--horizon', type=int, default=5)
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-batch', type=int, default=30000)
+    p.add_argument('--sac-steps', type=int, default=1000)
+    p.add_argument('--cpu-sac-steps', type=int, default=500)
     return p.parse_args()
 
 
@@ -147,6 +149,60 @@ def cpu_baseline(args):
                       '%d transitions in %.2f s' % (B, args.horizon, E, H, trans, dt)}
 
 
+def sac_leg(args, pool, env, dev, world):
+    """SAC grad-steps/s: args.sac_steps x (_training_batch + _do_training + _update_target), graph replay."""
+    import torch
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.sac import SAC
+    env_pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=ENV_ROWS)
+    rs = np.random.RandomState(1)
+    env_pool.add_samples({'observations': env[:ENV_ROWS], 'actions': rs.uniform(-1, 1, (ENV_ROWS, A)),
+                          'next_observations': env[:ENV_ROWS] + 0.1 * torch.randn_like(env[:ENV_ROWS]),
+                          'rewards': rs.normal(size=(ENV_ROWS, 1)), 'terminals': np.zeros((ENV_ROWS, 1), bool)})
+    sac = SAC(O, A, HP, batch_size=256, real_ratio=0.05, target_entropy=-3)
+    sac._do_training(0, env_pool, pool, n_steps=50, seed=5)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    sac._do_training(50, env_pool, pool, n_steps=args.sac_steps, seed=5)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    lg = sac.logs()
+    assert all(np.isfinite(v) for v in lg.values()), lg
+    return args.sac_steps / dt
+
+
+def cpu_baseline_sac(args):
+    """Oracle SAC step (numpy restatement of mopo.py:204-466, 834-853) on the host."""
+    from oracle import sac as osac
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get('num_threads', 1) for i in threadpool_info() if i.get('user_api') == 'blas'] or [1])
+    except Exception:
+        threads = 1
+    rs = np.random.RandomState(0)
+    st = osac.SACState(osac.init_params(O, A, HP, seed=2, dtype=np.float32))
+    for k in ('params', 'target'):
+        setattr(st, k, [p.astype(np.float32) for p in getattr(st, k)])
+    n = 256
+    batch = {'observations': rs.normal(size=(n, O)).astype(np.float32), 'actions': rs.uniform(-1, 1, (n, A)).astype(np.float32),
+             'next_observations': rs.normal(size=(n, O)).astype(np.float32), 'rewards': rs.normal(size=(n, 1)).astype(np.float32),
+             'terminals': np.zeros((n, 1), bool)}
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_sac_steps):
+        osac.sac_step(st, batch, rs.normal(size=(n, A)).astype(np.float32), rs.normal(size=(n, A)).astype(np.float32))
+    dt = time.perf_counter() - t0
+    return {'value': args.cpu_sac_steps / dt, 'unit': 'grad-steps/s', 'cores': int(threads), 'kind': 'port',
+            'sample': 'oracle numpy SAC step (fp32 arrays), batch 256, %d steps in %.2f s' % (args.cpu_sac_steps, dt)}
+
+
 def main():
     args = parse()
     import torch
@@ -180,6 +236,7 @@ def main():
         dt = float(t.item())
         if staging is not None:
             total = total  # counts are already global (gathered)
+    sac_rate = sac_leg(args, pool, env, dev, world)
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
@@ -204,9 +261,13 @@ def main():
                      'frac': achieved / MFMA_F32_PEAK_TFLOPS, 'traffic': None,
                      'flop_per_launch': rows_per_launch * FLOP_BNN_ROW, 'avg_launch_ms': bnn_ms},
         'kernel_ms_avg': kernel_ms,
+        'sac': {'metric': 'SAC grad-steps/s (batch 256 = 12 env + 244 model rows, mopo.py:801-850)',
+                'per_gpu': sac_rate, 'aggregate_replicas': sac_rate * world, 'steps_timed': args.sac_steps,
+                'us_per_step': 1e6 / sac_rate, 'parallelism': 'replicas only (one independent learner per GPU)'},
     }
     if not args.no_cpu_baseline and world == 1:
         out['cpu_baseline'] = cpu_baseline(args)
+        out['cpu_baseline_sac'] = cpu_baseline_sac(args)
     print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

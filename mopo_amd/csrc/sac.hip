@@ -157,6 +157,7 @@ struct Sac {
   hipGraph_t graph = nullptr;
   mopo_pool_desc genv{}, gmod{};
   hipStream_t gstream = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
   uint64_t gseed = 0;
 };
 
@@ -606,6 +607,9 @@ extern "C" int mopo_sac_destroy(mopo_sac_t hh) {
   if (!h) return 0;
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
   if (h->graph) (void)hipGraphDestroy(h->graph);
+  if (h->ev_in) (void)hipEventDestroy(h->ev_in);
+  if (h->ev_out) (void)hipEventDestroy(h->ev_out);
+  if (h->gstream) (void)hipStreamDestroy(h->gstream);
   if (h->mem) (void)hipFree(h->mem);
   delete h;
   return 0;
@@ -665,19 +669,31 @@ extern "C" int mopo_sac_step(mopo_sac_t hh, const mopo_pool_desc* env, const mop
       if (sac_step_impl(h, env, mod, seed, nullptr, nullptr, nullptr, s)) return -1;
     return 0;
   }
-  if (!h->gexec || !same_desc(h->genv, *env) || !same_desc(h->gmod, *mod) || h->gseed != seed || h->gstream != s) {
+  // graphs are captured and replayed on the handle's own stream (the caller's may be the legacy
+  // NULL stream, which cannot capture); event edges order it after / before the caller's work
+  if (!h->gstream) {
+    MOPO_HIP(hipStreamCreateWithFlags(&h->gstream, hipStreamNonBlocking));
+    MOPO_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
+    MOPO_HIP(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
+  }
+  hipStream_t gs = h->gstream;
+  if (!h->gexec || !same_desc(h->genv, *env) || !same_desc(h->gmod, *mod) || h->gseed != seed) {
     if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
     if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
-    MOPO_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    const int rc = sac_step_impl(h, env, mod, seed, nullptr, nullptr, nullptr, s);
+    MOPO_HIP(hipStreamBeginCapture(gs, hipStreamCaptureModeThreadLocal));
+    const int rc = sac_step_impl(h, env, mod, seed, nullptr, nullptr, nullptr, gs);
     hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(s, &g);
+    const hipError_t e = hipStreamEndCapture(gs, &g);
     if (rc) { if (g) (void)hipGraphDestroy(g); return -1; }
     if (e != hipSuccess) return fail(std::string("mopo_sac_step: capture failed: ") + hipGetErrorString(e));
     h->graph = g;
     MOPO_HIP(hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0));
-    h->genv = *env; h->gmod = *mod; h->gseed = seed; h->gstream = s;
+    h->genv = *env; h->gmod = *mod; h->gseed = seed;
   }
-  for (int i = 0; i < n_steps; ++i) MOPO_HIP(hipGraphLaunch(h->gexec, s));
+  MOPO_HIP(hipEventRecord(h->ev_in, s));
+  MOPO_HIP(hipStreamWaitEvent(gs, h->ev_in, 0));
+  for (int i = 0; i < n_steps; ++i) MOPO_HIP(hipGraphLaunch(h->gexec, gs));
+  MOPO_HIP(hipEventRecord(h->ev_out, gs));
+  MOPO_HIP(hipStreamWaitEvent(s, h->ev_out, 0));
   return 0;
 }
