@@ -49,33 +49,52 @@ __device__ __forceinline__ float load_feat(const void* p, int f64, int64_t idx) 
   return f64 ? (float)reinterpret_cast<const double*>(p)[idx] : reinterpret_cast<const float*>(p)[idx];
 }
 
-// acc[r][nb] += sum over KG k-groups:  W(frag kg,nb) x in[r][kg]
-template <int KG, int NB, int R>
-__device__ __forceinline__ void layer_mfma(const float* __restrict__ wf, const f32x4 (&in)[R][KG],
-                                           f32x4 (&acc)[R][NB], int lane) {
+// ---- LDS-staged weight streaming ------------------------------------------------------------
+// A workgroup of WAVES waves shares one member; every k-group slice of a layer (NB fragments,
+// 1 KiB each, contiguous in HBM) is copied HBM->LDS once per workgroup with global_load_lds
+// (no VGPR round trip), double-buffered: the slice for k-group kg+1 is in flight while the waves
+// run the 4*NB*R MFMAs of k-group kg.  One barrier per k-group (its implicit vmcnt(0) retires the
+// slice issued one k-group earlier, so the copy latency hides behind a full k-group of MFMAs).
+typedef __attribute__((address_space(3))) void* lds_void_t;
+
+template <int NB, int WAVES>
+struct Stage {
+  static constexpr int PER = (NB + WAVES - 1) / WAVES;  // fragments per wave (uniform vmcnt)
+  static constexpr int SLOTS = PER * WAVES;
+};
+
+template <int NB, int WAVES>
+__device__ __forceinline__ void stage_slice(const float* __restrict__ src, float* lds, int w, int lane) {
+#pragma unroll
+  for (int i = 0; i < Stage<NB, WAVES>::PER; ++i) {
+    const int f = w + i * WAVES;
+    const int fs = f < NB ? f : NB - 1;  // pad slots re-read a valid fragment (never consumed)
+    __builtin_amdgcn_global_load_lds((const void*)(src + (fs * 64 + lane) * 4), (lds_void_t)(lds + f * 256), 16, 0, 0);
+  }
+}
+
+// acc[r][nb] = sum over KG k-groups of W(kg, nb) x in[r][kg]; wf = this member's layer fragments
+template <int KG, int NB, int R, int WAVES, int SLOT>
+__device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f32x4 (&in)[R][KG], f32x4 (&acc)[R][NB],
+                                          float* lds, int w, int lane) {
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[r][nb] = zero4();
-  f32x4 wc[NB];
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb) wc[nb] = ld4(wf + (nb * 64 + lane) * 4);
+  __syncthreads();  // every wave is done reading both buffers (previous layer)
+  stage_slice<NB, WAVES>(wf, lds, w, lane);
 #pragma unroll
   for (int kg = 0; kg < KG; ++kg) {
-    f32x4 wn[NB];
-    if (kg + 1 < KG) {
+    __syncthreads();  // vmcnt(0): slice kg landed (all waves); buffer (kg+1)&1 free
+    if (kg + 1 < KG) stage_slice<NB, WAVES>(wf + (kg + 1) * NB * 256, lds + ((kg + 1) & 1) * SLOT, w, lane);
+    const float* b = lds + (kg & 1) * SLOT;
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) wn[nb] = ld4(wf + (((kg + 1) * NB + nb) * 64 + lane) * 4);
-    }
+    for (int nb = 0; nb < NB; ++nb) {
+      const f32x4 fr = *reinterpret_cast<const f32x4*>(b + (nb * 64 + lane) * 4);
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r][nb] = mfma4(wc[nb][t], in[r][kg][t], acc[r][nb]);
-    if (kg + 1 < KG) {
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) wc[nb] = wn[nb];
+        for (int r = 0; r < R; ++r) acc[r][nb] = mfma4(fr[t], in[r][kg][t], acc[r][nb]);
     }
   }
 }
@@ -94,14 +113,19 @@ __device__ __forceinline__ void bias_swish(const float* __restrict__ b, const f3
   }
 }
 
-template <int KG0, int NBH, int NBO, int R, int MODE>
-__global__ __launch_bounds__(64) void bnn_fwd_kernel(const BnnDev w, const FwdArgs a) {
-  const int lane = threadIdx.x, m = lane & 15, g = lane >> 4;
+template <int KG0, int NBH, int NBO, int R, int MODE, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_kernel(const BnnDev w, const FwdArgs a) {
+  constexpr int NBMAX = NBH > NBO ? NBH : NBO;
+  constexpr int SLOT = Stage<NBMAX, WAVES>::SLOTS * 256;  // floats per buffer
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
-  const int e = blockIdx.x / a.ntiles, tile = blockIdx.x % a.ntiles;
+  const int groups = ceil_div(a.ntiles, WAVES);
+  const int e = blockIdx.x / groups, grp = blockIdx.x % groups;
+  const int tile = grp * WAVES + wv;
   const int64_t row0 = (int64_t)tile * 16 * R;
-  if (row0 >= count) return;
-  const int IN = w.IN, O = w.O, H = w.H, D = w.D;
+  if ((int64_t)grp * WAVES * 16 * R >= count) return;  // whole workgroup past the live rows
+  const int IN = w.IN, O = w.O, D = w.D;
 
   // ---- layer-0 input: scaler transform (utils.py:96), f64 inputs cast to f32 as TF's feed does
   f32x4 x0[R][KG0];
@@ -125,16 +149,15 @@ __global__ __launch_bounds__(64) void bnn_fwd_kernel(const BnnDev w, const FwdAr
   }
   f32x4 acc[R][NBH], hcur[R][NBH];
   const int64_t hp = (int64_t)NBH * 16;
-  layer_mfma<KG0, NBH, R>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lane);
+  layer_lds<KG0, NBH, R, WAVES, SLOT>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv, lane);
   bias_swish<NBH, R>(w.b0 + e * hp, acc, hcur, g);
   for (int l = 0; l < 3; ++l) {  // hidden layers 1..3 (constructor.py:31-33)
-    layer_mfma<NBH, NBH, R>(w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lane);
+    layer_lds<NBH, NBH, R, WAVES, SLOT>(w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lds, wv, lane);
     bias_swish<NBH, R>(w.bh + ((int64_t)l * w.E + e) * hp, acc, hcur, g);
   }
   // ---- heads on the 4th hidden output (bnn.py:661-667): n < D mean, D <= n < 2D log-var
   f32x4 hd[R][NBO];
-  layer_mfma<NBH, NBO, R>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lane);
-  (void)H;
+  layer_lds<NBH, NBO, R, WAVES, SLOT>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds, wv, lane);
 
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -179,15 +202,17 @@ __global__ __launch_bounds__(64) void bnn_fwd_kernel(const BnnDev w, const FwdAr
   }
 }
 
+constexpr int FWD_WAVES = 4;
+
 template <int KG0, int NBH, int NBO, int R>
 static int launch_fwd_t(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   a.ntiles = (int)ceil_div((int)a.B, 16 * R);
-  dim3 grid(a.ntiles * h->E), block(64);
   if (a.ntiles == 0) return 0;
+  dim3 grid(ceil_div(a.ntiles, FWD_WAVES) * h->E), block(64 * FWD_WAVES);
   if (mode == FWD_PREDICT)
-    hipLaunchKernelGGL((bnn_fwd_kernel<KG0, NBH, NBO, R, FWD_PREDICT>), grid, block, 0, s, h->dev, a);
+    hipLaunchKernelGGL((bnn_fwd_kernel<KG0, NBH, NBO, R, FWD_PREDICT, FWD_WAVES>), grid, block, 0, s, h->dev, a);
   else
-    hipLaunchKernelGGL((bnn_fwd_kernel<KG0, NBH, NBO, R, FWD_ROLLOUT>), grid, block, 0, s, h->dev, a);
+    hipLaunchKernelGGL((bnn_fwd_kernel<KG0, NBH, NBO, R, FWD_ROLLOUT, FWD_WAVES>), grid, block, 0, s, h->dev, a);
   MOPO_HIP(hipGetLastError());
   return 0;
 }
@@ -197,7 +222,7 @@ static int launch_fwd_h(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s)
   switch (h->dev.NBH) {
     case 2: return launch_fwd_t<KG0, 2, NBO, 2>(h, mode, a, s);
     case 4: return launch_fwd_t<KG0, 4, NBO, 2>(h, mode, a, s);
-    case 13: return launch_fwd_t<KG0, 13, NBO, 2>(h, mode, a, s);
+    case 13: return launch_fwd_t<KG0, 13, NBO, 1>(h, mode, a, s);
     case 25: return launch_fwd_t<KG0, 25, NBO, 1>(h, mode, a, s);
   }
   return fail("bnn: unsupported hidden size (supported: 32, 64, 200, 400; got H=" +
