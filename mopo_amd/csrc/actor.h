@@ -4,7 +4,8 @@
 namespace mopo {
 
 struct ActorArgs {
-  const float* P;  // flat SAC params; pi block at offset 0 (TF [in,out] layout)
+  const float* P;    // flat SAC params; pi block at offset 0 (TF [in,out] layout) -- biases read here
+  const float* Wpk;  // pi weights repacked fragment-major by pack_actor
   int O, A, Hp;
   const void* obs; int obs_f64;
   int64_t B;               // grid rows
@@ -24,5 +25,7 @@ struct ActorArgs {
 };
 
 int launch_actor(const ActorArgs& a, hipStream_t s);
+int64_t actor_packed_floats(int O, int Hp);
+int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s);
 
 }  // namespace mopo

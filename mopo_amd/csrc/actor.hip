@@ -4,84 +4,88 @@
 // (mopo/algorithms/mopo.py:468-485, 275-308, 286-296):
 //   net = relu(relu(s W1 + b1) W2 + b2); mu = net Wmu + bmu; log_std = clip(net Wls + bls, -20, 2)
 //   pi = tanh(mu + eps * exp(log_std)),  mu_out = tanh(mu)
-// Same register-resident transposed-MFMA scheme as the BNN forward (bnn.hip), reading the
-// weights straight from the SAC parameter buffer in TF [in, out] layout (the policy changes
-// every SAC step, so no repacking).  One 64-thread wave per 16-row tile.
+// Same register-resident transposed-MFMA scheme and LDS-staged weight slices as the ensemble
+// forward (mlp_tile.h).  The policy changes every SAC step, so its weights are repacked into
+// fragment-major order once per rollout (pack_actor, ~0.3 MB) from the SAC parameter buffer.
 #include "actor.h"
+#include "mlp_tile.h"
 
 namespace mopo {
 
-// A-operand fragment from a TF-layout [K][N] matrix: lane (n = lane&15, g) gets
-// W[kg*16 + 4g + t][nb*16 + n], t = 0..3
-__device__ __forceinline__ f32x4 ld_tf(const float* __restrict__ W, int K, int N, int kg, int nb, int lane) {
-  const int n = nb * 16 + (lane & 15), k0 = kg * 16 + 4 * (lane >> 4);
-  f32x4 v;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) v[t] = (n < N && k0 + t < K) ? W[(k0 + t) * N + n] : 0.f;
-  return v;
+// combined head fragments: n < A -> Wmu[:, n], A <= n < 2A -> Wls[:, n - A]
+__global__ void pack_head_kernel(const float* Wm, const float* Wl, int Hp, int A, int KG, float* dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= KG * 256) return;
+  const int t = i & 3, lane = (i >> 2) & 63, kg = i >> 8;
+  const int k = kg * 16 + 4 * (lane >> 4) + t, n = lane & 15;
+  float v = 0.f;
+  if (k < Hp) v = n < A ? Wm[k * A + n] : (n < 2 * A ? Wl[k * A + (n - A)] : 0.f);
+  dst[i] = v;
 }
 
-template <int KG, int NB>
-__device__ __forceinline__ void tf_layer(const float* __restrict__ W, int K, int N, const f32x4 (&in)[KG],
-                                         f32x4 (&acc)[NB], int lane) {
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb) acc[nb] = zero4();
-#pragma unroll
-  for (int kg = 0; kg < KG; ++kg) {
-    f32x4 w[NB];
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) w[nb] = ld_tf(W, K, N, kg, nb, lane);
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) acc[nb] = mfma4(w[nb][t], in[kg][t], acc[nb]);
-  }
+int64_t actor_packed_floats(int O, int Hp) {
+  const int KG0 = ceil_div(O, 16), NB = ceil_div(Hp, 16);
+  return (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256 + (int64_t)NB * 256;
+}
+
+int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s) {
+  const int KG0 = ceil_div(O, 16), NB = ceil_div(Hp, 16);
+  const float* W1 = P;
+  const float* W2 = W1 + O * Hp + Hp;
+  const float* Wm = W2 + Hp * Hp + Hp;
+  const float* Wl = Wm + Hp * A + A;
+  if (pack_frags(W1, dst, 1, O, Hp, KG0, NB, s)) return -1;
+  if (pack_frags(W2, dst + (int64_t)KG0 * NB * 256, 1, Hp, Hp, NB, NB, s)) return -1;
+  hipLaunchKernelGGL(pack_head_kernel, dim3(ceil_div(NB * 256, 256)), dim3(256), 0, s, Wm, Wl, Hp, A, NB,
+                     dst + (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256);
+  MOPO_HIP(hipGetLastError());
+  return 0;
 }
 
 template <int NB>
-__device__ __forceinline__ void bias_relu(const float* __restrict__ b, int N, const f32x4 (&acc)[NB],
-                                          f32x4 (&out)[NB], int g) {
+__device__ __forceinline__ void bias_relu(const float* __restrict__ b, const f32x4 (&acc)[1][NB], f32x4 (&out)[1][NB],
+                                          int g) {
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb)
+  for (int nb = 0; nb < NB; ++nb) {
+    const f32x4 bb = ld4(b + nb * 16 + 4 * g);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int n = nb * 16 + 4 * g + t;
-      const float v = acc[nb][t] + (n < N ? b[n] : 0.f);
-      out[nb][t] = fmaxf(v, 0.f);
-    }
+    for (int t = 0; t < 4; ++t) out[0][nb][t] = fmaxf(acc[0][nb][t] + bb[t], 0.f);
+  }
 }
 
 __device__ __forceinline__ void actor_noise(uint64_t seed, uint32_t step, int64_t uid, int A, float* z) {
   for (int blk = 0; blk * 4 < A; ++blk) {
     u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32) ^ ((uint32_t)blk << 20), step, RNG_ACT};
     u32x4 r = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    float z0, z1, z2, z3;
-    box_muller(r.x, r.y, z0, z1);
-    box_muller(r.z, r.w, z2, z3);
-    float zz[4] = {z0, z1, z2, z3};
+    float zz[4];
+    box_muller(r.x, r.y, zz[0], zz[1]);
+    box_muller(r.z, r.w, zz[2], zz[3]);
     for (int i = 0; i < 4 && blk * 4 + i < A; ++i) z[blk * 4 + i] = zz[i];
   }
 }
 
+constexpr int ACT_WAVES = 4;
+
 template <int KG0, int NBP>
-__global__ __launch_bounds__(64) void actor_kernel(const ActorArgs a) {
-  __shared__ float head[16][17];
-  const int lane = threadIdx.x, m = lane & 15, g = lane >> 4;
+__global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_kernel(const ActorArgs a) {
+  constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
+  __shared__ float head[ACT_WAVES][16][17];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
-  const int64_t row0 = (int64_t)blockIdx.x * 16;
-  if (row0 >= count) return;
+  if ((int64_t)blockIdx.x * ACT_WAVES * 16 >= count) return;  // whole workgroup past the live rows
+  const int64_t row0 = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16;
   const int O = a.O, A = a.A, Hp = a.Hp;
-  const float* W1 = a.P;
-  const float* b1 = W1 + O * Hp;
-  const float* W2 = b1 + Hp;
-  const float* b2 = W2 + Hp * Hp;
-  const float* Wm = b2 + Hp;
-  const float* bm = Wm + Hp * A;
-  const float* Wl = bm + A;
-  const float* bl = Wl + Hp * A;
+  const float* b1 = a.P + O * Hp;
+  const float* b2 = b1 + Hp + Hp * Hp;
+  const float* bm = b2 + Hp + Hp * A;
+  const float* bl = bm + A + Hp * A;
+  const float* w1f = a.Wpk;
+  const float* w2f = w1f + KG0 * NBP * 256;
+  const float* whf = w2f + NBP * NBP * 256;
   const int64_t row = row0 + m;
   const bool ok = row < count;
-  f32x4 x0[KG0];
+  f32x4 x0[1][KG0];
 #pragma unroll
   for (int kg = 0; kg < KG0; ++kg)
 #pragma unroll
@@ -91,32 +95,20 @@ __global__ __launch_bounds__(64) void actor_kernel(const ActorArgs a) {
       if (ok && k < O)
         v = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
                       : reinterpret_cast<const float*>(a.obs)[row * O + k];
-      x0[kg][t] = v;
+      x0[0][kg][t] = v;
     }
-  f32x4 acc[NBP], h[NBP];
-  tf_layer<KG0, NBP>(W1, O, Hp, x0, acc, lane);
-  bias_relu<NBP>(b1, Hp, acc, h, g);
-  tf_layer<NBP, NBP>(W2, Hp, Hp, h, acc, lane);
-  bias_relu<NBP>(b2, Hp, acc, h, g);
-  // head: one 16-wide block, n < A -> mu, A <= n < 2A -> log_std
-  f32x4 hd = zero4();
-#pragma unroll
-  for (int kg = 0; kg < NBP; ++kg) {
-    const int n = lane & 15, k0 = kg * 16 + 4 * g;
-    f32x4 w;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int k = k0 + t;
-      w[t] = (k < Hp && n < 2 * A) ? (n < A ? Wm[k * A + n] : Wl[k * A + (n - A)]) : 0.f;
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) hd = mfma4(w[t], h[kg][t], hd);
-  }
+  f32x4 acc[1][NBP], h[1][NBP];
+  layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT>(w1f, x0, acc, lds, wv, lane);   // mlp hidden 1 (mopo.py:277-278)
+  bias_relu<NBP>(b1, acc, h, g);
+  layer_lds<NBP, NBP, 1, ACT_WAVES, SLOT>(w2f, h, acc, lds, wv, lane);    // hidden 2, relu (mopo.py:301)
+  bias_relu<NBP>(b2, acc, h, g);
+  f32x4 hd[1][1];
+  layer_lds<NBP, 1, 1, ACT_WAVES, SLOT>(whf, h, hd, lds, wv, lane);       // mu | log_std heads (:302-303)
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int n = 4 * g + t;
-    float bias = n < A ? bm[n] : (n < 2 * A ? bl[n - A] : 0.f);
-    head[m][n] = hd[t] + bias;
+    const float bias = n < A ? bm[n] : (n < 2 * A ? bl[n - A] : 0.f);
+    head[wv][m][n] = hd[0][0][t] + bias;
   }
   __syncthreads();
   if (g != 0 || !ok) return;
@@ -128,17 +120,15 @@ __global__ __launch_bounds__(64) void actor_kernel(const ActorArgs a) {
     actor_noise(a.seed, a.step, uid, A, z);
   }
   int64_t pos = -1;
-  if (a.pool_act) {
-    pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool_state[0] + row) % a.pool_max;
-  }
+  if (a.pool_act) pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool_state[0] + row) % a.pool_max;
   for (int j = 0; j < A; ++j) {
-    const float mu = head[m][j];
-    const float ls = fminf(fmaxf(head[m][A + j], -20.f), 2.f);  // mopo.py:304
-    const float sd = expf(ls);                                  // mopo.py:305
-    const float u = mu + z[j] * sd;                             // mopo.py:306
-    const float act = tanhf(u);                                 // mopo.py:295
+    const float mu = head[wv][m][j];
+    const float ls = fminf(fmaxf(head[wv][m][A + j], -20.f), 2.f);  // mopo.py:304
+    const float sd = expf(ls);                                      // mopo.py:305
+    const float u = mu + z[j] * sd;                                 // mopo.py:306
+    const float act = tanhf(u);                                     // mopo.py:295
     if (a.act) a.act[row * A + j] = act;
-    if (a.mu) a.mu[row * A + j] = tanhf(mu);                    // mopo.py:294
+    if (a.mu) a.mu[row * A + j] = tanhf(mu);                        // mopo.py:294
     if (pos >= 0) a.pool_act[pos * A + j] = act;
   }
   if (pos >= 0) {  // the observation half of the pool row (mopo.py:750), stored f32
@@ -151,7 +141,7 @@ __global__ __launch_bounds__(64) void actor_kernel(const ActorArgs a) {
     int32_t sel;
     if (a.sel_in) {
       sel = a.sel_in[row];
-    } else {
+    } else {  // perf mode of np.random.choice(elites, B) (bnn.py:343)
       u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32), a.step, RNG_MODEL};
       u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
       sel = a.elites[(int)(((uint64_t)r.x * (uint64_t)a.n_elites) >> 32)];
@@ -164,7 +154,8 @@ int launch_actor(const ActorArgs& a, hipStream_t s) {
   if (a.B == 0) return 0;
   MOPO_REQUIRE(a.A >= 1 && 2 * a.A <= 16, "actor: act_dim must be in [1, 8]");
   MOPO_REQUIRE(a.O >= 1 && a.O <= 32, "actor: obs_dim must be in [1, 32]");
-  dim3 grid(ceil_div((int)a.B, 16)), block(64);
+  MOPO_REQUIRE(a.Wpk, "actor: packed weights required");
+  dim3 grid(ceil_div((int)a.B, 16 * ACT_WAVES)), block(64 * ACT_WAVES);
   const int KG0 = ceil_div(a.O, 16);
   if (a.Hp == 256 && KG0 == 2)
     hipLaunchKernelGGL((actor_kernel<2, 16>), grid, block, 0, s, a);
@@ -194,11 +185,20 @@ extern "C" int mopo_actor_forward(const float* P, int O, int A, int H, const voi
                                   const float* eps, uint64_t seed, uint32_t step, float* act, float* mu,
                                   void* stream) {
   MOPO_REQUIRE(P && obs, "mopo_actor_forward: NULL pointer");
-  ActorArgs a{};
-  a.P = P; a.O = O; a.A = A; a.Hp = H;
-  a.obs = obs; a.obs_f64 = obs_f64; a.B = B;
-  a.eps = eps; a.seed = seed; a.step = step;
-  a.act = act; a.mu = mu;
-  a.stage_base = -1;
-  return launch_actor(a, (hipStream_t)stream);
+  if (B == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  float* wpk = nullptr;
+  MOPO_HIP(hipMallocAsync((void**)&wpk, actor_packed_floats(O, H) * sizeof(float), s));
+  int rc = pack_actor(P, O, A, H, wpk, s);
+  if (rc == 0) {
+    ActorArgs a{};
+    a.P = P; a.Wpk = wpk; a.O = O; a.A = A; a.Hp = H;
+    a.obs = obs; a.obs_f64 = obs_f64; a.B = B;
+    a.eps = eps; a.seed = seed; a.step = step;
+    a.act = act; a.mu = mu;
+    a.stage_base = -1;
+    rc = launch_actor(a, s);
+  }
+  (void)hipFreeAsync(wpk, s);
+  return rc;
 }

@@ -12,7 +12,7 @@
 // is needed.  Weights stream from L2 as 1 KiB fragments (one dwordx4 per lane per 4 MFMAs),
 // double-buffered in registers across k-groups.  Items are member-major so the waves resident
 // on one XCD share one member's weights in L2.
-#include "internal.h"
+#include "mlp_tile.h"
 
 #include <vector>
 #include <cstring>
@@ -45,58 +45,16 @@ __global__ void pack_bias_kernel(const float* __restrict__ src, float* __restric
 }
 
 // ---------------------------------------------------------------------------------------
+int pack_frags(const float* src, float* dst, int E, int K, int N, int KG, int NB, hipStream_t s) {
+  const int64_t tot = (int64_t)E * KG * NB * 256;
+  const int blocks = (int)std::min<int64_t>((tot + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_frags_kernel, dim3(blocks), dim3(256), 0, s, src, dst, E, K, N, KG, NB);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
 __device__ __forceinline__ float load_feat(const void* p, int f64, int64_t idx) {
   return f64 ? (float)reinterpret_cast<const double*>(p)[idx] : reinterpret_cast<const float*>(p)[idx];
-}
-
-// ---- LDS-staged weight streaming ------------------------------------------------------------
-// A workgroup of WAVES waves shares one member; every k-group slice of a layer (NB fragments,
-// 1 KiB each, contiguous in HBM) is copied HBM->LDS once per workgroup with global_load_lds
-// (no VGPR round trip), double-buffered: the slice for k-group kg+1 is in flight while the waves
-// run the 4*NB*R MFMAs of k-group kg.  One barrier per k-group (its implicit vmcnt(0) retires the
-// slice issued one k-group earlier, so the copy latency hides behind a full k-group of MFMAs).
-typedef __attribute__((address_space(3))) void* lds_void_t;
-
-template <int NB, int WAVES>
-struct Stage {
-  static constexpr int PER = (NB + WAVES - 1) / WAVES;  // fragments per wave (uniform vmcnt)
-  static constexpr int SLOTS = PER * WAVES;
-};
-
-template <int NB, int WAVES>
-__device__ __forceinline__ void stage_slice(const float* __restrict__ src, float* lds, int w, int lane) {
-#pragma unroll
-  for (int i = 0; i < Stage<NB, WAVES>::PER; ++i) {
-    const int f = w + i * WAVES;
-    const int fs = f < NB ? f : NB - 1;  // pad slots re-read a valid fragment (never consumed)
-    __builtin_amdgcn_global_load_lds((const void*)(src + (fs * 64 + lane) * 4), (lds_void_t)(lds + f * 256), 16, 0, 0);
-  }
-}
-
-// acc[r][nb] = sum over KG k-groups of W(kg, nb) x in[r][kg]; wf = this member's layer fragments
-template <int KG, int NB, int R, int WAVES, int SLOT>
-__device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f32x4 (&in)[R][KG], f32x4 (&acc)[R][NB],
-                                          float* lds, int w, int lane) {
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[r][nb] = zero4();
-  __syncthreads();  // every wave is done reading both buffers (previous layer)
-  stage_slice<NB, WAVES>(wf, lds, w, lane);
-#pragma unroll
-  for (int kg = 0; kg < KG; ++kg) {
-    __syncthreads();  // vmcnt(0): slice kg landed (all waves); buffer (kg+1)&1 free
-    if (kg + 1 < KG) stage_slice<NB, WAVES>(wf + (kg + 1) * NB * 256, lds + ((kg + 1) & 1) * SLOT, w, lane);
-    const float* b = lds + (kg & 1) * SLOT;
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const f32x4 fr = *reinterpret_cast<const f32x4*>(b + (nb * 64 + lane) * 4);
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r][nb] = mfma4(fr[t], in[r][kg][t], acc[r][nb]);
-    }
-  }
 }
 
 // bias + swish, acc -> next-layer input (fc.py:21,99-106)

@@ -30,6 +30,8 @@ struct Rollout {
   double* obs[2];
   int64_t* uid[2];
   float* act;
+  float* wpk = nullptr;  // policy weights, fragment-major (pack_actor), repacked every run
+  int wpk_hp = 0;
   uint32_t* pen;
   int32_t* sel;
   float* mean_sel;
@@ -217,12 +219,21 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
                        a->d_start_idx, O, B, a->seed, step0, a->uid_offset, h->obs[0], h->uid[0], h->cnt);
   }
   MOPO_HIP(hipGetLastError());
+  if (!h->wpk || h->wpk_hp != a->pi_hidden) {
+    if (h->wpk) (void)hipFree(h->wpk);
+    MOPO_HIP(hipMalloc(&h->wpk, actor_packed_floats(O, a->pi_hidden) * sizeof(float)));
+    h->wpk_hp = a->pi_hidden;
+  }
+  {
+    KTimer t(h, KC_START, s);
+    if (pack_actor(a->d_pi_params, O, A, a->pi_hidden, h->wpk, s)) return -1;
+  }
   const bool compact = a->term_kind != MOPO_TERM_HALFCHEETAH;
   int oc = 0, uc = 0;
   for (int i = 0; i < a->horizon; ++i) {
     const uint32_t st = step0 + 1 + i;
     ActorArgs aa{};
-    aa.P = a->d_pi_params; aa.O = O; aa.A = A; aa.Hp = a->pi_hidden;
+    aa.P = a->d_pi_params; aa.Wpk = h->wpk; aa.O = O; aa.A = A; aa.Hp = a->pi_hidden;
     aa.obs = h->obs[oc]; aa.obs_f64 = 1; aa.B = B; aa.d_count = h->cnt;
     aa.eps = a->d_eps_act ? a->d_eps_act + (int64_t)i * B * A : nullptr;
     aa.seed = a->seed; aa.step = st; aa.d_uid = h->uid[uc];
@@ -336,6 +347,7 @@ extern "C" int mopo_rollout_destroy(mopo_rollout_t hh) {
   if (!h) return 0;
   for (auto& e : h->ev) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
   if (h->mem) (void)hipFree(h->mem);
+  if (h->wpk) (void)hipFree(h->wpk);
   delete h;
   return 0;
 }

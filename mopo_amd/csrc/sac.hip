@@ -31,6 +31,10 @@ struct GemmProb {
   int relu;                          // C = max(C, 0)
   const float* mask; int ldm;        // C *= (mask(i,j) > 0)   (relu' from the saved activation)
   float* colsum;                     // colsum[j] = sum_k B(k,j)   (bias gradient), by tile-row 0
+  // rank-1 masked operands (the critic's 1-wide output layer backward, fused into its consumer):
+  // when a_u != NULL:  A(i,k) = a_u[i] * a_v[k] * (a_m[i*a_ldm + k] > 0);  same for B with (k, j)
+  const float* a_u; const float* a_v; const float* a_m; int a_ldm;
+  const float* b_u; const float* b_v; const float* b_m; int b_ldm;
 };
 
 struct GemmGroup {
@@ -39,7 +43,24 @@ struct GemmGroup {
   GemmProb p[MAXP];
 };
 
+__device__ __forceinline__ float opA(const GemmProb& p, int i, int k) {
+  if (p.a_u) return p.a_m[(int64_t)i * p.a_ldm + k] > 0.f ? p.a_u[i] * p.a_v[k] : 0.f;
+  return p.ta ? p.A[(int64_t)k * p.lda + i] : p.A[(int64_t)i * p.lda + k];
+}
+__device__ __forceinline__ float opB(const GemmProb& p, int k, int j) {
+  if (p.b_u) return p.b_m[(int64_t)k * p.b_ldm + j] > 0.f ? p.b_u[k] * p.b_v[j] : 0.f;
+  return p.tb ? p.B[(int64_t)j * p.ldb + k] : p.B[(int64_t)k * p.ldb + j];
+}
+
+constexpr int GKC = 256;  // K chunk staged in LDS
+
+// One 16x16 output tile per 256-thread block.  The A[16 x K] and B[K x 16] panels are staged in
+// LDS with loads ordered along each operand's contiguous axis (all issued before the first use:
+// one memory latency per chunk), then the four waves split K and run v_mfma_f32_16x16x4_f32 out
+// of LDS; partial tiles are summed through LDS and the epilogue fuses bias / relu / relu'-mask.
 __global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
+  __shared__ float As[GKC][16];
+  __shared__ float Bs[GKC][16];
   __shared__ float part[4][256];
   __shared__ float csum[16][17];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -51,31 +72,36 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
   const int tm = t / tn_cnt, tn = t % tn_cnt;
   const int i0 = tm * 16, j0 = tn * 16;
   const int li = lane & 15, lk = lane >> 4;
-  // K split over the 4 waves in chunks of 4
-  const int ksteps = ceil_div(p.K, 4);
-  const int per = ceil_div(ksteps, 4);
-  const int kb = w * per * 4, ke = min(p.K, (w + 1) * per * 4);
+  const bool a_kfast = p.a_u || !p.ta, b_jfast = p.b_u || !p.tb;
+  const bool do_cs = p.colsum && tm == 0;
   f32x4 acc0 = zero4(), acc1 = zero4();
-  const int ai = i0 + li, bj = j0 + li;
-  int s = 0;
-  for (int k0 = kb; k0 < ke; k0 += 4, ++s) {
-    const int k = k0 + lk;
-    float a = 0.f, b = 0.f;
-    if (ai < p.M && k < ke) a = p.ta ? p.A[(int64_t)k * p.lda + ai] : p.A[(int64_t)ai * p.lda + k];
-    if (bj < p.N && k < ke) b = p.tb ? p.B[(int64_t)bj * p.ldb + k] : p.B[(int64_t)k * p.ldb + bj];
-    if (s & 1) acc1 = mfma4(a, b, acc1);
-    else acc0 = mfma4(a, b, acc0);
+  float cs = 0.f;
+  for (int kc = 0; kc < p.K; kc += GKC) {
+    const int kn = min(GKC, p.K - kc);
+    const int kpad = (kn + 3) & ~3;
+    for (int idx = tid; idx < 16 * kpad; idx += 256) {
+      int i, k, j;
+      if (a_kfast) { i = idx / kpad; k = idx % kpad; } else { i = idx & 15; k = idx >> 4; }
+      As[k][i] = (i0 + i < p.M && k < kn) ? opA(p, i0 + i, kc + k) : 0.f;
+      if (b_jfast) { j = idx & 15; k = idx >> 4; } else { j = idx / kpad; k = idx % kpad; }
+      Bs[k][j] = (j0 + j < p.N && k < kn) ? opB(p, kc + k, j0 + j) : 0.f;
+    }
+    __syncthreads();
+    const int ksteps = kpad >> 2, per = (ksteps + 3) >> 2;
+    const int sb = w * per, se = min(ksteps, sb + per);
+    for (int s = sb; s < se; ++s) {
+      const int k = 4 * s + lk;
+      const float a = As[k][li], b = Bs[k][li];
+      if (s & 1) acc1 = mfma4(a, b, acc1);
+      else acc0 = mfma4(a, b, acc0);
+    }
+    if (do_cs)
+      for (int k = tid >> 4; k < kn; k += 16) cs += Bs[k][tid & 15];
+    __syncthreads();
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[w][(lk * 4 + r) * 16 + li] = acc0[r] + acc1[r];  // D: col li, row 4*lk+r
-  // bias-gradient column sums of B over all K (tile row 0 only)
-  if (p.colsum && tm == 0) {
-    const int j = tid & 15, q = tid >> 4;
-    float cs = 0.f;
-    if (j0 + j < p.N)
-      for (int k = q; k < p.K; k += 16) cs += p.tb ? p.B[(int64_t)(j0 + j) * p.ldb + k] : p.B[(int64_t)k * p.ldb + j0 + j];
-    csum[q][j] = cs;
-  }
+  if (do_cs) csum[tid >> 4][tid & 15] = cs;
   __syncthreads();
   {
     const int i = tid >> 4, j = tid & 15;
@@ -88,10 +114,10 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
       p.C[(int64_t)gi * p.ldc + gj] = v;
     }
   }
-  if (p.colsum && tm == 0 && tid < 16) {
-    float cs = 0.f;
-    for (int q = 0; q < 16; ++q) cs += csum[q][tid];
-    if (j0 + tid < p.N) p.colsum[j0 + tid] = cs;
+  if (do_cs && tid < 16) {
+    float c = 0.f;
+    for (int q = 0; q < 16; ++q) c += csum[q][tid];
+    if (j0 + tid < p.N) p.colsum[j0 + tid] = c;
   }
 }
 
@@ -163,33 +189,52 @@ struct Sac {
 
 // ---- batch gather (_training_batch, mopo.py:801-821): rows [0, n_env) from the env pool, rest
 // from the model pool; each index uniform over the pool's live size (Philox) unless injected
-__global__ void sac_gather_kernel(const mopo_pool_desc env, const mopo_pool_desc mod, int n, int n_env, int O, int A,
-                                  const int64_t* idx_in, int64_t* idx_out, uint64_t seed, const int64_t* iter,
-                                  float* sa, float* xpi, float* xn, float* rew, float* term) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const bool from_env = r < n_env;
-  const mopo_pool_desc& p = from_env ? env : mod;
-  int64_t src;
-  if (idx_in) {
-    src = idx_in[r];
-  } else {
-    const uint64_t size = (uint64_t)p.d_state[1];
-    u32x4 c{(uint32_t)r, (uint32_t)(*iter), (uint32_t)((uint64_t)(*iter) >> 32), RNG_SAC};
-    u32x4 q = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    src = (int64_t)(((uint64_t)q.x * size) >> 32);
+// One block per GR rows: phase 1 draws the GR source rows, phase 2 copies their fields with
+// consecutive threads on consecutive columns (all loads independent -> one memory latency).
+constexpr int GR = 16;
+__global__ __launch_bounds__(256) void sac_gather_kernel(const mopo_pool_desc env, const mopo_pool_desc mod, int n,
+                                                         int n_env, int O, int A, const int64_t* idx_in,
+                                                         int64_t* idx_out, uint64_t seed, const int64_t* iter,
+                                                         float* sa, float* xpi, float* xn, float* rew, float* term) {
+  __shared__ int64_t src_s[GR];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * GR;
+  if (tid < GR && r0 + tid < n) {
+    const int r = r0 + tid;
+    int64_t src;
+    if (idx_in) {
+      src = idx_in[r];
+    } else {
+      const uint64_t size = (uint64_t)(r < n_env ? env.d_state[1] : mod.d_state[1]);
+      const int64_t it = *iter;
+      u32x4 c{(uint32_t)r, (uint32_t)it, (uint32_t)((uint64_t)it >> 32), RNG_SAC};
+      u32x4 q = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+      src = (int64_t)(((uint64_t)q.x * size) >> 32);
+    }
+    src_s[tid] = src;
+    idx_out[r] = src;
   }
-  idx_out[r] = src;
-  const int W = O + A;
-  for (int k = 0; k < O; ++k) {
-    const float v = p.d_obs[src * O + k];
-    sa[r * W + k] = v;
-    xpi[r * W + k] = v;
-    xn[r * W + k] = p.d_next_obs[src * O + k];
+  __syncthreads();
+  const int W = O + A, C = 2 * O + A + 2;  // obs | act | next_obs | rew | term
+  for (int e = tid; e < GR * C; e += 256) {
+    const int rr = e / C, c = e % C, r = r0 + rr;
+    if (r >= n) continue;
+    const bool fe = r < n_env;
+    const int64_t src = src_s[rr];
+    if (c < O) {
+      const float v = (fe ? env.d_obs : mod.d_obs)[src * O + c];
+      sa[r * W + c] = v;
+      xpi[r * W + c] = v;
+    } else if (c < O + A) {
+      sa[r * W + c] = (fe ? env.d_act : mod.d_act)[src * A + (c - O)];
+    } else if (c < 2 * O + A) {
+      xn[r * W + (c - O - A)] = (fe ? env.d_next_obs : mod.d_next_obs)[src * O + (c - O - A)];
+    } else if (c == 2 * O + A) {
+      rew[r] = (fe ? env.d_rew : mod.d_rew)[src];
+    } else {
+      term[r] = (float)(fe ? env.d_term : mod.d_term)[src];
+    }
   }
-  for (int k = 0; k < A; ++k) sa[r * W + O + k] = p.d_act[src * A + k];
-  rew[r] = p.d_rew[src];
-  term[r] = (float)p.d_term[src];
 }
 
 __device__ __forceinline__ float softplus_f(float x) { return softplusf(x); }
@@ -369,14 +414,20 @@ __global__ __launch_bounds__(256) void sac_adam_kernel(int64_t total, int64_t n_
   }
 }
 
-__global__ void sac_finalize_kernel(int nblk, const float* norm_part, float* logs, float* beta_pow, int64_t* iter) {
+__global__ __launch_bounds__(256) void sac_finalize_kernel(int nblk, const float* norm_part, float* logs,
+                                                           float* beta_pow, int64_t* iter) {
+  __shared__ float sh[256];
   float a = 0.f, b = 0.f;
-  for (int i = 0; i < nblk; ++i) { a += norm_part[2 * i]; b += norm_part[2 * i + 1]; }
-  logs[LOG_PI_GNORM] = sqrtf(a);
-  logs[LOG_Q_GNORM] = 0.5f * sqrtf(b);                                // grads of Q_loss = (l1+l2)/2 wrt q1
-  beta_pow[0] *= 0.9f;
-  beta_pow[1] *= 0.999f;
-  *iter += 1;
+  for (int i = threadIdx.x; i < nblk; i += 256) { a += norm_part[2 * i]; b += norm_part[2 * i + 1]; }
+  a = block_sum(a, sh);
+  b = block_sum(b, sh);
+  if (threadIdx.x == 0) {
+    logs[LOG_PI_GNORM] = sqrtf(a);
+    logs[LOG_Q_GNORM] = 0.5f * sqrtf(b);                              // grads of Q_loss = (l1+l2)/2 wrt q1
+    beta_pow[0] *= 0.9f;                                              // TF1 beta power updates (f32)
+    beta_pow[1] *= 0.999f;
+    *iter += 1;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -411,7 +462,7 @@ static int sac_step_impl(Sac* h, const mopo_pool_desc* env, const mopo_pool_desc
   const float* P = h->P;
   const float* T = h->T;
   float* G = h->G;
-  hipLaunchKernelGGL(sac_gather_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, *env, *mod, n, d.n_env, O, A, idx_in,
+  hipLaunchKernelGGL(sac_gather_kernel, dim3(ceil_div(n, GR)), dim3(256), 0, s, *env, *mod, n, d.n_env, O, A, idx_in,
                      h->idx, seed, h->iter, h->sa, h->xpi, h->xn, h->rew, h->term);
   MOPO_HIP(hipGetLastError());
   auto Wq = [&](int qi, int k) { return P + o.q[qi][k]; };
@@ -486,19 +537,19 @@ static int sac_step_impl(Sac* h, const mopo_pool_desc* env, const mopo_pool_desc
                      h->logp_s, h->logp_n, h->rew, h->term, h->out[0], P + o.total, h->dq[0], h->dq[1], h->dq[2],
                      h->dq[3], G + o.total, h->logs);
   MOPO_HIP(hipGetLastError());
-  // ---- critic backward: output layer (rank-1), then hidden layers
-  hipLaunchKernelGGL(q_out_bwd_kernel, dim3(ceil_div(n * H, 256), 4), dim3(256), 0, s, n, H, h->dq_dev, h->w3_dev,
-                     h->h2q_dev, h->dh2_dev);
-  MOPO_HIP(hipGetLastError());
+  // ---- critic backward.  The 1-wide output layer's backward dh2 = dq (x) W3 * (h2 > 0) is rank-1,
+  // so it is never materialised: the consumers below read it as a rank-1 masked operand.
   {
     std::vector<GemmProb> g;
     for (int i = 0; i < 4; ++i) {  // dh1 = dh2 W2^T * (h1 > 0); instances Q1(sa) Q2(sa) Q1(pi) Q2(pi)
       const int qi = i & 1;
-      auto a = mk(n, H, H, h->dh2[i], H, 0, Wq(qi, 2), H, 1, h->dh1[i], H); a.mask = h->h1[2 + i]; a.ldm = H;
+      auto a = mk(n, H, H, nullptr, H, 0, Wq(qi, 2), H, 1, h->dh1[i], H); a.mask = h->h1[2 + i]; a.ldm = H;
+      a.a_u = h->dq[i]; a.a_v = Wq(qi, 4); a.a_m = h->h2[2 + i]; a.a_ldm = H;
       g.push_back(a);
     }
     for (int qi = 0; qi < 2; ++qi) {  // dW2 = h1^T dh2 (+db2), dW3 = h2^T dq (+db3)
-      auto w2 = mk(H, H, n, h->h1[2 + qi], H, 1, h->dh2[qi], H, 0, G + o.q[qi][2], H); w2.colsum = G + o.q[qi][3];
+      auto w2 = mk(H, H, n, h->h1[2 + qi], H, 1, nullptr, H, 0, G + o.q[qi][2], H); w2.colsum = G + o.q[qi][3];
+      w2.b_u = h->dq[qi]; w2.b_v = Wq(qi, 4); w2.b_m = h->h2[2 + qi]; w2.b_ldm = H;
       g.push_back(w2);
       auto w3 = mk(H, 1, n, h->h2[2 + qi], H, 1, h->dq[qi], 1, 0, G + o.q[qi][4], 1); w3.colsum = G + o.q[qi][5];
       g.push_back(w3);
@@ -536,7 +587,7 @@ static int sac_step_impl(Sac* h, const mopo_pool_desc* env, const mopo_pool_desc
   hipLaunchKernelGGL(sac_adam_kernel, dim3(h->adam_blocks), dim3(256), 0, s, o.total, o.n_pi, o.n_q, h->P, h->G, h->M,
                      h->V, h->T, h->beta_pow, h->lr, h->tau, h->norm_part);
   MOPO_HIP(hipGetLastError());
-  hipLaunchKernelGGL(sac_finalize_kernel, dim3(1), dim3(1), 0, s, h->adam_blocks, h->norm_part, h->logs, h->beta_pow,
+  hipLaunchKernelGGL(sac_finalize_kernel, dim3(1), dim3(256), 0, s, h->adam_blocks, h->norm_part, h->logs, h->beta_pow,
                      h->iter);
   MOPO_HIP(hipGetLastError());
   return 0;
@@ -559,7 +610,7 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   h->d.P = h->o.total;
   h->lr = lr; h->gamma = gamma; h->tau = tau; h->rscale = reward_scale; h->tent = target_entropy;
   const int64_t tot = h->o.total + 1, n = batch, W = O + A;
-  h->adam_blocks = (int)std::min<int64_t>(512, (tot + 255) / 256);
+  h->adam_blocks = (int)std::min<int64_t>(256, (tot + 255) / 256);
   std::vector<std::pair<void**, size_t>> reg;
   auto f = [&](float** p, size_t cnt) { reg.push_back({(void**)p, cnt * 4}); };
   f(&h->P, tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->T, tot);
