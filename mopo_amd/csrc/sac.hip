@@ -43,16 +43,77 @@ struct GemmGroup {
   GemmProb p[MAXP];
 };
 
-__device__ __forceinline__ float opA(const GemmProb& p, int i, int k) {
-  if (p.a_u) return p.a_m[(int64_t)i * p.a_ldm + k] > 0.f ? p.a_u[i] * p.a_v[k] : 0.f;
-  return p.ta ? p.A[(int64_t)k * p.lda + i] : p.A[(int64_t)i * p.lda + k];
-}
-__device__ __forceinline__ float opB(const GemmProb& p, int k, int j) {
-  if (p.b_u) return p.b_m[(int64_t)k * p.b_ldm + j] > 0.f ? p.b_u[k] * p.b_v[j] : 0.f;
-  return p.tb ? p.B[(int64_t)j * p.ldb + k] : p.B[(int64_t)k * p.ldb + j];
-}
 
 constexpr int GKC = 256;  // K chunk staged in LDS
+
+// One 16-wide panel (A: rows i0..i0+15, or B: cols j0..j0+15) x K-chunk, staged as S[k][r].
+// MODE 0: plain, 1: transposed, 2: rank-1 masked (see GemmProb).  Addresses are clamped so every
+// load is valid and unconditional; out-of-range elements are zeroed by a select afterwards.
+struct PanelRegs { float x[16], u[16], w[16]; };
+
+template <int MODE, bool IS_A>
+__device__ __forceinline__ void panel_rk(int q, int tid, int& r, int& k) {
+  constexpr bool rfast = IS_A ? (MODE == 1) : (MODE != 1);
+  if (rfast) { r = tid & 15; k = (tid >> 4) + 16 * q; }
+  else { k = (tid & 63) + 64 * (q & 3); r = (tid >> 6) + 4 * (q >> 2); }
+}
+
+template <int MODE, bool IS_A>
+__device__ __forceinline__ void load_panel(const GemmProb& p, int r0, int kc, int tid, PanelRegs& R) {
+  const int Rmax = IS_A ? p.M : p.N;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    int r, k;
+    panel_rk<MODE, IS_A>(q, tid, r, k);
+    const int rc = min(r0 + r, Rmax - 1), kk = min(kc + k, p.K - 1);
+    if (MODE == 2) {
+      const float* m = IS_A ? p.a_m : p.b_m;
+      const int ldm = IS_A ? p.a_ldm : p.b_ldm;
+      R.u[q] = IS_A ? p.a_u[rc] : p.b_u[kk];
+      R.w[q] = IS_A ? p.a_v[kk] : p.b_v[rc];
+      R.x[q] = IS_A ? m[(int64_t)rc * ldm + kk] : m[(int64_t)kk * ldm + rc];
+    } else if (IS_A) {
+      R.x[q] = MODE == 0 ? p.A[(int64_t)rc * p.lda + kk] : p.A[(int64_t)kk * p.lda + rc];
+    } else {
+      R.x[q] = MODE == 0 ? p.B[(int64_t)kk * p.ldb + rc] : p.B[(int64_t)rc * p.ldb + kk];
+    }
+  }
+}
+
+// pin the loads as unconditional (else hipcc sinks each into a branch followed by vmcnt(0))
+template <int MODE>
+__device__ __forceinline__ void pin_panel(PanelRegs& R) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    asm volatile("" : "+v"(R.x[q]));
+    if (MODE == 2) asm volatile("" : "+v"(R.u[q]), "+v"(R.w[q]));
+  }
+}
+
+template <int MODE, bool IS_A>
+__device__ __forceinline__ void store_panel(const GemmProb& p, int r0, int kn, int tid, const PanelRegs& R,
+                                            float (*S)[16]) {
+  const int Rmax = IS_A ? p.M : p.N;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    int r, k;
+    panel_rk<MODE, IS_A>(q, tid, r, k);
+    const float v = MODE == 2 ? (R.x[q] > 0.f ? R.u[q] * R.w[q] : 0.f) : R.x[q];
+    S[k][r] = (r0 + r < Rmax && k < kn) ? v : 0.f;
+  }
+}
+
+template <int AM, int BM>
+__device__ __forceinline__ void stage_ab(const GemmProb& p, int i0, int j0, int kc, int kn, int tid, float (*As)[16],
+                                         float (*Bs)[16]) {
+  PanelRegs ra, rb;
+  load_panel<AM, true>(p, i0, kc, tid, ra);
+  load_panel<BM, false>(p, j0, kc, tid, rb);
+  pin_panel<AM>(ra);
+  pin_panel<BM>(rb);
+  store_panel<AM, true>(p, i0, kn, tid, ra, As);
+  store_panel<BM, false>(p, j0, kn, tid, rb, Bs);
+}
 
 // One 16x16 output tile per 256-thread block.  The A[16 x K] and B[K x 16] panels are staged in
 // LDS with loads ordered along each operand's contiguous axis (all issued before the first use:
@@ -72,19 +133,26 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
   const int tm = t / tn_cnt, tn = t % tn_cnt;
   const int i0 = tm * 16, j0 = tn * 16;
   const int li = lane & 15, lk = lane >> 4;
-  const bool a_kfast = p.a_u || !p.ta, b_jfast = p.b_u || !p.tb;
   const bool do_cs = p.colsum && tm == 0;
   f32x4 acc0 = zero4(), acc1 = zero4();
   float cs = 0.f;
   for (int kc = 0; kc < p.K; kc += GKC) {
     const int kn = min(GKC, p.K - kc);
     const int kpad = (kn + 3) & ~3;
-    for (int idx = tid; idx < 16 * kpad; idx += 256) {
-      int i, k, j;
-      if (a_kfast) { i = idx / kpad; k = idx % kpad; } else { i = idx & 15; k = idx >> 4; }
-      As[k][i] = (i0 + i < p.M && k < kn) ? opA(p, i0 + i, kc + k) : 0.f;
-      if (b_jfast) { j = idx & 15; k = idx >> 4; } else { j = idx / kpad; k = idx % kpad; }
-      Bs[k][j] = (j0 + j < p.N && k < kn) ? opB(p, kc + k, j0 + j) : 0.f;
+    // 16 elements of each panel per thread; the per-operand mode is dispatched once (uniform
+    // branch) so that all 32+ loads are unconditional (clamped addresses, select after the load)
+    // and issue back to back -- one memory latency per chunk instead of one per element.
+    const int am = p.a_u ? 2 : p.ta, bm = p.b_u ? 2 : p.tb;
+    switch (am * 3 + bm) {
+      case 0: stage_ab<0, 0>(p, i0, j0, kc, kn, tid, As, Bs); break;
+      case 1: stage_ab<0, 1>(p, i0, j0, kc, kn, tid, As, Bs); break;
+      case 2: stage_ab<0, 2>(p, i0, j0, kc, kn, tid, As, Bs); break;
+      case 3: stage_ab<1, 0>(p, i0, j0, kc, kn, tid, As, Bs); break;
+      case 4: stage_ab<1, 1>(p, i0, j0, kc, kn, tid, As, Bs); break;
+      case 5: stage_ab<1, 2>(p, i0, j0, kc, kn, tid, As, Bs); break;
+      case 6: stage_ab<2, 0>(p, i0, j0, kc, kn, tid, As, Bs); break;
+      case 7: stage_ab<2, 1>(p, i0, j0, kc, kn, tid, As, Bs); break;
+      default: stage_ab<2, 2>(p, i0, j0, kc, kn, tid, As, Bs); break;
     }
     __syncthreads();
     const int ksteps = kpad >> 2, per = (ksteps + 3) >> 2;
