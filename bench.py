@@ -92,27 +92,12 @@ def rollout_step(args, ro, pool, pi, env, staging, epoch, rank, world):
     import torch
     if world == 1:
         return ro.run(env, pi, pool, args.batch, args.horizon, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=epoch)
-    import torch.distributed as dist
+    from mopo_amd.distributed import allgather_transitions, unpack_rows
     steps = ro.run(env, pi, staging, args.batch, args.horizon, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=epoch,
                    staged=True, uid_offset=rank * args.batch)
     # RCCL all-gather of the staged transitions (+ per-step counts) into every rank's pool
-    n = args.horizon * args.batch
-    f = staging.fields
-    packed = torch.cat([f['observations'][:n], f['actions'][:n], f['rewards'][:n],
-                        f['terminals'][:n].float(), f['next_observations'][:n]], 1)
-    gathered = torch.empty((world,) + tuple(packed.shape), dtype=packed.dtype, device=packed.device)
-    dist.all_gather_into_tensor(gathered, packed)
-    counts = torch.empty((world, args.horizon), dtype=torch.int64, device=steps.device)
-    dist.all_gather_into_tensor(counts, steps.contiguous())
-    cnt = counts.cpu().numpy()
-    g = gathered.view(world, args.horizon, args.batch, -1)
-    parts = []
-    for i in range(args.horizon):          # global order: step-major, then rank-major row shards
-        for r in range(world):
-            parts.append(g[r, i, :int(cnt[r, i])])
-    rows = torch.cat(parts, 0)
-    pool.add_samples({'observations': rows[:, :O], 'actions': rows[:, O:O + A], 'rewards': rows[:, O + A:O + A + 1],
-                      'terminals': rows[:, O + A + 1:O + A + 2] > 0.5, 'next_observations': rows[:, O + A + 2:]})
+    rows, counts = allgather_transitions(staging.fields, steps, args.horizon, args.batch, O, A)
+    pool.add_samples(unpack_rows(rows, O, A))
     return counts.sum(0)
 
 

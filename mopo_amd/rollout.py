@@ -83,7 +83,7 @@ class ModelRollout:
 
         args = L.RolloutArgs(
             d_env_obs=L.ptr(env_obs), env_size=int(env_obs.shape[0]), d_start_idx=dptr(start_idx, torch.int64),
-            d_pi_params=L.ptr(pi_params), pi_hidden=int(pi_hidden), d_elites=L.ptr(el), n_elites=int(el.numel()),
+            d_pi_params=pi_params if isinstance(pi_params, int) else L.ptr(pi_params), pi_hidden=int(pi_hidden), d_elites=L.ptr(el), n_elites=int(el.numel()),
             B=B, horizon=int(horizon), penalty_coeff=float(penalty_coeff), term_kind=int(term_kind),
             seed=int(seed) & (2 ** 64 - 1), epoch=int(epoch), uid_offset=int(uid_offset),
             d_eps_act=dptr(eps_act, torch.float32), d_eps_obs=dptr(eps_obs, torch.float64),

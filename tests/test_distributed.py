@@ -1,0 +1,80 @@
+"""CPU (gloo, world_size 2): the multi-GPU rollout's collective leg -- all-gather of staged
+transitions + per-step counts and reassembly in the single-GPU global order."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+O, A, H, B = 17, 6, 3, 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def staging_for(rank):
+    """Rank-local staging: step i rows carry (rank, step, row) in their observation columns."""
+    n = H * B
+    f = {'observations': torch.zeros(n, O), 'actions': torch.full((n, A), float(rank)),
+         'rewards': torch.zeros(n, 1), 'terminals': torch.zeros(n, 1, dtype=torch.bool),
+         'next_observations': torch.zeros(n, O)}
+    for i in range(H):
+        for r in range(B):
+            f['observations'][i * B + r, 0] = rank
+            f['observations'][i * B + r, 1] = i
+            f['observations'][i * B + r, 2] = r
+            f['rewards'][i * B + r, 0] = 100 * rank + 10 * i + r
+            f['terminals'][i * B + r, 0] = (r + i + rank) % 3 == 0
+    steps = torch.tensor([B, B - rank, 2 + rank][:H], dtype=torch.int64)   # ragged live counts
+    return f, steps
+
+
+def _worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from mopo_amd.distributed import allgather_transitions, unpack_rows
+    f, steps = staging_for(rank)
+    rows, counts = allgather_transitions(f, steps, H, B, O, A)
+    out = unpack_rows(rows, O, A)
+    q.put((rank, {k: v.numpy() for k, v in out.items()}, counts.numpy()))
+    dist.destroy_process_group()
+
+
+def test_allgather_global_order_world2():
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=60) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda t: t[0])
+    # expected: step-major, then rank-major, live rows only, in row order
+    exp_rows = []
+    for i in range(H):
+        for r in range(world):
+            f, steps = staging_for(r)
+            for j in range(int(steps[i])):
+                exp_rows.append((r, i, j, float(f['rewards'][i * B + j, 0]), bool(f['terminals'][i * B + j, 0])))
+    for rank, out, counts in res:
+        got = [(int(o[0]), int(o[1]), int(o[2]), float(rw[0]), bool(t[0]))
+               for o, rw, t in zip(out['observations'], out['rewards'], out['terminals'])]
+        assert got == exp_rows
+        np.testing.assert_array_equal(counts, np.stack([staging_for(r)[1].numpy() for r in range(world)]))
+        assert (out['actions'][:, 0] == out['observations'][:, 0]).all()   # rows moved whole
+    # both ranks hold identical pools
+    for k in res[0][1]:
+        np.testing.assert_array_equal(res[0][1][k], res[1][1][k])
