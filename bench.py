@@ -52,11 +52,18 @@ def dist_setup(args):
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        torch.cuda.set_device(0)
-    return rank, world, torch.device('cuda', local if world > 1 else 0)
+        # one rank per GPU; MOPO_DIST_BACKEND=gloo + wrapping devices is for rehearsing the
+        # collective path with several ranks on one GPU (the driver's runs use RCCL)
+        backend = os.environ.get('MOPO_DIST_BACKEND', 'nccl')
+        dev_i = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev_i)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev_i))
+        else:
+            dist.init_process_group(backend)
+        return rank, world, torch.device('cuda', dev_i)
+    torch.cuda.set_device(0)
+    return rank, world, torch.device('cuda', 0)
 
 
 def build(args, dev, rank):
