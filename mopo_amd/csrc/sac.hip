@@ -134,6 +134,13 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
   const int i0 = tm * 16, j0 = tn * 16;
   const int li = lane & 15, lk = lane >> 4;
   const bool do_cs = p.colsum && tm == 0;
+  // epilogue operands are fetched up front so their latency overlaps the panel loads
+  const int ei = tid >> 4, ej = tid & 15;
+  const int gi = i0 + ei, gj = j0 + ej;
+  const int gic = min(gi, p.M - 1), gjc = min(gj, p.N - 1);
+  float e_bias = p.bias ? p.bias[gjc] : 0.f;
+  float e_mask = p.mask ? p.mask[(int64_t)gic * p.ldm + gjc] : 1.f;
+  asm volatile("" : "+v"(e_bias), "+v"(e_mask));
   f32x4 acc0 = zero4(), acc1 = zero4();
   float cs = 0.f;
   for (int kc = 0; kc < p.K; kc += GKC) {
@@ -155,13 +162,20 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
       default: stage_ab<2, 2>(p, i0, j0, kc, kn, tid, As, Bs); break;
     }
     __syncthreads();
-    const int ksteps = kpad >> 2, per = (ksteps + 3) >> 2;
-    const int sb = w * per, se = min(ksteps, sb + per);
-    for (int s = sb; s < se; ++s) {
-      const int k = 4 * s + lk;
-      const float a = As[k][li], b = Bs[k][li];
-      if (s & 1) acc1 = mfma4(a, b, acc1);
-      else acc0 = mfma4(a, b, acc0);
+    (void)kpad;
+    // the staged panels are zero-padded to GKC rows, so every wave runs exactly 16 k-steps of its
+    // quarter with no guards: all 32 LDS reads first, then 16 MFMAs on two accumulators
+    float ra[16], rb[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = 4 * (w * 16 + s) + lk;
+      ra[s] = As[k][li];
+      rb[s] = Bs[k][li];
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s & 1) acc1 = mfma4(ra[s], rb[s], acc1);
+      else acc0 = mfma4(ra[s], rb[s], acc0);
     }
     if (do_cs)
       for (int k = tid >> 4; k < kn; k += 16) cs += Bs[k][tid & 15];
@@ -172,13 +186,11 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
   if (do_cs) csum[tid >> 4][tid & 15] = cs;
   __syncthreads();
   {
-    const int i = tid >> 4, j = tid & 15;
     float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
-    const int gi = i0 + i, gj = j0 + j;
     if (gi < p.M && gj < p.N) {
-      if (p.bias) v += p.bias[gj];
+      v += e_bias;
       if (p.relu) v = fmaxf(v, 0.f);
-      if (p.mask && !(p.mask[(int64_t)gi * p.ldm + gj] > 0.f)) v = 0.f;
+      if (!(e_mask > 0.f)) v = 0.f;
       p.C[(int64_t)gi * p.ldc + gj] = v;
     }
   }
@@ -228,6 +240,7 @@ struct Sac {
   float *P, *G, *M, *V, *T;       // [total + 1]: last element = log_alpha
   float* beta_pow;                // [2] f32 beta1_power, beta2_power (TF1 non-slot vars)
   int64_t* iter;                  // device step counter (Philox)
+  unsigned* ticket;               // last-block ticket of the Adam kernel
   float* logs;                    // [LOG_N]
   float* norm_part;               // [nblk][2]
   int adam_blocks = 0;
@@ -348,18 +361,33 @@ __global__ void pi_head_fwd_kernel(int n, int O, int A, const float* head_s, con
   (nxt ? logp_n : logp_s)[r] = logp - corr;
 }
 
-__device__ float block_sum(float v, float* sh) {
-  // deterministic tree reduction over blockDim.x (power of two <= 1024)
-  const int tid = threadIdx.x;
-  sh[tid] = v;
+// Deterministic block-wide sums of NV values at once: butterfly within each wave (__shfl_xor),
+// then the per-wave partials added in wave order.  Two barriers for all NV sums.
+// sh must hold 16 * NV floats; blockDim.x a multiple of 64 (<= 1024).
+template <int NV>
+__device__ __forceinline__ void block_sums(float (&v)[NV], float* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[i] += __shfl_xor(v[i], off);
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) sh[w * NV + i] = v[i];
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (tid < s) sh[tid] += sh[tid + s];
-    __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float s = 0.f;
+    for (int q = 0; q < nw; ++q) s += sh[q * NV + i];
+    v[i] = s;
   }
-  float r = sh[0];
   __syncthreads();
-  return r;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  float a[1] = {v};
+  block_sums<1>(a, sh);
+  return a[0];
 }
 
 // ---- losses, output gradients, alpha gradient, logs (single block, one thread per row)
@@ -390,12 +418,12 @@ __global__ __launch_bounds__(1024) void sac_loss_kernel(int n, int A, float gamm
     }
   }
   const float fn = (float)n;
-  const float l1 = block_sum(ok ? (q1 - y) * (q1 - y) : 0.f, sh) / fn * 0.5f;   // mopo.py:403
-  const float l2 = block_sum(ok ? (q2 - y) * (q2 - y) : 0.f, sh) / fn * 0.5f;
-  const float m1 = block_sum(q1, sh) / fn, m2 = block_sum(q2, sh) / fn;
-  const float mlp = block_sum(lps, sh) / fn;
-  const float ment = block_sum(ent, sh) / fn;
-  const float pil = block_sum(ok ? alpha * lps - fminf(q1p, q2p) : 0.f, sh) / fn;  // mopo.py:371-377
+  float red[7] = {ok ? (q1 - y) * (q1 - y) : 0.f, ok ? (q2 - y) * (q2 - y) : 0.f, q1, q2, lps, ent,
+                  ok ? alpha * lps - fminf(q1p, q2p) : 0.f};
+  block_sums<7>(red, sh);
+  const float l1 = red[0] / fn * 0.5f, l2 = red[1] / fn * 0.5f;           // mopo.py:403-404
+  const float m1 = red[2] / fn, m2 = red[3] / fn, mlp = red[4] / fn, ment = red[5] / fn;
+  const float pil = red[6] / fn;                                          // mopo.py:371-377
   if (r == 0) {
     *g_alpha = -(mlp + tent);                                       // d/dlog_alpha of -mean(la*(logp+H))
     logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;
@@ -455,8 +483,9 @@ __global__ __launch_bounds__(256) void pi_head_bwd_kernel(int n, int O, int A, i
 
 // ---- four TF1 Adams (identical step counts -> one lr_t) + Polyak, and grad-norm partials
 __global__ __launch_bounds__(256) void sac_adam_kernel(int64_t total, int64_t n_pi, int64_t n_q, float* P, const float* G,
-                                                       float* Mm, float* Vv, float* T, const float* beta_pow, float lr,
-                                                       float tau, float* norm_part) {
+                                                       float* Mm, float* Vv, float* T, float* beta_pow, float lr,
+                                                       float tau, float* norm_part, unsigned* ticket, float* logs,
+                                                       int64_t* iter) {
   __shared__ float sh[256];
   const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
   const float lr_t = lr * sqrtf(1.f - beta_pow[1]) / (1.f - beta_pow[0]);
@@ -474,29 +503,42 @@ __global__ __launch_bounds__(256) void sac_adam_kernel(int64_t total, int64_t n_
     P[i] = p;
     if (i < total) T[i] = (1.f - tau) * T[i] + tau * p;             // mopo.py:446-447 (after the updates)
   }
-  npi = block_sum(npi, sh);
-  nq = block_sum(nq, sh);
+  float nn[2] = {npi, nq};
+  block_sums<2>(nn, sh);
+  // publish this block's partial norms; the last-arriving block reduces them in block order
+  // (agent-scope release -> relaxed ticket -> acquire; cdna_hip_programming.md §6 Guideline 16)
+  __shared__ int last;
   if (threadIdx.x == 0) {
-    norm_part[blockIdx.x * 2] = npi;
-    norm_part[blockIdx.x * 2 + 1] = nq;
+    norm_part[blockIdx.x * 2] = nn[0];
+    norm_part[blockIdx.x * 2 + 1] = nn[1];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == gridDim.x - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
-}
-
-__global__ __launch_bounds__(256) void sac_finalize_kernel(int nblk, const float* norm_part, float* logs,
-                                                           float* beta_pow, int64_t* iter) {
-  __shared__ float sh[256];
+  __syncthreads();
+  if (!last) return;
   float a = 0.f, b = 0.f;
-  for (int i = threadIdx.x; i < nblk; i += 256) { a += norm_part[2 * i]; b += norm_part[2 * i + 1]; }
-  a = block_sum(a, sh);
-  b = block_sum(b, sh);
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {
+    a += __hip_atomic_load(norm_part + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b += __hip_atomic_load(norm_part + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  float ab[2] = {a, b};
+  block_sums<2>(ab, sh);
   if (threadIdx.x == 0) {
-    logs[LOG_PI_GNORM] = sqrtf(a);
-    logs[LOG_Q_GNORM] = 0.5f * sqrtf(b);                              // grads of Q_loss = (l1+l2)/2 wrt q1
+    logs[LOG_PI_GNORM] = sqrtf(ab[0]);
+    logs[LOG_Q_GNORM] = 0.5f * sqrtf(ab[1]);                          // grads of Q_loss = (l1+l2)/2 wrt q1
     beta_pow[0] *= 0.9f;                                              // TF1 beta power updates (f32)
     beta_pow[1] *= 0.999f;
     *iter += 1;
+    *ticket = 0u;                                                     // stream order: next launch sees 0
   }
 }
+
 
 // ---------------------------------------------------------------------------------------------
 static GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C,
@@ -601,7 +643,7 @@ static int sac_step_impl(Sac* h, const mopo_pool_desc* env, const mopo_pool_desc
     if (launch_group(g, s)) return -1;
   }
   // ---- losses
-  hipLaunchKernelGGL(sac_loss_kernel, dim3(1), dim3(1024), 0, s, n, A, h->gamma, h->rscale, h->tent, h->outp_dev,
+  hipLaunchKernelGGL(sac_loss_kernel, dim3(1), dim3(ceil_div(n, 64) * 64), 0, s, n, A, h->gamma, h->rscale, h->tent, h->outp_dev,
                      h->logp_s, h->logp_n, h->rew, h->term, h->out[0], P + o.total, h->dq[0], h->dq[1], h->dq[2],
                      h->dq[3], G + o.total, h->logs);
   MOPO_HIP(hipGetLastError());
@@ -653,10 +695,7 @@ static int sac_step_impl(Sac* h, const mopo_pool_desc* env, const mopo_pool_desc
   }
   // ---- Adam x4 + Polyak, norms, counters
   hipLaunchKernelGGL(sac_adam_kernel, dim3(h->adam_blocks), dim3(256), 0, s, o.total, o.n_pi, o.n_q, h->P, h->G, h->M,
-                     h->V, h->T, h->beta_pow, h->lr, h->tau, h->norm_part);
-  MOPO_HIP(hipGetLastError());
-  hipLaunchKernelGGL(sac_finalize_kernel, dim3(1), dim3(256), 0, s, h->adam_blocks, h->norm_part, h->logs, h->beta_pow,
-                     h->iter);
+                     h->V, h->T, h->beta_pow, h->lr, h->tau, h->norm_part, h->ticket, h->logs, h->iter);
   MOPO_HIP(hipGetLastError());
   return 0;
 }
@@ -684,6 +723,7 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   f(&h->P, tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->T, tot);
   f(&h->beta_pow, 2); f(&h->logs, LOG_N); f(&h->norm_part, 2 * h->adam_blocks);
   reg.push_back({(void**)&h->iter, 8});
+  reg.push_back({(void**)&h->ticket, 4});
   f(&h->sa, n * W); f(&h->xpi, n * W); f(&h->xn, n * W); f(&h->rew, n); f(&h->term, n);
   for (int i = 0; i < 8; ++i) { f(&h->h1[i], n * H); f(&h->h2[i], n * H); f(&h->out[i], n * 2 * A); }
   f(&h->logp_s, n); f(&h->logp_n, n); f(&h->eps_s, n * A); f(&h->eps_n, n * A);

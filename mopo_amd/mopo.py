@@ -1,0 +1,146 @@
+"""MOPO outer loop on the MI355X path (host mirror of ``mopo.algorithms.mopo.MOPO``).
+
+Reference: mopo/algorithms/mopo.py — ``__init__`` (46-201), ``_train`` (490-648),
+``_set_rollout_length`` (675-687), ``_reallocate_model_pool`` (689-711), ``_rollout_model``
+(723-765), ``_do_training_repeats`` (780-799), ``_training_batch`` (801-821), ``_do_training``
+(834-850), ``get_diagnostics`` (876-918).
+
+Differences that are deliberate: the rollout and the SAC steps run on the device
+(csrc/rollout.hip, csrc/sac.hip); the epoch's 1000 SAC steps are issued as one replayed hipGraph
+batch (the reference runs them one ``session.run`` at a time, with the same batch rule per step);
+MuJoCo evaluation (``_evaluation_paths``) is out of scope -- no simulator in this image -- so
+``evaluation/*`` diagnostics are absent.  Model training (BNN.train) is a later-round item: the
+ensemble must be loaded (``model_load_dir`` .mat, bnn.py:276-281) or set via ``model.set_params``.
+"""
+import time
+from collections import OrderedDict
+
+import numpy as np
+
+from .bnn import construct_model
+from .fake_env import FakeEnv
+from .replay_pool import SimpleReplayPool
+from .rollout import ModelRollout
+from .sac import SAC
+
+
+class MOPO:
+    def __init__(self, pool, static_fns, obs_dim, act_dim, lr=3e-4, reward_scale=1.0, target_entropy='auto',
+                 discount=0.99, tau=5e-3, target_update_interval=1, model_train_freq=250, num_networks=7,
+                 num_elites=5, model_retain_epochs=20, rollout_batch_size=100e3, real_ratio=0.1, rollout_length=1,
+                 hidden_dim=200, separate_mean_var=False, penalty_coeff=0., penalty_learned_var=False,
+                 model_name=None, model_load_dir=None, deterministic=False, network_kwargs=None, epoch_length=1000,
+                 n_epochs=1000, n_train_repeat=1, batch_size=256, seed=88, reparameterize=True, **kwargs):
+        if target_update_interval != 1:
+            raise NotImplementedError('target_update_interval != 1 (all D4RL configs use 1)')
+        self._pool = pool                                   # device SimpleReplayPool of env data
+        self._static_fns = static_fns
+        self._obs_dim, self._act_dim = obs_dim, act_dim
+        self._model = construct_model(obs_dim=obs_dim, act_dim=act_dim, hidden_dim=hidden_dim,
+                                      num_networks=num_networks, num_elites=num_elites,
+                                      separate_mean_var=separate_mean_var, name=model_name,
+                                      load_dir=model_load_dir, deterministic=deterministic)
+        self.fake_env = FakeEnv(self._model, static_fns, penalty_coeff=penalty_coeff,
+                                penalty_learned_var=penalty_learned_var)
+        self._rollout_schedule = [20, 100, rollout_length, rollout_length]                 # mopo.py:137
+        self._model_retain_epochs = model_retain_epochs
+        self._model_train_freq = model_train_freq
+        self._rollout_batch_size = int(rollout_batch_size)
+        self._deterministic = deterministic
+        self._real_ratio = real_ratio
+        self._epoch_length, self._n_epochs, self._n_train_repeat = epoch_length, n_epochs, n_train_repeat
+        self._epoch = 0
+        self._num_train_steps = 0
+        self._seed = seed
+        hs = (network_kwargs or {}).get('hidden_sizes', [256, 256])
+        if len(hs) != 2 or hs[0] != hs[1]:
+            raise NotImplementedError('policy/Q hidden_sizes must be [H, H] (reference: [256, 256])')
+        self._sac = SAC(obs_dim, act_dim, hidden=hs[0], batch_size=batch_size, real_ratio=real_ratio, lr=lr,
+                        discount=discount, tau=tau, reward_scale=reward_scale, target_entropy=target_entropy,
+                        seed=seed, reparameterize=reparameterize)
+        self._pi_hidden = hs[0]
+        self._rollout = None
+        self._rollout_length = rollout_length
+
+    # -- mopo.py:675-687
+    def _set_rollout_length(self):
+        min_epoch, max_epoch, min_length, max_length = self._rollout_schedule
+        if self._epoch <= min_epoch:
+            y = min_length
+        else:
+            dx = min((self._epoch - min_epoch) / (max_epoch - min_epoch), 1)
+            y = dx * (max_length - min_length) + min_length
+        self._rollout_length = int(y)
+
+    # -- mopo.py:689-711
+    def _reallocate_model_pool(self):
+        rollouts_per_epoch = self._rollout_batch_size * self._epoch_length / self._model_train_freq
+        model_steps_per_epoch = int(self._rollout_length * rollouts_per_epoch)
+        new_pool_size = self._model_retain_epochs * model_steps_per_epoch
+        if not hasattr(self, '_model_pool'):
+            self._model_pool = SimpleReplayPool(obs_dim=self._obs_dim, act_dim=self._act_dim, max_size=new_pool_size)
+        elif self._model_pool._max_size != new_pool_size:
+            samples = self._model_pool.return_all_samples()
+            new_pool = SimpleReplayPool(obs_dim=self._obs_dim, act_dim=self._act_dim, max_size=new_pool_size)
+            new_pool.add_samples(samples)
+            assert self._model_pool.size == new_pool.size
+            self._model_pool = new_pool
+
+    # -- mopo.py:723-765 (device-resident, perf-mode RNG)
+    def _rollout_model(self, rollout_batch_size, **kwargs):
+        if self._rollout is None or self._rollout.max_batch < rollout_batch_size or \
+                self._rollout.max_horizon < self._rollout_length:
+            self._rollout = ModelRollout(self._model, rollout_batch_size, max(self._rollout_length, 1))
+        env_obs = self._pool.fields['observations'][:self._pool.size]
+        steps = self._rollout.run(env_obs, self._sac.policy_params_ptr, self._model_pool, rollout_batch_size,
+                                  self._rollout_length, self.fake_env.term_kind, self.fake_env.penalty_coeff,
+                                  self._model._model_inds, seed=self._seed, epoch=self._epoch,
+                                  pi_hidden=self._pi_hidden)
+        added = int(steps.sum().item())
+        return {'mean_rollout_length': added / rollout_batch_size}
+
+    # -- mopo.py:780-799 + 834-853: n steps of (_training_batch, _do_training, _update_target)
+    def _do_training_repeats(self, n_steps):
+        self._sac._do_training(self._num_train_steps, self._pool, self._model_pool, n_steps=n_steps,
+                               seed=self._seed + 7919 * self._epoch)
+        self._num_train_steps += n_steps
+        return self._sac.logs()
+
+    def _train_epoch(self):
+        """One epoch of mopo.py:536-573 with model_train_freq == epoch_length (all D4RL configs)."""
+        t0 = time.perf_counter()
+        self._set_rollout_length()
+        self._reallocate_model_pool()
+        metrics = self._rollout_model(self._rollout_batch_size)
+        import torch
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        logs = self._do_training_repeats(self._epoch_length * self._n_train_repeat)
+        t2 = time.perf_counter()
+        diag = OrderedDict()
+        diag.update(('model/' + k, v) for k, v in metrics.items())
+        diag.update(('training/' + k, v) for k, v in logs.items())
+        diag.update({'Q_loss': (logs['Q/q1_loss'] + logs['sac_Q/q2_loss']) / 2, 'alpha': logs['sac_pi/alpha'],
+                     'epoch': self._epoch, 'train-steps': self._num_train_steps,
+                     'times/epoch_rollout_model': t1 - t0, 'times/train': t2 - t1})
+        return diag
+
+    def train(self, n_epochs=None):
+        """Generator of per-epoch diagnostics (mopo.py:650-651)."""
+        if self._model_train_freq != self._epoch_length:
+            raise NotImplementedError('model_train_freq must equal epoch_length (all D4RL configs: 1000)')
+        for self._epoch in range(self._epoch, n_epochs or self._n_epochs):
+            yield self._train_epoch()
+
+    def get_diagnostics(self):
+        return self._sac.get_diagnostics()
+
+
+def from_config(params, pool, static_fns, model_load_dir=None, **overrides):
+    """Build MOPO from ``mopo_amd.config.get_params(...)`` (examples/config/d4rl dicts)."""
+    from .config import DIMS
+    kw = dict(params['kwargs'])
+    kw.update(overrides)
+    obs_dim, act_dim = DIMS[params['domain']]
+    kw.setdefault('model_load_dir', model_load_dir)
+    return MOPO(pool, static_fns, obs_dim, act_dim, **kw)

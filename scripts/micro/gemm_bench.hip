@@ -1,0 +1,49 @@
+// Micro-benchmark of the SAC grouped GEMM kernel (includes csrc/sac.hip to reach internals).
+#include "../../mopo_amd/csrc/sac.hip"
+#include <cstdio>
+
+using namespace mopo;
+
+__global__ void empty_kernel(const GemmGroup g) {
+  if (threadIdx.x == 0 && g.n < 0) g.p[0].C[0] = 1.f;
+}
+
+static float time_graph(std::vector<GemmProb> ps, int reps, hipStream_t s, bool empty) {
+  hipGraph_t gr; hipGraphExec_t ge;
+  (void)hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+  for (int i = 0; i < 16; ++i) {
+    if (!empty) launch_group(ps, s);
+    else { GemmGroup g{}; g.n = 1; g.p[0] = ps[0]; hipLaunchKernelGGL(empty_kernel, dim3(256), dim3(256), 0, s, g); }
+  }
+  (void)hipStreamEndCapture(s, &gr);
+  (void)hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
+  hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+  for (int w = 0; w < 3; ++w) (void)hipGraphLaunch(ge, s);
+  (void)hipEventRecord(a, s);
+  for (int r = 0; r < reps; ++r) (void)hipGraphLaunch(ge, s);
+  (void)hipEventRecord(b, s);
+  (void)hipEventSynchronize(b);
+  float ms; (void)hipEventElapsedTime(&ms, a, b);
+  return ms * 1e3f / reps / 16;
+}
+
+int main() {
+  hipStream_t s; (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  const int n = 256, H = 256;
+  float *X, *W, *Y, *M;
+  (void)hipMalloc(&X, 8 * n * H * 4); (void)hipMalloc(&W, 8 * H * H * 4); (void)hipMalloc(&Y, 8 * n * H * 4);
+  (void)hipMalloc(&M, n * H * 4);
+  (void)hipMemset(X, 0, 8 * n * H * 4); (void)hipMemset(W, 0, 8 * H * H * 4); (void)hipMemset(M, 0, n * H * 4);
+  auto fwd = [&](int i) { auto p = mk(n, H, H, X + i * n * H, H, 0, W + i * H * H, H, 0, Y + i * n * H, H); p.relu = 1; p.bias = W; return p; };
+  auto bwd = [&](int i) { auto p = mk(n, H, H, X + i * n * H, H, 0, W + i * H * H, H, 1, Y + i * n * H, H); p.mask = M; p.ldm = H; return p; };
+  auto wgt = [&](int i) { auto p = mk(H, H, n, X + i * n * H, H, 1, Y + i * n * H, H, 0, W + i * H * H, H); p.colsum = M; return p; };
+  printf("empty kernel (same kernarg):  %.2f us\n", time_graph({fwd(0)}, 200, s, true));
+  printf("1 tile 16x16x16:              %.2f us\n", time_graph({mk(16, 16, 16, X, 16, 0, W, 16, 0, Y, 16)}, 200, s, false));
+  printf("1 tile 16x16x256:             %.2f us\n", time_graph({mk(16, 16, 256, X, 256, 0, W, 16, 0, Y, 16)}, 200, s, false));
+  printf("fwd 1 x 256x256x256:          %.2f us\n", time_graph({fwd(0)}, 200, s, false));
+  printf("fwd 4 x 256x256x256:          %.2f us\n", time_graph({fwd(0), fwd(1), fwd(2), fwd(3)}, 200, s, false));
+  printf("bwd-data 4 x (W^T, mask):     %.2f us\n", time_graph({bwd(0), bwd(1), bwd(2), bwd(3)}, 200, s, false));
+  printf("wgrad 2 x (X^T dY, colsum):   %.2f us\n", time_graph({wgt(0), wgt(1)}, 200, s, false));
+  printf("fwd K=23 4 x 256x256:         %.2f us\n", time_graph({mk(n, H, 23, X, 23, 0, W, H, 0, Y, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + n * H, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + 2 * n * H, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + 3 * n * H, H)}, 200, s, false));
+  return 0;
+}
