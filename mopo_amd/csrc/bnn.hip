@@ -36,6 +36,23 @@ __global__ void pack_frags_kernel(const float* __restrict__ src, float* __restri
   }
 }
 
+// bf16 fragments for v_mfma_f32_16x16x32_bf16 (k-group of 32, permuted k order: mlp_tile.h):
+// frag (kg, nb), lane l (n = l&15, g = l>>4), element j = W[e][32 kg + bf16_kperm(g, j)][16 nb + n]
+__global__ void pack_frags_bf16_kernel(const float* __restrict__ src, short* __restrict__ dst, int E, int K, int N,
+                                       int KG, int NB) {
+  int64_t total = (int64_t)E * KG * NB * 512;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int j = i & 7, lane = (i >> 3) & 63;
+    int64_t f = i >> 9;
+    int nb = f % NB;
+    int kg = (f / NB) % KG;
+    int e = f / ((int64_t)NB * KG);
+    int k = kg * 32 + bf16_kperm(lane >> 4, j), n = nb * 16 + (lane & 15);
+    dst[i] = to_bf16((k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f);
+  }
+}
+
 __global__ void pack_bias_kernel(const float* __restrict__ src, float* __restrict__ dst, int E, int N,
                                  int NP) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -68,6 +85,50 @@ __device__ __forceinline__ void bias_swish(const float* __restrict__ b, const f3
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int t = 0; t < 4; ++t) out[r][nb][t] = swishf(acc[r][nb][t] + bb[t]);
+  }
+}
+
+// heads -> outputs for one row per lane group (bnn.py:661-675; rollout mode: fake_env.py:66-81, 110)
+template <int NBO, int MODE>
+__device__ __forceinline__ void head_epilogue(const BnnDev& w, const FwdArgs& a, const f32x4 (&hd)[NBO], int e,
+                                              int64_t row, int64_t count, int g) {
+  const int D = w.D;
+  const bool ok = row < count;
+  float ss = 0.f;  // sum of std^2 over D (learned-var penalty, fake_env.py:110)
+  const bool selected = (MODE == FWD_ROLLOUT) && ok && a.sel[row] == e;
+#pragma unroll
+  for (int nb = 0; nb < NBO; ++nb) {
+    f32x4 bb = ld4(w.bhd + e * NBO * 16 + nb * 16 + 4 * g);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int n = nb * 16 + 4 * g + t;
+      float v = hd[nb][t] + bb[t];
+      if (n < D) {
+        if (MODE == FWD_PREDICT) {
+          if (ok) a.mean[((int64_t)e * a.B + row) * D + n] = v;
+        } else if (selected) {
+          a.mean_sel[row * D + n] = v;
+        }
+      } else if (n < 2 * D) {
+        const int d = n - D;
+        const float mx = w.maxlv[d], mn = w.minlv[d];
+        float lv = mx - softplusf(mx - v);  // bnn.py:669
+        lv = mn + softplusf(lv - mn);       // bnn.py:670
+        const float var = expf(lv);         // bnn.py:675
+        if (MODE == FWD_PREDICT) {
+          if (ok) a.var[((int64_t)e * a.B + row) * D + d] = var;
+        } else {
+          const float sd = sqrtf(var);      // fake_env.py:67
+          ss += sd * sd;
+          if (selected) a.std_sel[row * D + d] = sd;
+        }
+      }
+    }
+  }
+  if (MODE == FWD_ROLLOUT) {
+    ss += __shfl_xor(ss, 16);
+    ss += __shfl_xor(ss, 32);
+    if (g == 0 && ok) atomicMax(a.pen_bits + row, __float_as_uint(sqrtf(ss)));  // >= 0: uint order
   }
 }
 
@@ -106,7 +167,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_kernel(const BnnDev w, 
       }
   }
   f32x4 acc[R][NBH], hcur[R][NBH];
-  const int64_t hp = (int64_t)NBH * 16;
+  const int64_t hp = w.BS;  // per-member bias stride
   layer_lds<KG0, NBH, R, WAVES, SLOT>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv, lane);
   bias_swish<NBH, R>(w.b0 + e * hp, acc, hcur, g);
   for (int l = 0; l < 3; ++l) {  // hidden layers 1..3 (constructor.py:31-33)
@@ -118,46 +179,61 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_kernel(const BnnDev w, 
   layer_lds<NBH, NBO, R, WAVES, SLOT>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds, wv, lane);
 
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int64_t row = row0 + r * 16 + m;
-    const bool ok = row < count;
-    float ss = 0.f;  // sum of std^2 over D (learned-var penalty, fake_env.py:110)
-    const bool selected = (MODE == FWD_ROLLOUT) && ok && a.sel[row] == e;
+  for (int r = 0; r < R; ++r) head_epilogue<NBO, MODE>(w, a, hd[r], e, row0 + r * 16 + m, count, g);
+  (void)D;
+}
+
+// ---- bf16 forward (dtype 1): bf16 weights/activations, f32 accumulate and f32 epilogues.
+// NB2 = hidden blocks rounded up to even (k-groups of 32 pair two accumulator blocks).
+template <int NB2, int NBO, int MODE, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_bf16_kernel(const BnnDev w, const FwdArgs a) {
+  constexpr int KG = NB2 / 2;
+  constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
+  constexpr int SLOT = Stage<NBMAX, WAVES>::SLOTS * 256;
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
+  const int groups = ceil_div(a.ntiles, WAVES);
+  const int e = blockIdx.x / groups, grp = blockIdx.x % groups;
+  const int64_t row = (int64_t)(grp * WAVES + wv) * 16 + m;
+  if ((int64_t)grp * WAVES * 16 >= count) return;
+  const int IN = w.IN, O = w.O;
+  const bool ok = row < count;
+  bf16x8 x0[1];
 #pragma unroll
-    for (int nb = 0; nb < NBO; ++nb) {
-      f32x4 bb = ld4(w.bhd + e * NBO * 16 + nb * 16 + 4 * g);
+  for (int j = 0; j < 8; ++j) {
+    const int k = bf16_kperm(g, j);
+    float v = 0.f;
+    if (ok && k < IN) {
+      float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
+                        : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
+      v = (raw - w.mu[k]) / w.sigma[k];
+    }
+    x0[0][j] = to_bf16(v);
+  }
+  const int64_t bs = w.BS;
+  f32x4 acc[NB2];
+  bf16x8 hin[KG];
+  auto to_input = [&](const float* b) {  // bias + swish in f32, then the bf16 B operand
+#pragma unroll
+    for (int c = 0; c < KG; ++c) {
+      const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), b1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const int n = nb * 16 + 4 * g + t;
-        float v = hd[r][nb][t] + bb[t];
-        if (n < D) {
-          if (MODE == FWD_PREDICT) {
-            if (ok) a.mean[((int64_t)e * a.B + row) * D + n] = v;
-          } else if (selected) {
-            a.mean_sel[row * D + n] = v;
-          }
-        } else if (n < 2 * D) {
-          const int d = n - D;
-          const float mx = w.maxlv[d], mn = w.minlv[d];
-          float lv = mx - softplusf(mx - v);  // bnn.py:669
-          lv = mn + softplusf(lv - mn);       // bnn.py:670
-          const float var = expf(lv);         // bnn.py:675
-          if (MODE == FWD_PREDICT) {
-            if (ok) a.var[((int64_t)e * a.B + row) * D + d] = var;
-          } else {
-            const float sd = sqrtf(var);      // fake_env.py:67
-            ss += sd * sd;
-            if (selected) a.std_sel[row * D + d] = sd;
-          }
-        }
+        hin[c][t] = to_bf16(swishf(acc[2 * c][t] + b0[t]));
+        hin[c][4 + t] = to_bf16(swishf(acc[2 * c + 1][t] + b1[t]));
       }
     }
-    if (MODE == FWD_ROLLOUT) {
-      ss += __shfl_xor(ss, 16);
-      ss += __shfl_xor(ss, 32);
-      if (g == 0 && ok) atomicMax(a.pen_bits + row, __float_as_uint(sqrtf(ss)));  // >= 0: uint order
-    }
+  };
+  layer_lds_bf16<1, NB2, WAVES, SLOT>(w.w0b + (int64_t)e * NB2 * 256, x0, acc, lds, wv, lane);
+  to_input(w.b0 + e * bs);
+  for (int l = 0; l < 3; ++l) {
+    layer_lds_bf16<KG, NB2, WAVES, SLOT>(w.whb + ((int64_t)l * w.E + e) * KG * NB2 * 256, hin, acc, lds, wv, lane);
+    to_input(w.bh + ((int64_t)l * w.E + e) * bs);
   }
+  f32x4 hd[NBO];
+  layer_lds_bf16<KG, NBO, WAVES, SLOT>(w.whdb + (int64_t)e * KG * NBO * 256, hin, hd, lds, wv, lane);
+  head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g);
 }
 
 constexpr int FWD_WAVES = 4;
@@ -187,8 +263,39 @@ static int launch_fwd_h(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s)
               std::to_string(h->H) + ")");
 }
 
+template <int NB2, int NBO>
+static int launch_bf16_t(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
+  a.ntiles = (int)ceil_div((int)a.B, 16);
+  if (a.ntiles == 0) return 0;
+  dim3 grid(ceil_div(a.ntiles, FWD_WAVES) * h->E), block(64 * FWD_WAVES);
+  if (mode == FWD_PREDICT)
+    hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_PREDICT, FWD_WAVES>), grid, block, 0, s, h->dev, a);
+  else
+    hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_ROLLOUT, FWD_WAVES>), grid, block, 0, s, h->dev, a);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+static int launch_bf16(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) {
+  if (h->dev.IN > 32) return fail("bnn bf16: obs_dim + act_dim must be <= 32");
+  if (h->dev.NBO == 3) {
+    switch (h->dev.NB2) {
+      case 2: return launch_bf16_t<2, 3>(h, mode, a, s);
+      case 4: return launch_bf16_t<4, 3>(h, mode, a, s);
+      case 14: return launch_bf16_t<14, 3>(h, mode, a, s);
+      case 26: return launch_bf16_t<26, 3>(h, mode, a, s);
+    }
+  } else if (h->dev.NBO == 2) {
+    switch (h->dev.NB2) {
+      case 14: return launch_bf16_t<14, 2>(h, mode, a, s);
+    }
+  }
+  return fail("bnn bf16: unsupported hidden/output size");
+}
+
 int launch_bnn_fwd(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) {
   if (!h->has_params) return fail("bnn: parameters not set (mopo_bnn_set_params)");
+  if (h->dtype == 1) return launch_bf16(h, mode, a, s);
   if (h->dev.KG0 != 2) return fail("bnn: obs_dim + act_dim must be in (16, 32]");
   switch (h->dev.NBO) {
     case 3: return launch_fwd_h<2, 3>(h, mode, a, s);
@@ -215,6 +322,8 @@ extern "C" int mopo_bnn_create(mopo_bnn_t* out, int E, int obs_dim, int act_dim,
   d.KG0 = ceil_div(d.IN, 16);
   d.NBH = ceil_div(hidden, 16);
   d.NBO = ceil_div(2 * d.D, 16);
+  d.NB2 = (d.NBH + 1) / 2 * 2;
+  d.BS = d.NB2 * 16;
   *out = reinterpret_cast<mopo_bnn_t>(h);
   return 0;
 }
@@ -235,7 +344,7 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
   BnnDev& d = h->dev;
   const int E = h->E, IN = d.IN, H = h->H, D = d.D;
   const int KG0 = d.KG0, NBH = d.NBH, NBO = d.NBO;
-  const int64_t hp = NBH * 16;
+  const int64_t hp = d.BS;  // bias stride (covers the bf16 path's even block count)
   // sizes (floats) of the packed regions
   const int64_t s_w0 = (int64_t)E * KG0 * NBH * 256, s_wh = 3LL * E * NBH * NBH * 256,
                 s_whd = (int64_t)E * NBH * NBO * 256, s_b0 = E * hp, s_bh = 3 * E * hp,
@@ -297,6 +406,29 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
   }
   rc |= pack(head.data(), head.size(), whd, H, 2 * D, NBH, NBO);
   rc |= packb(headb.data(), bhd, 2 * D, NBO * 16);
+  if (h->dtype == 1 && rc == 0) {
+    // bf16 fragments: [E][1][NB2] | [3][E][KG][NB2] | [E][KG][NBO], 256 floats (= 512 bf16) each
+    const int NB2 = d.NB2, KG = NB2 / 2;
+    const int64_t f0 = (int64_t)E * NB2, fh = 3LL * E * KG * NB2, fd = (int64_t)E * KG * NBO;
+    if (!h->bbuf) MOPO_HIP(hipMalloc(&h->bbuf, (f0 + fh + fd) * 256 * sizeof(float)));
+    float* b0f = reinterpret_cast<float*>(h->bbuf);
+    float* bhf = b0f + f0 * 256;
+    float* bdf = bhf + fh * 256;
+    auto packh = [&](const float* src, size_t nsrc, float* dst, int K, int N, int KGb, int NB) -> int {
+      MOPO_HIP(hipMemcpy(stage, src, nsrc * sizeof(float), hipMemcpyHostToDevice));
+      int64_t tot = (int64_t)E * KGb * NB * 512;
+      int blocks = (int)std::min<int64_t>((tot + 255) / 256, 4096);
+      hipLaunchKernelGGL(pack_frags_bf16_kernel, dim3(blocks), dim3(256), 0, 0, stage, (short*)dst, E, K, N, KGb, NB);
+      MOPO_HIP(hipGetLastError());
+      MOPO_HIP(hipDeviceSynchronize());
+      return 0;
+    };
+    rc |= packh(W[0], (size_t)E * IN * H, b0f, IN, H, 1, NB2);
+    for (int l = 0; l < 3; ++l)
+      rc |= packh(W[1 + l], (size_t)E * H * H, bhf + (int64_t)l * E * KG * NB2 * 256, H, H, KG, NB2);
+    rc |= packh(head.data(), head.size(), bdf, H, 2 * D, KG, NBO);
+    d.w0b = b0f; d.whb = bhf; d.whdb = bdf;
+  }
   (void)hipFree(stage);
   if (rc) return -1;
   MOPO_HIP(hipMemcpy(mu, arrs[0], IN * sizeof(float), hipMemcpyHostToDevice));

@@ -25,10 +25,13 @@ struct BnnDev {
   const float* sigma; // [IN]
   const float* maxlv; // [D]
   const float* minlv; // [D]
-  // bf16 copies (dtype 1); same fragment order with 8 bf16 per lane per 32-deep k-group
-  const uint16_t* w0b;
-  const uint16_t* whb;
-  const uint16_t* whdb;
+  int BS;             // per-member bias stride (floats): even(NBH) * 16
+  // bf16 fragments (dtype 1): 1 KiB = 64 lanes x 8 bf16 per (32-deep k-group, 16-wide block),
+  // addressed in float units like the f32 fragments; hidden width padded to NB2 = even(NBH)
+  int NB2;
+  const float* w0b;   // [E][1][NB2]
+  const float* whb;   // [3][E][NB2/2][NB2]
+  const float* whdb;  // [E][NB2/2][NBO]
 };
 
 struct Bnn {

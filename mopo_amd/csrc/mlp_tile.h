@@ -54,4 +54,40 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f3
   }
 }
 
+// ---- bf16 variant (v_mfma_f32_16x16x32_bf16, f32 accumulate) --------------------------------
+// A k-group is 32 deep; lane (row m, group g) supplies 8 bf16 of its row.  The k order inside a
+// group is permuted so the B operand comes straight from the previous layer's two accumulator
+// blocks 2c, 2c+1 (feature 16*nb + 4g + r held by lane (m, g) in register r):
+//   element j of lane group g  <->  feature 32c + (j < 4 ? 4g + j : 16 + 4g + (j - 4)).
+// The weight fragments are packed with the same permutation (pack_frags_bf16_kernel).
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x4 mfma_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__host__ __device__ __forceinline__ int bf16_kperm(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
+
+__device__ __forceinline__ short to_bf16(float x) { return __builtin_bit_cast(short, (__bf16)x); }
+
+template <int KG, int NB, int WAVES, int SLOT>
+__device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, const bf16x8 (&in)[KG], f32x4 (&acc)[NB],
+                                               float* lds, int w, int lane) {
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = zero4();
+  __syncthreads();
+  stage_slice<NB, WAVES>(wf, lds, w, lane);
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) {
+    __syncthreads();
+    if (kg + 1 < KG) stage_slice<NB, WAVES>(wf + (kg + 1) * NB * 256, lds + ((kg + 1) & 1) * SLOT, w, lane);
+    const float* b = lds + (kg & 1) * SLOT;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const bf16x8 fr = *reinterpret_cast<const bf16x8*>(b + (nb * 64 + lane) * 4);
+      acc[nb] = mfma_bf16(fr, in[kg], acc[nb]);
+    }
+  }
+}
+
 }  // namespace mopo
