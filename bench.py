@@ -28,6 +28,7 @@ O, A, E, ELITES, H, HP = 17, 6, 7, 5, 200, 256
 ENV_ROWS = 101000
 FLOP_BNN_ROW = 2 * E * ((O + A) * H + 3 * H * H + 2 * H * (O + 1))       # 1,845,200
 FLOP_ACTOR_ROW = 2 * (O * HP + HP * HP + HP * 2 * A)                      # 145,920
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01_v2_pmc_summary.json')
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
 
 
@@ -141,6 +142,9 @@ def cpu_baseline(args):
                       '%d transitions in %.2f s' % (B, args.horizon, E, H, trans, dt)}
 
 
+SAC_DIAG = {}
+
+
 def sac_leg(args, pool, env, dev, world):
     """SAC grad-steps/s: args.sac_steps x (_training_batch + _do_training + _update_target), graph replay."""
     import torch
@@ -158,6 +162,7 @@ def sac_leg(args, pool, env, dev, world):
         torch.distributed.barrier()
     t0 = time.perf_counter()
     sac._do_training(50, env_pool, pool, n_steps=args.sac_steps, seed=5)
+    t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -168,6 +173,7 @@ def sac_leg(args, pool, env, dev, world):
         dt = float(t.item())
     lg = sac.logs()
     assert all(np.isfinite(v) for v in lg.values()), lg
+    SAC_DIAG['enqueue_us_per_step'] = t_enq / args.sac_steps * 1e6
     return args.sac_steps / dt
 
 
@@ -239,6 +245,7 @@ def main():
     kernel_ms = {k: ms[i] / max(nl[i], 1) for i, k in enumerate(['start', 'actor', 'ensemble_fwd', 'fakeenv_post',
                                                                   'compact', 'advance'])}
     value = total / dt
+    traffic = pmc_traffic(args)
     out = {
         'metric': 'model-rollout transitions/s (halfcheetah-mixed)',
         'value': value, 'unit': 'transitions/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
@@ -250,12 +257,15 @@ def main():
                    'rollout_batch_per_gpu': args.batch, 'horizon': args.horizon, 'parallelism': 'dp%d' % world},
         'roofline': {'bound': 'mfma', 'kernel': 'bnn_fwd_kernel (ensemble forward, f32 MFMA 16x16x4)',
                      'achieved': achieved, 'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                     'frac': achieved / MFMA_F32_PEAK_TFLOPS, 'traffic': None,
+                     'frac': achieved / MFMA_F32_PEAK_TFLOPS, 'traffic': traffic,
+                     'traffic_note': 'HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction, '
+                                     'MI355X_MICROARCH.md HBM) from the committed --pmc passes, '
+                                     'profiles/r01_v2_pmc_summary.json (same workload)',
                      'flop_per_launch': rows_per_launch * FLOP_BNN_ROW, 'avg_launch_ms': bnn_ms},
         'kernel_ms_avg': kernel_ms,
         'sac': {'metric': 'SAC grad-steps/s (batch 256 = 12 env + 244 model rows, mopo.py:801-850)',
                 'per_gpu': sac_rate, 'aggregate_replicas': sac_rate * world, 'steps_timed': args.sac_steps,
-                'us_per_step': 1e6 / sac_rate, 'parallelism': 'replicas only (one independent learner per GPU)'},
+                'us_per_step': 1e6 / sac_rate, **SAC_DIAG, 'parallelism': 'replicas only (one independent learner per GPU)'},
     }
     if not args.no_cpu_baseline and world == 1:
         out['cpu_baseline'] = cpu_baseline(args)
@@ -263,6 +273,17 @@ def main():
     print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def pmc_traffic(args):
+    """HBM bytes per bnn_fwd launch from the committed PMC summary (scripts/pmc.sh, default workload)."""
+    if (args.batch, args.horizon) != (50000, 5) or not os.path.exists(PMC_SUMMARY):
+        return None
+    ks = json.load(open(PMC_SUMMARY))['kernels']
+    for k, v in ks.items():
+        if k.startswith('mopo::bnn_fwd_kernel') and 'hbm_bytes' in v:
+            return v['hbm_bytes']
+    return None
 
 
 from ctypes import c_double as C_double, c_int64 as C_int64  # noqa: E402

@@ -35,21 +35,116 @@ struct GemmProb {
   // when a_u != NULL:  A(i,k) = a_u[i] * a_v[k] * (a_m[i*a_ldm + k] > 0);  same for B with (k, j)
   const float* a_u; const float* a_v; const float* a_m; int a_ldm;
   const float* b_u; const float* b_v; const float* b_m; int b_ldm;
+  int adam;                          // C (and colsum) are gradient slices of AdamCtx::G: apply Adam
+  // two-segment plain B (operand mode 3): columns [0, split) from B, [split, N) from B2 (same ldb),
+  // bias likewise from bias / bias2 -- the policy output layer [W_mean | W_log_std]
+  const float* B2; int split; const float* bias2;
+  int head;                          // 1: pi(s), 2: pi(s'): squashed-Gaussian head epilogue (HeadCtx)
+};
+
+// ---- squashed Gaussian head, forward (mopo.py:282-308, 286-296) for one batch row of pi(s) or
+// pi(s'): action = tanh(mu + eps * exp(clip(log_std))) into the row's action slot, its log-prob
+// (with the tanh correction) and the noise used.  eps is Philox(seed, step counter, row) unless
+// injected (parity mode).
+struct HeadCtx {
+  int O, A;
+  const float* eps_in[2];            // injected noise or NULL
+  float* eps_out[2];
+  float* x[2];                       // [n][O + A] rows whose action part receives tanh(u)
+  float* logp[2];
+  uint64_t seed;
+  const int64_t* iter;
+};
+
+__device__ __forceinline__ void head_fwd_row(const HeadCtx& hc, int nxt, int r, const float* hm, const float* hl) {
+  const int A = hc.A;
+  float z[8];
+  const float* ein = hc.eps_in[nxt];
+  if (ein) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = j < A ? ein[r * A + j] : 0.f;
+  } else {
+    const int64_t it = *hc.iter;
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      u32x4 c{(uint32_t)r | ((uint32_t)nxt << 31), (uint32_t)it ^ ((uint32_t)blk << 24), (uint32_t)((uint64_t)it >> 32),
+              RNG_SAC + 16};
+      u32x4 q = philox(c, (uint32_t)hc.seed, (uint32_t)(hc.seed >> 32));
+      box_muller(q.x, q.y, z[4 * blk], z[4 * blk + 1]);
+      box_muller(q.z, q.w, z[4 * blk + 2], z[4 * blk + 3]);
+    }
+  }
+  float logp = 0.f, corr = 0.f;
+  float* x = hc.x[nxt] + r * (hc.O + A) + hc.O;
+  float* eo = hc.eps_out[nxt] + r * A;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (j >= A) break;
+    const float mu = hm[j];
+    const float ls = fminf(fmaxf(hl[j], -20.f), 2.f);
+    const float sd = expf(ls);
+    const float u = mu + z[j] * sd;
+    const float zz = (u - mu) / (sd + 1e-8f);
+    logp += -0.5f * (zz * zz + 2.f * ls + 1.8378770664093453f);
+    corr += 2.f * (0.6931471805599453f - u - softplusf(-2.f * u));
+    x[j] = tanhf(u);
+    eo[j] = z[j];
+  }
+  hc.logp[nxt][r] = logp - corr;
+}
+
+// Fused optimizer (the four TF1 Adams + Polyak, mopo.py:407-447): a weight-gradient tile is final
+// when its epilogue runs (K spans the whole batch), so the epilogue updates the parameters it
+// covers right there.  Parameters are double-buffered (read Pc, write Pn) because the same launch
+// and later backward launches still read the pre-step weights; M, V and T are updated in place
+// (each element is touched by exactly one tile, and T is only read by earlier forward stages).
+struct AdamCtx {
+  const float* G; const float* Pc; float* Pn; float* M; float* V; float* T;
+  const float* lr_t;                 // this step's step size (sac_loss_kernel)
+  float tau; int64_t total, n_pi, n_q; // grad-norm logs: [0, n_pi) policy, [n_pi, n_pi + n_q) Q1
+  float* norm_part;                  // [slot][2] squared-gradient partials (pi, q) per block
+  int slot0;                         // this launch's first slot
 };
 
 struct GemmGroup {
   int n;
   int prefix[MAXP + 1];
+  AdamCtx ad;
+  HeadCtx hd;
   GemmProb p[MAXP];
 };
+
+struct AdamIn { float p, m, v, t; };
+
+__device__ __forceinline__ AdamIn adam_load(const AdamCtx& ad, int64_t i) {
+  return AdamIn{ad.Pc[i], ad.M[i], ad.V[i], ad.T[i]};
+}
+
+// TF1 Adam (m += (g - m)(1 - b1), v += (g^2 - v)(1 - b2), p -= lr_t m / (sqrt(v) + eps)) + Polyak
+__device__ __forceinline__ void adam_apply(const AdamCtx& ad, int64_t i, float g, AdamIn a, float lr_t) {
+  const float m = a.m + (g - a.m) * (1.f - 0.9f);
+  const float v = a.v + (g * g - a.v) * (1.f - 0.999f);
+  const float p = a.p - (m * lr_t) / (sqrtf(v) + 1e-8f);
+  ad.M[i] = m;
+  ad.V[i] = v;
+  ad.Pn[i] = p;
+  if (i < ad.total) ad.T[i] = (1.f - ad.tau) * a.t + ad.tau * p;   // mopo.py:446-447 (after the updates)
+}
 
 
 constexpr int GKC = 256;  // K chunk staged in LDS
 
 // One 16-wide panel (A: rows i0..i0+15, or B: cols j0..j0+15) x K-chunk, staged as S[k][r].
-// MODE 0: plain, 1: transposed, 2: rank-1 masked (see GemmProb).  Addresses are clamped so every
-// load is valid and unconditional; out-of-range elements are zeroed by a select afterwards.
+// MODE 0: plain, 1: transposed, 2: rank-1 masked (see GemmProb).  Loads are raw buffer loads through
+// a descriptor sized to the operand's extent: a 32-bit byte offset per element (no 64-bit address
+// pairs) and hardware range checking (reads past the extent return 0), so every load is issued
+// unconditionally; elements outside the tile or the K chunk are zeroed by a select at the store.
 struct PanelRegs { float x[16], u[16], w[16]; };
+
+// Panels are S[k][r ^ psw(k)]: 64 4-byte banks, a 16-float row puts k and k+4 on the same banks, so
+// without the XOR the k-fast stores (64 consecutive k per wave) hit 4 banks 16 ways.  With it the
+// k-fast and r-fast stores and the MFMA operand reads (16 r x 4 k per instruction) are conflict-free.
+__device__ __forceinline__ int psw(int k) { return (k >> 2) & 15; }
 
 template <int MODE, bool IS_A>
 __device__ __forceinline__ void panel_rk(int q, int tid, int& r, int& k) {
@@ -58,36 +153,81 @@ __device__ __forceinline__ void panel_rk(int q, int tid, int& r, int& k) {
   else { k = (tid & 63) + 64 * (q & 3); r = (tid >> 6) + 4 * (q >> 2); }
 }
 
+// buffer descriptor over n floats at p (wave-uniform inputs only)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)(n * 4), 0x00020000);
+}
+
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t d, int idx) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(d, idx * 4, 0, 0));
+}
+
 template <int MODE, bool IS_A>
 __device__ __forceinline__ void load_panel(const GemmProb& p, int r0, int kc, int tid, PanelRegs& R) {
-  const int Rmax = IS_A ? p.M : p.N;
+  const int Rn = IS_A ? p.M : p.N;  // panel axis extent
+  if (MODE == 2) {
+    const int ldm = IS_A ? p.a_ldm : p.b_ldm;
+    // A(i,k) = u[i] v[k] (m[i,k] > 0);  B(k,j) = u[k] v[j] (m[k,j] > 0).  The A panel is k-fast
+    // (element q: row 4(q>>2) + tid>>6, column 64(q&3) + (tid&63)), so it needs only 4 u and 4 v
+    // values per thread; the B panel is r-fast (column tid&15, row 16q + tid>>4): 16 u, 1 v.
+    const auto dm = IS_A ? rsrc(p.a_m, (int64_t)(Rn - 1) * ldm + p.K) : rsrc(p.b_m, (int64_t)(p.K - 1) * ldm + Rn);
+    const auto du = IS_A ? rsrc(p.a_u, Rn) : rsrc(p.b_u, p.K);
+    const auto dv = IS_A ? rsrc(p.a_v, p.K) : rsrc(p.b_v, Rn);
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    int r, k;
-    panel_rk<MODE, IS_A>(q, tid, r, k);
-    const int rc = min(r0 + r, Rmax - 1), kk = min(kc + k, p.K - 1);
-    if (MODE == 2) {
-      const float* m = IS_A ? p.a_m : p.b_m;
-      const int ldm = IS_A ? p.a_ldm : p.b_ldm;
-      R.u[q] = IS_A ? p.a_u[rc] : p.b_u[kk];
-      R.w[q] = IS_A ? p.a_v[kk] : p.b_v[rc];
-      R.x[q] = IS_A ? m[(int64_t)rc * ldm + kk] : m[(int64_t)kk * ldm + rc];
-    } else if (IS_A) {
-      R.x[q] = MODE == 0 ? p.A[(int64_t)rc * p.lda + kk] : p.A[(int64_t)kk * p.lda + rc];
-    } else {
-      R.x[q] = MODE == 0 ? p.B[(int64_t)kk * p.ldb + rc] : p.B[(int64_t)rc * p.ldb + kk];
+    for (int q = 0; q < 16; ++q) {
+      int r, k;
+      panel_rk<MODE, IS_A>(q, tid, r, k);
+      const int gr = r0 + r, gk = kc + k;
+      if (IS_A) {
+        if ((q & 3) == 0) R.u[q >> 2] = bload(du, gr);
+        if (q < 4) R.w[q] = bload(dv, gk);
+      } else {
+        R.u[q] = bload(du, gk);
+        if (q == 0) R.w[0] = bload(dv, gr);
+      }
+      R.x[q] = bload(dm, IS_A ? gr * ldm + gk : gk * ldm + gr);
+    }
+  } else if (MODE == 3) {
+    // two-segment B: per-lane segment select, so flat loads with clamped addresses
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      int r, k;
+      panel_rk<MODE, IS_A>(q, tid, r, k);
+      const int gr = min(r0 + r, Rn - 1), gk = min(kc + k, p.K - 1);
+      const float* src = gr < p.split ? p.B + gr : p.B2 + (gr - p.split);
+      R.x[q] = src[(int64_t)gk * p.ldb];
+    }
+  } else {
+    const float* base = IS_A ? p.A : p.B;
+    const int ld = IS_A ? p.lda : p.ldb;
+    // element (r, k) of the panel's operand lives at r*ld + k (row-major in r) or k*ld + r
+    constexpr bool r_major = IS_A ? (MODE == 0) : (MODE == 1);
+    const auto d = r_major ? rsrc(base, (int64_t)(Rn - 1) * ld + p.K) : rsrc(base, (int64_t)(p.K - 1) * ld + Rn);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      int r, k;
+      panel_rk<MODE, IS_A>(q, tid, r, k);
+      const int gr = r0 + r, gk = kc + k;
+      R.x[q] = bload(d, r_major ? gr * ld + gk : gk * ld + gr);
     }
   }
 }
 
-// pin the loads as unconditional (else hipcc sinks each into a branch followed by vmcnt(0))
-template <int MODE>
+// keep the loads batched ahead of the first use
+template <int MODE, bool IS_A>
 __device__ __forceinline__ void pin_panel(PanelRegs& R) {
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     asm volatile("" : "+v"(R.x[q]));
-    if (MODE == 2) asm volatile("" : "+v"(R.u[q]), "+v"(R.w[q]));
+    if (MODE == 2 && (IS_A ? q < 4 : true)) asm volatile("" : "+v"(R.u[q]));
+    if (MODE == 2 && (IS_A ? q < 4 : q == 0)) asm volatile("" : "+v"(R.w[q]));
   }
+}
+
+// element q of a rank-1 panel: u * v (the A panel indexes u by q>>2 and v by q&3, see load_panel)
+template <bool IS_A>
+__device__ __forceinline__ float rank1_uv(const PanelRegs& R, int q) {
+  return IS_A ? R.u[q >> 2] * R.w[q & 3] : R.u[q] * R.w[0];
 }
 
 template <int MODE, bool IS_A>
@@ -98,9 +238,15 @@ __device__ __forceinline__ void store_panel(const GemmProb& p, int r0, int kn, i
   for (int q = 0; q < 16; ++q) {
     int r, k;
     panel_rk<MODE, IS_A>(q, tid, r, k);
-    const float v = MODE == 2 ? (R.x[q] > 0.f ? R.u[q] * R.w[q] : 0.f) : R.x[q];
-    S[k][r] = (r0 + r < Rmax && k < kn) ? v : 0.f;
+    const float v = MODE == 2 ? (R.x[q] > 0.f ? rank1_uv<IS_A>(R, q) : 0.f) : R.x[q];
+    S[k][r ^ psw(k)] = (r0 + r < Rmax && k < kn) ? v : 0.f;
   }
+}
+
+// operand modes (A: 0 plain, 1 transposed, 2 rank-1; B: the same, 3 two-segment) as am * 4 + bm
+__host__ __device__ __forceinline__ int operand_modes(const GemmProb& p) {
+  const int am = p.a_u ? 2 : p.ta, bm = p.b_u ? 2 : p.B2 ? 3 : p.tb;
+  return am * 4 + bm;
 }
 
 template <int AM, int BM>
@@ -109,8 +255,8 @@ __device__ __forceinline__ void stage_ab(const GemmProb& p, int i0, int j0, int 
   PanelRegs ra, rb;
   load_panel<AM, true>(p, i0, kc, tid, ra);
   load_panel<BM, false>(p, j0, kc, tid, rb);
-  pin_panel<AM>(ra);
-  pin_panel<BM>(rb);
+  pin_panel<AM, true>(ra);
+  pin_panel<BM, false>(rb);
   store_panel<AM, true>(p, i0, kn, tid, ra, As);
   store_panel<BM, false>(p, j0, kn, tid, rb, Bs);
 }
@@ -119,11 +265,12 @@ __device__ __forceinline__ void stage_ab(const GemmProb& p, int i0, int j0, int 
 // LDS with loads ordered along each operand's contiguous axis (all issued before the first use:
 // one memory latency per chunk), then the four waves split K and run v_mfma_f32_16x16x4_f32 out
 // of LDS; partial tiles are summed through LDS and the epilogue fuses bias / relu / relu'-mask.
-__global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
+__global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGroup g) {
   __shared__ float As[GKC][16];
   __shared__ float Bs[GKC][16];
   __shared__ float part[4][256];
   __shared__ float csum[16][17];
+  __shared__ float hv[16][17];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int pi = 0;
   while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
@@ -138,39 +285,49 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
   const int ei = tid >> 4, ej = tid & 15;
   const int gi = i0 + ei, gj = j0 + ej;
   const int gic = min(gi, p.M - 1), gjc = min(gj, p.N - 1);
-  float e_bias = p.bias ? p.bias[gjc] : 0.f;
+  float e_bias = p.bias ? (p.bias2 && gjc >= p.split ? p.bias2[gjc - p.split] : p.bias[gjc]) : 0.f;
   float e_mask = p.mask ? p.mask[(int64_t)gic * p.ldm + gjc] : 1.f;
   asm volatile("" : "+v"(e_bias), "+v"(e_mask));
+  const AdamCtx& ad = g.ad;
+  const int64_t a_idx = p.adam ? (int64_t)(p.C - ad.G) + (int64_t)gic * p.ldc + gjc : 0;
+  const int64_t c_idx = p.adam && p.colsum ? (int64_t)(p.colsum - ad.G) + min(j0 + (tid & 15), p.N - 1) : 0;
+  AdamIn a_in{0.f, 0.f, 0.f, 0.f}, c_in{0.f, 0.f, 0.f, 0.f};
+  float lr_t = 0.f;
+  if (p.adam) {
+    a_in = adam_load(ad, a_idx);
+    if (p.colsum && tm == 0 && tid < 16) c_in = adam_load(ad, c_idx);
+    lr_t = *ad.lr_t;
+    asm volatile("" : "+v"(a_in.p), "+v"(a_in.m), "+v"(a_in.v), "+v"(a_in.t));
+  }
   f32x4 acc0 = zero4(), acc1 = zero4();
   float cs = 0.f;
   for (int kc = 0; kc < p.K; kc += GKC) {
     const int kn = min(GKC, p.K - kc);
-    const int kpad = (kn + 3) & ~3;
+    // re-derive the thread index inside the chunk loop: otherwise the ~100 per-thread LDS and
+    // buffer offsets are hoisted out of it and stay live across the loop (VGPRs -> occupancy)
+    int t = tid;
+    asm volatile("" : "+v"(t));
     // 16 elements of each panel per thread; the per-operand mode is dispatched once (uniform
-    // branch) so that all 32+ loads are unconditional (clamped addresses, select after the load)
-    // and issue back to back -- one memory latency per chunk instead of one per element.
-    const int am = p.a_u ? 2 : p.ta, bm = p.b_u ? 2 : p.tb;
-    switch (am * 3 + bm) {
-      case 0: stage_ab<0, 0>(p, i0, j0, kc, kn, tid, As, Bs); break;
-      case 1: stage_ab<0, 1>(p, i0, j0, kc, kn, tid, As, Bs); break;
-      case 2: stage_ab<0, 2>(p, i0, j0, kc, kn, tid, As, Bs); break;
-      case 3: stage_ab<1, 0>(p, i0, j0, kc, kn, tid, As, Bs); break;
-      case 4: stage_ab<1, 1>(p, i0, j0, kc, kn, tid, As, Bs); break;
-      case 5: stage_ab<1, 2>(p, i0, j0, kc, kn, tid, As, Bs); break;
-      case 6: stage_ab<2, 0>(p, i0, j0, kc, kn, tid, As, Bs); break;
-      case 7: stage_ab<2, 1>(p, i0, j0, kc, kn, tid, As, Bs); break;
-      default: stage_ab<2, 2>(p, i0, j0, kc, kn, tid, As, Bs); break;
+    // branch) so that all 32+ loads are unconditional and issue back to back -- one memory latency
+    // per chunk instead of one per element.
+    switch (operand_modes(p)) {  // the combinations sac_step_impl uses (launch_group rejects others)
+      case 0: stage_ab<0, 0>(p, i0, j0, kc, kn, t, As, Bs); break;
+      case 1: stage_ab<0, 1>(p, i0, j0, kc, kn, t, As, Bs); break;
+      case 3: stage_ab<0, 3>(p, i0, j0, kc, kn, t, As, Bs); break;
+      case 4: stage_ab<1, 0>(p, i0, j0, kc, kn, t, As, Bs); break;
+      case 6: stage_ab<1, 2>(p, i0, j0, kc, kn, t, As, Bs); break;
+      default: stage_ab<2, 1>(p, i0, j0, kc, kn, t, As, Bs); break;
     }
     __syncthreads();
-    (void)kpad;
     // the staged panels are zero-padded to GKC rows, so every wave runs exactly 16 k-steps of its
     // quarter with no guards: all 32 LDS reads first, then 16 MFMAs on two accumulators
     float ra[16], rb[16];
+    const int tli = t & 15, tlk = (t >> 4) & 3, tw = t >> 6;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const int k = 4 * (w * 16 + s) + lk;
-      ra[s] = As[k][li];
-      rb[s] = Bs[k][li];
+      const int k = 4 * (tw * 16 + s) + tlk;
+      ra[s] = As[k][tli ^ psw(k)];
+      rb[s] = Bs[k][tli ^ psw(k)];
     }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
@@ -178,13 +335,14 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
       else acc0 = mfma4(ra[s], rb[s], acc0);
     }
     if (do_cs)
-      for (int k = tid >> 4; k < kn; k += 16) cs += Bs[k][tid & 15];
+      for (int k = tid >> 4; k < kn; k += 16) cs += Bs[k][(tid & 15) ^ psw(k)];
     __syncthreads();
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[w][(lk * 4 + r) * 16 + li] = acc0[r] + acc1[r];  // D: col li, row 4*lk+r
   if (do_cs) csum[tid >> 4][tid & 15] = cs;
   __syncthreads();
+  float gsq = 0.f;
   {
     float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
     if (gi < p.M && gj < p.N) {
@@ -192,12 +350,41 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GemmGroup g) {
       if (p.relu) v = fmaxf(v, 0.f);
       if (!(e_mask > 0.f)) v = 0.f;
       p.C[(int64_t)gi * p.ldc + gj] = v;
+      if (p.head) hv[ei][ej] = v;
+      if (p.adam) {
+        adam_apply(ad, a_idx, v, a_in, lr_t);
+        gsq = v * v;
+      }
     }
   }
   if (do_cs && tid < 16) {
     float c = 0.f;
     for (int q = 0; q < 16; ++q) c += csum[q][tid];
-    if (j0 + tid < p.N) p.colsum[j0 + tid] = c;
+    if (j0 + tid < p.N) {
+      p.colsum[j0 + tid] = c;
+      if (p.adam) {
+        adam_apply(ad, c_idx, c, c_in, lr_t);
+        gsq += c * c;
+      }
+    }
+  }
+  if (p.head) {  // the tile holds all 2A head outputs of its 16 rows: one thread per row
+    __syncthreads();
+    if (tid < 16 && i0 + tid < p.M) head_fwd_row(g.hd, p.head - 1, i0 + tid, &hv[tid][0], &hv[tid][g.hd.A]);
+  }
+  if (ad.norm_part) {  // per-block squared-gradient partial (grad-norm logs; summed by sac_logs_kernel)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) gsq += __shfl_xor(gsq, off);
+    __syncthreads();
+    if (lane == 0) part[0][w] = gsq;
+    __syncthreads();
+    if (tid == 0) {
+      const float b = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+      const int64_t off = p.adam ? (int64_t)(p.C - ad.G) : -1;
+      float* np = ad.norm_part + 2 * (int64_t)(ad.slot0 + blockIdx.x);
+      np[0] = off >= 0 && off < ad.n_pi ? b : 0.f;
+      np[1] = off >= ad.n_pi && off < ad.n_pi + ad.n_q ? b : 0.f;
+    }
   }
 }
 
@@ -229,7 +416,12 @@ static Offs make_offs(int O, int A, int H) {
 
 enum {
   LOG_Q1_LOSS = 0, LOG_Q2_LOSS, LOG_Q1, LOG_Q2, LOG_ALPHA, LOG_ENTROPY, LOG_LOGP, LOG_PI_GNORM, LOG_Q_GNORM,
-  LOG_PI_LOSS, LOG_N = 16
+  LOG_PI_LOSS, LOG_PI_GSQ, LOG_Q_GSQ, LOG_N = 16
+};
+
+struct Batch {
+  float *sa, *xpi, *xn, *rew, *term;  // [s, a], [s, pi(s)], [s', pi(s')], r, done
+  int64_t* idx;                       // [n] sampled rows
 };
 
 struct Sac {
@@ -238,30 +430,25 @@ struct Sac {
   float lr, gamma, tau, rscale, tent;
   void* mem = nullptr;
   float *P, *G, *M, *V, *T;       // [total + 1]: last element = log_alpha
-  float* beta_pow;                // [2] f32 beta1_power, beta2_power (TF1 non-slot vars)
+  float* Pb[2];                   // parameter ping-pong: Pb[0] == P is the canonical copy between calls
+  float* norm_part = nullptr;     // [nslots][2]
+  float* loss_part = nullptr;     // [ceil(n / QL_ROWS)][8] sac_qloss_kernel block partials
+  unsigned* ticket = nullptr;     // its last-block ticket
+  int nslots = 0;
+  float* beta_pow;                // [3] f32 beta1_power, beta2_power (TF1 non-slot vars), this step's lr_t
   int64_t* iter;                  // device step counter (Philox)
-  unsigned* ticket;               // last-block ticket of the Adam kernel
   float* logs;                    // [LOG_N]
-  float* norm_part;               // [nblk][2]
-  int adam_blocks = 0;
   // activations
-  float *sa, *xpi, *xn, *rew, *term;
+  Batch bt[2];                    // double-buffered batch (step parity)
   float *h1[8], *h2[8], *out[8];  // 0 pi(s) 1 pi(s') 2 Q1(s,a) 3 Q2(s,a) 4 Q1(s,pi) 5 Q2(s,pi) 6 Qt1 7 Qt2
   float *logp_s, *logp_n, *eps_s, *eps_n;
   float *dq[4];                   // dq for instances 2,3,4,5
-  float *dh2[4], *dh1[4];
+  float *dh1[4];
   float *dx1, *dx2, *dhead, *dh2p, *dh1p;
-  int64_t* idx;                   // [n] sampled rows
-  // device arrays of pointers for the multi-instance element-wise kernels
-  float** outp_dev;               // [8] out[]
-  float** dq_dev;                 // [4]
-  float** w3_dev;                 // [4] main W3 of Q1, Q2, Q1, Q2
-  float** h2q_dev;                // [4] h2[2..5]
-  float** dh2_dev;                // [4]
   // graph
   bool use_graph = true;
-  hipGraphExec_t gexec = nullptr;
-  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
+  hipGraph_t graph[3] = {nullptr, nullptr, nullptr};
   mopo_pool_desc genv{}, gmod{};
   hipStream_t gstream = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
@@ -269,97 +456,61 @@ struct Sac {
 };
 
 // ---- batch gather (_training_batch, mopo.py:801-821): rows [0, n_env) from the env pool, rest
-// from the model pool; each index uniform over the pool's live size (Philox) unless injected
-// One block per GR rows: phase 1 draws the GR source rows, phase 2 copies their fields with
-// consecutive threads on consecutive columns (all loads independent -> one memory latency).
-constexpr int GR = 16;
-__global__ __launch_bounds__(256) void sac_gather_kernel(const mopo_pool_desc env, const mopo_pool_desc mod, int n,
-                                                         int n_env, int O, int A, const int64_t* idx_in,
-                                                         int64_t* idx_out, uint64_t seed, const int64_t* iter,
-                                                         float* sa, float* xpi, float* xn, float* rew, float* term) {
-  __shared__ int64_t src_s[GR];
-  const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * GR;
-  if (tid < GR && r0 + tid < n) {
-    const int r = r0 + tid;
-    int64_t src;
-    if (idx_in) {
-      src = idx_in[r];
-    } else {
-      const uint64_t size = (uint64_t)(r < n_env ? env.d_state[1] : mod.d_state[1]);
-      const int64_t it = *iter;
-      u32x4 c{(uint32_t)r, (uint32_t)it, (uint32_t)((uint64_t)it >> 32), RNG_SAC};
-      u32x4 q = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-      src = (int64_t)(((uint64_t)q.x * size) >> 32);
-    }
-    src_s[tid] = src;
-    idx_out[r] = src;
+// from the model pool; each index uniform over the pool's live size (Philox) unless injected.
+// One thread per (row, field column): every thread derives its row's source index itself (the
+// Philox draw is cheap), so the kernel is two dependent memory latencies (pool size + counter,
+// then the field) with no barrier.
+constexpr int GATHER_TPB = 256;
+struct GatherArgs {
+  mopo_pool_desc env, mod;
+  int n_env, O, A;
+  const int64_t* idx_in;             // injected rows or NULL (Philox draw)
+  uint64_t seed;
+  const int64_t* iter;
+  Batch out;
+};
+
+// field c of batch row r (obs | act | next_obs | rew | term)
+__device__ __forceinline__ void gather_elem(const GatherArgs& g, int r, int c) {
+  const int O = g.O, A = g.A, W = O + A;
+  const bool fe = r < g.n_env;
+  const mopo_pool_desc& p = fe ? g.env : g.mod;
+  int64_t src;
+  if (g.idx_in) {
+    src = g.idx_in[r];
+  } else {
+    const uint64_t size = (uint64_t)p.d_state[1];
+    const int64_t it = *g.iter;
+    u32x4 cc{(uint32_t)r, (uint32_t)it, (uint32_t)((uint64_t)it >> 32), RNG_SAC};
+    u32x4 q = philox(cc, (uint32_t)g.seed, (uint32_t)(g.seed >> 32));
+    src = (int64_t)(((uint64_t)q.x * size) >> 32);
   }
-  __syncthreads();
-  const int W = O + A, C = 2 * O + A + 2;  // obs | act | next_obs | rew | term
-  for (int e = tid; e < GR * C; e += 256) {
-    const int rr = e / C, c = e % C, r = r0 + rr;
-    if (r >= n) continue;
-    const bool fe = r < n_env;
-    const int64_t src = src_s[rr];
-    if (c < O) {
-      const float v = (fe ? env.d_obs : mod.d_obs)[src * O + c];
-      sa[r * W + c] = v;
-      xpi[r * W + c] = v;
-    } else if (c < O + A) {
-      sa[r * W + c] = (fe ? env.d_act : mod.d_act)[src * A + (c - O)];
-    } else if (c < 2 * O + A) {
-      xn[r * W + (c - O - A)] = (fe ? env.d_next_obs : mod.d_next_obs)[src * O + (c - O - A)];
-    } else if (c == 2 * O + A) {
-      rew[r] = (fe ? env.d_rew : mod.d_rew)[src];
-    } else {
-      term[r] = (float)(fe ? env.d_term : mod.d_term)[src];
-    }
+  const Batch& b = g.out;
+  if (c == 0) b.idx[r] = src;
+  if (c < O) {
+    const float v = p.d_obs[src * O + c];
+    b.sa[r * W + c] = v;
+    b.xpi[r * W + c] = v;
+  } else if (c < O + A) {
+    b.sa[r * W + c] = p.d_act[src * A + (c - O)];
+  } else if (c < 2 * O + A) {
+    b.xn[r * W + (c - O - A)] = p.d_next_obs[src * O + (c - O - A)];
+  } else if (c == 2 * O + A) {
+    b.rew[r] = p.d_rew[src];
+  } else {
+    b.term[r] = (float)p.d_term[src];
   }
+}
+
+__global__ __launch_bounds__(GATHER_TPB) void sac_gather_kernel(const GatherArgs g, int n) {
+  const int C = 2 * g.O + g.A + 2;
+  const int e = blockIdx.x * GATHER_TPB + threadIdx.x;
+  if (e >= n * C) return;
+  const int r = e / C;
+  gather_elem(g, r, e - r * C);
 }
 
 __device__ __forceinline__ float softplus_f(float x) { return softplusf(x); }
-
-// ---- squashed Gaussian head, forward (mopo.py:282-308, 286-296) for pi(s) and pi(s')
-__global__ void pi_head_fwd_kernel(int n, int O, int A, const float* head_s, const float* head_n, const float* eps_in_s,
-                                   const float* eps_in_n, float* eps_s, float* eps_n, uint64_t seed,
-                                   const int64_t* iter, float* xpi, float* xn, float* logp_s, float* logp_n) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * n) return;
-  const bool nxt = t >= n;
-  const int r = nxt ? t - n : t;
-  const float* hd = (nxt ? head_n : head_s) + r * 2 * A;
-  const float* ein = nxt ? eps_in_n : eps_in_s;
-  float* eo = (nxt ? eps_n : eps_s) + r * A;
-  float z[8];
-  if (ein) {
-    for (int j = 0; j < A; ++j) z[j] = ein[r * A + j];
-  } else {
-    for (int blk = 0; blk * 4 < A; ++blk) {
-      u32x4 c{(uint32_t)r | ((uint32_t)nxt << 31), (uint32_t)(*iter) ^ ((uint32_t)blk << 24),
-              (uint32_t)((uint64_t)(*iter) >> 32), RNG_SAC + 16};
-      u32x4 q = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-      float zz[4];
-      box_muller(q.x, q.y, zz[0], zz[1]);
-      box_muller(q.z, q.w, zz[2], zz[3]);
-      for (int i = 0; i < 4 && blk * 4 + i < A; ++i) z[blk * 4 + i] = zz[i];
-    }
-  }
-  float logp = 0.f, corr = 0.f;
-  float* x = (nxt ? xn : xpi) + r * (O + A) + O;
-  for (int j = 0; j < A; ++j) {
-    const float mu = hd[j];
-    const float ls = fminf(fmaxf(hd[A + j], -20.f), 2.f);
-    const float sd = expf(ls);
-    const float u = mu + z[j] * sd;
-    const float zz = (u - mu) / (sd + 1e-8f);
-    logp += -0.5f * (zz * zz + 2.f * ls + 1.8378770664093453f);
-    corr += 2.f * (0.6931471805599453f - u - softplus_f(-2.f * u));
-    x[j] = tanhf(u);
-    eo[j] = z[j];
-  }
-  (nxt ? logp_n : logp_s)[r] = logp - corr;
-}
 
 // Deterministic block-wide sums of NV values at once: butterfly within each wave (__shfl_xor),
 // then the per-wave partials added in wave order.  Two barriers for all NV sums.
@@ -390,65 +541,158 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   return a[0];
 }
 
-// ---- losses, output gradients, alpha gradient, logs (single block, one thread per row)
-__global__ __launch_bounds__(1024) void sac_loss_kernel(int n, int A, float gamma, float rscale, float tent,
-                                                        float* const* outs, const float* logp_s, const float* logp_n,
-                                                        const float* rew, const float* term, const float* head_s,
-                                                        const float* log_alpha, float* dq1, float* dq2, float* dq1p,
-                                                        float* dq2p, float* g_alpha, float* logs) {
-  __shared__ float sh[1024];
-  const int r = threadIdx.x;
-  const bool ok = r < n;
-  const float alpha = expf(*log_alpha);                             // mopo.py:361
-  float q1 = 0, q2 = 0, q1p = 0, q2p = 0, lps = 0, ent = 0, y = 0;
-  if (ok) {
-    q1 = outs[2][r]; q2 = outs[3][r]; q1p = outs[4][r]; q2p = outs[5][r];
-    const float qt = fminf(outs[6][r], outs[7][r]);                 // mopo.py:368
-    y = rscale * rew[r] + gamma * ((1.f - term[r]) * (qt - alpha * logp_n[r]));  // mopo.py:380-386
-    lps = logp_s[r];
-    const float inv_n = 1.f / (float)n;
-    dq1[r] = (q1 - y) * inv_n;                                      // d(0.5 mean (q-y)^2)
-    dq2[r] = (q2 - y) * inv_n;
-    const bool sel1 = q1p <= q2p;                                   // tf.minimum grad -> x where x <= y
-    dq1p[r] = sel1 ? -inv_n : 0.f;
-    dq2p[r] = sel1 ? 0.f : -inv_n;
-    for (int j = 0; j < A; ++j) {                                   // pi_entropy (mopo.py:341)
-      const float ls = fminf(fmaxf(head_s[r * 2 * A + A + j], -20.f), 2.f);
-      ent += logf(expf(ls) + 1e-8f) + 0.5f * logf(2.f * 3.14159265358979f * 2.718281828459045f);
+// ---- critic output layers of Q1/Q2(s, pi(s)) and the targets Qt1/Qt2(s', pi(s')), fused with the
+// losses, output gradients, alpha gradient and logs (mopo.py:361-404).
+// Block = 16 batch rows; wave w computes instance 4 + w (q = h2 . w3 + b3, 4 lanes per row, K split
+// in 64-wide quarters); then one thread per row forms y, the row-local output gradients and its
+// share of the seven batch means.  Block partials are reduced by the last block to arrive (agent-
+// scope release -> ticket -> acquire, in block order: deterministic), which also applies the alpha
+// Adam, fixes this step's lr_t for the fused optimizer epilogues and advances the TF1 beta powers
+// and the step counter (nothing later in the step reads it).
+constexpr int QL_ROWS = 16;
+struct QLossArgs {
+  int n, H, A;
+  float gamma, rscale, tent, lr;
+  const float* h2[4];               // instances Q1(s,pi) Q2(s,pi) Qt1(s',pi') Qt2(s',pi')
+  const float* w3[4];
+  const float* b3[4];
+  float* q[4];                      // outputs (out[4..7])
+  const float* q1; const float* q2; // Q1/Q2(s, a) from the forward output stage
+  const float* logp_s; const float* logp_n; const float* rew; const float* term; const float* head_s;
+  const float* log_alpha;
+  float* dq1; float* dq2; float* dq1p; float* dq2p; float* g_alpha;
+  float* logs; float* beta_pow; int64_t* iter;
+  float* part;                      // [blocks][8]
+  unsigned* ticket;
+  AdamCtx ad;
+};
+
+__global__ __launch_bounds__(256) void sac_qloss_kernel(const QLossArgs a) {
+  __shared__ float qs[4][QL_ROWS];
+  __shared__ float red_s[8];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r0 = blockIdx.x * QL_ROWS;
+  // the loss inputs of this block's rows (wave 0, one lane per row) and the alpha Adam state are
+  // fetched first, so their latency hides under the output-layer dot products
+  const int lr_row = min(r0 + lane, a.n - 1);
+  float in_q1 = 0.f, in_q2 = 0.f, in_rew = 0.f, in_term = 0.f, in_lps = 0.f, in_lpn = 0.f, lsr[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lsr[j] = 0.f;
+  if (w == 0 && lane < QL_ROWS) {
+    in_q1 = a.q1[lr_row]; in_q2 = a.q2[lr_row]; in_rew = a.rew[lr_row]; in_term = a.term[lr_row];
+    in_lps = a.logp_s[lr_row]; in_lpn = a.logp_n[lr_row];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lsr[j] = j < a.A ? a.head_s[lr_row * 2 * a.A + a.A + j] : 0.f;
+  }
+  const float alpha = expf(*a.log_alpha);                           // mopo.py:361
+  AdamIn al_in{0.f, 0.f, 0.f, 0.f};
+  if (tid == 0) al_in = adam_load(a.ad, a.ad.total);
+  {
+    const int rr = lane >> 2, part = lane & 3, r = r0 + rr;
+    const int rc = min(r, a.n - 1);
+    const int KQ = a.H / 4;         // H % 16 == 0 (checked at create)
+    const f32x4* hp = reinterpret_cast<const f32x4*>(a.h2[w] + (int64_t)rc * a.H + part * KQ);
+    const float* wp = a.w3[w] + part * KQ;  // Q2's W3 sits at an odd offset of the flat vector
+    float acc = 0.f;
+#pragma unroll 16
+    for (int k = 0; k < KQ / 4; ++k) {  // unrolled: the 16 row / weight loads of H = 256 issue together
+      const f32x4 x = hp[k];
+      acc += x[0] * wp[4 * k] + x[1] * wp[4 * k + 1] + x[2] * wp[4 * k + 2] + x[3] * wp[4 * k + 3];
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    const float qv = acc + *a.b3[w];
+    if (part == 0) {
+      qs[w][rr] = qv;
+      if (r < a.n) a.q[w][r] = qv;
     }
   }
-  const float fn = (float)n;
-  float red[7] = {ok ? (q1 - y) * (q1 - y) : 0.f, ok ? (q2 - y) * (q2 - y) : 0.f, q1, q2, lps, ent,
-                  ok ? alpha * lps - fminf(q1p, q2p) : 0.f};
-  block_sums<7>(red, sh);
-  const float l1 = red[0] / fn * 0.5f, l2 = red[1] / fn * 0.5f;           // mopo.py:403-404
-  const float m1 = red[2] / fn, m2 = red[3] / fn, mlp = red[4] / fn, ment = red[5] / fn;
-  const float pil = red[6] / fn;                                          // mopo.py:371-377
-  if (r == 0) {
-    *g_alpha = -(mlp + tent);                                       // d/dlog_alpha of -mean(la*(logp+H))
+  __syncthreads();
+  if (w == 0) {
+    const int r = r0 + lane;
+    const bool ok = lane < QL_ROWS && r < a.n;
+    float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ok) {
+      const float q1 = in_q1, q2 = in_q2, q1p = qs[0][lane], q2p = qs[1][lane];
+      const float qt = fminf(qs[2][lane], qs[3][lane]);            // mopo.py:368
+      const float y = a.rscale * in_rew + a.gamma * ((1.f - in_term) * (qt - alpha * in_lpn));  // :380-386
+      const float lps = in_lps;
+      const float inv_n = 1.f / (float)a.n;
+      a.dq1[r] = (q1 - y) * inv_n;                                  // d(0.5 mean (q-y)^2)
+      a.dq2[r] = (q2 - y) * inv_n;
+      const bool sel1 = q1p <= q2p;                                 // tf.minimum grad -> x where x <= y
+      a.dq1p[r] = sel1 ? -inv_n : 0.f;
+      a.dq2p[r] = sel1 ? 0.f : -inv_n;
+      float ent = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {                                 // pi_entropy (mopo.py:341)
+        if (j >= a.A) break;
+        const float ls = fminf(fmaxf(lsr[j], -20.f), 2.f);
+        ent += logf(expf(ls) + 1e-8f) + 0.5f * logf(2.f * 3.14159265358979f * 2.718281828459045f);
+      }
+      red[0] = (q1 - y) * (q1 - y); red[1] = (q2 - y) * (q2 - y); red[2] = q1; red[3] = q2;
+      red[4] = lps; red[5] = ent; red[6] = alpha * lps - fminf(q1p, q2p);
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) red[i] += __shfl_xor(red[i], off);
+    if (lane == 0) {
+      float* pp = a.part + 8 * (int64_t)blockIdx.x;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) pp[i] = red[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (t == gridDim.x - 1);
+      if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  // after the acquire, plain loads see every block's partials; one load per thread, all in flight
+  // together, then the sums in block order (deterministic)
+  __shared__ float pall[8 * 64];
+  for (int i = tid; i < 8 * (int)gridDim.x; i += 256) pall[i] = a.part[i];
+  __syncthreads();
+  if (tid < 7) {
+    float acc = 0.f;
+    for (int b = 0; b < (int)gridDim.x; ++b) acc += pall[8 * b + tid];
+    red_s[tid] = acc;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float fn = (float)a.n;
+    const float l1 = red_s[0] / fn * 0.5f, l2 = red_s[1] / fn * 0.5f; // mopo.py:403-404
+    const float m1 = red_s[2] / fn, m2 = red_s[3] / fn, mlp = red_s[4] / fn, ment = red_s[5] / fn;
+    const float pil = red_s[6] / fn;                                // mopo.py:371-377
+    const float ga = -(mlp + a.tent);                               // d/dlog_alpha of -mean(la*(logp+H))
+    *a.g_alpha = ga;
+    float* logs = a.logs;
     logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;
     logs[LOG_ALPHA] = alpha; logs[LOG_ENTROPY] = ment; logs[LOG_LOGP] = mlp; logs[LOG_PI_LOSS] = pil;
+    const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
+    const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+    a.beta_pow[2] = lr_t;
+    a.beta_pow[0] = b1p * 0.9f;
+    a.beta_pow[1] = b2p * 0.999f;
+    *a.iter += 1;
+    adam_apply(a.ad, a.ad.total, ga, al_in, lr_t);
+    *a.ticket = 0u;                                                 // stream order: next launch sees 0
   }
 }
 
-// ---- dh2 = dq (x) W3 * (h2 > 0) for the 4 critic instances (rank-1 output layer backward)
-__global__ void q_out_bwd_kernel(int n, int H, const float* const* dq, const float* const* W3, const float* const* h2,
-                                 float* const* dh2) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int inst = blockIdx.y;
-  if (t >= (int64_t)n * H) return;
-  const int r = t / H, j = t % H;
-  const float h = h2[inst][t];
-  dh2[inst][t] = h > 0.f ? dq[inst][r] * W3[inst][j] : 0.f;
-}
-
-// ---- squashed Gaussian head backward + dh2 of the policy trunk (one block per batch row)
+// ---- squashed Gaussian head backward + dh2 of the policy trunk (one block per batch row).
+// With `prefetch`, the block's second wave also gathers row r of the NEXT step's batch (the step
+// counter was advanced by this step's loss kernel), taking the gather off the step's critical path.
 __global__ __launch_bounds__(256) void pi_head_bwd_kernel(int n, int O, int A, int H, const float* head_s,
                                                           const float* eps_s, const float* dx1, const float* dx2,
                                                           const float* log_alpha, const float* Wm, const float* Wl,
-                                                          const float* h2p, float* dhead, float* dh2p) {
+                                                          const float* h2p, float* dhead, float* dh2p,
+                                                          const GatherArgs next, int prefetch) {
   __shared__ float dmu_s[8], dls_s[8];
   const int r = blockIdx.x, tid = threadIdx.x;
+  if (prefetch && tid >= 64 && tid < 64 + 2 * O + A + 2) gather_elem(next, r, tid - 64);
   if (tid < A) {
     const int j = tid;
     const float g = expf(*log_alpha) / (float)n;                    // d L_pi / d logp (stop_gradient(alpha))
@@ -475,70 +719,37 @@ __global__ __launch_bounds__(256) void pi_head_bwd_kernel(int n, int O, int A, i
   }
   __syncthreads();
   for (int j = tid; j < H; j += blockDim.x) {
+    float wm[8], wl[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      wm[k] = k < A ? Wm[j * A + k] : 0.f;
+      wl[k] = k < A ? Wl[j * A + k] : 0.f;
+    }
+    const float hv = h2p[(int64_t)r * H + j];
     float v = 0.f;
-    for (int k = 0; k < A; ++k) v += dmu_s[k] * Wm[j * A + k] + dls_s[k] * Wl[j * A + k];
-    dh2p[(int64_t)r * H + j] = h2p[(int64_t)r * H + j] > 0.f ? v : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < A) v += dmu_s[k] * wm[k] + dls_s[k] * wl[k];
+    dh2p[(int64_t)r * H + j] = hv > 0.f ? v : 0.f;
   }
 }
 
-// ---- four TF1 Adams (identical step counts -> one lr_t) + Polyak, and grad-norm partials
-__global__ __launch_bounds__(256) void sac_adam_kernel(int64_t total, int64_t n_pi, int64_t n_q, float* P, const float* G,
-                                                       float* Mm, float* Vv, float* T, float* beta_pow, float lr,
-                                                       float tau, float* norm_part, unsigned* ticket, float* logs,
-                                                       int64_t* iter) {
-  __shared__ float sh[256];
-  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
-  const float lr_t = lr * sqrtf(1.f - beta_pow[1]) / (1.f - beta_pow[0]);
-  float npi = 0.f, nq = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= total; i += (int64_t)gridDim.x * blockDim.x) {
-    const float g = G[i];
-    if (i < n_pi) npi += g * g;
-    else if (i < n_pi + n_q) nq += g * g;
-    float m = Mm[i], v = Vv[i];
-    m += (g - m) * (1.f - b1);
-    v += (g * g - v) * (1.f - b2);
-    Mm[i] = m;
-    Vv[i] = v;
-    const float p = P[i] - (m * lr_t) / (sqrtf(v) + eps);
-    P[i] = p;
-    if (i < total) T[i] = (1.f - tau) * T[i] + tau * p;             // mopo.py:446-447 (after the updates)
-  }
-  float nn[2] = {npi, nq};
-  block_sums<2>(nn, sh);
-  // publish this block's partial norms; the last-arriving block reduces them in block order
-  // (agent-scope release -> relaxed ticket -> acquire; cdna_hip_programming.md §6 Guideline 16)
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    norm_part[blockIdx.x * 2] = nn[0];
-    norm_part[blockIdx.x * 2 + 1] = nn[1];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == gridDim.x - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
+// grad-norm logs of the last step (once per mopo_sac_step call): the per-block partials of the
+// fused optimizer epilogues, plus the alpha gradient (counted with neither network)
+__global__ __launch_bounds__(256) void sac_logs_kernel(const float* norm_part, int nslots, float* logs) {
+  __shared__ float sh[64];
   float a = 0.f, b = 0.f;
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {
-    a += __hip_atomic_load(norm_part + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    b += __hip_atomic_load(norm_part + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = threadIdx.x; i < nslots; i += blockDim.x) {
+    a += norm_part[2 * i];
+    b += norm_part[2 * i + 1];
   }
   float ab[2] = {a, b};
   block_sums<2>(ab, sh);
   if (threadIdx.x == 0) {
     logs[LOG_PI_GNORM] = sqrtf(ab[0]);
-    logs[LOG_Q_GNORM] = 0.5f * sqrtf(ab[1]);                          // grads of Q_loss = (l1+l2)/2 wrt q1
-    beta_pow[0] *= 0.9f;                                              // TF1 beta power updates (f32)
-    beta_pow[1] *= 0.999f;
-    *iter += 1;
-    *ticket = 0u;                                                     // stream order: next launch sees 0
+    logs[LOG_Q_GNORM] = 0.5f * sqrtf(ab[1]);                        // grads of Q_loss = (l1+l2)/2 wrt q1
   }
 }
-
 
 // ---------------------------------------------------------------------------------------------
 static GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C,
@@ -548,42 +759,78 @@ static GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, const f
   return p;
 }
 
-static int launch_group(std::vector<GemmProb> ps, hipStream_t s) {
+static int launch_group(std::vector<GemmProb> ps, hipStream_t s, const AdamCtx* ad = nullptr, int* slot = nullptr,
+                        const HeadCtx* hd = nullptr) {
   GemmGroup g{};
   g.n = (int)ps.size();
   if (g.n > MAXP) return fail("sac: gemm group too large");
   int tot = 0;
   for (int i = 0; i < g.n; ++i) {
+    const GemmProb& q = ps[i];
+    const int c = operand_modes(q);
+    if (!(c == 0 || c == 1 || c == 3 || c == 4 || c == 6 || c == 9)) return fail("sac: unsupported gemm operand modes");
+    if ((int64_t)q.M * q.K >= (1ll << 29) || (int64_t)q.N * q.K >= (1ll << 29)) return fail("sac: gemm operand too large");
     g.p[i] = ps[i];
     g.prefix[i] = tot;
     tot += ceil_div(ps[i].M, 16) * ceil_div(ps[i].N, 16);
   }
   g.prefix[g.n] = tot;
+  if (ad) {
+    g.ad = *ad;
+    g.ad.slot0 = *slot;
+    *slot += tot;
+  }
+  if (hd) g.hd = *hd;
+  for (int i = 0; i < g.n; ++i)
+    if (g.p[i].head && (!hd || g.p[i].N > 16 || g.p[i].N != 2 * hd->A)) return fail("sac: bad head problem");
   hipLaunchKernelGGL(gemm_group_kernel, dim3(tot), dim3(256), 0, s, g);
   MOPO_HIP(hipGetLastError());
   return 0;
 }
 
-static int sac_step_impl(Sac* h, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
-                         const int64_t* idx_in, const float* eps_in_s, const float* eps_in_n, hipStream_t s) {
+static GatherArgs gather_args(Sac* h, int par, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
+                              const int64_t* idx_in) {
+  GatherArgs g{};
+  g.env = *env; g.mod = *mod; g.n_env = h->d.n_env; g.O = h->d.O; g.A = h->d.A;
+  g.idx_in = idx_in; g.seed = seed; g.iter = h->iter; g.out = h->bt[par];
+  return g;
+}
+
+static int launch_gather(Sac* h, int par, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
+                         const int64_t* idx_in, hipStream_t s) {
+  const SacDims& d = h->d;
+  hipLaunchKernelGGL(sac_gather_kernel, dim3(ceil_div(d.n * (2 * d.O + d.A + 2), GATHER_TPB)), dim3(GATHER_TPB), 0, s,
+                     gather_args(h, par, env, mod, seed, idx_in), d.n);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+// One SAC step on batch bt[par], reading parameters Pb[par] and writing the updated ones to
+// Pb[1 - par].  With `prefetch`, the policy-head backward kernel also gathers the next step's batch
+// into bt[1 - par] (a separate gather launch, or a forked graph branch, costs more than it hides).
+static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
+                         const float* eps_in_s, const float* eps_in_n, hipStream_t s, bool prefetch) {
   const SacDims& d = h->d;
   const Offs& o = h->o;
   const int n = d.n, O = d.O, A = d.A, H = d.H, W = O + A;
-  const float* P = h->P;
+  const float* P = h->Pb[par];
+  AdamCtx ad{};
+  ad.G = h->G; ad.Pc = h->Pb[par]; ad.Pn = h->Pb[1 - par]; ad.M = h->M; ad.V = h->V; ad.T = h->T;
+  ad.lr_t = h->beta_pow + 2; ad.tau = h->tau; ad.total = o.total; ad.n_pi = o.n_pi; ad.n_q = o.n_q;
+  ad.norm_part = h->norm_part;
+  int slot = 0;
   const float* T = h->T;
   float* G = h->G;
-  hipLaunchKernelGGL(sac_gather_kernel, dim3(ceil_div(n, GR)), dim3(256), 0, s, *env, *mod, n, d.n_env, O, A, idx_in,
-                     h->idx, seed, h->iter, h->sa, h->xpi, h->xn, h->rew, h->term);
-  MOPO_HIP(hipGetLastError());
+  const Batch& bt = h->bt[par];
   auto Wq = [&](int qi, int k) { return P + o.q[qi][k]; };
   auto Tq = [&](int qi, int k) { return T + o.q[qi][k]; };
   // ---- forward stage 1-3: pi(s), pi(s'), Q1(s,a), Q2(s,a)
   {
     std::vector<GemmProb> g;
-    auto a = mk(n, H, O, h->sa, W, 0, P + o.pW1, H, 0, h->h1[0], H); a.bias = P + o.pb1; a.relu = 1; g.push_back(a);
-    auto b = mk(n, H, O, h->xn, W, 0, P + o.pW1, H, 0, h->h1[1], H); b.bias = P + o.pb1; b.relu = 1; g.push_back(b);
+    auto a = mk(n, H, O, bt.sa, W, 0, P + o.pW1, H, 0, h->h1[0], H); a.bias = P + o.pb1; a.relu = 1; g.push_back(a);
+    auto b = mk(n, H, O, bt.xn, W, 0, P + o.pW1, H, 0, h->h1[1], H); b.bias = P + o.pb1; b.relu = 1; g.push_back(b);
     for (int qi = 0; qi < 2; ++qi) {
-      auto c = mk(n, H, W, h->sa, W, 0, Wq(qi, 0), H, 0, h->h1[2 + qi], H); c.bias = Wq(qi, 1); c.relu = 1; g.push_back(c);
+      auto c = mk(n, H, W, bt.sa, W, 0, Wq(qi, 0), H, 0, h->h1[2 + qi], H); c.bias = Wq(qi, 1); c.relu = 1; g.push_back(c);
     }
     if (launch_group(g, s)) return -1;
   }
@@ -597,26 +844,30 @@ static int sac_step_impl(Sac* h, const mopo_pool_desc* env, const mopo_pool_desc
     if (launch_group(g, s)) return -1;
   }
   {
+    // output layers: policy [mean | log_std] (one 2A-wide tile per 16 rows, whose epilogue runs the
+    // squashed-Gaussian head), Q1/Q2(s, a)
     std::vector<GemmProb> g;
     for (int i = 0; i < 2; ++i) {
-      auto m = mk(n, A, H, h->h2[i], H, 0, P + o.pWm, A, 0, h->out[i], 2 * A); m.bias = P + o.pbm; g.push_back(m);
-      auto l = mk(n, A, H, h->h2[i], H, 0, P + o.pWl, A, 0, h->out[i] + A, 2 * A); l.bias = P + o.pbl; g.push_back(l);
+      auto m = mk(n, 2 * A, H, h->h2[i], H, 0, P + o.pWm, A, 0, h->out[i], 2 * A);
+      m.B2 = P + o.pWl; m.split = A; m.bias = P + o.pbm; m.bias2 = P + o.pbl; m.head = 1 + i;
+      g.push_back(m);
     }
     for (int qi = 0; qi < 2; ++qi) {
       auto q = mk(n, 1, H, h->h2[2 + qi], H, 0, Wq(qi, 4), 1, 0, h->out[2 + qi], 1); q.bias = Wq(qi, 5); g.push_back(q);
     }
-    if (launch_group(g, s)) return -1;
+    HeadCtx hc{};
+    hc.O = O; hc.A = A; hc.eps_in[0] = eps_in_s; hc.eps_in[1] = eps_in_n; hc.eps_out[0] = h->eps_s;
+    hc.eps_out[1] = h->eps_n; hc.x[0] = bt.xpi; hc.x[1] = bt.xn; hc.logp[0] = h->logp_s; hc.logp[1] = h->logp_n;
+    hc.seed = seed; hc.iter = h->iter;
+    if (launch_group(g, s, nullptr, nullptr, &hc)) return -1;
   }
-  hipLaunchKernelGGL(pi_head_fwd_kernel, dim3(ceil_div(2 * n, 256)), dim3(256), 0, s, n, O, A, h->out[0], h->out[1],
-                     eps_in_s, eps_in_n, h->eps_s, h->eps_n, seed, h->iter, h->xpi, h->xn, h->logp_s, h->logp_n);
-  MOPO_HIP(hipGetLastError());
   // ---- forward stage 4-6: Q1/Q2(s, pi(s)) with main params, Qt1/Qt2(s', pi(s')) with target params
   {
     std::vector<GemmProb> g;
     for (int i = 0; i < 4; ++i) {
       const int qi = i & 1;
       const bool tgt = i >= 2;
-      const float* x = tgt ? h->xn : h->xpi;
+      const float* x = tgt ? bt.xn : bt.xpi;
       auto a = mk(n, H, W, x, W, 0, tgt ? Tq(qi, 0) : Wq(qi, 0), H, 0, h->h1[4 + i], H);
       a.bias = tgt ? Tq(qi, 1) : Wq(qi, 1); a.relu = 1; g.push_back(a);
     }
@@ -632,21 +883,27 @@ static int sac_step_impl(Sac* h, const mopo_pool_desc* env, const mopo_pool_desc
     }
     if (launch_group(g, s)) return -1;
   }
+  // ---- critic output layers (s, pi) / targets + losses (one launch)
   {
-    std::vector<GemmProb> g;
+    QLossArgs q{};
+    q.n = n; q.H = H; q.A = A; q.gamma = h->gamma; q.rscale = h->rscale; q.tent = h->tent; q.lr = h->lr;
     for (int i = 0; i < 4; ++i) {
       const int qi = i & 1;
       const bool tgt = i >= 2;
-      auto a = mk(n, 1, H, h->h2[4 + i], H, 0, tgt ? Tq(qi, 4) : Wq(qi, 4), 1, 0, h->out[4 + i], 1);
-      a.bias = tgt ? Tq(qi, 5) : Wq(qi, 5); g.push_back(a);
+      q.h2[i] = h->h2[4 + i];
+      q.w3[i] = tgt ? Tq(qi, 4) : Wq(qi, 4);
+      q.b3[i] = tgt ? Tq(qi, 5) : Wq(qi, 5);
+      q.q[i] = h->out[4 + i];
     }
-    if (launch_group(g, s)) return -1;
+    q.q1 = h->out[2]; q.q2 = h->out[3];
+    q.logp_s = h->logp_s; q.logp_n = h->logp_n; q.rew = bt.rew; q.term = bt.term; q.head_s = h->out[0];
+    q.log_alpha = P + o.total;
+    q.dq1 = h->dq[0]; q.dq2 = h->dq[1]; q.dq1p = h->dq[2]; q.dq2p = h->dq[3]; q.g_alpha = G + o.total;
+    q.logs = h->logs; q.beta_pow = h->beta_pow; q.iter = h->iter; q.part = h->loss_part; q.ticket = h->ticket;
+    q.ad = ad;
+    hipLaunchKernelGGL(sac_qloss_kernel, dim3(ceil_div(n, QL_ROWS)), dim3(256), 0, s, q);
+    MOPO_HIP(hipGetLastError());
   }
-  // ---- losses
-  hipLaunchKernelGGL(sac_loss_kernel, dim3(1), dim3(ceil_div(n, 64) * 64), 0, s, n, A, h->gamma, h->rscale, h->tent, h->outp_dev,
-                     h->logp_s, h->logp_n, h->rew, h->term, h->out[0], P + o.total, h->dq[0], h->dq[1], h->dq[2],
-                     h->dq[3], G + o.total, h->logs);
-  MOPO_HIP(hipGetLastError());
   // ---- critic backward.  The 1-wide output layer's backward dh2 = dq (x) W3 * (h2 > 0) is rank-1,
   // so it is never materialised: the consumers below read it as a rank-1 masked operand.
   {
@@ -657,47 +914,59 @@ static int sac_step_impl(Sac* h, const mopo_pool_desc* env, const mopo_pool_desc
       a.a_u = h->dq[i]; a.a_v = Wq(qi, 4); a.a_m = h->h2[2 + i]; a.a_ldm = H;
       g.push_back(a);
     }
+    if (launch_group(g, s, &ad, &slot)) return -1;
+  }
+  {
+    // dW2 / dW3 only need the rank-1 dh2 (not dh1), so they ride with the smaller second launch
+    std::vector<GemmProb> g;
     for (int qi = 0; qi < 2; ++qi) {  // dW2 = h1^T dh2 (+db2), dW3 = h2^T dq (+db3)
       auto w2 = mk(H, H, n, h->h1[2 + qi], H, 1, nullptr, H, 0, G + o.q[qi][2], H); w2.colsum = G + o.q[qi][3];
+      w2.adam = 1;
       w2.b_u = h->dq[qi]; w2.b_v = Wq(qi, 4); w2.b_m = h->h2[2 + qi]; w2.b_ldm = H;
       g.push_back(w2);
       auto w3 = mk(H, 1, n, h->h2[2 + qi], H, 1, h->dq[qi], 1, 0, G + o.q[qi][4], 1); w3.colsum = G + o.q[qi][5];
+      w3.adam = 1;
       g.push_back(w3);
     }
-    if (launch_group(g, s)) return -1;
-  }
-  {
-    std::vector<GemmProb> g;
     g.push_back(mk(n, W, H, h->dh1[2], H, 0, Wq(0, 0), H, 1, h->dx1, W));   // d/dx of Q1(s, pi)
     g.push_back(mk(n, W, H, h->dh1[3], H, 0, Wq(1, 0), H, 1, h->dx2, W));   // d/dx of Q2(s, pi)
     for (int qi = 0; qi < 2; ++qi) {  // dW1 = [s,a]^T dh1 (+db1)
-      auto w1 = mk(W, H, n, h->sa, W, 1, h->dh1[qi], H, 0, G + o.q[qi][0], H); w1.colsum = G + o.q[qi][1];
+      auto w1 = mk(W, H, n, bt.sa, W, 1, h->dh1[qi], H, 0, G + o.q[qi][0], H); w1.colsum = G + o.q[qi][1];
+      w1.adam = 1;
       g.push_back(w1);
     }
-    if (launch_group(g, s)) return -1;
+    if (launch_group(g, s, &ad, &slot)) return -1;
   }
   // ---- policy backward
   hipLaunchKernelGGL(pi_head_bwd_kernel, dim3(n), dim3(256), 0, s, n, O, A, H, h->out[0], h->eps_s, h->dx1, h->dx2,
-                     P + o.total, P + o.pWm, P + o.pWl, h->h2[0], h->dhead, h->dh2p);
+                     P + o.total, P + o.pWm, P + o.pWl, h->h2[0], h->dhead, h->dh2p,
+                     gather_args(h, 1 - par, env, mod, seed, nullptr), prefetch ? 1 : 0);
   MOPO_HIP(hipGetLastError());
   {
     std::vector<GemmProb> g;
     auto a = mk(n, H, H, h->dh2p, H, 0, P + o.pW2, H, 1, h->dh1p, H); a.mask = h->h1[0]; a.ldm = H; g.push_back(a);
-    auto w2 = mk(H, H, n, h->h1[0], H, 1, h->dh2p, H, 0, G + o.pW2, H); w2.colsum = G + o.pb2; g.push_back(w2);
-    auto wm = mk(H, A, n, h->h2[0], H, 1, h->dhead, 2 * A, 0, G + o.pWm, A); wm.colsum = G + o.pbm; g.push_back(wm);
-    auto wl = mk(H, A, n, h->h2[0], H, 1, h->dhead + A, 2 * A, 0, G + o.pWl, A); wl.colsum = G + o.pbl; g.push_back(wl);
-    if (launch_group(g, s)) return -1;
+    auto w2 = mk(H, H, n, h->h1[0], H, 1, h->dh2p, H, 0, G + o.pW2, H); w2.colsum = G + o.pb2; w2.adam = 1; g.push_back(w2);
+    auto wm = mk(H, A, n, h->h2[0], H, 1, h->dhead, 2 * A, 0, G + o.pWm, A); wm.colsum = G + o.pbm; wm.adam = 1;
+    g.push_back(wm);
+    auto wl = mk(H, A, n, h->h2[0], H, 1, h->dhead + A, 2 * A, 0, G + o.pWl, A); wl.colsum = G + o.pbl; wl.adam = 1;
+    g.push_back(wl);
+    if (launch_group(g, s, &ad, &slot)) return -1;
   }
   {
     std::vector<GemmProb> g;
-    auto w1 = mk(O, H, n, h->sa, W, 1, h->dh1p, H, 0, G + o.pW1, H); w1.colsum = G + o.pb1; g.push_back(w1);
-    if (launch_group(g, s)) return -1;
+    auto w1 = mk(O, H, n, bt.sa, W, 1, h->dh1p, H, 0, G + o.pW1, H); w1.colsum = G + o.pb1; w1.adam = 1; g.push_back(w1);
+    if (launch_group(g, s, &ad, &slot)) return -1;
   }
-  // ---- Adam x4 + Polyak, norms, counters
-  hipLaunchKernelGGL(sac_adam_kernel, dim3(h->adam_blocks), dim3(256), 0, s, o.total, o.n_pi, o.n_q, h->P, h->G, h->M,
-                     h->V, h->T, h->beta_pow, h->lr, h->tau, h->norm_part, h->ticket, h->logs, h->iter);
-  MOPO_HIP(hipGetLastError());
+  if (slot != h->nslots) return fail("sac: grad-norm slot count mismatch");
   return 0;
+}
+
+// blocks of the four backward launches (one grad-norm slot each); mirrors sac_step_impl
+static int count_slots(const SacDims& d) {
+  auto t = [](int M, int N) { return ceil_div(M, 16) * ceil_div(N, 16); };
+  const int n = d.n, H = d.H, O = d.O, A = d.A, W = O + A;
+  return 4 * t(n, H) + 2 * t(H, H) + 2 * t(H, 1) + 2 * t(n, W) + 2 * t(W, H) + t(n, H) + t(H, H) + 2 * t(H, A) +
+         t(O, H);
 }
 
 }  // namespace mopo
@@ -710,6 +979,7 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   MOPO_REQUIRE(out && h_params, "mopo_sac_create: NULL argument");
   MOPO_REQUIRE(O >= 1 && A >= 1 && A <= 8 && H >= 1, "mopo_sac_create: bad dims (act_dim <= 8)");
   MOPO_REQUIRE(batch >= 1 && batch <= 1024, "mopo_sac_create: batch must be in [1, 1024]");
+  MOPO_REQUIRE(H % 16 == 0, "mopo_sac_create: hidden width must be a multiple of 16");
   MOPO_REQUIRE(n_env >= 0 && n_env <= batch, "mopo_sac_create: n_env must be in [0, batch]");
   Sac* h = new Sac();
   h->d = SacDims{O, A, H, batch, n_env, 0};
@@ -717,24 +987,24 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   h->d.P = h->o.total;
   h->lr = lr; h->gamma = gamma; h->tau = tau; h->rscale = reward_scale; h->tent = target_entropy;
   const int64_t tot = h->o.total + 1, n = batch, W = O + A;
-  h->adam_blocks = (int)std::min<int64_t>(256, (tot + 255) / 256);
+  h->nslots = count_slots(h->d);
   std::vector<std::pair<void**, size_t>> reg;
   auto f = [&](float** p, size_t cnt) { reg.push_back({(void**)p, cnt * 4}); };
-  f(&h->P, tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->T, tot);
-  f(&h->beta_pow, 2); f(&h->logs, LOG_N); f(&h->norm_part, 2 * h->adam_blocks);
-  reg.push_back({(void**)&h->iter, 8});
+  f(&h->Pb[1], tot); f(&h->norm_part, 2 * (size_t)h->nslots);
+  f(&h->loss_part, 8 * (size_t)ceil_div(batch, QL_ROWS));
   reg.push_back({(void**)&h->ticket, 4});
-  f(&h->sa, n * W); f(&h->xpi, n * W); f(&h->xn, n * W); f(&h->rew, n); f(&h->term, n);
+  f(&h->P, tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->T, tot);
+  f(&h->beta_pow, 3); f(&h->logs, LOG_N);
+  reg.push_back({(void**)&h->iter, 8});
+  for (int b = 0; b < 2; ++b) {
+    Batch& t = h->bt[b];
+    f(&t.sa, n * W); f(&t.xpi, n * W); f(&t.xn, n * W); f(&t.rew, n); f(&t.term, n);
+    reg.push_back({(void**)&t.idx, (size_t)n * 8});
+  }
   for (int i = 0; i < 8; ++i) { f(&h->h1[i], n * H); f(&h->h2[i], n * H); f(&h->out[i], n * 2 * A); }
   f(&h->logp_s, n); f(&h->logp_n, n); f(&h->eps_s, n * A); f(&h->eps_n, n * A);
-  for (int i = 0; i < 4; ++i) { f(&h->dq[i], n); f(&h->dh2[i], n * H); f(&h->dh1[i], n * H); }
+  for (int i = 0; i < 4; ++i) { f(&h->dq[i], n); f(&h->dh1[i], n * H); }
   f(&h->dx1, n * W); f(&h->dx2, n * W); f(&h->dhead, n * 2 * A); f(&h->dh2p, n * H); f(&h->dh1p, n * H);
-  reg.push_back({(void**)&h->idx, (size_t)n * 8});
-  reg.push_back({(void**)&h->outp_dev, 8 * sizeof(float*)});
-  reg.push_back({(void**)&h->dq_dev, 4 * sizeof(float*)});
-  reg.push_back({(void**)&h->w3_dev, 4 * sizeof(float*)});
-  reg.push_back({(void**)&h->h2q_dev, 4 * sizeof(float*)});
-  reg.push_back({(void**)&h->dh2_dev, 4 * sizeof(float*)});
   size_t total = 0;
   for (auto& r : reg) total += (r.second + 255) & ~(size_t)255;
   if (hipMalloc(&h->mem, total) != hipSuccess) { delete h; return fail("mopo_sac_create: out of device memory"); }
@@ -744,28 +1014,29 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   // parameters, target = main (target_init, mopo.py:449-450), log_alpha, beta powers
   std::vector<float> pv(h_params, h_params + h->o.total);
   pv.push_back(log_alpha);
+  h->Pb[0] = h->P;
   MOPO_HIP(hipMemcpy(h->P, pv.data(), tot * 4, hipMemcpyHostToDevice));
+  MOPO_HIP(hipMemcpy(h->Pb[1], pv.data(), tot * 4, hipMemcpyHostToDevice));
   MOPO_HIP(hipMemcpy(h->T, pv.data(), tot * 4, hipMemcpyHostToDevice));
   float bp[2] = {0.9f, 0.999f};
   MOPO_HIP(hipMemcpy(h->beta_pow, bp, 8, hipMemcpyHostToDevice));
-  float* outs[8];
-  for (int i = 0; i < 8; ++i) outs[i] = h->out[i];
-  MOPO_HIP(hipMemcpy(h->outp_dev, outs, sizeof(outs), hipMemcpyHostToDevice));
-  MOPO_HIP(hipMemcpy(h->dq_dev, h->dq, 4 * sizeof(float*), hipMemcpyHostToDevice));
-  float* w3[4] = {h->P + h->o.q[0][4], h->P + h->o.q[1][4], h->P + h->o.q[0][4], h->P + h->o.q[1][4]};
-  MOPO_HIP(hipMemcpy(h->w3_dev, w3, sizeof(w3), hipMemcpyHostToDevice));
-  float* h2q[4] = {h->h2[2], h->h2[3], h->h2[4], h->h2[5]};
-  MOPO_HIP(hipMemcpy(h->h2q_dev, h2q, sizeof(h2q), hipMemcpyHostToDevice));
-  MOPO_HIP(hipMemcpy(h->dh2_dev, h->dh2, 4 * sizeof(float*), hipMemcpyHostToDevice));
   *out = reinterpret_cast<mopo_sac_t>(h);
   return 0;
+}
+
+static void drop_graphs(Sac* h) {
+  for (int i = 0; i < 3; ++i) {
+    if (h->gexec[i]) (void)hipGraphExecDestroy(h->gexec[i]);
+    if (h->graph[i]) (void)hipGraphDestroy(h->graph[i]);
+    h->gexec[i] = nullptr;
+    h->graph[i] = nullptr;
+  }
 }
 
 extern "C" int mopo_sac_destroy(mopo_sac_t hh) {
   Sac* h = reinterpret_cast<Sac*>(hh);
   if (!h) return 0;
-  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
-  if (h->graph) (void)hipGraphDestroy(h->graph);
+  drop_graphs(h);
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   if (h->ev_out) (void)hipEventDestroy(h->ev_out);
   if (h->gstream) (void)hipStreamDestroy(h->gstream);
@@ -809,7 +1080,40 @@ extern "C" int mopo_sac_set_graph(mopo_sac_t hh, int enable) {
   return 0;
 }
 
+static int launch_logs(Sac* h, hipStream_t s) {
+  hipLaunchKernelGGL(sac_logs_kernel, dim3(1), dim3(256), 0, s, h->norm_part, h->nslots, h->logs);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
 static bool same_desc(const mopo_pool_desc& a, const mopo_pool_desc& b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
+
+// Steps alternate parameter buffers (parity 0 reads Pb[0] and writes Pb[1], parity 1 the
+// reverse); a call ends with the parameters back in Pb[0] (one copy after an odd step count).
+static int copy_back(Sac* h, hipStream_t s) {
+  MOPO_HIP(hipMemcpyAsync(h->Pb[0], h->Pb[1], (h->o.total + 1) * 4, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+constexpr int GRAPH_STEPS = 8;  // steps per replay of the long graph (amortises the launch gap)
+
+// which = 0: GRAPH_STEPS steps, 1: two steps (parity 0, 1), 2: one step + copy back.  Every step
+// prefetches the other parity's batch, so a graph's last step prepares the next graph's first.
+static int capture(Sac* h, int which, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed) {
+  hipStream_t gs = h->gstream;
+  MOPO_HIP(hipStreamBeginCapture(gs, hipStreamCaptureModeThreadLocal));
+  const int steps = which == 0 ? GRAPH_STEPS : which == 1 ? 2 : 1;
+  int rc = 0;
+  for (int i = 0; i < steps && !rc; ++i) rc = sac_step_impl(h, i & 1, env, mod, seed, nullptr, nullptr, gs, true);
+  if (!rc && which == 2) rc = copy_back(h, gs);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(gs, &g);
+  if (rc) { if (g) (void)hipGraphDestroy(g); return -1; }
+  if (e != hipSuccess) return fail(std::string("mopo_sac_step: capture failed: ") + hipGetErrorString(e));
+  h->graph[which] = g;
+  MOPO_HIP(hipGraphInstantiate(&h->gexec[which], g, nullptr, nullptr, 0));
+  return 0;
+}
 
 extern "C" int mopo_sac_step(mopo_sac_t hh, const mopo_pool_desc* env, const mopo_pool_desc* mod, int n_steps,
                              uint64_t seed, const int64_t* d_idx, const float* d_eps_s, const float* d_eps_n,
@@ -817,41 +1121,46 @@ extern "C" int mopo_sac_step(mopo_sac_t hh, const mopo_pool_desc* env, const mop
   Sac* h = reinterpret_cast<Sac*>(hh);
   MOPO_REQUIRE(h && env && mod, "mopo_sac_step: NULL argument");
   MOPO_REQUIRE(env->d_state && mod->d_state, "mopo_sac_step: pool state required");
+  MOPO_REQUIRE(n_steps >= 0, "mopo_sac_step: n_steps must be >= 0");
+  if (n_steps == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const bool injected = d_idx || d_eps_s || d_eps_n;
   if (injected) {
     MOPO_REQUIRE(n_steps == 1, "mopo_sac_step: injected streams drive exactly one step");
-    return sac_step_impl(h, env, mod, seed, d_idx, d_eps_s, d_eps_n, s);
+    if (launch_gather(h, 0, env, mod, seed, d_idx, s) ||
+        sac_step_impl(h, 0, env, mod, seed, d_eps_s, d_eps_n, s, false) || copy_back(h, s))
+      return -1;
+    return launch_logs(h, s);
   }
   if (!h->use_graph) {
+    if (launch_gather(h, 0, env, mod, seed, nullptr, s)) return -1;
     for (int i = 0; i < n_steps; ++i)
-      if (sac_step_impl(h, env, mod, seed, nullptr, nullptr, nullptr, s)) return -1;
-    return 0;
+      if (sac_step_impl(h, i & 1, env, mod, seed, nullptr, nullptr, s, true)) return -1;
+    if ((n_steps & 1) && copy_back(h, s)) return -1;
+    return launch_logs(h, s);
   }
   // graphs are captured and replayed on the handle's own stream (the caller's may be the legacy
-  // NULL stream, which cannot capture); event edges order it after / before the caller's work
+  // NULL stream, which cannot capture); event edges order it after / before the caller's work.
+  // gexec[0] = GRAPH_STEPS steps, gexec[1] = two, gexec[2] = one step + copy back.
   if (!h->gstream) {
     MOPO_HIP(hipStreamCreateWithFlags(&h->gstream, hipStreamNonBlocking));
     MOPO_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     MOPO_HIP(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
   }
   hipStream_t gs = h->gstream;
-  if (!h->gexec || !same_desc(h->genv, *env) || !same_desc(h->gmod, *mod) || h->gseed != seed) {
-    if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
-    if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
-    MOPO_HIP(hipStreamBeginCapture(gs, hipStreamCaptureModeThreadLocal));
-    const int rc = sac_step_impl(h, env, mod, seed, nullptr, nullptr, nullptr, gs);
-    hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(gs, &g);
-    if (rc) { if (g) (void)hipGraphDestroy(g); return -1; }
-    if (e != hipSuccess) return fail(std::string("mopo_sac_step: capture failed: ") + hipGetErrorString(e));
-    h->graph = g;
-    MOPO_HIP(hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0));
+  if (!h->gexec[0] || !same_desc(h->genv, *env) || !same_desc(h->gmod, *mod) || h->gseed != seed) {
+    drop_graphs(h);
+    if (capture(h, 0, env, mod, seed) || capture(h, 1, env, mod, seed) || capture(h, 2, env, mod, seed)) return -1;
     h->genv = *env; h->gmod = *mod; h->gseed = seed;
   }
   MOPO_HIP(hipEventRecord(h->ev_in, s));
   MOPO_HIP(hipStreamWaitEvent(gs, h->ev_in, 0));
-  for (int i = 0; i < n_steps; ++i) MOPO_HIP(hipGraphLaunch(h->gexec, gs));
+  if (launch_gather(h, 0, env, mod, seed, nullptr, gs)) return -1;  // first step's batch
+  int i = 0;
+  for (; i + GRAPH_STEPS <= n_steps; i += GRAPH_STEPS) MOPO_HIP(hipGraphLaunch(h->gexec[0], gs));
+  for (; i + 2 <= n_steps; i += 2) MOPO_HIP(hipGraphLaunch(h->gexec[1], gs));
+  if (i < n_steps) MOPO_HIP(hipGraphLaunch(h->gexec[2], gs));
+  if (launch_logs(h, gs)) return -1;
   MOPO_HIP(hipEventRecord(h->ev_out, gs));
   MOPO_HIP(hipStreamWaitEvent(s, h->ev_out, 0));
   return 0;

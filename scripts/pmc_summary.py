@@ -1,0 +1,60 @@
+"""Reduce the rocprofv3 --pmc passes written by scripts/pmc.sh (gpurun_out/pmc1..4) to one JSON.
+
+Per kernel: mean FETCH_SIZE / WRITE_SIZE per dispatch (rocprofv3 reports KiB; converted to bytes),
+the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md §HBM (wide 16-B/lane reads are tallied at
+half their bytes -> x2), MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/XCDs x CUs
+x 4 SIMDs) and the wave-cycle wait share.  Usage: python scripts/pmc_summary.py OUT.json [pmc_dir]
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+XCDS, CUS = 8, 256
+
+
+def load(d):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for i in range(1, 5):
+        f = os.path.join(d, 'pmc%d' % i, 'run_counter_collection.csv')
+        if not os.path.exists(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            n = r['Kernel_Name'].split('(')[0].replace('void ', '')
+            agg[n][r['Counter_Name']].append(float(r['Counter_Value']))
+    return agg
+
+
+def summarize(agg):
+    out = {}
+    for n, d in agg.items():
+        m = {c: sum(v) / len(v) for c, v in d.items()}
+        e = {'dispatches': max(len(v) for v in d.values())}
+        if 'FETCH_SIZE' in m:
+            e['fetch_bytes_raw'] = m['FETCH_SIZE'] * 1024
+            e['fetch_bytes_corrected'] = 2 * m['FETCH_SIZE'] * 1024
+        if 'WRITE_SIZE' in m:
+            e['write_bytes'] = m['WRITE_SIZE'] * 1024
+        if 'fetch_bytes_corrected' in e and 'write_bytes' in e:
+            e['hbm_bytes'] = e['fetch_bytes_corrected'] + e['write_bytes']
+        if 'SQ_VALU_MFMA_BUSY_CYCLES' in m and m.get('GRBM_GUI_ACTIVE'):
+            e['mfma_busy_frac'] = m['SQ_VALU_MFMA_BUSY_CYCLES'] / (m['GRBM_GUI_ACTIVE'] / XCDS * CUS * 4)
+            e['gui_active_cycles_per_xcd'] = m['GRBM_GUI_ACTIVE'] / XCDS
+        if 'SQ_WAVES' in m:
+            e['waves'] = m['SQ_WAVES']
+        if m.get('SQ_WAVE_CYCLES'):
+            e['wait_inst_any_frac'] = m.get('SQ_WAIT_INST_ANY', 0) / m['SQ_WAVE_CYCLES']
+        out[n] = e
+    return out
+
+
+if __name__ == '__main__':
+    dst = sys.argv[1]
+    src = sys.argv[2] if len(sys.argv) > 2 else 'gpurun_out'
+    s = summarize(load(src))
+    s = {k: v for k, v in s.items() if 'mopo::' in k}
+    json.dump({'source': 'rocprofv3 --pmc passes of scripts/pmc.sh (bench.py --steps 3 --warmup 1 '
+                         '--sac-steps 50, default workload)', 'kernels': s}, open(dst, 'w'), indent=1)
+    for k, v in s.items():
+        print(k, {a: round(b, 4) if isinstance(b, float) else b for a, b in v.items()})

@@ -1,0 +1,39 @@
+"""SAC kernel durations from a rocprofv3 kernel trace: mean duration per kernel name (and calls per
+step), and the step period as the mean interval between consecutive (q)loss-kernel starts.
+Usage: python scripts/sac_trace.py run_kernel_trace.csv"""
+import collections
+import csv
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
+sac = [r for r in rows if any(k in r['Kernel_Name'] for k in ('gemm_group', 'sac_', 'pi_head'))]
+loss = [int(r['Start_Timestamp']) for r in sac if 'loss_kernel' in r['Kernel_Name']]
+skip = len(loss) // 4
+t0, t1 = loss[skip], loss[-1]
+steps = len(loss) - 1 - skip
+dur = collections.defaultdict(list)
+busy = 0
+for r in sac:
+    st = int(r['Start_Timestamp'])
+    if t0 <= st < t1:
+        d = (int(r['End_Timestamp']) - st) / 1e3
+        dur[r['Kernel_Name'].split('(')[0]].append(d)
+        busy += d
+for n, v in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
+    print('%-34s %5.1f calls/step  %6.2f us avg  %6.1f us/step' % (n, len(v) / steps, sum(v) / len(v), sum(v) / steps))
+print('step period %.1f us (loss-to-loss, %d steps); kernel-busy %.1f us/step'
+      % ((t1 - t0) / 1e3 / steps, steps, busy / steps))
+
+# per position within the period (dispatch order after a loss kernel)
+pos = collections.defaultdict(list)
+cur = -1
+for r in sac:
+    st = int(r['Start_Timestamp'])
+    if 'loss_kernel' in r['Kernel_Name']:
+        cur = 0
+    if cur < 0 or not (t0 <= st < t1):
+        continue
+    pos[(cur, r['Kernel_Name'].split('(')[0], r.get('Grid_Size_X', ''))].append((int(r['End_Timestamp']) - st) / 1e3)
+    cur += 1
+for (i, n, gx), v in sorted(pos.items()):
+    print('  %2d %-30s grid %7s  %6.2f us' % (i, n, gx, sum(v) / len(v)))
