@@ -4,14 +4,14 @@
 // TensorStandardScaler.transform (mopo/models/utils.py:96) and FC.compute_output_tensor
 // (mopo/models/fc.py:84-106).
 //
-// Work decomposition: one wave (= one 64-thread workgroup) owns one (member e, tile of 16*R
-// rows) item and runs all five layers for it with the activations held entirely in VGPRs:
-// every layer is the transposed product Out^T[n][m] = W^T[n][k] X^T[k][m] on
-// v_mfma_f32_16x16x4_f32, whose accumulator layout (feature on the register axis, row on the
-// lane axis) is exactly the B operand of the next layer, so no LDS round trip and no barrier
-// is needed.  Weights stream from L2 as 1 KiB fragments (one dwordx4 per lane per 4 MFMAs),
-// double-buffered in registers across k-groups.  Items are member-major so the waves resident
-// on one XCD share one member's weights in L2.
+// Work decomposition: a workgroup of 4 waves owns one ensemble member and 64 rows (16 per wave)
+// and runs all five layers with the activations held in VGPRs: every layer is the transposed
+// product Out^T[n][m] = W^T[n][k] X^T[k][m] on v_mfma_f32_16x16x4_f32, whose accumulator layout
+// (feature on the register axis, row on the lane axis) is exactly the B operand of the next layer,
+// so activations never leave registers.  Weights stream HBM/L2 -> LDS as 1 KiB fragments with
+// global_load_lds, double-buffered per 16-deep k-group and shared by the 4 waves (mlp_tile.h);
+// each layer's bias rides along with its last slice.  Workgroups are member-major so the ones
+// resident on an XCD share one member's weights in L2.
 #include "mlp_tile.h"
 
 #include <vector>
@@ -74,17 +74,17 @@ __device__ __forceinline__ float load_feat(const void* p, int f64, int64_t idx) 
   return f64 ? (float)reinterpret_cast<const double*>(p)[idx] : reinterpret_cast<const float*>(p)[idx];
 }
 
-// bias + swish, acc -> next-layer input (fc.py:21,99-106)
+// bias + swish, acc -> next-layer input (fc.py:21,99-106); the layer's bias was staged in LDS
 template <int NB, int R>
-__device__ __forceinline__ void bias_swish(const float* __restrict__ b, const f32x4 (&acc)[R][NB],
-                                           f32x4 (&out)[R][NB], int g) {
+__device__ __forceinline__ void bias_swish(const float* lds_bias, const f32x4 (&acc)[R][NB], f32x4 (&out)[R][NB],
+                                           int g) {
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    f32x4 bb = ld4(b + nb * 16 + 4 * g);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(lds_bias + nb * 16 + 4 * g);
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) out[r][nb][t] = swishf(acc[r][nb][t] + bb[t]);
+      for (int t = 0; t < 4; ++t) out[r][nb][t] = swish_fast(acc[r][nb][t] + bb[t]);
   }
 }
 
@@ -137,6 +137,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_kernel(const BnnDev w, 
   constexpr int NBMAX = NBH > NBO ? NBH : NBO;
   constexpr int SLOT = Stage<NBMAX, WAVES>::SLOTS * 256;  // floats per buffer
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
+  __shared__ __attribute__((aligned(16))) float lds_bias[(NBH * 4 + 63) / 64 * 256];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
@@ -168,11 +169,13 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_kernel(const BnnDev w, 
   }
   f32x4 acc[R][NBH], hcur[R][NBH];
   const int64_t hp = w.BS;  // per-member bias stride
-  layer_lds<KG0, NBH, R, WAVES, SLOT>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv, lane);
-  bias_swish<NBH, R>(w.b0 + e * hp, acc, hcur, g);
+  layer_lds<KG0, NBH, R, WAVES, SLOT>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv, lane, w.b0 + e * hp,
+                                      lds_bias);
+  bias_swish<NBH, R>(lds_bias, acc, hcur, g);
   for (int l = 0; l < 3; ++l) {  // hidden layers 1..3 (constructor.py:31-33)
-    layer_lds<NBH, NBH, R, WAVES, SLOT>(w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lds, wv, lane);
-    bias_swish<NBH, R>(w.bh + ((int64_t)l * w.E + e) * hp, acc, hcur, g);
+    layer_lds<NBH, NBH, R, WAVES, SLOT>(w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lds, wv, lane,
+                                        w.bh + ((int64_t)l * w.E + e) * hp, lds_bias);
+    bias_swish<NBH, R>(lds_bias, acc, hcur, g);
   }
   // ---- heads on the 4th hidden output (bnn.py:661-667): n < D mean, D <= n < 2D log-var
   f32x4 hd[R][NBO];
@@ -220,8 +223,8 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_bf16_kernel(const BnnDe
       const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), b1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        hin[c][t] = to_bf16(swishf(acc[2 * c][t] + b0[t]));
-        hin[c][4 + t] = to_bf16(swishf(acc[2 * c + 1][t] + b1[t]));
+        hin[c][t] = to_bf16(swish_fast(acc[2 * c][t] + b0[t]));
+        hin[c][4 + t] = to_bf16(swish_fast(acc[2 * c + 1][t] + b1[t]));
       }
     }
   };

@@ -41,6 +41,13 @@ __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<
 // ------------------------------------------------------------------ activations (TF1 f32 semantics)
 __device__ __forceinline__ float swishf(float x) { return x * (1.0f / (1.0f + expf(-x))); }
 
+// swish on the hardware transcendentals: x * rcp(1 + 2^(-x log2 e)) -- v_exp_f32 / v_rcp_f32 (1 ulp
+// each) instead of the range-reduced expf and the IEEE divide (~25 VALU instructions per element in
+// the ensemble forward's epilogues).  For x -> -inf the exp overflows to inf and rcp gives 0.
+__device__ __forceinline__ float swish_fast(float x) {
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x * 1.4426950408889634f));
+}
+
 // tf.nn.softplus (Eigen): threshold = log(eps_f32) + 2
 __device__ __forceinline__ float softplusf(float x) {
   const float thr = -13.942385f;  // logf(1.1920929e-7f) + 2
