@@ -23,9 +23,17 @@ __global__ void pack_head_kernel(const float* Wm, const float* Wl, int Hp, int A
   dst[i] = v;
 }
 
+// packed layout: W1 frags | W2 frags | head frags | b1 [NB*16] | b2 [NB*16] | [bmu | bls] [16]
+// (biases zero-padded to whole 16-blocks so the kernel stages them into LDS with global_load_lds)
 int64_t actor_packed_floats(int O, int Hp) {
   const int KG0 = ceil_div(O, 16), NB = ceil_div(Hp, 16);
-  return (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256 + (int64_t)NB * 256;
+  return (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256 + (int64_t)NB * 256 + 2LL * NB * 16 + 16;
+}
+
+// dst[i] = i < n ? src[i] : 0 for i < np
+__global__ void copy_pad_kernel(const float* src, int n, float* dst, int np) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < np) dst[i] = i < n ? src[i] : 0.f;
 }
 
 int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s) {
@@ -36,18 +44,24 @@ int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s) 
   const float* Wl = Wm + Hp * A + A;
   if (pack_frags(W1, dst, 1, O, Hp, KG0, NB, s)) return -1;
   if (pack_frags(W2, dst + (int64_t)KG0 * NB * 256, 1, Hp, Hp, NB, NB, s)) return -1;
-  hipLaunchKernelGGL(pack_head_kernel, dim3(ceil_div(NB * 256, 256)), dim3(256), 0, s, Wm, Wl, Hp, A, NB,
-                     dst + (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256);
+  float* hf = dst + (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256;
+  hipLaunchKernelGGL(pack_head_kernel, dim3(ceil_div(NB * 256, 256)), dim3(256), 0, s, Wm, Wl, Hp, A, NB, hf);
+  float* bp = hf + (int64_t)NB * 256;
+  hipLaunchKernelGGL(copy_pad_kernel, dim3(ceil_div(NB * 16, 256)), dim3(256), 0, s, W1 + O * Hp, Hp, bp, NB * 16);
+  hipLaunchKernelGGL(copy_pad_kernel, dim3(ceil_div(NB * 16, 256)), dim3(256), 0, s, W2 + Hp * Hp, Hp, bp + NB * 16,
+                     NB * 16);
+  hipLaunchKernelGGL(copy_pad_kernel, dim3(1), dim3(64), 0, s, Wm + Hp * A, A, bp + 2 * NB * 16, A);
+  hipLaunchKernelGGL(copy_pad_kernel, dim3(1), dim3(64), 0, s, Wl + Hp * A, A, bp + 2 * NB * 16 + A, 16 - A);
   MOPO_HIP(hipGetLastError());
   return 0;
 }
 
+// bias (staged in LDS by layer_lds) + relu
 template <int NB>
-__device__ __forceinline__ void bias_relu(const float* __restrict__ b, const f32x4 (&acc)[1][NB], f32x4 (&out)[1][NB],
-                                          int g) {
+__device__ __forceinline__ void bias_relu(const float* b, const f32x4 (&acc)[1][NB], f32x4 (&out)[1][NB], int g) {
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    const f32x4 bb = ld4(b + nb * 16 + 4 * g);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(b + nb * 16 + 4 * g);
 #pragma unroll
     for (int t = 0; t < 4; ++t) out[0][nb][t] = fmaxf(acc[0][nb][t] + bb[t], 0.f);
   }
@@ -71,18 +85,19 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_kernel(const ActorArg
   constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
   __shared__ float head[ACT_WAVES][16][17];
+  __shared__ __attribute__((aligned(16))) float lds_bias[(NBP * 4 + 63) / 64 * 256];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   if ((int64_t)blockIdx.x * ACT_WAVES * 16 >= count) return;  // whole workgroup past the live rows
   const int64_t row0 = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16;
   const int O = a.O, A = a.A, Hp = a.Hp;
-  const float* b1 = a.P + O * Hp;
-  const float* b2 = b1 + Hp + Hp * Hp;
-  const float* bm = b2 + Hp + Hp * A;
-  const float* bl = bm + A + Hp * A;
   const float* w1f = a.Wpk;
   const float* w2f = w1f + KG0 * NBP * 256;
   const float* whf = w2f + NBP * NBP * 256;
+  const float* b1 = whf + NBP * 256;  // padded biases (pack_actor)
+  const float* b2 = b1 + NBP * 16;
+  const float* bh = b2 + NBP * 16;
+  (void)Hp;
   const int64_t row = row0 + m;
   const bool ok = row < count;
   f32x4 x0[1][KG0];
@@ -98,17 +113,16 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_kernel(const ActorArg
       x0[0][kg][t] = v;
     }
   f32x4 acc[1][NBP], h[1][NBP];
-  layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT>(w1f, x0, acc, lds, wv, lane);   // mlp hidden 1 (mopo.py:277-278)
-  bias_relu<NBP>(b1, acc, h, g);
-  layer_lds<NBP, NBP, 1, ACT_WAVES, SLOT>(w2f, h, acc, lds, wv, lane);    // hidden 2, relu (mopo.py:301)
-  bias_relu<NBP>(b2, acc, h, g);
+  layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT>(w1f, x0, acc, lds, wv, lane, b1, lds_bias);  // hidden 1 (:277-278)
+  bias_relu<NBP>(lds_bias, acc, h, g);
+  layer_lds<NBP, NBP, 1, ACT_WAVES, SLOT>(w2f, h, acc, lds, wv, lane, b2, lds_bias);   // hidden 2, relu (:301)
+  bias_relu<NBP>(lds_bias, acc, h, g);
   f32x4 hd[1][1];
-  layer_lds<NBP, 1, 1, ACT_WAVES, SLOT>(whf, h, hd, lds, wv, lane);       // mu | log_std heads (:302-303)
+  layer_lds<NBP, 1, 1, ACT_WAVES, SLOT>(whf, h, hd, lds, wv, lane, bh, lds_bias);      // mu | log_std (:302-303)
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int n = 4 * g + t;
-    const float bias = n < A ? bm[n] : (n < 2 * A ? bl[n - A] : 0.f);
-    head[wv][m][n] = hd[0][0][t] + bias;
+    head[wv][m][n] = hd[0][0][t] + lds_bias[n];
   }
   __syncthreads();
   if (g != 0 || !ok) return;

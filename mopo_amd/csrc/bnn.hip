@@ -84,21 +84,31 @@ __device__ __forceinline__ void bias_swish(const float* lds_bias, const f32x4 (&
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) out[r][nb][t] = swish_fast(acc[r][nb][t] + bb[t]);
+      for (int t = 0; t < 4; ++t) {
+#ifndef BNN_KNOB_NOSWISH
+        out[r][nb][t] = swish_fast(acc[r][nb][t] + bb[t]);
+#else
+        out[r][nb][t] = acc[r][nb][t] + bb[t];
+#endif
+      }
   }
 }
 
 // heads -> outputs for one row per lane group (bnn.py:661-675; rollout mode: fake_env.py:66-81, 110)
+// hx = the member's head aux block [bias | max_logvar | min_logvar] (NBO*16 each, logvar bounds at
+// columns D..2D-1), staged in LDS by the head layer; sel_e = the row's selected member (rollout)
 template <int NBO, int MODE>
 __device__ __forceinline__ void head_epilogue(const BnnDev& w, const FwdArgs& a, const f32x4 (&hd)[NBO], int e,
-                                              int64_t row, int64_t count, int g) {
+                                              int64_t row, int64_t count, int g, const float* hx, int sel_e) {
   const int D = w.D;
   const bool ok = row < count;
   float ss = 0.f;  // sum of std^2 over D (learned-var penalty, fake_env.py:110)
-  const bool selected = (MODE == FWD_ROLLOUT) && ok && a.sel[row] == e;
+  const bool selected = (MODE == FWD_ROLLOUT) && ok && sel_e == e;
 #pragma unroll
   for (int nb = 0; nb < NBO; ++nb) {
-    f32x4 bb = ld4(w.bhd + e * NBO * 16 + nb * 16 + 4 * g);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(hx + nb * 16 + 4 * g);
+    const f32x4 bmx = *reinterpret_cast<const f32x4*>(hx + NBO * 16 + nb * 16 + 4 * g);
+    const f32x4 bmn = *reinterpret_cast<const f32x4*>(hx + 2 * NBO * 16 + nb * 16 + 4 * g);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int n = nb * 16 + 4 * g + t;
@@ -111,14 +121,15 @@ __device__ __forceinline__ void head_epilogue(const BnnDev& w, const FwdArgs& a,
         }
       } else if (n < 2 * D) {
         const int d = n - D;
-        const float mx = w.maxlv[d], mn = w.minlv[d];
-        float lv = mx - softplusf(mx - v);  // bnn.py:669
-        lv = mn + softplusf(lv - mn);       // bnn.py:670
-        const float var = expf(lv);         // bnn.py:675
+        const float mx = bmx[t], mn = bmn[t];
+        float lv = mx - softplus_fast(mx - v);  // bnn.py:669
+        lv = mn + softplus_fast(lv - mn);       // bnn.py:670
+        const float l2 = lv * 1.4426950408889634f;
         if (MODE == FWD_PREDICT) {
+          const float var = __builtin_amdgcn_exp2f(l2);         // bnn.py:675
           if (ok) a.var[((int64_t)e * a.B + row) * D + d] = var;
         } else {
-          const float sd = sqrtf(var);      // fake_env.py:67
+          const float sd = __builtin_amdgcn_exp2f(0.5f * l2);   // sqrt(exp(lv)), fake_env.py:67
           ss += sd * sd;
           if (selected) a.std_sel[row * D + d] = sd;
         }
@@ -133,11 +144,12 @@ __device__ __forceinline__ void head_epilogue(const BnnDev& w, const FwdArgs& a,
 }
 
 template <int KG0, int NBH, int NBO, int R, int MODE, int WAVES>
-__global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_kernel(const BnnDev w, const FwdArgs a) {
+__global__ __launch_bounds__(WAVES * 64, WAVES >= 8 ? 1 : 2) void bnn_fwd_kernel(const BnnDev w, const FwdArgs a) {
   constexpr int NBMAX = NBH > NBO ? NBH : NBO;
   constexpr int SLOT = Stage<NBMAX, WAVES>::SLOTS * 256;  // floats per buffer
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
-  __shared__ __attribute__((aligned(16))) float lds_bias[(NBH * 4 + 63) / 64 * 256];
+  constexpr int BIASQ = NBH > 3 * NBO ? NBH * 4 : 3 * NBO * 4;  // quads: hidden bias / head aux
+  __shared__ __attribute__((aligned(16))) float lds_bias[(BIASQ + 63) / 64 * 256];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
@@ -146,6 +158,12 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_kernel(const BnnDev w, 
   const int64_t row0 = (int64_t)tile * 16 * R;
   if ((int64_t)grp * WAVES * 16 * R >= count) return;  // whole workgroup past the live rows
   const int IN = w.IN, O = w.O, D = w.D;
+  int sel_e[R];  // the selected member of each row, fetched early (used by the head epilogue)
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + r * 16 + m;
+    sel_e[r] = (MODE == FWD_ROLLOUT && row < count) ? a.sel[row] : -1;
+  }
 
   // ---- layer-0 input: scaler transform (utils.py:96), f64 inputs cast to f32 as TF's feed does
   f32x4 x0[R][KG0];
@@ -179,10 +197,16 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_kernel(const BnnDev w, 
   }
   // ---- heads on the 4th hidden output (bnn.py:661-667): n < D mean, D <= n < 2D log-var
   f32x4 hd[R][NBO];
-  layer_lds<NBH, NBO, R, WAVES, SLOT>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds, wv, lane);
+  layer_lds<NBH, NBO, R, WAVES, SLOT, 3 * NBO * 4>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds, wv, lane,
+                                                  w.bhd + (int64_t)e * 3 * NBO * 16, lds_bias);
 
+#ifndef BNN_KNOB_NOHEAD
 #pragma unroll
-  for (int r = 0; r < R; ++r) head_epilogue<NBO, MODE>(w, a, hd[r], e, row0 + r * 16 + m, count, g);
+  for (int r = 0; r < R; ++r)
+    head_epilogue<NBO, MODE>(w, a, hd[r], e, row0 + r * 16 + m, count, g, lds_bias, sel_e[r]);
+#else
+  if (hd[0][0][0] == 12345.f) a.pen_bits[0] = 1;
+#endif
   (void)D;
 }
 
@@ -236,10 +260,17 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_bf16_kernel(const BnnDe
   }
   f32x4 hd[NBO];
   layer_lds_bf16<KG, NBO, WAVES, SLOT>(w.whdb + (int64_t)e * KG * NBO * 256, hin, hd, lds, wv, lane);
-  head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g);
+  head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
+                           (MODE == FWD_ROLLOUT && ok) ? a.sel[row] : -1);
 }
 
-constexpr int FWD_WAVES = 4;
+#ifndef BNN_R13
+#define BNN_R13 1  // row blocks per wave at H = 200
+#endif
+#ifndef BNN_FWD_WAVES
+#define BNN_FWD_WAVES 4
+#endif
+constexpr int FWD_WAVES = BNN_FWD_WAVES;
 
 template <int KG0, int NBH, int NBO, int R>
 static int launch_fwd_t(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
@@ -259,7 +290,7 @@ static int launch_fwd_h(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s)
   switch (h->dev.NBH) {
     case 2: return launch_fwd_t<KG0, 2, NBO, 2>(h, mode, a, s);
     case 4: return launch_fwd_t<KG0, 4, NBO, 2>(h, mode, a, s);
-    case 13: return launch_fwd_t<KG0, 13, NBO, 1>(h, mode, a, s);
+    case 13: return launch_fwd_t<KG0, 13, NBO, BNN_R13>(h, mode, a, s);
     case 25: return launch_fwd_t<KG0, 25, NBO, 1>(h, mode, a, s);
   }
   return fail("bnn: unsupported hidden size (supported: 32, 64, 200, 400; got H=" +
@@ -351,7 +382,7 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
   // sizes (floats) of the packed regions
   const int64_t s_w0 = (int64_t)E * KG0 * NBH * 256, s_wh = 3LL * E * NBH * NBH * 256,
                 s_whd = (int64_t)E * NBH * NBO * 256, s_b0 = E * hp, s_bh = 3 * E * hp,
-                s_bhd = (int64_t)E * NBO * 16;
+                s_bhd = (int64_t)E * 3 * NBO * 16;
   const int64_t total = s_w0 + s_wh + s_whd + s_b0 + s_bh + s_bhd + 2 * 64 + 2 * 64;
   if (!h->buf) MOPO_HIP(hipMalloc(&h->buf, total * sizeof(float)));
   float* base = h->buf;
@@ -408,7 +439,18 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
     rc |= packb(Bv[1 + l], bh + l * E * hp, H, (int)hp);
   }
   rc |= pack(head.data(), head.size(), whd, H, 2 * D, NBH, NBO);
-  rc |= packb(headb.data(), bhd, 2 * D, NBO * 16);
+  {  // head aux [E][bias | max_logvar | min_logvar], NBO*16 each (logvar bounds at columns D..2D-1)
+    std::vector<float> aux((size_t)s_bhd, 0.f);
+    for (int e = 0; e < E; ++e) {
+      float* x = aux.data() + (size_t)e * 3 * NBO * 16;
+      for (int j = 0; j < 2 * D; ++j) x[j] = headb[(size_t)e * 2 * D + j];
+      for (int dd = 0; dd < D; ++dd) {
+        x[NBO * 16 + D + dd] = arrs[h->smv ? 14 : 12][dd];
+        x[2 * NBO * 16 + D + dd] = arrs[h->smv ? 15 : 13][dd];
+      }
+    }
+    MOPO_HIP(hipMemcpy(bhd, aux.data(), aux.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
   if (h->dtype == 1 && rc == 0) {
     // bf16 fragments: [E][1][NB2] | [3][E][KG][NB2] | [E][KG][NBO], 256 floats (= 512 bf16) each
     const int NB2 = d.NB2, KG = NB2 / 2;

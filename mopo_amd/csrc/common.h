@@ -41,6 +41,15 @@ __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<
 // ------------------------------------------------------------------ activations (TF1 f32 semantics)
 __device__ __forceinline__ float swishf(float x) { return x * (1.0f / (1.0f + expf(-x))); }
 
+// tf.nn.softplus (Eigen select form, thresholds as softplusf) on v_exp_f32 / v_log_f32
+__device__ __forceinline__ float softplus_fast(float x) {
+  const float thr = -13.942385f;
+  const float ex = __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
+  if (x > -thr) return x;
+  if (x < thr) return ex;
+  return __builtin_amdgcn_logf(ex + 1.0f) * 0.6931471805599453f;
+}
+
 // swish on the hardware transcendentals: x * rcp(1 + 2^(-x log2 e)) -- v_exp_f32 / v_rcp_f32 (1 ulp
 // each) instead of the range-reduced expf and the IEEE divide (~25 VALU instructions per element in
 // the ensemble forward's epilogues).  For x -> -inf the exp overflows to inf and rcp gives 0.

@@ -29,20 +29,20 @@ __device__ __forceinline__ void stage_slice(const float* __restrict__ src, float
 }
 
 // acc[r][nb] = sum over KG k-groups of W(kg, nb) x in[r][kg]; wf = this member's layer fragments.
-// If `bias` is given, the layer's NB*16 bias values are copied to lds_bias (1 KiB global_load_lds
+// If `bias` is given, the layer's BQ*4 bias values (default NB*16) are copied to lds_bias (1 KiB global_load_lds
 // pieces, one per wave) together with the last k-group's slice, so the barrier that publishes that slice
 // also publishes the bias for the epilogue (bias_swish reads it from LDS).
-template <int NB, int WAVES>
+template <int BQ, int WAVES>
 __device__ __forceinline__ void stage_bias(const float* __restrict__ bias, float* lds_bias, int w, int lane) {
-  constexpr int PIECES = (NB * 4 + 63) / 64;  // 1 KiB (64 quads) per wave-wide copy
+  constexpr int PIECES = (BQ + 63) / 64;  // BQ quads; 1 KiB (64 quads) per wave-wide copy
   static_assert(PIECES <= WAVES, "bias larger than one copy per wave");
   if (w < PIECES) {
-    const int q = min(w * 64 + lane, NB * 4 - 1);
+    const int q = min(w * 64 + lane, BQ - 1);
     __builtin_amdgcn_global_load_lds((const void*)(bias + q * 4), (lds_void_t)(lds_bias + w * 256), 16, 0, 0);
   }
 }
 
-template <int KG, int NB, int R, int WAVES, int SLOT>
+template <int KG, int NB, int R, int WAVES, int SLOT, int BQ = NB * 4>
 __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f32x4 (&in)[R][KG], f32x4 (&acc)[R][NB],
                                           float* lds, int w, int lane, const float* __restrict__ bias = nullptr,
                                           float* lds_bias = nullptr) {
@@ -50,14 +50,23 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f3
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[r][nb] = zero4();
+  // BNN_KNOB_* (scripts/micro/bnn_knobs.hip): timing-only builds with one part removed
+#ifndef BNN_KNOB_NOBARRIER
   __syncthreads();  // every wave is done reading both buffers (previous layer)
+#endif
+#ifndef BNN_KNOB_NOSTAGE
   stage_slice<NB, WAVES>(wf, lds, w, lane);
-  if (KG == 1 && bias) stage_bias<NB, WAVES>(bias, lds_bias, w, lane);
+  if (KG == 1 && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
+#endif
 #pragma unroll
   for (int kg = 0; kg < KG; ++kg) {
+#ifndef BNN_KNOB_NOBARRIER
     __syncthreads();  // vmcnt(0): slice kg landed (all waves); buffer (kg+1)&1 free
+#endif
+#ifndef BNN_KNOB_NOSTAGE
     if (kg + 1 < KG) stage_slice<NB, WAVES>(wf + (kg + 1) * NB * 256, lds + ((kg + 1) & 1) * SLOT, w, lane);
-    if (kg + 2 == KG && bias) stage_bias<NB, WAVES>(bias, lds_bias, w, lane);
+    if (kg + 2 == KG && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
+#endif
     const float* b = lds + (kg & 1) * SLOT;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
@@ -65,7 +74,13 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f3
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r][nb] = mfma4(fr[t], in[r][kg][t], acc[r][nb]);
+        for (int r = 0; r < R; ++r) {
+#ifndef BNN_KNOB_NOMFMA
+          acc[r][nb] = mfma4(fr[t], in[r][kg][t], acc[r][nb]);
+#else
+          acc[r][nb][t] += fr[t] * in[r][kg][t];
+#endif
+        }
     }
   }
 }
