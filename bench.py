@@ -43,6 +43,7 @@ def parse():
     p.add_argument('--cpu-batch', type=int, default=30000)
     p.add_argument('--sac-steps', type=int, default=1000)
     p.add_argument('--cpu-sac-steps', type=int, default=500)
+    p.add_argument('--no-c3', action='store_true', help='skip the secondary C3 (bf16 walker2d) line')
     return p.parse_args()
 
 
@@ -142,6 +143,68 @@ def cpu_baseline(args):
                       '%d transitions in %.2f s' % (B, args.horizon, E, H, trans, dt)}
 
 
+def cpu_baseline_1core(args):
+    """The same oracle rollout with BLAS limited to one thread, on a smaller sample."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:
+        return None
+    a1 = argparse.Namespace(**vars(args))
+    a1.cpu_batch = 15000
+    with threadpool_limits(limits=1):
+        r = cpu_baseline(a1)
+    r['cores'] = 1
+    return r
+
+
+BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense MFMA
+
+
+def c3_leg(args, dev):
+    """BASELINE config C3: walker2d-style rollout, bf16 ensemble (f32 accumulate / post-processing),
+    E=7, H=200, B=100,000, horizon 1, live walker2d terminations, penalty 1.0 (synthetic weights)."""
+    import torch
+    from mopo_amd.bnn import construct_model
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout, init_sac_params
+    from mopo_amd.static import TERM_WALKER2D
+    B, h = 100000, 1
+    rs = np.random.RandomState(3)
+    env_obs = rs.normal(size=(ENV_ROWS, O)).astype(np.float32)
+    env_obs[:, 0] = rs.uniform(0.7, 2.1, ENV_ROWS)                          # walker height
+    env_obs[:, 1] = rs.uniform(-1.1, 1.1, ENV_ROWS)                         # walker angle
+    model = construct_model(obs_dim=O, act_dim=A, hidden_dim=H, num_networks=E, num_elites=ELITES,
+                            separate_mean_var=True, seed=1, dtype='bf16')
+    mats = model.get_params()
+    x = np.concatenate([env_obs, rs.uniform(-1, 1, (ENV_ROWS, A))], 1)
+    mats[0] = x.mean(0, keepdims=True).astype(np.float32)
+    mats[1] = x.std(0, keepdims=True).astype(np.float32)
+    model.set_params(mats)
+    model.set_elites([0, 1, 2, 3, 4])
+    pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=5 * B)
+    ro = ModelRollout(model, B, h)
+    pi = torch.from_numpy(init_sac_params(O, A, HP, seed=2)).to(dev)
+    env = torch.from_numpy(env_obs).to(dev)
+    tk = TERM_WALKER2D
+    ro.run(env, pi, pool, B, h, tk, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=0)
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    tot = [ro.run(env, pi, pool, B, h, tk, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=1 + i) for i in range(reps)]
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n = int(sum(int(t.sum().item()) for t in tot))
+    v = n / dt
+    flop_row = FLOP_BNN_ROW
+    return {'metric': 'model-rollout transitions/s (C3: walker2d-style, bf16 ensemble)', 'value': v,
+            'unit': 'transitions/s', 'dtype': 'bf16 (f32 accumulate)', 'ms_per_rollout': dt / reps * 1e3,
+            'config': {'workload': 'E=7, H=200, obs=17, act=6, rollout_batch=100000, horizon=1, walker2d '
+                                   'terminations, penalty_coeff=1.0', 'rollout_batch_per_gpu': B, 'horizon': h},
+            'bnn_flop_per_row': flop_row,
+            'ensemble_tflops_upper_bound': v * flop_row / 1e12,
+            'bf16_peak_tflops': BF16_PEAK_TFLOPS}
+
+
 SAC_DIAG = {}
 
 
@@ -235,6 +298,7 @@ def main():
         if staging is not None:
             total = total  # counts are already global (gathered)
     sac_rate = sac_leg(args, pool, env, dev, world)
+    c3 = c3_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
@@ -267,8 +331,11 @@ def main():
                 'per_gpu': sac_rate, 'aggregate_replicas': sac_rate * world, 'steps_timed': args.sac_steps,
                 'us_per_step': 1e6 / sac_rate, **SAC_DIAG, 'parallelism': 'replicas only (one independent learner per GPU)'},
     }
+    if c3 is not None:
+        out['extra_configs'] = {'C3': c3}
     if not args.no_cpu_baseline and world == 1:
         out['cpu_baseline'] = cpu_baseline(args)
+        out['cpu_baseline_1core'] = cpu_baseline_1core(args)
         out['cpu_baseline_sac'] = cpu_baseline_sac(args)
     print(json.dumps(out))
     if world > 1:
