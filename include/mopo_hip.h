@@ -19,6 +19,9 @@
  *   mopo_pool_gather  FlexibleReplayPool.random_batch / batch_by_indices (flexible_replay_pool.py:85-135)
  *   mopo_sac_*        MOPO._do_training / _update_target (mopo/algorithms/mopo.py:834-853,
  *                     graph mopo.py:204-466); SAC API sac.py:26-47
+ *   mopo_bnn_train_*  BNN.train (mopo/models/bnn.py:369-503; loss :226-249, 677-701; Adam
+ *                     constructor.py:41), format_samples_for_training (constructor.py:46-57),
+ *                     caller MOPO._train_model (mopo/algorithms/mopo.py:713-721)
  *   mopo_mt_*         numpy legacy RandomState (MT19937) as used by fake_env.py:72,
  *                     bnn.py:343, flexible_replay_pool.py:87
  */
@@ -121,6 +124,42 @@ int mopo_pool_gather(const mopo_pool_desc* pool, int obs_dim, int act_dim, const
 /* uniform random indices in [0, size) from Philox (perf mode of random_indices). */
 int mopo_pool_random_indices(const mopo_pool_desc* pool, int64_t n, uint64_t seed, uint32_t step,
                              int64_t* d_idx, void* stream);
+
+/* ---- ensemble training (BNN.train, bnn.py:369-503) -------------------------------------
+ * Training state of an smv ensemble (E members, 4 swish layers of width H, mean + log-var heads).
+ * The host drives the loop (holdout split, bootstrap indices, early stopping, elites: bnn.py:369-503)
+ * with numpy's stream; these calls are its device parts.  lr: tf.train.AdamOptimizer (1e-3,
+ * constructor.py:41).  max_batch: minibatch rows per member (256, mopo.py:529); max_eval: rows of
+ * one mse evaluation (holdout <= 1000, bnn.py:392). */
+typedef struct mopo_bnn_train_s* mopo_bnn_train_t;
+int mopo_bnn_train_create(mopo_bnn_train_t* out, int E, int obs_dim, int act_dim, int hidden, int max_batch,
+                          int max_eval, float lr);
+int mopo_bnn_train_destroy(mopo_bnn_train_t h);
+/* The 16 .mat arrays (smv layout, as mopo_bnn_set_params; host f32).  set resets the optimizer. */
+int mopo_bnn_train_set_params(mopo_bnn_train_t h, const float* const* h_arrays);
+int mopo_bnn_train_get_params(mopo_bnn_train_t h, float* const* h_arrays);
+/* format_samples_for_training (constructor.py:46-57) of pool rows d_rows[n] (NULL: rows 0..n-1):
+ * d_inputs [n, O+A] = [obs | act], d_targets [n, O+1] = [rew | next_obs - obs]. */
+int mopo_bnn_format_samples(const mopo_pool_desc* pool, int obs_dim, int act_dim, const int64_t* d_rows,
+                            int64_t n, float* d_inputs, float* d_targets, void* stream);
+/* TensorStandardScaler.fit (utils.py:69-86) on d_inputs [n, O+A]. */
+int mopo_bnn_train_fit_scaler(mopo_bnn_train_t h, const float* d_inputs, int64_t n, void* stream);
+/* One epoch of minibatch Adam steps (bnn.py:425-432): minibatch b of member e is rows
+ * d_idxs[e * n_idx + b * batch .. +batch) (int32) of d_inputs / d_targets; the last one may be partial. */
+int mopo_bnn_train_epoch(mopo_bnn_train_t h, const float* d_inputs, const float* d_targets, const int32_t* d_idxs,
+                         int64_t n_idx, int batch, void* stream);
+/* _compile_losses(inc_var_loss=False) (bnn.py:677-701) per member over rows d_rows[e * n + r]
+ * (NULL: rows 0..n-1 for every member, the tiled holdout set) -> d_losses[E] f32. */
+int mopo_bnn_train_eval_mse(mopo_bnn_train_t h, const float* d_inputs, const float* d_targets,
+                            const int32_t* d_rows, int n, float* d_losses, void* stream);
+/* shuffle_rows (bnn.py:385-387): d_idxs[e] <- d_idxs[e][argsort(d_keys[e])], keys f64 [E, n]
+ * (the np.random.uniform draws). */
+int mopo_bnn_train_shuffle(mopo_bnn_train_t h, int32_t* d_idxs, const double* d_keys, int64_t n, void* stream);
+/* _save_state(member) / _set_state (bnn.py:264-285). */
+int mopo_bnn_train_snapshot(mopo_bnn_train_t h, int member, void* stream);
+int mopo_bnn_train_restore(mopo_bnn_train_t h, void* stream);
+/* h_logs[0] = data term of the last minibatch's training loss. */
+int mopo_bnn_train_logs(mopo_bnn_train_t h, float* h_logs, int n);
 
 /* ---- fused model rollout (MOPO._rollout_model) ----------------------------------------- */
 typedef struct mopo_rollout_s* mopo_rollout_t;

@@ -55,6 +55,19 @@ SIGNATURES = {
     'mopo_pool_gather': (c_int, [C.POINTER(PoolDesc), c_int, c_int, c_void_p, c_i64, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
     'mopo_pool_random_indices': (c_int, [C.POINTER(PoolDesc), c_i64, c_u64, c_u32, c_void_p, c_void_p]),
+    'mopo_bnn_train_create': (c_int, [C.POINTER(c_void_p), c_int, c_int, c_int, c_int, c_int, c_int, C.c_float]),
+    'mopo_bnn_train_destroy': (c_int, [c_void_p]),
+    'mopo_bnn_train_set_params': (c_int, [c_void_p, C.POINTER(c_void_p)]),
+    'mopo_bnn_train_get_params': (c_int, [c_void_p, C.POINTER(c_void_p)]),
+    'mopo_bnn_format_samples': (c_int, [C.POINTER(PoolDesc), c_int, c_int, c_void_p, c_i64, c_void_p, c_void_p,
+                                        c_void_p]),
+    'mopo_bnn_train_fit_scaler': (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
+    'mopo_bnn_train_epoch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p]),
+    'mopo_bnn_train_eval_mse': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    'mopo_bnn_train_shuffle': (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
+    'mopo_bnn_train_snapshot': (c_int, [c_void_p, c_int, c_void_p]),
+    'mopo_bnn_train_restore': (c_int, [c_void_p, c_void_p]),
+    'mopo_bnn_train_logs': (c_int, [c_void_p, c_void_p, c_int]),
     'mopo_rollout_create': (c_int, [C.POINTER(c_void_p), c_void_p, c_i64, c_int]),
     'mopo_rollout_destroy': (c_int, [c_void_p]),
     'mopo_rollout_run': (c_int, [c_void_p, C.POINTER(RolloutArgs), C.POINTER(PoolDesc), c_void_p]),

@@ -5,12 +5,17 @@ Mirrors the reference surface used on the hot path:
   * ``BNN.predict(inputs, factored=True)``   mopo/models/bnn.py:508-546
   * ``BNN.random_inds(batch_size)``          mopo/models/bnn.py:342-344
   * ``BNN.load_params`` / ``.mat`` layout    mopo/models/bnn.py:276-281, 588-592
+  * ``BNN.train(inputs, targets, ...)``      mopo/models/bnn.py:369-503 (+ validate :351-362)
   * ``num_nets``, ``num_elites``, ``_model_inds``, ``scaler.cached_mu/cached_sigma``
-The forward runs in the HIP kernel ``bnn_fwd_kernel`` (csrc/bnn.hip); there is no CPU path.
-Ensemble training (BNN.train, bnn.py:369-503) is a later-round item.
+The forward runs in the HIP kernel ``bnn_fwd_kernel`` (csrc/bnn.hip); training steps in
+csrc/bnn_train.hip (the loop control and numpy's RNG stream stay here, in the reference's order).
+There is no CPU path.
 """
 import ctypes as C
+import itertools
 import os
+import time
+from collections import OrderedDict
 
 import numpy as np
 
@@ -71,6 +76,10 @@ class BNN:
         self._h = h
 
     def __del__(self):
+        t = getattr(self, '_train_h', None)
+        if t is not None and t.value:
+            L.lib().mopo_bnn_train_destroy(t)
+            self._train_h = None
         h = getattr(self, '_h', None)
         if h is not None and h.value:
             L.lib().mopo_bnn_destroy(h)
@@ -149,6 +158,126 @@ class BNN:
         if is_np:
             return mean.cpu().numpy(), var.cpu().numpy()
         return mean, var
+
+    # -- training (bnn.py:369-503) ---------------------------------------------------------------------
+    def _trainer(self, batch_size, max_eval):
+        t = getattr(self, '_train_h', None)
+        if t is None or self._train_dims != (batch_size, max_eval):
+            if t is not None:
+                L.lib().mopo_bnn_train_destroy(t)
+            t = C.c_void_p()
+            L.check(L.lib().mopo_bnn_train_create(C.byref(t), self.num_nets, self.obs_dim, self.act_dim,
+                                                  self.hidden_dim, int(batch_size), int(max_eval), 1e-3))
+            self._train_h, self._train_dims = t, (batch_size, max_eval)
+        return t
+
+    def _train_params(self, t, mats=None):
+        if mats is not None:
+            arr = (C.c_void_p * 16)(*[m.ctypes.data for m in mats])
+            L.check(L.lib().mopo_bnn_train_set_params(t, arr))
+            return None
+        out = [np.empty_like(m) for m in self._mats]
+        arr = (C.c_void_p * 16)(*[m.ctypes.data for m in out])
+        L.check(L.lib().mopo_bnn_train_get_params(t, arr))
+        return out
+
+    def train(self, inputs, targets, batch_size=32, max_epochs=None, max_epochs_since_update=5,
+              hide_progress=False, holdout_ratio=0.0, max_logging=1000, max_grad_updates=None, timer=None,
+              max_t=None, permuted=False):
+        """BNN.train (bnn.py:369-503).  ``inputs`` [N, O+A] / ``targets`` [N, O+1]: numpy (the
+        reference API) or cuda tensors.  ``permuted=True``: the rows are already in
+        ``np.random.permutation`` order (the permutation was drawn by the caller, as
+        ``MOPO._train_model`` does when it formats the device pool in that order)."""
+        import torch
+        if not self.separate_mean_var:
+            raise NotImplementedError('training is implemented for separate_mean_var=True (all D4RL configs)')
+        E = self.num_nets
+        N = int(inputs.shape[0])
+        num_holdout = min(int(N * holdout_ratio), max_logging)
+        if not permuted:
+            permutation = np.random.permutation(N)                                  # bnn.py:391-394
+            if isinstance(inputs, np.ndarray):
+                inputs, targets = inputs[permutation], targets[permutation]
+            else:
+                p = torch.from_numpy(permutation).to(inputs.device)
+                inputs, targets = inputs[p], targets[p]
+        dev = 'cuda'
+
+        def dt(x):
+            if isinstance(x, np.ndarray):
+                return torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(dev)
+            return x.to(dev, torch.float32).contiguous()
+
+        x_all, y_all = dt(inputs), dt(targets)
+        hold_x, hold_y = x_all[:num_holdout], y_all[:num_holdout]
+        x, y = x_all[num_holdout:], y_all[num_holdout:]
+        n = N - num_holdout
+        t = self._trainer(batch_size, max(max_logging, 1))
+        self._train_params(t, self._mats)
+        L.check(L.lib().mopo_bnn_train_fit_scaler(t, L.ptr(x), n, None))          # bnn.py:399-400
+        idxs = torch.from_numpy(np.random.randint(n, size=[E, n]).astype(np.int32)).to(dev)  # :402
+        self._start_train()
+        losses_d = torch.empty(E, dtype=torch.float32, device=dev)
+        break_train, grad_updates, epoch = False, 0, 0
+        self._max_epochs_since_update = max_epochs_since_update
+        t0 = time.time()
+        for epoch in (range(max_epochs) if max_epochs is not None else itertools.count()):
+            L.check(L.lib().mopo_bnn_train_epoch(t, L.ptr(x), L.ptr(y), L.ptr(idxs), n, int(batch_size), None))
+            grad_updates += int(np.ceil(n / batch_size))
+            keys = torch.from_numpy(np.random.uniform(size=[E, n])).to(dev)      # shuffle_rows :385-387
+            L.check(L.lib().mopo_bnn_train_shuffle(t, L.ptr(idxs), L.ptr(keys), n, None))
+            if not hide_progress and holdout_ratio >= 1e-12 and num_holdout > 0:
+                L.check(L.lib().mopo_bnn_train_eval_mse(t, L.ptr(hold_x), L.ptr(hold_y), None, num_holdout,
+                                                        L.ptr(losses_d), None))
+                holdout_losses = losses_d.cpu().numpy().astype(np.float64)
+                break_train = self._save_best(t, epoch, holdout_losses)
+            if break_train or (max_grad_updates and grad_updates > max_grad_updates):
+                break
+            if max_t and time.time() - t0 > max_t:
+                break
+        L.check(L.lib().mopo_bnn_train_restore(t, None))                           # _set_state :491
+        if num_holdout > 0:
+            L.check(L.lib().mopo_bnn_train_eval_mse(t, L.ptr(hold_x), L.ptr(hold_y), None, num_holdout,
+                                                    L.ptr(losses_d), None))
+            holdout_losses = losses_d.cpu().numpy().astype(np.float64)
+        else:
+            holdout_losses = np.full(E, np.nan)
+        self._end_train(holdout_losses)
+        self.set_params(self._train_params(t))                                     # repack for inference
+        self._train_epochs, self._train_grad_updates = epoch + 1, grad_updates
+        val_loss = np.sort(holdout_losses)[:self.num_elites].mean()
+        return OrderedDict({'val_loss': val_loss})
+
+    def _start_train(self):                                                         # bnn.py:324-327
+        self._snapshots = {i: (None, 1e10) for i in range(self.num_nets)}
+        self._epochs_since_update = 0
+
+    def _save_best(self, t, epoch, holdout_losses):                                  # bnn.py:301-322
+        updated = False
+        for i in range(len(holdout_losses)):
+            current = holdout_losses[i]
+            _, best = self._snapshots[i]
+            if (best - current) / best > 0.01:
+                self._snapshots[i] = (epoch, current)
+                L.check(L.lib().mopo_bnn_train_snapshot(t, i, None))
+                updated = True
+        self._epochs_since_update = 0 if updated else self._epochs_since_update + 1
+        return self._epochs_since_update > self._max_epochs_since_update
+
+    def _end_train(self, holdout_losses):                                            # bnn.py:329-332
+        self._model_inds = np.argsort(holdout_losses)[:self.num_elites].tolist()
+        self._holdout_losses = holdout_losses
+
+    def validate(self, inputs, targets):
+        """bnn.py:351-362: mean of the num_elites smallest per-member mse losses."""
+        import torch
+        t = self._trainer(*getattr(self, '_train_dims', (256, max(int(inputs.shape[0]), 1))))
+        self._train_params(t, self._mats)
+        x = torch.from_numpy(np.ascontiguousarray(inputs, np.float32)).cuda()
+        y = torch.from_numpy(np.ascontiguousarray(targets, np.float32)).cuda()
+        out = torch.empty(self.num_nets, dtype=torch.float32, device='cuda')
+        L.check(L.lib().mopo_bnn_train_eval_mse(t, L.ptr(x), L.ptr(y), None, int(x.shape[0]), L.ptr(out), None))
+        return np.sort(out.cpu().numpy())[:self.num_elites].mean()
 
     def random_inds(self, batch_size):
         """bnn.py:342-344 (numpy legacy global stream, as the reference)."""

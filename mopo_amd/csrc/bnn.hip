@@ -330,10 +330,11 @@ static int launch_bf16(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) 
 int launch_bnn_fwd(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) {
   if (!h->has_params) return fail("bnn: parameters not set (mopo_bnn_set_params)");
   if (h->dtype == 1) return launch_bf16(h, mode, a, s);
-  if (h->dev.KG0 != 2) return fail("bnn: obs_dim + act_dim must be in (16, 32]");
+  if (h->dev.KG0 != 1 && h->dev.KG0 != 2) return fail("bnn: obs_dim + act_dim must be <= 32");
+  const bool k1 = h->dev.KG0 == 1;  // hopper: 11 + 3 inputs
   switch (h->dev.NBO) {
-    case 3: return launch_fwd_h<2, 3>(h, mode, a, s);
-    case 2: return launch_fwd_h<2, 2>(h, mode, a, s);
+    case 3: return k1 ? launch_fwd_h<1, 3>(h, mode, a, s) : launch_fwd_h<2, 3>(h, mode, a, s);
+    case 2: return k1 ? launch_fwd_h<1, 2>(h, mode, a, s) : launch_fwd_h<2, 2>(h, mode, a, s);
   }
   return fail("bnn: unsupported output dim");
 }

@@ -1,0 +1,687 @@
+// Probabilistic-ensemble training step (BNN.train) on CDNA4.
+//
+// Replaces the TF training graph of BNN.finalize (mopo/models/bnn.py:226-249: Gaussian NLL of
+// _compile_losses :677-701 + weight decay fc.py:156-157 + 0.01 (sum maxlv - sum minlv), one
+// tf.train.AdamOptimizer(1e-3) over all optvars, constructor.py:41) and the per-minibatch
+// session.run of BNN.train (bnn.py:425-432); _compile_losses(inc_var_loss=False) for the holdout
+// losses (bnn.py:463-475, 486-493); shuffle_rows (:385-387); _save_state / _set_state (:264-285).
+// The loop control (holdout split, bootstrap indices, early stopping, elites) stays on the host
+// (mopo_amd/bnn.py), drawing from numpy's global stream in the reference's order.
+//
+// One minibatch step = 12 launches: gather (bootstrap rows, scaler), 5 grouped-GEMM forward
+// launches (E problems each: swish layers write the pre-activation for the backward), the
+// loss kernel (output gradients, max/min log-var gradients + their Adam, this step's lr_t), and
+// 5 grouped-GEMM backward launches, whose weight-gradient tiles apply weight decay and the TF1 Adam
+// in their epilogue (gemm_group.h; parameters ping-pong between two buffers).  Full-batch steps are
+// captured into hipGraphs (8 / 2 / 1+copy-back steps); the epoch's partial last batch runs eagerly.
+//
+// Parameter layout (training master copy, f32): per member, the reference's optvars with the two
+// smv heads concatenated column-wise so one GEMM serves both:
+//   W0 [E][IN][H] b0 [E][H]  W1..W3 [E][H][H] b1..b3 [E][H]  Whd [E][H][2D] bhd [E][2D]
+//   maxlv [D] minlv [D]        (Whd[e][k][n]: n < D mean head, n >= D log-var head)
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include <hipcub/hipcub.hpp>
+
+#include "gemm_group.h"
+
+namespace mopo {
+
+namespace {
+
+constexpr int NHID = 4;
+const float WDECAY[NHID + 1] = {0.000025f, 0.00005f, 0.000075f, 0.000075f, 0.0001f};  // constructor.py:30-36
+
+struct Layout {
+  int E, IN, H, D;
+  int64_t W[NHID + 1], b[NHID + 1];  // offsets (layer NHID = concatenated heads)
+  int64_t mx, mn, total;
+};
+
+Layout make_layout(int E, int IN, int H, int D) {
+  Layout L{};
+  L.E = E; L.IN = IN; L.H = H; L.D = D;
+  int64_t c = 0;
+  for (int l = 0; l <= NHID; ++l) {
+    const int in = l == 0 ? IN : H, out = l == NHID ? 2 * D : H;
+    L.W[l] = c; c += (int64_t)E * in * out;
+    L.b[l] = c; c += (int64_t)E * out;
+  }
+  L.mx = c; c += D;
+  L.mn = c; c += D;
+  L.total = c;
+  return L;
+}
+
+struct Train {
+  Layout L{};
+  int maxM = 0, max_batch = 0, max_eval = 0;
+  float lr = 1e-3f;
+  void* mem = nullptr;
+  float *Pb[2] = {nullptr, nullptr}, *G = nullptr, *M = nullptr, *V = nullptr, *S = nullptr;  // S: snapshots
+  float* beta_pow = nullptr;   // [3]: beta1^t, beta2^t, this step's lr_t
+  int* bstep = nullptr;        // minibatch index within the epoch (device)
+  unsigned* ticket = nullptr;
+  float* part = nullptr;       // loss-kernel block partials
+  float* logs = nullptr;       // [4]: last train loss (data term), ...
+  float *mu = nullptr, *sigma = nullptr;
+  float *X = nullptr, *T = nullptr, *Z[NHID] = {}, *Hh[NHID] = {}, *OUT = nullptr, *dOUT = nullptr, *dZ[NHID] = {};
+  std::vector<int> snap;       // members with a snapshot
+  // graphs (full-batch steps), keyed by the epoch's data pointers
+  hipStream_t gs = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
+  hipGraph_t graph[3] = {nullptr, nullptr, nullptr};
+  const void* gkey[4] = {nullptr, nullptr, nullptr, nullptr};
+  int64_t gkey_n = -1; int gkey_b = -1;
+  // shuffle workspace
+  void* sort_tmp = nullptr; size_t sort_tmp_bytes = 0;
+  double* sort_keys = nullptr; int32_t* sort_vals_in = nullptr; int32_t* sort_vals = nullptr; int* seg = nullptr;
+  int64_t sort_cap = 0;
+};
+
+constexpr int LOSS_TPB = 256;
+
+// ---- minibatch gather: X[e][r] = scaler(inputs[row]), T[e][r] = targets[row] ----------------
+// row = rows[e * stride + base + r] with base = (*bstep) * batch (training) or 0 (evaluation);
+// rows == NULL: row = r for every member.
+__global__ void train_gather_kernel(const float* __restrict__ inputs, const float* __restrict__ targets,
+                                    const int32_t* __restrict__ rows, int64_t stride, const int* __restrict__ bstep,
+                                    int batch, int M, int E, int IN, int D, const float* __restrict__ mu,
+                                    const float* __restrict__ sigma, float* __restrict__ X, float* __restrict__ T) {
+  const int W = IN + D;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= (int64_t)E * M * W) return;
+  const int c = i % W;
+  const int64_t er = i / W;
+  const int r = er % M, e = er / M;
+  const int64_t base = bstep ? (int64_t)(*bstep) * batch : 0;
+  const int64_t row = rows ? rows[e * stride + base + r] : r;
+  if (c < IN) X[er * IN + c] = (inputs[row * IN + c] - mu[c]) / sigma[c];   // utils.py:96
+  else T[er * D + (c - IN)] = targets[row * D + (c - IN)];
+}
+
+// ---- training loss gradient (bnn.py:241-249, 677-701): block = (dim d, 256 (member, row) pairs)
+// mean = OUT[..., d], raw log-var = OUT[..., D + d];  lv1 = mx - softplus(mx - raw),
+// lv = mn + softplus(lv1 - mn) (bnn.py:669-670).  d/dmean = 2 (mean - y) e^-lv / (M D),
+// d/dlv = (1 - (mean - y)^2 e^-lv) / (M D); softplus' = sigmoid.
+// The last block to finish reduces the per-dim partials (in block order), adds the 0.01 terms,
+// applies Adam to max/min log-var, fixes this step's lr_t and advances beta powers and bstep.
+struct LossArgs {
+  int E, M, D;
+  const float* OUT; const float* T; float* dOUT;
+  float* part; unsigned* ticket; float* logs; float* beta_pow; int* bstep; float lr;
+  int64_t off_mx, off_mn;
+  float* G;                          // gradient buffer (max/min log-var slots written here)
+  AdamCtx ad;
+};
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+__global__ __launch_bounds__(LOSS_TPB) void train_loss_kernel(const LossArgs a) {
+  __shared__ float sh[64];
+  __shared__ int last;
+  const int D = a.D, n = a.E * a.M;
+  const int per_d = ceil_div(n, LOSS_TPB);
+  const int d = blockIdx.x / per_d, chunk = blockIdx.x % per_d;
+  const int i = chunk * LOSS_TPB + threadIdx.x;  // (member, row) pair
+  const float mx = a.ad.Pc[a.off_mx + d], mn = a.ad.Pc[a.off_mn + d];
+  float c_mx = 0.f, c_mn = 0.f, c_loss = 0.f;
+  if (i < n) {
+    const float* o = a.OUT + (int64_t)i * 2 * D;
+    const float mean = o[d], raw = o[D + d], y = a.T[(int64_t)i * D + d];
+    const float s = 1.f / ((float)a.M * (float)D);
+    const float lv1 = mx - softplusf(mx - raw);
+    const float lv = mn + softplusf(lv1 - mn);
+    const float inv = expf(-lv);
+    const float err = mean - y;
+    const float dlv = (1.f - err * err * inv) * s;
+    const float sb = sigm(lv1 - mn), sa = sigm(mx - raw);
+    const float dlv1 = dlv * sb;
+    float* g = a.dOUT + (int64_t)i * 2 * D;
+    g[d] = 2.f * err * inv * s;
+    g[D + d] = dlv1 * sa;
+    c_mn = dlv * (1.f - sb);
+    c_mx = dlv1 * (1.f - sa);
+    c_loss = (err * err * inv + lv) * s;
+  }
+  float v[3] = {c_mx, c_mn, c_loss};
+  {  // block sums (butterfly per wave, waves in order)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) sh[w * 3 + k] = v[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t[3] = {0.f, 0.f, 0.f};
+      for (int q = 0; q < LOSS_TPB / 64; ++q)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) t[k] += sh[q * 3 + k];
+      float* pp = a.part + 4 * (int64_t)blockIdx.x;
+      pp[0] = t[0]; pp[1] = t[1]; pp[2] = t[2];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (tk == gridDim.x - 1);
+      if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  // this step's TF1 Adam step size from the pre-update beta powers (every thread reads them
+  // before thread 0 advances them below)
+  const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
+  const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  __syncthreads();
+  if ((int)threadIdx.x < D) {
+    const int dd = threadIdx.x;
+    float gmx = 0.f, gmn = 0.f, loss = 0.f;
+    for (int c = 0; c < per_d; ++c) {
+      const float* pp = a.part + 4 * (int64_t)(dd * per_d + c);
+      gmx += pp[0]; gmn += pp[1]; loss += pp[2];
+    }
+    gmx += 0.01f;                                                   // 0.01 * sum(max_logvar)
+    gmn -= 0.01f;                                                   // -0.01 * sum(min_logvar)
+    a.G[a.off_mx + dd] = gmx;
+    a.G[a.off_mn + dd] = gmn;
+    adam_apply(a.ad, a.off_mx + dd, gmx, adam_load(a.ad, a.off_mx + dd), lr_t);
+    adam_apply(a.ad, a.off_mn + dd, gmn, adam_load(a.ad, a.off_mn + dd), lr_t);
+    sh[dd] = loss;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float loss = 0.f;
+    for (int dd = 0; dd < D; ++dd) loss += sh[dd];
+    a.logs[0] = loss;                                               // data term of the train loss
+    a.beta_pow[2] = lr_t;
+    a.beta_pow[0] = b1p * 0.9f;
+    a.beta_pow[1] = b2p * 0.999f;
+    if (a.bstep) *a.bstep += 1;
+    *a.ticket = 0u;
+  }
+}
+
+// ---- mse loss per member (inc_var_loss=False): mean over rows and dims of (mean - y)^2 --------
+__global__ __launch_bounds__(256) void train_mse_kernel(const float* __restrict__ OUT, const float* __restrict__ T,
+                                                        int M, int D, float* __restrict__ losses) {
+  __shared__ float sh[4];
+  const int e = blockIdx.x;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < M * D; i += blockDim.x) {
+    const int r = i / D, d = i % D;
+    const float err = OUT[((int64_t)e * M + r) * 2 * D + d] - T[((int64_t)e * M + r) * D + d];
+    acc += err * err;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) losses[e] = (sh[0] + sh[1] + sh[2] + sh[3]) / ((float)M * (float)D);
+}
+
+// ---- scaler fit (utils.py:69-86): mean / std over rows, f64 accumulation, std < 1e-12 -> 1 ----
+__global__ __launch_bounds__(256) void scaler_fit_kernel(const float* __restrict__ x, int64_t n, int IN,
+                                                         float* __restrict__ mu, float* __restrict__ sigma) {
+  __shared__ double sh[4];
+  const int c = blockIdx.x;
+  double s = 0.0;
+  for (int64_t r = threadIdx.x; r < n; r += blockDim.x) s += x[r * IN + c];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const double mean = (sh[0] + sh[1] + sh[2] + sh[3]) / (double)n;
+  __syncthreads();
+  double q = 0.0;
+  for (int64_t r = threadIdx.x; r < n; r += blockDim.x) {
+    const double dv = x[r * IN + c] - mean;
+    q += dv * dv;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double sd = sqrt((sh[0] + sh[1] + sh[2] + sh[3]) / (double)n);
+    mu[c] = (float)mean;
+    sigma[c] = sd < 1e-12 ? 1.f : (float)sd;
+  }
+}
+
+// ---- format_samples_for_training (constructor.py:46-57) over pool rows ---------------------
+__global__ void format_kernel(const mopo_pool_desc p, int O, int A, const int64_t* __restrict__ rows, int64_t n,
+                              float* __restrict__ inputs, float* __restrict__ targets) {
+  const int IN = O + A, D = O + 1, W = IN + D;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n * W) return;
+  const int64_t r = i / W;
+  const int c = i % W;
+  const int64_t src = rows ? rows[r] : r;
+  if (c < O) inputs[r * IN + c] = p.d_obs[src * O + c];
+  else if (c < IN) inputs[r * IN + c] = p.d_act[src * A + (c - O)];
+  else if (c == IN) targets[r * D] = p.d_rew[src];
+  else targets[r * D + (c - IN)] = p.d_next_obs[src * O + (c - IN - 1)] - p.d_obs[src * O + (c - IN - 1)];
+}
+
+// ---- per-member variable copy (snapshots): dir 0: P -> S, 1: S -> P for member e ------------
+struct MemberSpan { int64_t off[2 * (NHID + 1)]; int64_t len[2 * (NHID + 1)]; };
+
+__global__ void member_copy_kernel(float* __restrict__ P, float* __restrict__ S, const MemberSpan sp, int e,
+                                   int dir) {
+  const int k = blockIdx.y;
+  const int64_t len = sp.len[k], off = sp.off[k] + (int64_t)e * len;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x) {
+    if (dir == 0) S[off + i] = P[off + i];
+    else P[off + i] = S[off + i];
+  }
+}
+
+MemberSpan member_span(const Layout& L) {
+  MemberSpan s{};
+  for (int l = 0; l <= NHID; ++l) {
+    const int in = l == 0 ? L.IN : L.H, out = l == NHID ? 2 * L.D : L.H;
+    s.off[2 * l] = L.W[l]; s.len[2 * l] = (int64_t)in * out;
+    s.off[2 * l + 1] = L.b[l]; s.len[2 * l + 1] = out;
+  }
+  return s;
+}
+
+// ---- shuffle_rows: idx[e] <- idx[e][order[e]] ---------------------------------------------
+__global__ void apply_order_kernel(const int32_t* __restrict__ order, const int32_t* __restrict__ src, int64_t n,
+                                   int E, int32_t* __restrict__ dst) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n * E) return;
+  const int64_t e = i / n;
+  dst[i] = src[e * n + order[i]];
+}
+
+__global__ void iota_kernel(int32_t* v, int64_t n, int E, int* seg) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n * E) v[i] = (int32_t)(i % n);
+  if (i <= E) seg[i] = (int)(i * n);
+}
+
+// ---------------------------------------------------------------------------------------------
+int launch_gather(Train* h, const float* in, const float* tg, const int32_t* rows, int64_t stride, bool use_bstep,
+                  int batch, int M, hipStream_t s) {
+  const Layout& L = h->L;
+  const int64_t tot = (int64_t)L.E * M * (L.IN + L.D);
+  hipLaunchKernelGGL(train_gather_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, in, tg, rows, stride,
+                     use_bstep ? h->bstep : nullptr, batch, M, L.E, L.IN, L.D, h->mu, h->sigma, h->X, h->T);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+// forward of the 4 swish layers + heads on X (M rows per member) with parameters P
+int forward(Train* h, const float* P, int M, hipStream_t s) {
+  const Layout& L = h->L;
+  const int E = L.E, H = L.H, IN = L.IN, D2 = 2 * L.D;
+  for (int l = 0; l <= NHID; ++l) {
+    const int K = l == 0 ? IN : H, N = l == NHID ? D2 : H;
+    const float* A = l == 0 ? h->X : h->Hh[l - 1];
+    std::vector<GemmProb> g;
+    for (int e = 0; e < E; ++e) {
+      auto p = mk(M, N, K, A + (int64_t)e * M * K, K, 0, P + L.W[l] + (int64_t)e * K * N, N, 0,
+                  (l == NHID ? h->OUT : h->Hh[l]) + (int64_t)e * M * N, N);
+      p.bias = P + L.b[l] + (int64_t)e * N;
+      if (l < NHID) { p.act = ACT_SWISH; p.Z = h->Z[l] + (int64_t)e * M * N; }
+      g.push_back(p);
+    }
+    if (launch_group(g, s)) return -1;
+  }
+  return 0;
+}
+
+// one minibatch Adam step on the gathered X/T (M rows per member): P = Pb[par] -> Pb[1 - par]
+int step_impl(Train* h, int par, int M, bool use_bstep, hipStream_t s) {
+  const Layout& L = h->L;
+  const int E = L.E, H = L.H, IN = L.IN, D = L.D, D2 = 2 * D;
+  const float* P = h->Pb[par];
+  if (forward(h, P, M, s)) return -1;
+  AdamCtx ad{};
+  ad.G = h->G; ad.Pc = h->Pb[par]; ad.Pn = h->Pb[1 - par]; ad.M = h->M; ad.V = h->V; ad.T = nullptr;
+  ad.lr_t = h->beta_pow + 2; ad.tau = 0.f; ad.total = L.total; ad.n_pi = 0; ad.n_q = 0; ad.norm_part = nullptr;
+  {
+    LossArgs a{};
+    a.E = E; a.M = M; a.D = D; a.OUT = h->OUT; a.T = h->T; a.dOUT = h->dOUT; a.part = h->part; a.ticket = h->ticket;
+    a.logs = h->logs; a.beta_pow = h->beta_pow; a.bstep = use_bstep ? h->bstep : nullptr; a.lr = h->lr;
+    a.off_mx = L.mx; a.off_mn = L.mn; a.G = h->G; a.ad = ad;
+    const int blocks = D * ceil_div(E * M, LOSS_TPB);
+    hipLaunchKernelGGL(train_loss_kernel, dim3(blocks), dim3(LOSS_TPB), 0, s, a);
+    MOPO_HIP(hipGetLastError());
+  }
+  // backward: launch l (l = NHID .. 0) forms dW_l (+ decay, Adam) and, for l >= 1, dZ_{l-1}
+  for (int l = NHID; l >= 0; --l) {
+    const int K = l == 0 ? IN : H, N = l == NHID ? D2 : H;  // layer l: [K -> N]
+    const float* dY = l == NHID ? h->dOUT : h->dZ[l];        // gradient at layer l's output (pre-activation)
+    const float* Xin = l == 0 ? h->X : h->Hh[l - 1];
+    std::vector<GemmProb> g;
+    for (int e = 0; e < E; ++e) {
+      const float* dYe = dY + (int64_t)e * M * N;
+      // dW_l = X_in^T dY  (+ db = colsum dY), fused decay + Adam
+      auto w = mk(K, N, M, Xin + (int64_t)e * M * K, K, 1, dYe, N, 0, h->G + L.W[l] + (int64_t)e * K * N, N);
+      w.colsum = h->G + L.b[l] + (int64_t)e * N;
+      w.adam = 1;
+      w.wd = WDECAY[l];
+      g.push_back(w);
+      if (l >= 1) {  // dZ_{l-1} = (dY W_l^T) * swish'(Z_{l-1})
+        auto dz = mk(M, K, N, dYe, N, 0, P + L.W[l] + (int64_t)e * K * N, N, 1, h->dZ[l - 1] + (int64_t)e * M * K, K);
+        dz.mask = h->Z[l - 1] + (int64_t)e * M * K; dz.ldm = K; dz.mask_kind = MASK_DSWISH;
+        g.push_back(dz);
+      }
+    }
+    if (launch_group(g, s, &ad, nullptr)) return -1;
+  }
+  return 0;
+}
+
+int copy_back(Train* h, hipStream_t s) {
+  MOPO_HIP(hipMemcpyAsync(h->Pb[0], h->Pb[1], h->L.total * 4, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+void drop_graphs(Train* h) {
+  for (int i = 0; i < 3; ++i) {
+    if (h->gexec[i]) (void)hipGraphExecDestroy(h->gexec[i]);
+    if (h->graph[i]) (void)hipGraphDestroy(h->graph[i]);
+    h->gexec[i] = nullptr;
+    h->graph[i] = nullptr;
+  }
+}
+
+constexpr int TRAIN_GRAPH_STEPS = 8;
+
+int capture(Train* h, int which, const float* in, const float* tg, const int32_t* idx, int64_t n_idx, int batch) {
+  hipStream_t gs = h->gs;
+  MOPO_HIP(hipStreamBeginCapture(gs, hipStreamCaptureModeThreadLocal));
+  const int steps = which == 0 ? TRAIN_GRAPH_STEPS : which == 1 ? 2 : 1;
+  int rc = 0;
+  for (int i = 0; i < steps && !rc; ++i) {
+    rc = launch_gather(h, in, tg, idx, n_idx, true, batch, batch, gs);
+    if (!rc) rc = step_impl(h, i & 1, batch, true, gs);
+  }
+  if (!rc && which == 2) rc = copy_back(h, gs);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(gs, &g);
+  if (rc) { if (g) (void)hipGraphDestroy(g); return -1; }
+  if (e != hipSuccess) return fail(std::string("bnn train: capture failed: ") + hipGetErrorString(e));
+  h->graph[which] = g;
+  MOPO_HIP(hipGraphInstantiate(&h->gexec[which], g, nullptr, nullptr, 0));
+  return 0;
+}
+
+}  // namespace
+}  // namespace mopo
+
+using namespace mopo;
+
+extern "C" int mopo_bnn_train_create(mopo_bnn_train_t* out, int E, int obs_dim, int act_dim, int hidden,
+                                     int max_batch, int max_eval, float lr) {
+  MOPO_REQUIRE(out, "mopo_bnn_train_create: out is NULL");
+  MOPO_REQUIRE(E >= 1 && E <= 16, "mopo_bnn_train_create: num_networks must be in [1, 16]");
+  MOPO_REQUIRE(obs_dim >= 1 && act_dim >= 1 && hidden >= 1, "mopo_bnn_train_create: bad dims");
+  MOPO_REQUIRE(obs_dim + 1 <= 64, "mopo_bnn_train_create: obs_dim + 1 must be <= 64");
+  MOPO_REQUIRE(max_batch >= 1 && max_eval >= 0, "mopo_bnn_train_create: bad batch sizes");
+  Train* h = new Train();
+  h->L = make_layout(E, obs_dim + act_dim, hidden, obs_dim + 1);
+  h->lr = lr;
+  h->max_batch = max_batch; h->max_eval = max_eval;
+  h->maxM = std::max(max_batch, max_eval);
+  const Layout& L = h->L;
+  const int64_t tot = (L.total + 3) / 4 * 4, mM = h->maxM;
+  const int loss_blocks = L.D * ceil_div(E * h->maxM, LOSS_TPB);
+  std::vector<std::pair<void**, size_t>> reg;
+  auto f = [&](float** p, int64_t cnt) { reg.push_back({(void**)p, (size_t)cnt * 4}); };
+  f(&h->Pb[0], tot); f(&h->Pb[1], tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->S, tot);
+  f(&h->beta_pow, 3); f(&h->part, 4 * (int64_t)loss_blocks); f(&h->logs, 4); f(&h->mu, L.IN); f(&h->sigma, L.IN);
+  reg.push_back({(void**)&h->bstep, 4});
+  reg.push_back({(void**)&h->ticket, 4});
+  f(&h->X, E * mM * L.IN); f(&h->T, E * mM * L.D); f(&h->OUT, E * mM * 2 * L.D); f(&h->dOUT, E * mM * 2 * L.D);
+  for (int l = 0; l < NHID; ++l) { f(&h->Z[l], E * mM * L.H); f(&h->Hh[l], E * mM * L.H); f(&h->dZ[l], E * mM * L.H); }
+  size_t bytes = 0;
+  for (auto& r : reg) bytes += (r.second + 255) & ~(size_t)255;
+  if (hipMalloc(&h->mem, bytes) != hipSuccess) { delete h; return fail("mopo_bnn_train_create: out of device memory"); }
+  if (hipMemset(h->mem, 0, bytes) != hipSuccess) { (void)hipFree(h->mem); delete h; return fail("memset failed"); }
+  char* m = (char*)h->mem;
+  for (auto& r : reg) { *r.first = m; m += (r.second + 255) & ~(size_t)255; }
+  const float bp[3] = {0.9f, 0.999f, 0.f};
+  MOPO_HIP(hipMemcpy(h->beta_pow, bp, sizeof(bp), hipMemcpyHostToDevice));
+  std::vector<float> one(L.IN, 1.f);
+  MOPO_HIP(hipMemcpy(h->sigma, one.data(), L.IN * 4, hipMemcpyHostToDevice));
+  *out = reinterpret_cast<mopo_bnn_train_t>(h);
+  return 0;
+}
+
+extern "C" int mopo_bnn_train_destroy(mopo_bnn_train_t hh) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  if (!h) return 0;
+  drop_graphs(h);
+  if (h->ev_in) (void)hipEventDestroy(h->ev_in);
+  if (h->ev_out) (void)hipEventDestroy(h->ev_out);
+  if (h->gs) (void)hipStreamDestroy(h->gs);
+  if (h->sort_keys) (void)hipFree(h->sort_keys);  // one allocation (keys | values | offsets | temp)
+  if (h->mem) (void)hipFree(h->mem);
+  delete h;
+  return 0;
+}
+
+// .mat order (smv, 16 arrays): mu, sigma, (W, b) x 5 mean layers, (Wv, bv), maxlv, minlv
+extern "C" int mopo_bnn_train_set_params(mopo_bnn_train_t hh, const float* const* a) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  MOPO_REQUIRE(h && a, "mopo_bnn_train_set_params: NULL argument");
+  const Layout& L = h->L;
+  const int E = L.E, H = L.H, D = L.D;
+  std::vector<float> P(L.total);
+  for (int l = 0; l < NHID; ++l) {
+    const int in = l == 0 ? L.IN : H;
+    std::memcpy(P.data() + L.W[l], a[2 + 2 * l], (size_t)E * in * H * 4);
+    std::memcpy(P.data() + L.b[l], a[3 + 2 * l], (size_t)E * H * 4);
+  }
+  for (int e = 0; e < E; ++e) {
+    for (int k = 0; k < H; ++k)
+      for (int j = 0; j < D; ++j) {
+        P[L.W[NHID] + ((int64_t)e * H + k) * 2 * D + j] = a[10][((int64_t)e * H + k) * D + j];
+        P[L.W[NHID] + ((int64_t)e * H + k) * 2 * D + D + j] = a[12][((int64_t)e * H + k) * D + j];
+      }
+    for (int j = 0; j < D; ++j) {
+      P[L.b[NHID] + (int64_t)e * 2 * D + j] = a[11][e * D + j];
+      P[L.b[NHID] + (int64_t)e * 2 * D + D + j] = a[13][e * D + j];
+    }
+  }
+  std::memcpy(P.data() + L.mx, a[14], D * 4);
+  std::memcpy(P.data() + L.mn, a[15], D * 4);
+  MOPO_HIP(hipMemcpy(h->Pb[0], P.data(), L.total * 4, hipMemcpyHostToDevice));
+  MOPO_HIP(hipMemcpy(h->Pb[1], P.data(), L.total * 4, hipMemcpyHostToDevice));
+  MOPO_HIP(hipMemcpy(h->mu, a[0], L.IN * 4, hipMemcpyHostToDevice));
+  MOPO_HIP(hipMemcpy(h->sigma, a[1], L.IN * 4, hipMemcpyHostToDevice));
+  // a fresh optimizer (the reference initialises the Adam slots with the graph, bnn.py:252)
+  MOPO_HIP(hipMemset(h->M, 0, L.total * 4));
+  MOPO_HIP(hipMemset(h->V, 0, L.total * 4));
+  const float bp[3] = {0.9f, 0.999f, 0.f};
+  MOPO_HIP(hipMemcpy(h->beta_pow, bp, sizeof(bp), hipMemcpyHostToDevice));
+  h->snap.clear();
+  return 0;
+}
+
+extern "C" int mopo_bnn_train_get_params(mopo_bnn_train_t hh, float* const* a) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  MOPO_REQUIRE(h && a, "mopo_bnn_train_get_params: NULL argument");
+  const Layout& L = h->L;
+  const int E = L.E, H = L.H, D = L.D;
+  MOPO_HIP(hipDeviceSynchronize());
+  std::vector<float> P(L.total);
+  MOPO_HIP(hipMemcpy(P.data(), h->Pb[0], L.total * 4, hipMemcpyDeviceToHost));
+  MOPO_HIP(hipMemcpy(a[0], h->mu, L.IN * 4, hipMemcpyDeviceToHost));
+  MOPO_HIP(hipMemcpy(a[1], h->sigma, L.IN * 4, hipMemcpyDeviceToHost));
+  for (int l = 0; l < NHID; ++l) {
+    const int in = l == 0 ? L.IN : H;
+    std::memcpy(a[2 + 2 * l], P.data() + L.W[l], (size_t)E * in * H * 4);
+    std::memcpy(a[3 + 2 * l], P.data() + L.b[l], (size_t)E * H * 4);
+  }
+  for (int e = 0; e < E; ++e) {
+    for (int k = 0; k < H; ++k)
+      for (int j = 0; j < D; ++j) {
+        a[10][((int64_t)e * H + k) * D + j] = P[L.W[NHID] + ((int64_t)e * H + k) * 2 * D + j];
+        a[12][((int64_t)e * H + k) * D + j] = P[L.W[NHID] + ((int64_t)e * H + k) * 2 * D + D + j];
+      }
+    for (int j = 0; j < D; ++j) {
+      a[11][e * D + j] = P[L.b[NHID] + (int64_t)e * 2 * D + j];
+      a[13][e * D + j] = P[L.b[NHID] + (int64_t)e * 2 * D + D + j];
+    }
+  }
+  std::memcpy(a[14], P.data() + L.mx, D * 4);
+  std::memcpy(a[15], P.data() + L.mn, D * 4);
+  return 0;
+}
+
+extern "C" int mopo_bnn_format_samples(const mopo_pool_desc* pool, int O, int A, const int64_t* d_rows, int64_t n,
+                                       float* d_inputs, float* d_targets, void* stream) {
+  MOPO_REQUIRE(pool && d_inputs && d_targets, "mopo_bnn_format_samples: NULL argument");
+  MOPO_REQUIRE(n >= 0, "mopo_bnn_format_samples: n < 0");
+  if (n == 0) return 0;
+  const int64_t tot = n * (2 * O + A + 1);
+  hipLaunchKernelGGL(format_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *pool, O, A,
+                     d_rows, n, d_inputs, d_targets);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int mopo_bnn_train_fit_scaler(mopo_bnn_train_t hh, const float* d_inputs, int64_t n, void* stream) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  MOPO_REQUIRE(h && d_inputs && n > 0, "mopo_bnn_train_fit_scaler: bad argument");
+  hipLaunchKernelGGL(scaler_fit_kernel, dim3(h->L.IN), dim3(256), 0, (hipStream_t)stream, d_inputs, n, h->L.IN, h->mu,
+                     h->sigma);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int mopo_bnn_train_epoch(mopo_bnn_train_t hh, const float* d_in, const float* d_tg, const int32_t* d_idxs,
+                                    int64_t n_idx, int batch, void* stream) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  MOPO_REQUIRE(h && d_in && d_tg && d_idxs, "mopo_bnn_train_epoch: NULL argument");
+  MOPO_REQUIRE(batch >= 1 && batch <= h->max_batch, "mopo_bnn_train_epoch: batch exceeds max_batch");
+  MOPO_REQUIRE(n_idx >= 1, "mopo_bnn_train_epoch: empty index set");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nb = (n_idx + batch - 1) / batch;
+  const int last = (int)(n_idx - (nb - 1) * batch);
+  const int64_t nfull = last == batch ? nb : nb - 1;
+  if (!h->gs) {
+    MOPO_HIP(hipStreamCreateWithFlags(&h->gs, hipStreamNonBlocking));
+    MOPO_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
+    MOPO_HIP(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
+  }
+  hipStream_t gs = h->gs;
+  MOPO_HIP(hipEventRecord(h->ev_in, s));
+  MOPO_HIP(hipStreamWaitEvent(gs, h->ev_in, 0));
+  MOPO_HIP(hipMemsetAsync(h->bstep, 0, 4, gs));
+  if (nfull > 0) {
+    if (!h->gexec[0] || h->gkey[0] != d_in || h->gkey[1] != d_tg || h->gkey[2] != d_idxs || h->gkey_n != n_idx ||
+        h->gkey_b != batch) {
+      drop_graphs(h);
+      if (capture(h, 0, d_in, d_tg, d_idxs, n_idx, batch) || capture(h, 1, d_in, d_tg, d_idxs, n_idx, batch) ||
+          capture(h, 2, d_in, d_tg, d_idxs, n_idx, batch))
+        return -1;
+      h->gkey[0] = d_in; h->gkey[1] = d_tg; h->gkey[2] = d_idxs; h->gkey_n = n_idx; h->gkey_b = batch;
+    }
+    int64_t i = 0;
+    for (; i + TRAIN_GRAPH_STEPS <= nfull; i += TRAIN_GRAPH_STEPS) MOPO_HIP(hipGraphLaunch(h->gexec[0], gs));
+    for (; i + 2 <= nfull; i += 2) MOPO_HIP(hipGraphLaunch(h->gexec[1], gs));
+    if (i < nfull) MOPO_HIP(hipGraphLaunch(h->gexec[2], gs));
+  }
+  if (nfull < nb) {  // the epoch's partial last minibatch (bnn.py:426: idxs[:, b*bs:(b+1)*bs])
+    if (launch_gather(h, d_in, d_tg, d_idxs, n_idx, true, batch, last, gs) || step_impl(h, 0, last, true, gs) ||
+        copy_back(h, gs))
+      return -1;
+  }
+  MOPO_HIP(hipEventRecord(h->ev_out, gs));
+  MOPO_HIP(hipStreamWaitEvent(s, h->ev_out, 0));
+  return 0;
+}
+
+extern "C" int mopo_bnn_train_eval_mse(mopo_bnn_train_t hh, const float* d_in, const float* d_tg, const int32_t* d_rows,
+                                       int n, float* d_losses, void* stream) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  MOPO_REQUIRE(h && d_in && d_tg && d_losses, "mopo_bnn_train_eval_mse: NULL argument");
+  MOPO_REQUIRE(n >= 1 && n <= h->maxM, "mopo_bnn_train_eval_mse: n must be in [1, max(max_batch, max_eval)]");
+  hipStream_t s = (hipStream_t)stream;
+  if (launch_gather(h, d_in, d_tg, d_rows, n, false, 0, n, s) || forward(h, h->Pb[0], n, s)) return -1;
+  hipLaunchKernelGGL(train_mse_kernel, dim3(h->L.E), dim3(256), 0, s, h->OUT, h->T, n, h->L.D, d_losses);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int mopo_bnn_train_shuffle(mopo_bnn_train_t hh, int32_t* d_idxs, const double* d_keys, int64_t n,
+                                      void* stream) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  MOPO_REQUIRE(h && d_idxs && d_keys && n >= 1, "mopo_bnn_train_shuffle: bad argument");
+  MOPO_REQUIRE(n * h->L.E < (1ll << 31), "mopo_bnn_train_shuffle: index set too large");
+  hipStream_t s = (hipStream_t)stream;
+  const int E = h->L.E;
+  const int64_t tot = n * E;
+  if (h->sort_cap < tot) {
+    if (h->sort_keys) (void)hipFree(h->sort_keys);
+    h->sort_tmp = nullptr; h->sort_keys = nullptr;
+    size_t tb = 0;
+    MOPO_HIP(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, (const double*)nullptr, (double*)nullptr,
+                                                         (const int32_t*)nullptr, (int32_t*)nullptr, (int)tot, E,
+                                                         (const int*)nullptr, (const int*)nullptr, 0, 64, s));
+    // one allocation: sorted keys | values in | values out (order) | segment offsets | temp storage
+    const size_t kb = (size_t)tot * 8, vb = (size_t)tot * 4, sb = (size_t)(E + 1) * 4;
+    char* m = nullptr;
+    MOPO_HIP(hipMalloc((void**)&m, kb + 2 * vb + sb + tb + 1024));
+    h->sort_keys = (double*)m;
+    h->sort_vals_in = (int32_t*)(m + kb);
+    h->sort_vals = (int32_t*)(m + kb + vb);
+    h->seg = (int*)(m + kb + 2 * vb);
+    h->sort_tmp = (void*)(((uintptr_t)(m + kb + 2 * vb + sb) + 255) & ~(uintptr_t)255);
+    h->sort_tmp_bytes = tb;
+    h->sort_cap = tot;
+  }
+  hipLaunchKernelGGL(iota_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, h->sort_vals_in, n, E, h->seg);
+  MOPO_HIP(hipGetLastError());
+  size_t tb = h->sort_tmp_bytes;
+  // stable ascending sort of the f64 uniforms per member row == np.argsort (distinct keys)
+  MOPO_HIP(hipcub::DeviceSegmentedRadixSort::SortPairs(h->sort_tmp, tb, d_keys, h->sort_keys, h->sort_vals_in,
+                                                       h->sort_vals, (int)tot, E, h->seg, h->seg + 1, 0, 64, s));
+  int32_t* tmp_idx = h->sort_vals_in;  // reuse: copy of the current indices
+  MOPO_HIP(hipMemcpyAsync(tmp_idx, d_idxs, tot * 4, hipMemcpyDeviceToDevice, s));
+  hipLaunchKernelGGL(apply_order_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, h->sort_vals, tmp_idx,
+                     n, E, d_idxs);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int mopo_bnn_train_snapshot(mopo_bnn_train_t hh, int member, void* stream) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  MOPO_REQUIRE(h && member >= 0 && member < h->L.E, "mopo_bnn_train_snapshot: bad member");
+  hipLaunchKernelGGL(member_copy_kernel, dim3(64, 2 * (NHID + 1)), dim3(256), 0, (hipStream_t)stream, h->Pb[0], h->S,
+                     member_span(h->L), member, 0);
+  MOPO_HIP(hipGetLastError());
+  if (std::find(h->snap.begin(), h->snap.end(), member) == h->snap.end()) h->snap.push_back(member);
+  return 0;
+}
+
+extern "C" int mopo_bnn_train_restore(mopo_bnn_train_t hh, void* stream) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  MOPO_REQUIRE(h, "mopo_bnn_train_restore: NULL handle");
+  for (int e : h->snap) {
+    hipLaunchKernelGGL(member_copy_kernel, dim3(64, 2 * (NHID + 1)), dim3(256), 0, (hipStream_t)stream, h->Pb[0], h->S,
+                       member_span(h->L), e, 1);
+    MOPO_HIP(hipGetLastError());
+  }
+  h->snap.clear();
+  return 0;
+}
+
+extern "C" int mopo_bnn_train_logs(mopo_bnn_train_t hh, float* h_logs, int n) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  MOPO_REQUIRE(h && h_logs && n >= 1 && n <= 4, "mopo_bnn_train_logs: bad argument");
+  MOPO_HIP(hipDeviceSynchronize());
+  MOPO_HIP(hipMemcpy(h_logs, h->logs, n * 4, hipMemcpyDeviceToHost));
+  return 0;
+}

@@ -1,0 +1,444 @@
+// Grouped small-GEMM kernel with fused epilogues (activation, activation-derivative masks,
+// bias-gradient column sums, TF1 Adam + Polyak, policy head), shared by the SAC step (sac.hip)
+// and the ensemble training step (bnn_train.hip).
+//
+// One 16x16 output tile per 256-thread block; K is split over the four waves and reduced through
+// LDS.  f32 MFMA (v_mfma_f32_16x16x4_f32).  The shapes these updates see are small (batch 256,
+// width 200-256), so the kernel is built for latency: many independent tiles of up to MAXP
+// problems per launch, every operand load unconditional (range-checked buffer loads), panels
+// staged through an XOR-swizzled LDS layout.  Everything here has internal linkage: each
+// translation unit that includes it gets its own copy of the kernel.
+#pragma once
+#include <vector>
+
+#include "internal.h"
+
+namespace mopo {
+
+// swish'(z) = s + z s (1 - s), s = sigmoid(z) (TF: the product rule through tf.sigmoid, fc.py:21)
+static __device__ __forceinline__ float dswish_fast(float z) {
+  const float s = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z * 1.4426950408889634f));
+  return s + z * s * (1.0f - s);
+}
+
+constexpr int MAXP = 16;
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2 };   // GemmProb::act
+enum { MASK_RELU = 0, MASK_DSWISH = 1 };             // GemmProb::mask_kind
+
+struct GemmProb {
+  int M, N, K;
+  const float* A; int lda; int ta;   // ta=0: A(i,k)=A[i*lda+k]; ta=1: A(i,k)=A[k*lda+i]
+  const float* B; int ldb; int tb;   // tb=0: B(k,j)=B[k*ldb+j]; tb=1: B(k,j)=B[j*ldb+k]
+  float* C; int ldc;
+  const float* bias;                 // C += bias[j]
+  int act;                           // ACT_RELU: C = max(C, 0); ACT_SWISH: C = swish(C), Z = pre-activation
+  float* Z;                          //   (ACT_SWISH, optional; same layout as C)
+  const float* mask; int ldm;        // MASK_RELU: C *= (mask(i,j) > 0) (relu' from the saved activation)
+  int mask_kind;                     // MASK_DSWISH: C *= swish'(mask(i,j)) (mask = saved pre-activation)
+  float wd;                          // adam: gradient += wd * param (TF l2_loss weight decay, fc.py:156-157)
+  float* colsum;                     // colsum[j] = sum_k B(k,j)   (bias gradient), by tile-row 0
+  // rank-1 masked operands (the critic's 1-wide output layer backward, fused into its consumer):
+  // when a_u != NULL:  A(i,k) = a_u[i] * a_v[k] * (a_m[i*a_ldm + k] > 0);  same for B with (k, j)
+  const float* a_u; const float* a_v; const float* a_m; int a_ldm;
+  const float* b_u; const float* b_v; const float* b_m; int b_ldm;
+  int adam;                          // C (and colsum) are gradient slices of AdamCtx::G: apply Adam
+  // two-segment plain B (operand mode 3): columns [0, split) from B, [split, N) from B2 (same ldb),
+  // bias likewise from bias / bias2 -- the policy output layer [W_mean | W_log_std]
+  const float* B2; int split; const float* bias2;
+  int head;                          // 1: pi(s), 2: pi(s'): squashed-Gaussian head epilogue (HeadCtx)
+};
+
+// ---- squashed Gaussian head, forward (mopo.py:282-308, 286-296) for one batch row of pi(s) or
+// pi(s'): action = tanh(mu + eps * exp(clip(log_std))) into the row's action slot, its log-prob
+// (with the tanh correction) and the noise used.  eps is Philox(seed, step counter, row) unless
+// injected (parity mode).
+struct HeadCtx {
+  int O, A;
+  const float* eps_in[2];            // injected noise or NULL
+  float* eps_out[2];
+  float* x[2];                       // [n][O + A] rows whose action part receives tanh(u)
+  float* logp[2];
+  uint64_t seed;
+  const int64_t* iter;
+};
+
+static __device__ __forceinline__ void head_fwd_row(const HeadCtx& hc, int nxt, int r, const float* hm, const float* hl) {
+  const int A = hc.A;
+  float z[8];
+  const float* ein = hc.eps_in[nxt];
+  if (ein) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = j < A ? ein[r * A + j] : 0.f;
+  } else {
+    const int64_t it = *hc.iter;
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      u32x4 c{(uint32_t)r | ((uint32_t)nxt << 31), (uint32_t)it ^ ((uint32_t)blk << 24), (uint32_t)((uint64_t)it >> 32),
+              RNG_SAC + 16};
+      u32x4 q = philox(c, (uint32_t)hc.seed, (uint32_t)(hc.seed >> 32));
+      box_muller(q.x, q.y, z[4 * blk], z[4 * blk + 1]);
+      box_muller(q.z, q.w, z[4 * blk + 2], z[4 * blk + 3]);
+    }
+  }
+  float logp = 0.f, corr = 0.f;
+  float* x = hc.x[nxt] + r * (hc.O + A) + hc.O;
+  float* eo = hc.eps_out[nxt] + r * A;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (j >= A) break;
+    const float mu = hm[j];
+    const float ls = fminf(fmaxf(hl[j], -20.f), 2.f);
+    const float sd = expf(ls);
+    const float u = mu + z[j] * sd;
+    const float zz = (u - mu) / (sd + 1e-8f);
+    logp += -0.5f * (zz * zz + 2.f * ls + 1.8378770664093453f);
+    corr += 2.f * (0.6931471805599453f - u - softplusf(-2.f * u));
+    x[j] = tanhf(u);
+    eo[j] = z[j];
+  }
+  hc.logp[nxt][r] = logp - corr;
+}
+
+// Fused optimizer (the four TF1 Adams + Polyak, mopo.py:407-447): a weight-gradient tile is final
+// when its epilogue runs (K spans the whole batch), so the epilogue updates the parameters it
+// covers right there.  Parameters are double-buffered (read Pc, write Pn) because the same launch
+// and later backward launches still read the pre-step weights; M, V and T are updated in place
+// (each element is touched by exactly one tile, and T is only read by earlier forward stages).
+struct AdamCtx {
+  const float* G; const float* Pc; float* Pn; float* M; float* V; float* T;
+  const float* lr_t;                 // this step's step size (sac_loss_kernel)
+  float tau; int64_t total, n_pi, n_q; // grad-norm logs: [0, n_pi) policy, [n_pi, n_pi + n_q) Q1
+  float* norm_part;                  // [slot][2] squared-gradient partials (pi, q) per block
+  int slot0;                         // this launch's first slot
+};
+
+struct GemmGroup {
+  int n;
+  int prefix[MAXP + 1];
+  AdamCtx ad;
+  HeadCtx hd;
+  GemmProb p[MAXP];
+};
+
+struct AdamIn { float p, m, v, t; };
+
+static __device__ __forceinline__ AdamIn adam_load(const AdamCtx& ad, int64_t i) {
+  return AdamIn{ad.Pc[i], ad.M[i], ad.V[i], ad.T ? ad.T[i] : 0.f};
+}
+
+// TF1 Adam (m += (g - m)(1 - b1), v += (g^2 - v)(1 - b2), p -= lr_t m / (sqrt(v) + eps)) + Polyak
+static __device__ __forceinline__ void adam_apply(const AdamCtx& ad, int64_t i, float g, AdamIn a, float lr_t) {
+  const float m = a.m + (g - a.m) * (1.f - 0.9f);
+  const float v = a.v + (g * g - a.v) * (1.f - 0.999f);
+  const float p = a.p - (m * lr_t) / (sqrtf(v) + 1e-8f);
+  ad.M[i] = m;
+  ad.V[i] = v;
+  ad.Pn[i] = p;
+  if (ad.T && i < ad.total) ad.T[i] = (1.f - ad.tau) * a.t + ad.tau * p;   // mopo.py:446-447 (after the updates)
+}
+
+
+constexpr int GKC = 256;  // K chunk staged in LDS
+
+// One 16-wide panel (A: rows i0..i0+15, or B: cols j0..j0+15) x K-chunk, staged as S[k][r].
+// MODE 0: plain, 1: transposed, 2: rank-1 masked (see GemmProb).  Loads are raw buffer loads through
+// a descriptor sized to the operand's extent: a 32-bit byte offset per element (no 64-bit address
+// pairs) and hardware range checking (reads past the extent return 0), so every load is issued
+// unconditionally; elements outside the tile or the K chunk are zeroed by a select at the store.
+struct PanelRegs { float x[16], u[16], w[16]; };
+
+// Panels are S[k][r ^ psw(k)]: 64 4-byte banks, a 16-float row puts k and k+4 on the same banks, so
+// without the XOR the k-fast stores (64 consecutive k per wave) hit 4 banks 16 ways.  With it the
+// k-fast and r-fast stores and the MFMA operand reads (16 r x 4 k per instruction) are conflict-free.
+static __device__ __forceinline__ int psw(int k) { return (k >> 2) & 15; }
+
+template <int MODE, bool IS_A>
+static __device__ __forceinline__ void panel_rk(int q, int tid, int& r, int& k) {
+  constexpr bool rfast = IS_A ? (MODE == 1) : (MODE != 1);
+  if (rfast) { r = tid & 15; k = (tid >> 4) + 16 * q; }
+  else { k = (tid & 63) + 64 * (q & 3); r = (tid >> 6) + 4 * (q >> 2); }
+}
+
+// buffer descriptor over n floats at p (wave-uniform inputs only)
+static __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)(n * 4), 0x00020000);
+}
+
+static __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t d, int idx) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(d, idx * 4, 0, 0));
+}
+
+template <int MODE, bool IS_A>
+static __device__ __forceinline__ void load_panel(const GemmProb& p, int r0, int kc, int tid, PanelRegs& R) {
+  const int Rn = IS_A ? p.M : p.N;  // panel axis extent
+  if (MODE == 2) {
+    const int ldm = IS_A ? p.a_ldm : p.b_ldm;
+    // A(i,k) = u[i] v[k] (m[i,k] > 0);  B(k,j) = u[k] v[j] (m[k,j] > 0).  The A panel is k-fast
+    // (element q: row 4(q>>2) + tid>>6, column 64(q&3) + (tid&63)), so it needs only 4 u and 4 v
+    // values per thread; the B panel is r-fast (column tid&15, row 16q + tid>>4): 16 u, 1 v.
+    const auto dm = IS_A ? rsrc(p.a_m, (int64_t)(Rn - 1) * ldm + p.K) : rsrc(p.b_m, (int64_t)(p.K - 1) * ldm + Rn);
+    const auto du = IS_A ? rsrc(p.a_u, Rn) : rsrc(p.b_u, p.K);
+    const auto dv = IS_A ? rsrc(p.a_v, p.K) : rsrc(p.b_v, Rn);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      int r, k;
+      panel_rk<MODE, IS_A>(q, tid, r, k);
+      const int gr = r0 + r, gk = kc + k;
+      if (IS_A) {
+        if ((q & 3) == 0) R.u[q >> 2] = bload(du, gr);
+        if (q < 4) R.w[q] = bload(dv, gk);
+      } else {
+        R.u[q] = bload(du, gk);
+        if (q == 0) R.w[0] = bload(dv, gr);
+      }
+      R.x[q] = bload(dm, IS_A ? gr * ldm + gk : gk * ldm + gr);
+    }
+  } else if (MODE == 3) {
+    // two-segment B: per-lane segment select, so flat loads with clamped addresses
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      int r, k;
+      panel_rk<MODE, IS_A>(q, tid, r, k);
+      const int gr = min(r0 + r, Rn - 1), gk = min(kc + k, p.K - 1);
+      const float* src = gr < p.split ? p.B + gr : p.B2 + (gr - p.split);
+      R.x[q] = src[(int64_t)gk * p.ldb];
+    }
+  } else {
+    const float* base = IS_A ? p.A : p.B;
+    const int ld = IS_A ? p.lda : p.ldb;
+    // element (r, k) of the panel's operand lives at r*ld + k (row-major in r) or k*ld + r
+    constexpr bool r_major = IS_A ? (MODE == 0) : (MODE == 1);
+    const auto d = r_major ? rsrc(base, (int64_t)(Rn - 1) * ld + p.K) : rsrc(base, (int64_t)(p.K - 1) * ld + Rn);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      int r, k;
+      panel_rk<MODE, IS_A>(q, tid, r, k);
+      const int gr = r0 + r, gk = kc + k;
+      R.x[q] = bload(d, r_major ? gr * ld + gk : gk * ld + gr);
+    }
+  }
+}
+
+// keep the loads batched ahead of the first use
+template <int MODE, bool IS_A>
+static __device__ __forceinline__ void pin_panel(PanelRegs& R) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    asm volatile("" : "+v"(R.x[q]));
+    if (MODE == 2 && (IS_A ? q < 4 : true)) asm volatile("" : "+v"(R.u[q]));
+    if (MODE == 2 && (IS_A ? q < 4 : q == 0)) asm volatile("" : "+v"(R.w[q]));
+  }
+}
+
+// element q of a rank-1 panel: u * v (the A panel indexes u by q>>2 and v by q&3, see load_panel)
+template <bool IS_A>
+static __device__ __forceinline__ float rank1_uv(const PanelRegs& R, int q) {
+  return IS_A ? R.u[q >> 2] * R.w[q & 3] : R.u[q] * R.w[0];
+}
+
+template <int MODE, bool IS_A>
+static __device__ __forceinline__ void store_panel(const GemmProb& p, int r0, int kn, int tid, const PanelRegs& R,
+                                            float (*S)[16]) {
+  const int Rmax = IS_A ? p.M : p.N;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    int r, k;
+    panel_rk<MODE, IS_A>(q, tid, r, k);
+    const float v = MODE == 2 ? (R.x[q] > 0.f ? rank1_uv<IS_A>(R, q) : 0.f) : R.x[q];
+    S[k][r ^ psw(k)] = (r0 + r < Rmax && k < kn) ? v : 0.f;
+  }
+}
+
+// operand modes (A: 0 plain, 1 transposed, 2 rank-1; B: the same, 3 two-segment) as am * 4 + bm
+__host__ static __device__ __forceinline__ int operand_modes(const GemmProb& p) {
+  const int am = p.a_u ? 2 : p.ta, bm = p.b_u ? 2 : p.B2 ? 3 : p.tb;
+  return am * 4 + bm;
+}
+
+template <int AM, int BM>
+static __device__ __forceinline__ void stage_ab(const GemmProb& p, int i0, int j0, int kc, int kn, int tid, float (*As)[16],
+                                         float (*Bs)[16]) {
+  PanelRegs ra, rb;
+  load_panel<AM, true>(p, i0, kc, tid, ra);
+  load_panel<BM, false>(p, j0, kc, tid, rb);
+  pin_panel<AM, true>(ra);
+  pin_panel<BM, false>(rb);
+  store_panel<AM, true>(p, i0, kn, tid, ra, As);
+  store_panel<BM, false>(p, j0, kn, tid, rb, Bs);
+}
+
+// One 16x16 output tile per 256-thread block.  The A[16 x K] and B[K x 16] panels are staged in
+// LDS with loads ordered along each operand's contiguous axis (all issued before the first use:
+// one memory latency per chunk), then the four waves split K and run v_mfma_f32_16x16x4_f32 out
+// of LDS; partial tiles are summed through LDS and the epilogue fuses bias / activation / the
+// activation-derivative mask, and (for weight gradients) the optimizer.
+static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGroup g) {
+  __shared__ float As[GKC][16];
+  __shared__ float Bs[GKC][16];
+  __shared__ float part[4][256];
+  __shared__ float csum[16][17];
+  __shared__ float hv[16][17];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int pi = 0;
+  while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
+  const GemmProb& p = g.p[pi];
+  const int t = blockIdx.x - g.prefix[pi];
+  const int tn_cnt = ceil_div(p.N, 16);
+  const int tm = t / tn_cnt, tn = t % tn_cnt;
+  const int i0 = tm * 16, j0 = tn * 16;
+  const int li = lane & 15, lk = lane >> 4;
+  const bool do_cs = p.colsum && tm == 0;
+  // epilogue operands are fetched up front so their latency overlaps the panel loads
+  const int ei = tid >> 4, ej = tid & 15;
+  const int gi = i0 + ei, gj = j0 + ej;
+  const int gic = min(gi, p.M - 1), gjc = min(gj, p.N - 1);
+  float e_bias = p.bias ? (p.bias2 && gjc >= p.split ? p.bias2[gjc - p.split] : p.bias[gjc]) : 0.f;
+  float e_mask = p.mask ? p.mask[(int64_t)gic * p.ldm + gjc] : 1.f;
+  asm volatile("" : "+v"(e_bias), "+v"(e_mask));
+  const AdamCtx& ad = g.ad;
+  const int64_t a_idx = p.adam ? (int64_t)(p.C - ad.G) + (int64_t)gic * p.ldc + gjc : 0;
+  const int64_t c_idx = p.adam && p.colsum ? (int64_t)(p.colsum - ad.G) + min(j0 + (tid & 15), p.N - 1) : 0;
+  AdamIn a_in{0.f, 0.f, 0.f, 0.f}, c_in{0.f, 0.f, 0.f, 0.f};
+  float lr_t = 0.f;
+  if (p.adam) {
+    a_in = adam_load(ad, a_idx);
+    if (p.colsum && tm == 0 && tid < 16) c_in = adam_load(ad, c_idx);
+    lr_t = *ad.lr_t;
+    asm volatile("" : "+v"(a_in.p), "+v"(a_in.m), "+v"(a_in.v), "+v"(a_in.t));
+  }
+  f32x4 acc0 = zero4(), acc1 = zero4();
+  float cs = 0.f;
+  for (int kc = 0; kc < p.K; kc += GKC) {
+    const int kn = min(GKC, p.K - kc);
+    // re-derive the thread index inside the chunk loop: otherwise the ~100 per-thread LDS and
+    // buffer offsets are hoisted out of it and stay live across the loop (VGPRs -> occupancy)
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    // 16 elements of each panel per thread; the per-operand mode is dispatched once (uniform
+    // branch) so that all 32+ loads are unconditional and issue back to back -- one memory latency
+    // per chunk instead of one per element.
+    switch (operand_modes(p)) {  // the combinations sac_step_impl uses (launch_group rejects others)
+      case 0: stage_ab<0, 0>(p, i0, j0, kc, kn, t, As, Bs); break;
+      case 1: stage_ab<0, 1>(p, i0, j0, kc, kn, t, As, Bs); break;
+      case 3: stage_ab<0, 3>(p, i0, j0, kc, kn, t, As, Bs); break;
+      case 4: stage_ab<1, 0>(p, i0, j0, kc, kn, t, As, Bs); break;
+      case 6: stage_ab<1, 2>(p, i0, j0, kc, kn, t, As, Bs); break;
+      default: stage_ab<2, 1>(p, i0, j0, kc, kn, t, As, Bs); break;
+    }
+    __syncthreads();
+    // the staged panels are zero-padded to GKC rows, so every wave runs exactly 16 k-steps of its
+    // quarter with no guards: all 32 LDS reads first, then 16 MFMAs on two accumulators
+    float ra[16], rb[16];
+    const int tli = t & 15, tlk = (t >> 4) & 3, tw = t >> 6;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = 4 * (tw * 16 + s) + tlk;
+      ra[s] = As[k][tli ^ psw(k)];
+      rb[s] = Bs[k][tli ^ psw(k)];
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s & 1) acc1 = mfma4(ra[s], rb[s], acc1);
+      else acc0 = mfma4(ra[s], rb[s], acc0);
+    }
+    if (do_cs)
+      for (int k = tid >> 4; k < kn; k += 16) cs += Bs[k][(tid & 15) ^ psw(k)];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[w][(lk * 4 + r) * 16 + li] = acc0[r] + acc1[r];  // D: col li, row 4*lk+r
+  if (do_cs) csum[tid >> 4][tid & 15] = cs;
+  __syncthreads();
+  float gsq = 0.f;
+  {
+    float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+    if (gi < p.M && gj < p.N) {
+      v += e_bias;
+      if (p.act == ACT_RELU) {
+        v = fmaxf(v, 0.f);
+      } else if (p.act == ACT_SWISH) {
+        if (p.Z) p.Z[(int64_t)gi * p.ldc + gj] = v;
+        v = swish_fast(v);
+      }
+      if (p.mask_kind == MASK_DSWISH) v *= dswish_fast(e_mask);
+      else if (!(e_mask > 0.f)) v = 0.f;
+      if (p.adam) v += p.wd * a_in.p;
+      p.C[(int64_t)gi * p.ldc + gj] = v;
+      if (p.head) hv[ei][ej] = v;
+      if (p.adam) {
+        adam_apply(ad, a_idx, v, a_in, lr_t);
+        gsq = v * v;
+      }
+    }
+  }
+  if (do_cs && tid < 16) {
+    float c = 0.f;
+    for (int q = 0; q < 16; ++q) c += csum[q][tid];
+    if (j0 + tid < p.N) {
+      p.colsum[j0 + tid] = c;
+      if (p.adam) {
+        adam_apply(ad, c_idx, c, c_in, lr_t);
+        gsq += c * c;
+      }
+    }
+  }
+  if (p.head) {  // the tile holds all 2A head outputs of its 16 rows: one thread per row
+    __syncthreads();
+    if (tid < 16 && i0 + tid < p.M) head_fwd_row(g.hd, p.head - 1, i0 + tid, &hv[tid][0], &hv[tid][g.hd.A]);
+  }
+  if (ad.norm_part) {  // per-block squared-gradient partial (grad-norm logs; summed by sac_logs_kernel)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) gsq += __shfl_xor(gsq, off);
+    __syncthreads();
+    if (lane == 0) part[0][w] = gsq;
+    __syncthreads();
+    if (tid == 0) {
+      const float b = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+      const int64_t off = p.adam ? (int64_t)(p.C - ad.G) : -1;
+      float* np = ad.norm_part + 2 * (int64_t)(ad.slot0 + blockIdx.x);
+      np[0] = off >= 0 && off < ad.n_pi ? b : 0.f;
+      np[1] = off >= ad.n_pi && off < ad.n_pi + ad.n_q ? b : 0.f;
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+static inline GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C,
+                   int ldc) {
+  GemmProb p{};
+  p.M = M; p.N = N; p.K = K; p.A = A; p.lda = lda; p.ta = ta; p.B = B; p.ldb = ldb; p.tb = tb; p.C = C; p.ldc = ldc;
+  return p;
+}
+
+static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const AdamCtx* ad = nullptr, int* slot = nullptr,
+                        const HeadCtx* hd = nullptr) {
+  GemmGroup g{};
+  g.n = (int)ps.size();
+  if (g.n > MAXP) return fail("gemm group too large");
+  int tot = 0;
+  for (int i = 0; i < g.n; ++i) {
+    const GemmProb& q = ps[i];
+    const int c = operand_modes(q);
+    if (!(c == 0 || c == 1 || c == 3 || c == 4 || c == 6 || c == 9)) return fail("unsupported gemm operand modes");
+    if ((int64_t)q.M * q.K >= (1ll << 29) || (int64_t)q.N * q.K >= (1ll << 29)) return fail("gemm operand too large");
+    g.p[i] = ps[i];
+    g.prefix[i] = tot;
+    tot += ceil_div(ps[i].M, 16) * ceil_div(ps[i].N, 16);
+  }
+  g.prefix[g.n] = tot;
+  if (ad) {
+    g.ad = *ad;
+    g.ad.slot0 = slot ? *slot : 0;
+    if (slot) *slot += tot;
+  }
+  if (hd) g.hd = *hd;
+  for (int i = 0; i < g.n; ++i)
+    if (g.p[i].head && (!hd || g.p[i].N > 16 || g.p[i].N != 2 * hd->A)) return fail("bad head problem");
+  hipLaunchKernelGGL(gemm_group_kernel, dim3(tot), dim3(256), 0, s, g);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace mopo
