@@ -44,6 +44,8 @@ def parse():
     p.add_argument('--sac-steps', type=int, default=1000)
     p.add_argument('--cpu-sac-steps', type=int, default=500)
     p.add_argument('--no-c3', action='store_true', help='skip the secondary C3 (bf16 walker2d) line')
+    p.add_argument('--train-epochs', type=int, default=2, help='timed BNN.train epochs (0: skip)')
+    p.add_argument('--cpu-train-steps', type=int, default=10)
     return p.parse_args()
 
 
@@ -205,6 +207,56 @@ def c3_leg(args, dev):
             'bf16_peak_tflops': BF16_PEAK_TFLOPS}
 
 
+def train_leg(args, env):
+    """BNN.train minibatch steps (bnn.py:425-432) at the halfcheetah-mixed size: E=7, H=200, 101k env
+    rows -> 100k train rows after the 1000-row holdout, batch 256 (mopo.py:529): 391 Adam steps per
+    epoch.  Reports grad-steps/s over args.train_epochs timed epochs (+ the per-epoch holdout eval)."""
+    import torch
+    from mopo_amd.bnn import construct_model
+    rs = np.random.RandomState(5)
+    N = ENV_ROWS
+    obs = env.cpu().numpy()
+    act = rs.uniform(-1, 1, (N, A)).astype(np.float32)
+    X = np.concatenate([obs, act], 1).astype(np.float32)
+    Y = np.concatenate([rs.normal(size=(N, 1)), 0.1 * rs.normal(size=(N, O))], 1).astype(np.float32)
+    m = construct_model(obs_dim=O, act_dim=A, hidden_dim=H, num_networks=E, num_elites=ELITES,
+                        separate_mean_var=True, seed=1)
+    x, y = torch.from_numpy(X).cuda(), torch.from_numpy(Y).cuda()
+    np.random.seed(0)
+    m.train(x, y, batch_size=256, max_epochs=1, holdout_ratio=0.2, permuted=True)   # warm-up + graph capture
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m.train(x, y, batch_size=256, max_epochs=args.train_epochs, holdout_ratio=0.2, permuted=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    steps = m._train_grad_updates
+    flop_step = 3 * 2 * E * 256 * ((O + A) * H + 3 * H * H + 2 * H * (O + 1))   # fwd + 2x bwd GEMMs
+    return {'metric': 'BNN.train grad-steps/s (E=7, H=200, batch 256 per member)', 'value': steps / dt,
+            'unit': 'grad-steps/s', 'ms_per_epoch': dt / args.train_epochs * 1e3, 'epochs_timed': args.train_epochs,
+            'steps_per_epoch': steps // max(m._train_epochs, 1), 'train_rows': N - 1000,
+            'tflops_achieved': steps * flop_step / dt / 1e12}
+
+
+def cpu_baseline_train(args):
+    """Oracle BNN training steps (numpy restatement of the TF graph, f32 arrays) on the host."""
+    from oracle import bnn as obnn
+    from oracle import bnn_train as ot
+    rs = np.random.RandomState(0)
+    p = obnn.init_params(E, O, A, hidden=H, seed=1)
+    st = ot.TrainState(p, dtype=np.float32)
+    X = rs.normal(size=(E, 256, O + A)).astype(np.float32)
+    Y = rs.normal(size=(E, 256, O + 1)).astype(np.float32)
+    st.step(X, Y, np.float32)
+    n = args.cpu_train_steps
+    t0 = time.perf_counter()
+    for _ in range(n):
+        st.step(X, Y, np.float32)
+    dt = time.perf_counter() - t0
+    return {'value': n / dt, 'unit': 'grad-steps/s', 'cores': 16, 'kind': 'port',
+            'sample': 'oracle numpy BNN train step (bnn.py:241-249 loss, hand backward, TF1 Adam), E=7, H=200, '
+                      'batch 256: %d steps in %.2f s' % (n, dt)}
+
+
 SAC_DIAG = {}
 
 
@@ -299,6 +351,7 @@ def main():
             total = total  # counts are already global (gathered)
     sac_rate = sac_leg(args, pool, env, dev, world)
     c3 = c3_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None
+    tr = train_leg(args, env) if (rank == 0 and world == 1 and args.train_epochs > 0) else None
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
@@ -333,10 +386,14 @@ def main():
     }
     if c3 is not None:
         out['extra_configs'] = {'C3': c3}
+    if tr is not None:
+        out['model_train'] = tr
     if not args.no_cpu_baseline and world == 1:
         out['cpu_baseline'] = cpu_baseline(args)
         out['cpu_baseline_1core'] = cpu_baseline_1core(args)
         out['cpu_baseline_sac'] = cpu_baseline_sac(args)
+        if args.train_epochs > 0:
+            out['cpu_baseline_train'] = cpu_baseline_train(args)
     print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

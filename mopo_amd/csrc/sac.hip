@@ -5,14 +5,14 @@
 // Semantics: every forward and gradient uses the pre-step parameters; then pi, q1, q2
 // and alpha are updated by their own Adam (identical step counts -> one shared lr_t); then Polyak.
 //
-// Structure: ~17 launches per step on one stream (batch gather, 3 grouped-GEMM forward stages for
-// pi(s), pi(s'), Q1/Q2(s,a), the squashed-Gaussian head, 3 for Q1/Q2(s,pi) and the targets, a
-// single-block loss kernel, 4 grouped-GEMM backward stages with fused relu masks and bias-gradient
-// column sums, the policy-head backward, one fused Adam+Polyak pass).  The sequence has fixed
-// pointers, so it is captured once into a hipGraph and replayed (no host work per step).
-// GEMMs are f32-in/f32-acc MFMA (v_mfma_f32_16x16x4_f32): a 16x16 output tile per 256-thread
-// block, K split across the four waves and reduced through LDS -- the shapes are tiny (batch 256,
-// width 256), so the kernel is built for latency (many small independent tiles), not throughput.
+// Structure: 11 launches per step on one stream, captured into hipGraphs of 8 / 2 / 1 steps (no
+// host work per step): 3 grouped-GEMM forward launches for pi(s), pi(s'), Q1/Q2(s,a) (the policy
+// output tile's epilogue runs the squashed-Gaussian head), 2 for Q1/Q2(s,pi) and the target
+// critics, sac_qloss_kernel (their 1-wide output layers, the losses and the alpha gradient), then 4
+// grouped-GEMM backward launches and the policy-head backward (which also gathers the next step's
+// batch).  The four TF1 Adams and Polyak run in the weight-gradient GEMM epilogues (gemm_group.h),
+// reading parameters Pb[p] and writing Pb[1 - p], so every gradient of the step sees pre-step
+// parameters.
 #include <vector>
 #include <cstring>
 

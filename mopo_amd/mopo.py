@@ -9,8 +9,9 @@ Differences that are deliberate: the rollout and the SAC steps run on the device
 (csrc/rollout.hip, csrc/sac.hip); the epoch's 1000 SAC steps are issued as one replayed hipGraph
 batch (the reference runs them one ``session.run`` at a time, with the same batch rule per step);
 MuJoCo evaluation (``_evaluation_paths``) is out of scope -- no simulator in this image -- so
-``evaluation/*`` diagnostics are absent.  Model training (BNN.train) is a later-round item: the
-ensemble must be loaded (``model_load_dir`` .mat, bnn.py:276-281) or set via ``model.set_params``.
+``evaluation/*`` diagnostics are absent.  The dynamics model is trained once before the epoch loop
+(mopo.py:526-531): one epoch when it was loaded from ``model_load_dir``, else to early stopping,
+on the device (``_train_model`` formats the env pool on the device in the holdout-permutation order).
 """
 import time
 from collections import OrderedDict
@@ -30,7 +31,8 @@ class MOPO:
                  num_elites=5, model_retain_epochs=20, rollout_batch_size=100e3, real_ratio=0.1, rollout_length=1,
                  hidden_dim=200, separate_mean_var=False, penalty_coeff=0., penalty_learned_var=False,
                  model_name=None, model_load_dir=None, deterministic=False, network_kwargs=None, epoch_length=1000,
-                 n_epochs=1000, n_train_repeat=1, batch_size=256, seed=88, reparameterize=True, **kwargs):
+                 n_epochs=1000, n_train_repeat=1, batch_size=256, seed=88, reparameterize=True, max_model_t=None,
+                 **kwargs):
         if target_update_interval != 1:
             raise NotImplementedError('target_update_interval != 1 (all D4RL configs use 1)')
         self._pool = pool                                   # device SimpleReplayPool of env data
@@ -61,6 +63,8 @@ class MOPO:
         self._pi_hidden = hs[0]
         self._rollout = None
         self._rollout_length = rollout_length
+        self._max_model_t = max_model_t
+        self._model_train_metrics = None
 
     # -- mopo.py:675-687
     def _set_rollout_length(self):
@@ -85,6 +89,21 @@ class MOPO:
             new_pool.add_samples(samples)
             assert self._model_pool.size == new_pool.size
             self._model_pool = new_pool
+
+    # -- mopo.py:713-721 + constructor.py:46-57
+    def _train_model(self, **kwargs):
+        import ctypes as C
+        import torch
+        from . import _lib as L
+        N, O, A = self._pool.size, self._obs_dim, self._act_dim
+        # bnn.py:392 draws np.random.permutation first; drawing it here keeps the stream order and
+        # lets the format kernel write the rows already permuted (holdout first)
+        perm = torch.from_numpy(np.random.permutation(N)).cuda()
+        x = torch.empty((N, O + A), dtype=torch.float32, device='cuda')
+        y = torch.empty((N, O + 1), dtype=torch.float32, device='cuda')
+        L.check(L.lib().mopo_bnn_format_samples(C.byref(self._pool.desc()), O, A, L.ptr(perm), N, L.ptr(x),
+                                                L.ptr(y), None))
+        return self._model.train(x, y, permuted=True, **kwargs)
 
     # -- mopo.py:723-765 (device-resident, perf-mode RNG)
     def _rollout_model(self, rollout_batch_size, **kwargs):
@@ -129,8 +148,16 @@ class MOPO:
         """Generator of per-epoch diagnostics (mopo.py:650-651)."""
         if self._model_train_freq != self._epoch_length:
             raise NotImplementedError('model_train_freq must equal epoch_length (all D4RL configs: 1000)')
+        if self._model_train_metrics is None:                                            # mopo.py:526-531
+            t0 = time.perf_counter()
+            max_epochs = 1 if self._model.model_loaded else None
+            self._model_train_metrics = self._train_model(batch_size=256, max_epochs=max_epochs, holdout_ratio=0.2,
+                                                          max_t=self._max_model_t)
+            self._model_train_metrics['train_time'] = time.perf_counter() - t0
         for self._epoch in range(self._epoch, n_epochs or self._n_epochs):
-            yield self._train_epoch()
+            d = self._train_epoch()
+            d.update(('model/' + k, v) for k, v in self._model_train_metrics.items())
+            yield d
 
     def get_diagnostics(self):
         return self._sac.get_diagnostics()

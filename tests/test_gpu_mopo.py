@@ -28,6 +28,10 @@ def test_mopo_two_epochs_from_config(tmp_path):
     for d in diags:
         assert d['model/mean_rollout_length'] == 5.0
         assert all(np.isfinite(v) for v in d.values())
+    # the dynamics model was trained first (mopo.py:526-531): random init -> to early stopping
+    m = algo._model
+    assert m._train_epochs >= 6 and d['model/val_loss'] == np.sort(m._holdout_losses)[:5].mean()
+    assert len(m._model_inds) == 5
     # model pool sized as mopo.py:693-695: retain 5 x length 5 x 2000 x (100/100)
     assert algo._model_pool._max_size == 5 * 5 * 2000
     assert algo._model_pool.size == 2 * 5 * 2000
