@@ -78,7 +78,7 @@ struct Train {
   int64_t gkey_n = -1; int gkey_b = -1;
   // shuffle workspace
   void* sort_tmp = nullptr; size_t sort_tmp_bytes = 0;
-  double* sort_keys = nullptr; int32_t* sort_vals_in = nullptr; int32_t* sort_vals = nullptr; int* seg = nullptr;
+  double* sort_keys = nullptr; int32_t* sort_vals_in = nullptr; int32_t* sort_vals = nullptr;
   int64_t sort_cap = 0;
 };
 
@@ -300,10 +300,16 @@ __global__ void apply_order_kernel(const int32_t* __restrict__ order, const int3
   dst[i] = src[e * n + order[i]];
 }
 
-__global__ void iota_kernel(int32_t* v, int64_t n, int E, int* seg) {
+// sort key of member e's k-th uniform: (e << 53) | u * 2^53.  numpy's random_sample is k / 2^53 with
+// an integer k < 2^53 (two MT19937 draws, 27 + 26 bits), so the integer is exact and orders as the
+// double does; value = the position within the member row.
+__global__ void sort_keys_kernel(const double* __restrict__ u, int64_t n, int E, uint64_t* __restrict__ keys,
+                                 int32_t* __restrict__ vals) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < n * E) v[i] = (int32_t)(i % n);
-  if (i <= E) seg[i] = (int)(i * n);
+  if (i >= n * E) return;
+  const uint64_t e = (uint64_t)(i / n);
+  keys[i] = (e << 53) | (uint64_t)(u[i] * 9007199254740992.0);
+  vals[i] = (int32_t)(i % n);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -623,31 +629,35 @@ extern "C" int mopo_bnn_train_shuffle(mopo_bnn_train_t hh, int32_t* d_idxs, cons
   hipStream_t s = (hipStream_t)stream;
   const int E = h->L.E;
   const int64_t tot = n * E;
+  int seg_bits = 0;
+  while ((1 << seg_bits) < E) ++seg_bits;
+  const int end_bit = 53 + seg_bits;
   if (h->sort_cap < tot) {
     if (h->sort_keys) (void)hipFree(h->sort_keys);
     h->sort_tmp = nullptr; h->sort_keys = nullptr;
     size_t tb = 0;
-    MOPO_HIP(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, (const double*)nullptr, (double*)nullptr,
-                                                         (const int32_t*)nullptr, (int32_t*)nullptr, (int)tot, E,
-                                                         (const int*)nullptr, (const int*)nullptr, 0, 64, s));
-    // one allocation: sorted keys | values in | values out (order) | segment offsets | temp storage
-    const size_t kb = (size_t)tot * 8, vb = (size_t)tot * 4, sb = (size_t)(E + 1) * 4;
+    MOPO_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                (const int32_t*)nullptr, (int32_t*)nullptr, (int)tot, 0, end_bit, s));
+    // one allocation: keys in | keys out | values in | values out | temp storage
+    const size_t kb = (size_t)tot * 8, vb = (size_t)tot * 4;
     char* m = nullptr;
-    MOPO_HIP(hipMalloc((void**)&m, kb + 2 * vb + sb + tb + 1024));
+    MOPO_HIP(hipMalloc((void**)&m, 2 * kb + 2 * vb + tb + 1024));
     h->sort_keys = (double*)m;
-    h->sort_vals_in = (int32_t*)(m + kb);
-    h->sort_vals = (int32_t*)(m + kb + vb);
-    h->seg = (int*)(m + kb + 2 * vb);
-    h->sort_tmp = (void*)(((uintptr_t)(m + kb + 2 * vb + sb) + 255) & ~(uintptr_t)255);
+    h->sort_vals_in = (int32_t*)(m + 2 * kb);
+    h->sort_vals = (int32_t*)(m + 2 * kb + vb);
+    h->sort_tmp = (void*)(((uintptr_t)(m + 2 * kb + 2 * vb) + 255) & ~(uintptr_t)255);
     h->sort_tmp_bytes = tb;
     h->sort_cap = tot;
   }
-  hipLaunchKernelGGL(iota_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, h->sort_vals_in, n, E, h->seg);
+  uint64_t* kin = reinterpret_cast<uint64_t*>(h->sort_keys);
+  uint64_t* kout = kin + h->sort_cap;
+  hipLaunchKernelGGL(sort_keys_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, d_keys, n, E, kin,
+                     h->sort_vals_in);
   MOPO_HIP(hipGetLastError());
   size_t tb = h->sort_tmp_bytes;
-  // stable ascending sort of the f64 uniforms per member row == np.argsort (distinct keys)
-  MOPO_HIP(hipcub::DeviceSegmentedRadixSort::SortPairs(h->sort_tmp, tb, d_keys, h->sort_keys, h->sort_vals_in,
-                                                       h->sort_vals, (int)tot, E, h->seg, h->seg + 1, 0, 64, s));
+  // one radix sort of (member, 53-bit integer of the uniform) == np.argsort within each member row
+  MOPO_HIP(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp, tb, kin, kout, h->sort_vals_in, h->sort_vals, (int)tot, 0,
+                                              end_bit, s));
   int32_t* tmp_idx = h->sort_vals_in;  // reuse: copy of the current indices
   MOPO_HIP(hipMemcpyAsync(tmp_idx, d_idxs, tot * 4, hipMemcpyDeviceToDevice, s));
   hipLaunchKernelGGL(apply_order_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, h->sort_vals, tmp_idx,

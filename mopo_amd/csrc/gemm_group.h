@@ -9,6 +9,7 @@
 // staged through an XOR-swizzled LDS layout.  Everything here has internal linkage: each
 // translation unit that includes it gets its own copy of the kernel.
 #pragma once
+#include <cstdlib>
 #include <vector>
 
 #include "internal.h"
@@ -151,13 +152,24 @@ struct PanelRegs { float x[16], u[16], w[16]; };
 // Panels are S[k][r ^ psw(k)]: 64 4-byte banks, a 16-float row puts k and k+4 on the same banks, so
 // without the XOR the k-fast stores (64 consecutive k per wave) hit 4 banks 16 ways.  With it the
 // k-fast and r-fast stores and the MFMA operand reads (16 r x 4 k per instruction) are conflict-free.
-static __device__ __forceinline__ int psw(int k) { return (k >> 2) & 15; }
+// 32-wide panels (gemm32 kernel, 128-deep chunks) use S[k][r ^ ((k >> 1) & 31)]: a 32-float row puts
+// k and k+2 on the same banks; the XOR spreads 64 consecutive k (k-fast stores) over all 64 banks and
+// keeps the r-fast stores (32 r x 2 k) and the MFMA operand reads (16 r x 4 k) conflict-free.
+template <int TW>
+static __device__ __forceinline__ int pswz(int k) { return TW == 16 ? ((k >> 2) & 15) : ((k >> 1) & 31); }
+static __device__ __forceinline__ int psw(int k) { return pswz<16>(k); }
 
-template <int MODE, bool IS_A>
+// element q (0..15) of this thread's share of a TW-wide panel chunk (TW = 16: 256 deep; 32: 128)
+template <int MODE, bool IS_A, int TW = 16>
 static __device__ __forceinline__ void panel_rk(int q, int tid, int& r, int& k) {
   constexpr bool rfast = IS_A ? (MODE == 1) : (MODE != 1);
-  if (rfast) { r = tid & 15; k = (tid >> 4) + 16 * q; }
-  else { k = (tid & 63) + 64 * (q & 3); r = (tid >> 6) + 4 * (q >> 2); }
+  if (TW == 16) {
+    if (rfast) { r = tid & 15; k = (tid >> 4) + 16 * q; }
+    else { k = (tid & 63) + 64 * (q & 3); r = (tid >> 6) + 4 * (q >> 2); }
+  } else {
+    if (rfast) { r = tid & 31; k = (tid >> 5) + 8 * q; }
+    else { k = (tid & 63) + 64 * (q & 1); r = (tid >> 6) + 4 * (q >> 1); }
+  }
 }
 
 // buffer descriptor over n floats at p (wave-uniform inputs only)
@@ -169,25 +181,26 @@ static __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t d, int idx)
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(d, idx * 4, 0, 0));
 }
 
-template <int MODE, bool IS_A>
+template <int MODE, bool IS_A, int TW = 16>
 static __device__ __forceinline__ void load_panel(const GemmProb& p, int r0, int kc, int tid, PanelRegs& R) {
+  constexpr int KPER = TW == 16 ? 4 : 2;  // k-fast panel: consecutive q share a row in runs of KPER
   const int Rn = IS_A ? p.M : p.N;  // panel axis extent
   if (MODE == 2) {
     const int ldm = IS_A ? p.a_ldm : p.b_ldm;
     // A(i,k) = u[i] v[k] (m[i,k] > 0);  B(k,j) = u[k] v[j] (m[k,j] > 0).  The A panel is k-fast
-    // (element q: row 4(q>>2) + tid>>6, column 64(q&3) + (tid&63)), so it needs only 4 u and 4 v
-    // values per thread; the B panel is r-fast (column tid&15, row 16q + tid>>4): 16 u, 1 v.
+    // (q / KPER picks the row, q % KPER the k run), so it needs 16/KPER u and KPER v values per
+    // thread; the B panel is r-fast (one column per thread, 16 k): 16 u, 1 v.
     const auto dm = IS_A ? rsrc(p.a_m, (int64_t)(Rn - 1) * ldm + p.K) : rsrc(p.b_m, (int64_t)(p.K - 1) * ldm + Rn);
     const auto du = IS_A ? rsrc(p.a_u, Rn) : rsrc(p.b_u, p.K);
     const auto dv = IS_A ? rsrc(p.a_v, p.K) : rsrc(p.b_v, Rn);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       int r, k;
-      panel_rk<MODE, IS_A>(q, tid, r, k);
+      panel_rk<MODE, IS_A, TW>(q, tid, r, k);
       const int gr = r0 + r, gk = kc + k;
       if (IS_A) {
-        if ((q & 3) == 0) R.u[q >> 2] = bload(du, gr);
-        if (q < 4) R.w[q] = bload(dv, gk);
+        if ((q % KPER) == 0) R.u[q / KPER] = bload(du, gr);
+        if (q < KPER) R.w[q] = bload(dv, gk);
       } else {
         R.u[q] = bload(du, gk);
         if (q == 0) R.w[0] = bload(dv, gr);
@@ -199,7 +212,7 @@ static __device__ __forceinline__ void load_panel(const GemmProb& p, int r0, int
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       int r, k;
-      panel_rk<MODE, IS_A>(q, tid, r, k);
+      panel_rk<MODE, IS_A, TW>(q, tid, r, k);
       const int gr = min(r0 + r, Rn - 1), gk = min(kc + k, p.K - 1);
       const float* src = gr < p.split ? p.B + gr : p.B2 + (gr - p.split);
       R.x[q] = src[(int64_t)gk * p.ldb];
@@ -213,7 +226,7 @@ static __device__ __forceinline__ void load_panel(const GemmProb& p, int r0, int
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       int r, k;
-      panel_rk<MODE, IS_A>(q, tid, r, k);
+      panel_rk<MODE, IS_A, TW>(q, tid, r, k);
       const int gr = r0 + r, gk = kc + k;
       R.x[q] = bload(d, r_major ? gr * ld + gk : gk * ld + gr);
     }
@@ -221,32 +234,35 @@ static __device__ __forceinline__ void load_panel(const GemmProb& p, int r0, int
 }
 
 // keep the loads batched ahead of the first use
-template <int MODE, bool IS_A>
+template <int MODE, bool IS_A, int TW = 16>
 static __device__ __forceinline__ void pin_panel(PanelRegs& R) {
+  constexpr int KPER = TW == 16 ? 4 : 2;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     asm volatile("" : "+v"(R.x[q]));
-    if (MODE == 2 && (IS_A ? q < 4 : true)) asm volatile("" : "+v"(R.u[q]));
-    if (MODE == 2 && (IS_A ? q < 4 : q == 0)) asm volatile("" : "+v"(R.w[q]));
+    if (MODE == 2 && (IS_A ? q < 16 / KPER : true)) asm volatile("" : "+v"(R.u[q]));
+    if (MODE == 2 && (IS_A ? q < KPER : q == 0)) asm volatile("" : "+v"(R.w[q]));
   }
 }
 
-// element q of a rank-1 panel: u * v (the A panel indexes u by q>>2 and v by q&3, see load_panel)
-template <bool IS_A>
+// element q of a rank-1 panel: u * v (the A panel indexes u by q / KPER and v by q % KPER)
+template <bool IS_A, int TW = 16>
 static __device__ __forceinline__ float rank1_uv(const PanelRegs& R, int q) {
-  return IS_A ? R.u[q >> 2] * R.w[q & 3] : R.u[q] * R.w[0];
+  constexpr int KPER = TW == 16 ? 4 : 2;
+  return IS_A ? R.u[q / KPER] * R.w[q % KPER] : R.u[q] * R.w[0];
 }
 
-template <int MODE, bool IS_A>
+// S: [chunk depth][TW] floats
+template <int MODE, bool IS_A, int TW = 16>
 static __device__ __forceinline__ void store_panel(const GemmProb& p, int r0, int kn, int tid, const PanelRegs& R,
-                                            float (*S)[16]) {
+                                                   float* S) {
   const int Rmax = IS_A ? p.M : p.N;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     int r, k;
-    panel_rk<MODE, IS_A>(q, tid, r, k);
-    const float v = MODE == 2 ? (R.x[q] > 0.f ? rank1_uv<IS_A>(R, q) : 0.f) : R.x[q];
-    S[k][r ^ psw(k)] = (r0 + r < Rmax && k < kn) ? v : 0.f;
+    panel_rk<MODE, IS_A, TW>(q, tid, r, k);
+    const float v = MODE == 2 ? (R.x[q] > 0.f ? rank1_uv<IS_A, TW>(R, q) : 0.f) : R.x[q];
+    S[k * TW + (r ^ pswz<TW>(k))] = (r0 + r < Rmax && k < kn) ? v : 0.f;
   }
 }
 
@@ -256,16 +272,29 @@ __host__ static __device__ __forceinline__ int operand_modes(const GemmProb& p) 
   return am * 4 + bm;
 }
 
-template <int AM, int BM>
-static __device__ __forceinline__ void stage_ab(const GemmProb& p, int i0, int j0, int kc, int kn, int tid, float (*As)[16],
-                                         float (*Bs)[16]) {
+template <int AM, int BM, int TW = 16>
+static __device__ __forceinline__ void stage_ab(const GemmProb& p, int i0, int j0, int kc, int kn, int tid, float* As,
+                                                float* Bs) {
   PanelRegs ra, rb;
-  load_panel<AM, true>(p, i0, kc, tid, ra);
-  load_panel<BM, false>(p, j0, kc, tid, rb);
-  pin_panel<AM, true>(ra);
-  pin_panel<BM, false>(rb);
-  store_panel<AM, true>(p, i0, kn, tid, ra, As);
-  store_panel<BM, false>(p, j0, kn, tid, rb, Bs);
+  load_panel<AM, true, TW>(p, i0, kc, tid, ra);
+  load_panel<BM, false, TW>(p, j0, kc, tid, rb);
+  pin_panel<AM, true, TW>(ra);
+  pin_panel<BM, false, TW>(rb);
+  store_panel<AM, true, TW>(p, i0, kn, tid, ra, As);
+  store_panel<BM, false, TW>(p, j0, kn, tid, rb, Bs);
+}
+
+template <int TW>
+static __device__ __forceinline__ void stage_dispatch(const GemmProb& p, int i0, int j0, int kc, int kn, int t,
+                                                      float* As, float* Bs) {
+  switch (operand_modes(p)) {  // the combinations the callers use (launch_group rejects others)
+    case 0: stage_ab<0, 0, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
+    case 1: stage_ab<0, 1, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
+    case 3: stage_ab<0, 3, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
+    case 4: stage_ab<1, 0, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
+    case 6: stage_ab<1, 2, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
+    default: stage_ab<2, 1, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
+  }
 }
 
 // One 16x16 output tile per 256-thread block.  The A[16 x K] and B[K x 16] panels are staged in
@@ -318,14 +347,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
     // 16 elements of each panel per thread; the per-operand mode is dispatched once (uniform
     // branch) so that all 32+ loads are unconditional and issue back to back -- one memory latency
     // per chunk instead of one per element.
-    switch (operand_modes(p)) {  // the combinations sac_step_impl uses (launch_group rejects others)
-      case 0: stage_ab<0, 0>(p, i0, j0, kc, kn, t, As, Bs); break;
-      case 1: stage_ab<0, 1>(p, i0, j0, kc, kn, t, As, Bs); break;
-      case 3: stage_ab<0, 3>(p, i0, j0, kc, kn, t, As, Bs); break;
-      case 4: stage_ab<1, 0>(p, i0, j0, kc, kn, t, As, Bs); break;
-      case 6: stage_ab<1, 2>(p, i0, j0, kc, kn, t, As, Bs); break;
-      default: stage_ab<2, 1>(p, i0, j0, kc, kn, t, As, Bs); break;
-    }
+    stage_dispatch<16>(p, i0, j0, kc, kn, t, &As[0][0], &Bs[0][0]);
     __syncthreads();
     // the staged panels are zero-padded to GKC rows, so every wave runs exactly 16 k-steps of its
     // quarter with no guards: all 32 LDS reads first, then 16 MFMAs on two accumulators
@@ -404,6 +426,138 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
 }
 
 
+// ---- epilogue helpers (gemm32_group_kernel) ---------------------------------------------------
+struct EpiPre { float bias, mask; AdamIn a; int64_t a_idx; };
+
+static __device__ __forceinline__ EpiPre epi_prefetch(const GemmProb& p, const AdamCtx& ad, int gi, int gj) {
+  const int gic = min(gi, p.M - 1), gjc = min(gj, p.N - 1);
+  EpiPre e;
+  e.bias = p.bias ? (p.bias2 && gjc >= p.split ? p.bias2[gjc - p.split] : p.bias[gjc]) : 0.f;
+  e.mask = p.mask ? p.mask[(int64_t)gic * p.ldm + gjc] : 1.f;
+  e.a_idx = p.adam ? (int64_t)(p.C - ad.G) + (int64_t)gic * p.ldc + gjc : 0;
+  e.a = AdamIn{0.f, 0.f, 0.f, 0.f};
+  if (p.adam) e.a = adam_load(ad, e.a_idx);
+  return e;
+}
+
+// bias, activation (+ pre-activation), activation-derivative mask, decay; store; fused Adam
+static __device__ __forceinline__ void epi_apply(const GemmProb& p, const AdamCtx& ad, int gi, int gj, float v,
+                                                 const EpiPre& e, float lr_t, float& gsq) {
+  v += e.bias;
+  if (p.act == ACT_RELU) {
+    v = fmaxf(v, 0.f);
+  } else if (p.act == ACT_SWISH) {
+    if (p.Z) p.Z[(int64_t)gi * p.ldc + gj] = v;
+    v = swish_fast(v);
+  }
+  if (p.mask_kind == MASK_DSWISH) v *= dswish_fast(e.mask);
+  else if (!(e.mask > 0.f)) v = 0.f;
+  if (p.adam) v += p.wd * e.a.p;
+  p.C[(int64_t)gi * p.ldc + gj] = v;
+  if (p.adam) {
+    adam_apply(ad, e.a_idx, v, e.a, lr_t);
+    gsq += v * v;
+  }
+}
+
+// One 32x32 output tile per 256-thread block (for launches whose problems are all >= 32 x 32):
+// each wave owns a 16x16 quadrant over the whole K (no cross-wave reduction), A[32 x 128] and
+// B[128 x 32] chunks are staged through LDS with the same unconditional loads as the 16-wide kernel
+// (16 per operand and thread), half the operand traffic per output of 16x16 tiles and a quarter of
+// the blocks.  Epilogue: the tile goes through LDS, 4 elements per thread (same fused operations).
+constexpr int GKC32 = 128;
+static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmGroup g) {
+  __shared__ float As[GKC32 * 32];
+  __shared__ float Bs[GKC32 * 32];
+  __shared__ float tile[32][33];
+  __shared__ float csum[8][33];
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int pi = 0;
+  while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
+  const GemmProb& p = g.p[pi];
+  const int t0 = blockIdx.x - g.prefix[pi];
+  const int tn_cnt = ceil_div(p.N, 32);
+  const int tm = t0 / tn_cnt, tn = t0 % tn_cnt;
+  const int i0 = tm * 32, j0 = tn * 32;
+  const int wi = w >> 1, wj = w & 1, li = lane & 15, lk = lane >> 4;
+  const bool do_cs = p.colsum && tm == 0;
+  const AdamCtx& ad = g.ad;
+  EpiPre pre[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) pre[q] = epi_prefetch(p, ad, i0 + (tid >> 5) + 8 * q, j0 + (tid & 31));
+  const int64_t c_idx = p.adam && p.colsum ? (int64_t)(p.colsum - ad.G) + min(j0 + (tid & 31), p.N - 1) : 0;
+  AdamIn c_in{0.f, 0.f, 0.f, 0.f};
+  float lr_t = 0.f;
+  if (p.adam) {
+    if (do_cs && tid < 32) c_in = adam_load(ad, c_idx);
+    lr_t = *ad.lr_t;
+  }
+  f32x4 acc0 = zero4(), acc1 = zero4();
+  float cs = 0.f;
+  for (int kc = 0; kc < p.K; kc += GKC32) {
+    const int kn = min(GKC32, p.K - kc);
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    stage_dispatch<32>(p, i0, j0, kc, kn, t, As, Bs);
+    __syncthreads();
+    const int ra_r = wi * 16 + (t & 15), rb_r = wj * 16 + (t & 15), tlk = (t >> 4) & 3;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      float ra[16], rb[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int k = 4 * (half * 16 + s) + tlk;
+        ra[s] = As[k * 32 + (ra_r ^ pswz<32>(k))];
+        rb[s] = Bs[k * 32 + (rb_r ^ pswz<32>(k))];
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        if (s & 1) acc1 = mfma4(ra[s], rb[s], acc1);
+        else acc0 = mfma4(ra[s], rb[s], acc0);
+      }
+    }
+    if (do_cs)
+      for (int k = tid >> 5; k < kn; k += 8) cs += Bs[k * 32 + ((tid & 31) ^ pswz<32>(k))];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) tile[wi * 16 + 4 * lk + r][wj * 16 + li] = acc0[r] + acc1[r];
+  if (do_cs) csum[tid >> 5][tid & 31] = cs;
+  __syncthreads();
+  float gsq = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int ei = (tid >> 5) + 8 * q, ej = tid & 31;
+    const int gi = i0 + ei, gj = j0 + ej;
+    if (gi < p.M && gj < p.N) epi_apply(p, ad, gi, gj, tile[ei][ej], pre[q], lr_t, gsq);
+  }
+  if (do_cs && tid < 32) {
+    float c = 0.f;
+    for (int q = 0; q < 8; ++q) c += csum[q][tid];
+    if (j0 + tid < p.N) {
+      p.colsum[j0 + tid] = c;
+      if (p.adam) {
+        adam_apply(ad, c_idx, c, c_in, lr_t);
+        gsq += c * c;
+      }
+    }
+  }
+  if (ad.norm_part) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) gsq += __shfl_xor(gsq, off);
+    if (lane == 0) red[w] = gsq;
+    __syncthreads();
+    if (tid == 0) {
+      const float b = red[0] + red[1] + red[2] + red[3];
+      const int64_t off = p.adam ? (int64_t)(p.C - ad.G) : -1;
+      float* np = ad.norm_part + 2 * (int64_t)(ad.slot0 + blockIdx.x);
+      np[0] = off >= 0 && off < ad.n_pi ? b : 0.f;
+      np[1] = off >= ad.n_pi && off < ad.n_pi + ad.n_q ? b : 0.f;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 static inline GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C,
                    int ldc) {
@@ -412,20 +566,40 @@ static inline GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, 
   return p;
 }
 
+// Tile policy: 16x16 (gemm_group_kernel).  MOPO_GEMM_TILE=32 selects gemm32_group_kernel for launches
+// whose problems are all >= 32 x 32 (no head epilogue).  Measured on MI355X: 32x32 tiles are slower
+// for both users (SAC step 115.7 vs 99.8 us, BNN.train 6.09k vs 6.51k steps/s): these launches are
+// latency-bound and the 16x16 tiles split K over four waves (16-deep MFMA chains instead of 64).
+static inline int gemm_tile_override() {
+  static const int v = [] {
+    const char* e = std::getenv("MOPO_GEMM_TILE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const AdamCtx* ad = nullptr, int* slot = nullptr,
-                        const HeadCtx* hd = nullptr) {
+                               const HeadCtx* hd = nullptr) {
   GemmGroup g{};
   g.n = (int)ps.size();
   if (g.n > MAXP) return fail("gemm group too large");
-  int tot = 0;
+  bool big = true, head = false;
   for (int i = 0; i < g.n; ++i) {
     const GemmProb& q = ps[i];
     const int c = operand_modes(q);
     if (!(c == 0 || c == 1 || c == 3 || c == 4 || c == 6 || c == 9)) return fail("unsupported gemm operand modes");
     if ((int64_t)q.M * q.K >= (1ll << 29) || (int64_t)q.N * q.K >= (1ll << 29)) return fail("gemm operand too large");
+    if (q.head && (!hd || q.N > 16 || q.N != 2 * hd->A)) return fail("bad head problem");
+    big = big && q.M >= 32 && q.N >= 32;
+    head = head || q.head;
+  }
+  const int ov = gemm_tile_override();
+  const int TW = (ov == 32 && big && !head) ? 32 : 16;
+  int tot = 0;
+  for (int i = 0; i < g.n; ++i) {
     g.p[i] = ps[i];
     g.prefix[i] = tot;
-    tot += ceil_div(ps[i].M, 16) * ceil_div(ps[i].N, 16);
+    tot += ceil_div(ps[i].M, TW) * ceil_div(ps[i].N, TW);
   }
   g.prefix[g.n] = tot;
   if (ad) {
@@ -434,9 +608,8 @@ static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const Ad
     if (slot) *slot += tot;
   }
   if (hd) g.hd = *hd;
-  for (int i = 0; i < g.n; ++i)
-    if (g.p[i].head && (!hd || g.p[i].N > 16 || g.p[i].N != 2 * hd->A)) return fail("bad head problem");
-  hipLaunchKernelGGL(gemm_group_kernel, dim3(tot), dim3(256), 0, s, g);
+  if (TW == 32) hipLaunchKernelGGL(gemm32_group_kernel, dim3(tot), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL(gemm_group_kernel, dim3(tot), dim3(256), 0, s, g);
   MOPO_HIP(hipGetLastError());
   return 0;
 }

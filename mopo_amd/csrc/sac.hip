@@ -66,7 +66,7 @@ struct Sac {
   float* norm_part = nullptr;     // [nslots][2]
   float* loss_part = nullptr;     // [ceil(n / QL_ROWS)][8] sac_qloss_kernel block partials
   unsigned* ticket = nullptr;     // its last-block ticket
-  int nslots = 0;
+  int nslots = 0, nslots_cap = 0;
   float* beta_pow;                // [3] f32 beta1_power, beta2_power (TF1 non-slot vars), this step's lr_t
   int64_t* iter;                  // device step counter (Philox)
   float* logs;                    // [LOG_N]
@@ -552,11 +552,12 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     auto w1 = mk(O, H, n, bt.sa, W, 1, h->dh1p, H, 0, G + o.pW1, H); w1.colsum = G + o.pb1; w1.adam = 1; g.push_back(w1);
     if (launch_group(g, s, &ad, &slot)) return -1;
   }
-  if (slot != h->nslots) return fail("sac: grad-norm slot count mismatch");
+  if (slot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
+  h->nslots = slot;  // blocks of the four backward launches (tile choice: launch_group)
   return 0;
 }
 
-// blocks of the four backward launches (one grad-norm slot each); mirrors sac_step_impl
+// upper bound of the blocks of the four backward launches (16x16 tiles; one grad-norm slot each)
 static int count_slots(const SacDims& d) {
   auto t = [](int M, int N) { return ceil_div(M, 16) * ceil_div(N, 16); };
   const int n = d.n, H = d.H, O = d.O, A = d.A, W = O + A;
@@ -582,10 +583,10 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   h->d.P = h->o.total;
   h->lr = lr; h->gamma = gamma; h->tau = tau; h->rscale = reward_scale; h->tent = target_entropy;
   const int64_t tot = h->o.total + 1, n = batch, W = O + A;
-  h->nslots = count_slots(h->d);
+  h->nslots_cap = h->nslots = count_slots(h->d);
   std::vector<std::pair<void**, size_t>> reg;
   auto f = [&](float** p, size_t cnt) { reg.push_back({(void**)p, cnt * 4}); };
-  f(&h->Pb[1], tot); f(&h->norm_part, 2 * (size_t)h->nslots);
+  f(&h->Pb[1], tot); f(&h->norm_part, 2 * (size_t)h->nslots_cap);
   f(&h->loss_part, 8 * (size_t)ceil_div(batch, QL_ROWS));
   reg.push_back({(void**)&h->ticket, 4});
   f(&h->P, tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->T, tot);
