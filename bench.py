@@ -207,6 +207,46 @@ def c3_leg(args, dev):
             'bf16_peak_tflops': BF16_PEAK_TFLOPS}
 
 
+def c5_leg(args, dev):
+    """BASELINE config C5 (stress), one GPU's share: E=32, H=400, 1M rows / 8 GPUs = 125k rows per GPU,
+    horizon 5, fp32 (synthetic weights; halfcheetah dims)."""
+    import torch
+    from mopo_amd.bnn import construct_model
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout, init_sac_params
+    E5, H5, B, h = 32, 400, 125000, 5
+    rs = np.random.RandomState(4)
+    env_obs = rs.normal(size=(ENV_ROWS, O)).astype(np.float32)
+    model = construct_model(obs_dim=O, act_dim=A, hidden_dim=H5, num_networks=E5, num_elites=5,
+                            separate_mean_var=True, seed=1)
+    mats = model.get_params()
+    x = np.concatenate([env_obs, rs.uniform(-1, 1, (ENV_ROWS, A))], 1)
+    mats[0] = x.mean(0, keepdims=True).astype(np.float32)
+    mats[1] = x.std(0, keepdims=True).astype(np.float32)
+    model.set_params(mats)
+    model.set_elites([0, 1, 2, 3, 4])
+    pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=2 * h * B)
+    ro = ModelRollout(model, B, h)
+    pi = torch.from_numpy(init_sac_params(O, A, HP, seed=2)).to(dev)
+    env = torch.from_numpy(env_obs).to(dev)
+    ro.run(env, pi, pool, B, h, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=0)
+    torch.cuda.synchronize()
+    reps = 2
+    t0 = time.perf_counter()
+    tot = [ro.run(env, pi, pool, B, h, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=1 + i) for i in range(reps)]
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n = int(sum(int(t.sum().item()) for t in tot))
+    flop_row = 2 * E5 * ((O + A) * H5 + 3 * H5 * H5 + 2 * H5 * (O + 1))
+    v = n / dt
+    return {'metric': 'model-rollout transitions/s (C5 stress, one GPU of eight)', 'value': v,
+            'unit': 'transitions/s', 'dtype': 'fp32', 'ms_per_rollout': dt / reps * 1e3,
+            'config': {'workload': 'E=32, H=400, obs=17, act=6, rollout_batch=125000 per GPU (1M / 8), horizon=5',
+                       'rollout_batch_per_gpu': B, 'horizon': h},
+            'bnn_flop_per_row': flop_row, 'ensemble_tflops_lower_bound': v * flop_row / 1e12,
+            'f32_peak_tflops': MFMA_F32_PEAK_TFLOPS}
+
+
 def train_leg(args, env):
     """BNN.train minibatch steps (bnn.py:425-432) at the halfcheetah-mixed size: E=7, H=200, 101k env
     rows -> 100k train rows after the 1000-row holdout, batch 256 (mopo.py:529): 391 Adam steps per
@@ -351,6 +391,7 @@ def main():
             total = total  # counts are already global (gathered)
     sac_rate = sac_leg(args, pool, env, dev, world)
     c3 = c3_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None
+    c5 = c5_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None
     tr = train_leg(args, env) if (rank == 0 and world == 1 and args.train_epochs > 0) else None
     if rank != 0:
         if world > 1:
@@ -385,7 +426,7 @@ def main():
                 'us_per_step': 1e6 / sac_rate, **SAC_DIAG, 'parallelism': 'replicas only (one independent learner per GPU)'},
     }
     if c3 is not None:
-        out['extra_configs'] = {'C3': c3}
+        out['extra_configs'] = {'C3': c3, 'C5_per_gpu': c5}
     if tr is not None:
         out['model_train'] = tr
     if not args.no_cpu_baseline and world == 1:

@@ -144,7 +144,11 @@ __device__ __forceinline__ void head_epilogue(const BnnDev& w, const FwdArgs& a,
 }
 
 template <int KG0, int NBH, int NBO, int R, int MODE, int WAVES>
-__global__ __launch_bounds__(WAVES * 64, WAVES >= 8 ? 1 : 2) void bnn_fwd_kernel(const BnnDev w, const FwdArgs a) {
+#ifndef BNN_MINB_WIDE
+#define BNN_MINB_WIDE 2  // workgroups per CU the H = 400 variant is compiled for
+#endif
+__global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WIDE : 2) void bnn_fwd_kernel(const BnnDev w,
+                                                                                                   const FwdArgs a) {
   constexpr int NBMAX = NBH > NBO ? NBH : NBO;
   constexpr int SLOT = Stage<NBMAX, WAVES>::SLOTS * 256;  // floats per buffer
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];

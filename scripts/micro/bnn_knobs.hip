@@ -8,7 +8,13 @@
 using namespace mopo;
 
 int main(int argc, char** argv) {
-  const int E = 7, O = 17, A = 6, H = 200, D = O + 1, IN = O + A;
+#ifndef KNOB_E
+#define KNOB_E 7
+#endif
+#ifndef KNOB_H
+#define KNOB_H 200
+#endif
+  const int E = KNOB_E, O = 17, A = 6, H = KNOB_H, D = O + 1, IN = O + A;
   const int64_t B = argc > 1 ? atoll(argv[1]) : 50000;
   mopo_bnn_t hb;
   if (mopo_bnn_create(&hb, E, O, A, H, 0, 0)) { printf("create: %s\n", mopo_last_error()); return 1; }
