@@ -89,12 +89,15 @@ def build(args, dev, rank):
     world = int(os.environ.get('WORLD_SIZE', '1'))
     pool_rows = 5 * args.horizon * args.batch * world                       # mopo.py:693-695 (x ranks)
     pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=pool_rows)
-    ro = ModelRollout(model, args.batch, args.horizon)
     pi = torch.from_numpy(init_sac_params(O, A, HP, seed=2)).to(dev)
     env = torch.from_numpy(env_obs).to(dev)
     staging = None
-    if world > 1:
-        staging = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=args.horizon * args.batch)
+    if world > 1:  # per-step staging blocks gathered while the next step computes
+        from mopo_amd.distributed import DistributedRollout
+        staging = DistributedRollout(model, args.batch, args.horizon, O, A, device=dev)
+        ro = staging.ro
+    else:
+        ro = ModelRollout(model, args.batch, args.horizon)
     return model, pool, ro, pi, env, staging
 
 
@@ -103,13 +106,8 @@ def rollout_step(args, ro, pool, pi, env, staging, epoch, rank, world):
     import torch
     if world == 1:
         return ro.run(env, pi, pool, args.batch, args.horizon, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=epoch)
-    from mopo_amd.distributed import allgather_transitions, unpack_rows
-    steps = ro.run(env, pi, staging, args.batch, args.horizon, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=epoch,
-                   staged=True, uid_offset=rank * args.batch)
-    # RCCL all-gather of the staged transitions (+ per-step counts) into every rank's pool
-    rows, counts = allgather_transitions(staging.fields, steps, args.horizon, args.batch, O, A)
-    pool.add_samples(unpack_rows(rows, O, A))
-    return counts.sum(0)
+    # RCCL all-gather of each step's staged transitions (overlapping the next step) into every rank's pool
+    return staging.run(env, pi, pool, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=epoch)
 
 
 def cpu_baseline(args):
@@ -387,8 +385,6 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
-        if staging is not None:
-            total = total  # counts are already global (gathered)
     sac_rate = sac_leg(args, pool, env, dev, world)
     c3 = c3_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None
     c5 = c5_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None

@@ -125,6 +125,14 @@ int mopo_pool_gather(const mopo_pool_desc* pool, int obs_dim, int act_dim, const
 int mopo_pool_random_indices(const mopo_pool_desc* pool, int64_t n, uint64_t seed, uint32_t step,
                              int64_t* d_idx, void* stream);
 
+/* Multi-GPU staging: a block of B staged rows laid out obs f32[B][O] | act f32[B][A] | rew f32[B] |
+ * next_obs f32[B][O] | term u8[B] (a pool descriptor over it has max_size B, no state).  add_blocks
+ * appends the first d_counts[b] rows of each block b = 0..n_blocks-1 in that order (the all-gathered
+ * per-step blocks, step-major then rank-major) and advances ptr/size on the device (no host sync). */
+int64_t mopo_pool_staged_block_bytes(int obs_dim, int act_dim, int64_t B);
+int mopo_pool_add_blocks(const mopo_pool_desc* pool, int obs_dim, int act_dim, const uint8_t* d_blocks,
+                         int64_t block_stride, int n_blocks, int64_t B, const int64_t* d_counts, void* stream);
+
 /* ---- ensemble training (BNN.train, bnn.py:369-503) -------------------------------------
  * Training state of an smv ensemble (E members, 4 swish layers of width H, mean + log-var heads).
  * The host drives the loop (holdout split, bootstrap indices, early stopping, elites: bnn.py:369-503)
@@ -204,6 +212,12 @@ int mopo_rollout_run_staged(mopo_rollout_t h, const mopo_rollout_args* a,
  * 0 start-gather, 1 actor, 2 ensemble forward, 3 FakeEnv post, 4 compaction, 5 pointer advance).
  * profile_read synchronises the recorded events, returns summed ms and launch counts for the
  * runs since the last read, and clears them. */
+/* Steps [step_begin, step_end) of one staged rollout (the first call starts at 0; later calls continue
+ * where the previous one stopped).  Rows of step i go to staging rows (i - step_begin) * B, so with one
+ * call per step each step fills its own staging block -- the multi-GPU path gathers step i while step
+ * i + 1 computes.  d_steps[i] receives the rows of step i. */
+int mopo_rollout_run_staged_steps(mopo_rollout_t h, const mopo_rollout_args* a, const mopo_pool_desc* staging,
+                                  int step_begin, int step_end, void* stream);
 int mopo_rollout_profile(mopo_rollout_t h, int enable);
 int mopo_rollout_profile_read(mopo_rollout_t h, double* ms, int64_t* launches, int n);
 

@@ -55,6 +55,11 @@ SIGNATURES = {
     'mopo_pool_gather': (c_int, [C.POINTER(PoolDesc), c_int, c_int, c_void_p, c_i64, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
     'mopo_pool_random_indices': (c_int, [C.POINTER(PoolDesc), c_i64, c_u64, c_u32, c_void_p, c_void_p]),
+    'mopo_pool_staged_block_bytes': (c_i64, [c_int, c_int, c_i64]),
+    'mopo_pool_add_blocks': (c_int, [C.POINTER(PoolDesc), c_int, c_int, c_void_p, c_i64, c_int, c_i64, c_void_p,
+                                     c_void_p]),
+    'mopo_rollout_run_staged_steps': (c_int, [c_void_p, C.POINTER(RolloutArgs), C.POINTER(PoolDesc), c_int, c_int,
+                                              c_void_p]),
     'mopo_bnn_train_create': (c_int, [C.POINTER(c_void_p), c_int, c_int, c_int, c_int, c_int, c_int, C.c_float]),
     'mopo_bnn_train_destroy': (c_int, [c_void_p]),
     'mopo_bnn_train_set_params': (c_int, [c_void_p, C.POINTER(c_void_p)]),

@@ -14,6 +14,11 @@
 // resident on an XCD share one member's weights in L2.
 #include "mlp_tile.h"
 
+// build-time knobs (defaults are the tuned configuration; scripts/micro/bnn_knobs.hip explores them)
+#ifndef BNN_KPB
+#define BNN_KPB 1  // k-groups staged per barrier in the hidden / head layers
+#endif
+
 #include <vector>
 #include <cstring>
 
@@ -150,7 +155,8 @@ template <int KG0, int NBH, int NBO, int R, int MODE, int WAVES>
 __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WIDE : 2) void bnn_fwd_kernel(const BnnDev w,
                                                                                                    const FwdArgs a) {
   constexpr int NBMAX = NBH > NBO ? NBH : NBO;
-  constexpr int SLOT = Stage<NBMAX, WAVES>::SLOTS * 256;  // floats per buffer
+  constexpr int KPB = BNN_KPB;                            // k-groups per barrier (hidden/head layers)
+  constexpr int SLOT = KPB == 1 ? Stage<NBMAX, WAVES>::SLOTS * 256 : KPB * NBMAX * 256;  // floats per buffer
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
   constexpr int BIASQ = NBH > 3 * NBO ? NBH * 4 : 3 * NBO * 4;  // quads: hidden bias / head aux
   __shared__ __attribute__((aligned(16))) float lds_bias[(BIASQ + 63) / 64 * 256];
@@ -195,14 +201,14 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
                                       lds_bias);
   bias_swish<NBH, R>(lds_bias, acc, hcur, g);
   for (int l = 0; l < 3; ++l) {  // hidden layers 1..3 (constructor.py:31-33)
-    layer_lds<NBH, NBH, R, WAVES, SLOT>(w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lds, wv, lane,
-                                        w.bh + ((int64_t)l * w.E + e) * hp, lds_bias);
+    layer_lds<NBH, NBH, R, WAVES, SLOT, NBH * 4, KPB>(w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lds,
+                                                     wv, lane, w.bh + ((int64_t)l * w.E + e) * hp, lds_bias);
     bias_swish<NBH, R>(lds_bias, acc, hcur, g);
   }
   // ---- heads on the 4th hidden output (bnn.py:661-667): n < D mean, D <= n < 2D log-var
   f32x4 hd[R][NBO];
-  layer_lds<NBH, NBO, R, WAVES, SLOT, 3 * NBO * 4>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds, wv, lane,
-                                                  w.bhd + (int64_t)e * 3 * NBO * 16, lds_bias);
+  layer_lds<NBH, NBO, R, WAVES, SLOT, 3 * NBO * 4, KPB>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds, wv, lane,
+                                                       w.bhd + (int64_t)e * 3 * NBO * 16, lds_bias);
 
 #ifndef BNN_KNOB_NOHEAD
 #pragma unroll

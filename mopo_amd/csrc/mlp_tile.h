@@ -42,7 +42,23 @@ __device__ __forceinline__ void stage_bias(const float* __restrict__ bias, float
   }
 }
 
-template <int KG, int NB, int R, int WAVES, int SLOT, int BQ = NB * 4>
+// KPB > 1: KPB consecutive k-groups (contiguous, k-group-major) are staged and consumed per
+// barrier, with the copies spread over the waves without padding slots (the barrier drains every
+// wave's own copies); SLOT must hold KPB * NB fragments.
+template <int NF, int WAVES>
+__device__ __forceinline__ void stage_frags(const float* __restrict__ src, float* lds, int w, int lane, int n_valid) {
+#pragma unroll
+  for (int i = 0; i < (NF + WAVES - 1) / WAVES; ++i) {
+    const int f = w + i * WAVES;
+    if (f < NF) {
+      const int fs = f < n_valid ? f : n_valid - 1;  // past the layer: re-read a valid fragment (unused)
+      __builtin_amdgcn_global_load_lds((const void*)(src + (fs * 64 + lane) * 4), (lds_void_t)(lds + f * 256), 16, 0,
+                                       0);
+    }
+  }
+}
+
+template <int KG, int NB, int R, int WAVES, int SLOT, int BQ = NB * 4, int KPB = 1>
 __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f32x4 (&in)[R][KG], f32x4 (&acc)[R][NB],
                                           float* lds, int w, int lane, const float* __restrict__ bias = nullptr,
                                           float* lds_bias = nullptr) {
@@ -50,37 +66,53 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f3
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[r][nb] = zero4();
+  constexpr int NBLK = (KG + KPB - 1) / KPB;
   // BNN_KNOB_* (scripts/micro/bnn_knobs.hip): timing-only builds with one part removed
 #ifndef BNN_KNOB_NOBARRIER
   __syncthreads();  // every wave is done reading both buffers (previous layer)
 #endif
 #ifndef BNN_KNOB_NOSTAGE
-  stage_slice<NB, WAVES>(wf, lds, w, lane);
-  if (KG == 1 && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
+  if (KPB == 1) stage_slice<NB, WAVES>(wf, lds, w, lane);
+  else stage_frags<KPB * NB, WAVES>(wf, lds, w, lane, KG * NB);
+  if (NBLK == 1 && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
 #endif
 #pragma unroll
-  for (int kg = 0; kg < KG; ++kg) {
+  for (int blk = 0; blk < NBLK; ++blk) {
 #ifndef BNN_KNOB_NOBARRIER
-    __syncthreads();  // vmcnt(0): slice kg landed (all waves); buffer (kg+1)&1 free
+    __syncthreads();  // vmcnt(0): block blk landed (all waves); buffer (blk+1)&1 free
 #endif
 #ifndef BNN_KNOB_NOSTAGE
-    if (kg + 1 < KG) stage_slice<NB, WAVES>(wf + (kg + 1) * NB * 256, lds + ((kg + 1) & 1) * SLOT, w, lane);
-    if (kg + 2 == KG && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
+    if (blk + 1 < NBLK) {
+      const float* src = wf + (blk + 1) * KPB * NB * 256;
+      float* dst = lds + ((blk + 1) & 1) * SLOT;
+      if (KPB == 1) stage_slice<NB, WAVES>(src, dst, w, lane);
+      else stage_frags<KPB * NB, WAVES>(src, dst, w, lane, (KG - (blk + 1) * KPB) * NB);
+    }
+    if (blk + 2 == NBLK && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
 #endif
-    const float* b = lds + (kg & 1) * SLOT;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const f32x4 fr = *reinterpret_cast<const f32x4*>(b + (nb * 64 + lane) * 4);
+    for (int j = 0; j < KPB; ++j) {
+      const int kg = blk * KPB + j;
+      if (kg < KG) {
+        const float* b = lds + (blk & 1) * SLOT + j * NB * 256;
+        // fragment nb + 1 is read before the MFMAs of fragment nb (one LDS read in flight)
+        f32x4 fr_next = *reinterpret_cast<const f32x4*>(b + lane * 4);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int nb = 0; nb < NB; ++nb) {
+          const f32x4 fr = fr_next;
+          if (nb + 1 < NB) fr_next = *reinterpret_cast<const f32x4*>(b + ((nb + 1) * 64 + lane) * 4);
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
 #ifndef BNN_KNOB_NOMFMA
-          acc[r][nb] = mfma4(fr[t], in[r][kg][t], acc[r][nb]);
+              acc[r][nb] = mfma4(fr[t], in[r][kg][t], acc[r][nb]);
 #else
-          acc[r][nb][t] += fr[t] * in[r][kg][t];
+              acc[r][nb][t] += fr[t] * in[r][kg][t];
 #endif
+            }
         }
+      }
     }
   }
 }

@@ -91,6 +91,59 @@ extern "C" int mopo_pool_add(const mopo_pool_desc* p, int O, int A, const float*
   return pool_advance(p->d_state, p->max_size, n, s);
 }
 
+// ---- append staged blocks in a given order (multi-GPU: the all-gathered per-step blocks, step-major
+// then rank-major = the row order of one single-GPU rollout over the concatenated shards).
+// Block b (at d_blocks + b * stride bytes) holds B rows as obs f32[B][O] | act f32[B][A] | rew f32[B] |
+// next_obs f32[B][O] | term u8[B] (mopo_pool_staged_block_offsets); its first counts[b] rows are live.
+__global__ void pool_add_blocks_kernel(const mopo_pool_desc p, int O, int A, const uint8_t* __restrict__ blocks,
+                                       int64_t stride, int nb, int64_t B, const int64_t* __restrict__ counts) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= B || i >= counts[b]) return;
+  int64_t prefix = 0;
+  for (int q = 0; q < b; ++q) prefix += counts[q];
+  const uint8_t* base = blocks + b * stride;
+  const float* obs = reinterpret_cast<const float*>(base);
+  const float* act = obs + B * O;
+  const float* rew = act + B * A;
+  const float* nobs = rew + B;
+  const uint8_t* term = reinterpret_cast<const uint8_t*>(nobs + B * O);
+  const int64_t pos = (p.d_state[0] + prefix + i) % p.max_size;
+  for (int k = 0; k < O; ++k) {
+    p.d_obs[pos * O + k] = obs[i * O + k];
+    p.d_next_obs[pos * O + k] = nobs[i * O + k];
+  }
+  for (int k = 0; k < A; ++k) p.d_act[pos * A + k] = act[i * A + k];
+  p.d_rew[pos] = rew[i];
+  p.d_term[pos] = term[i];
+}
+
+__global__ void pool_advance_counts_kernel(int64_t* state, int64_t max_size, const int64_t* counts, int nb) {
+  int64_t n = 0;
+  for (int q = 0; q < nb; ++q) n += counts[q];
+  state[0] = (state[0] + n) % max_size;
+  state[1] = min(state[1] + n, max_size);
+}
+
+extern "C" int64_t mopo_pool_staged_block_bytes(int O, int A, int64_t B) {
+  return ((B * (2 * O + A + 1) * 4 + B) + 255) / 256 * 256;
+}
+
+extern "C" int mopo_pool_add_blocks(const mopo_pool_desc* p, int O, int A, const uint8_t* d_blocks, int64_t stride,
+                                    int n_blocks, int64_t B, const int64_t* d_counts, void* stream) {
+  if (check_pool(p)) return -1;
+  MOPO_REQUIRE(d_blocks && d_counts && n_blocks >= 0 && B >= 0, "pool_add_blocks: bad argument");
+  MOPO_REQUIRE(stride >= mopo_pool_staged_block_bytes(O, A, B), "pool_add_blocks: stride smaller than a block");
+  if (n_blocks == 0 || B == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(pool_add_blocks_kernel, dim3((unsigned)((B + 255) / 256), n_blocks), dim3(256), 0, s, *p, O, A,
+                     d_blocks, stride, n_blocks, B, d_counts);
+  MOPO_HIP(hipGetLastError());
+  hipLaunchKernelGGL(pool_advance_counts_kernel, dim3(1), dim3(1), 0, s, p->d_state, p->max_size, d_counts, n_blocks);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
 extern "C" int mopo_pool_gather(const mopo_pool_desc* p, int O, int A, const int64_t* idx, int64_t n,
                                 float* dobs, float* dact, float* drew, float* dterm, float* dnobs, int64_t off,
                                 void* stream) {

@@ -39,6 +39,8 @@ struct Rollout {
   uint8_t* keep;
   int* blockcnt;
   int* cnt;  // [0] live rows this step, [1] survivors
+  // horizon state carried between step-range calls (mopo_rollout_run_staged_steps)
+  int oc = 0, uc = 0, next_step = 0;
 };
 
 constexpr int PB = 256;  // rows per block in post / compact
@@ -195,7 +197,10 @@ __global__ void step_advance_kernel(int* cnt, int64_t* steps, int i, int compact
   if (compacted) cnt[0] = cnt[1];
 }
 
-static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc* p, bool staged,
+// Horizon steps [i0, i1) of one rollout.  i0 == 0 draws the start states and repacks the policy;
+// later ranges continue from the state the previous call left (obs ping-pong, live counts).  Staged
+// rows of step i go to rows (i - i0) * B of the staging descriptor.
+static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc* p, bool staged, int i0, int i1,
                     hipStream_t s) {
   MOPO_REQUIRE(a && p, "rollout: NULL argument");
   MOPO_REQUIRE(a->B >= 0 && a->B <= h->Bmax, "rollout: B exceeds the handle's max_batch");
@@ -205,32 +210,36 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
   MOPO_REQUIRE(a->d_model_inds || (a->d_elites && a->n_elites > 0), "rollout: elites required");
   MOPO_REQUIRE(p->d_obs && p->d_act && p->d_rew && p->d_term && p->d_next_obs, "rollout: NULL pool field");
   MOPO_REQUIRE(staged || p->d_state, "rollout: pool state required");
-  MOPO_REQUIRE(!staged || p->max_size >= (int64_t)a->horizon * a->B, "rollout: staging buffer too small");
   MOPO_REQUIRE(a->d_steps, "rollout: d_steps output required");
-  if (a->B == 0 || a->horizon == 0) return 0;
+  MOPO_REQUIRE(0 <= i0 && i0 <= i1 && i1 <= a->horizon, "rollout: bad step range");
+  MOPO_REQUIRE(i0 == 0 || i0 == h->next_step, "rollout: step ranges must continue the previous call");
+  MOPO_REQUIRE(!staged || p->max_size >= (int64_t)(i1 - i0) * a->B, "rollout: staging buffer too small");
+  if (a->B == 0 || a->horizon == 0 || i0 == i1) return 0;
   Bnn* bnn = h->bnn;
   const int O = bnn->O, A = bnn->A, D = O + 1;
   const int64_t B = a->B;
   const int nblk = ceil_div((int)B, PB);
   const uint32_t step0 = a->epoch * 4096u;
-  {
+  if (i0 == 0) {
+    h->oc = 0;
+    h->uc = 0;
     KTimer t(h, KC_START, s);
     hipLaunchKernelGGL(rollout_start_kernel, dim3(nblk), dim3(PB), 0, s, a->d_env_obs, a->env_size,
                        a->d_start_idx, O, B, a->seed, step0, a->uid_offset, h->obs[0], h->uid[0], h->cnt);
   }
-  MOPO_HIP(hipGetLastError());
-  if (!h->wpk || h->wpk_hp != a->pi_hidden) {
-    if (h->wpk) (void)hipFree(h->wpk);
-    MOPO_HIP(hipMalloc(&h->wpk, actor_packed_floats(O, a->pi_hidden) * sizeof(float)));
-    h->wpk_hp = a->pi_hidden;
-  }
-  {
+  if (i0 == 0) {
+    MOPO_HIP(hipGetLastError());
+    if (!h->wpk || h->wpk_hp != a->pi_hidden) {
+      if (h->wpk) (void)hipFree(h->wpk);
+      MOPO_HIP(hipMalloc(&h->wpk, actor_packed_floats(O, a->pi_hidden) * sizeof(float)));
+      h->wpk_hp = a->pi_hidden;
+    }
     KTimer t(h, KC_START, s);
     if (pack_actor(a->d_pi_params, O, A, a->pi_hidden, h->wpk, s)) return -1;
   }
   const bool compact = a->term_kind != MOPO_TERM_HALFCHEETAH;
-  int oc = 0, uc = 0;
-  for (int i = 0; i < a->horizon; ++i) {
+  int oc = h->oc, uc = h->uc;
+  for (int i = i0; i < i1; ++i) {
     const uint32_t st = step0 + 1 + i;
     ActorArgs aa{};
     aa.P = a->d_pi_params; aa.Wpk = h->wpk; aa.O = O; aa.A = A; aa.Hp = a->pi_hidden;
@@ -239,7 +248,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     aa.seed = a->seed; aa.step = st; aa.d_uid = h->uid[uc];
     aa.act = h->act;
     aa.pool_obs = p->d_obs; aa.pool_act = p->d_act; aa.pool_state = p->d_state; aa.pool_max = p->max_size;
-    aa.stage_base = staged ? (int64_t)i * B : -1;
+    aa.stage_base = staged ? (int64_t)(i - i0) * B : -1;
     aa.pen_zero = h->pen;
     aa.sel_out = h->sel;
     aa.sel_in = a->d_model_inds ? a->d_model_inds + (int64_t)i * B : nullptr;
@@ -264,7 +273,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     pa.eps = a->d_eps_obs ? a->d_eps_obs + (int64_t)i * B * D : nullptr;
     pa.seed = a->seed; pa.step = st; pa.coeff = a->penalty_coeff; pa.term_kind = a->term_kind;
     pa.obs_next = h->obs[oc ^ 1]; pa.keep = h->keep; pa.blockcnt = h->blockcnt;
-    pa.pool = *p; pa.stage_base = staged ? (int64_t)i * B : -1;
+    pa.pool = *p; pa.stage_base = staged ? (int64_t)(i - i0) * B : -1;
     {
       KTimer t(h, KC_POST, s);
       hipLaunchKernelGGL(rollout_post_kernel, dim3(nblk), dim3(PB), 0, s, pa);
@@ -286,6 +295,9 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     }
     MOPO_HIP(hipGetLastError());
   }
+  h->oc = oc;
+  h->uc = uc;
+  h->next_step = i1;
   return 0;
 }
 
@@ -356,12 +368,21 @@ extern "C" int mopo_rollout_run(mopo_rollout_t hh, const mopo_rollout_args* a, c
                                 void* stream) {
   Rollout* h = reinterpret_cast<Rollout*>(hh);
   MOPO_REQUIRE(h, "mopo_rollout_run: NULL handle");
-  return run_impl(h, a, p, false, (hipStream_t)stream);
+  MOPO_REQUIRE(a, "mopo_rollout_run: NULL args");
+  return run_impl(h, a, p, false, 0, a->horizon, (hipStream_t)stream);
 }
 
 extern "C" int mopo_rollout_run_staged(mopo_rollout_t hh, const mopo_rollout_args* a, const mopo_pool_desc* p,
                                        void* stream) {
   Rollout* h = reinterpret_cast<Rollout*>(hh);
   MOPO_REQUIRE(h, "mopo_rollout_run_staged: NULL handle");
-  return run_impl(h, a, p, true, (hipStream_t)stream);
+  MOPO_REQUIRE(a, "mopo_rollout_run_staged: NULL args");
+  return run_impl(h, a, p, true, 0, a->horizon, (hipStream_t)stream);
+}
+
+extern "C" int mopo_rollout_run_staged_steps(mopo_rollout_t hh, const mopo_rollout_args* a, const mopo_pool_desc* p,
+                                             int step_begin, int step_end, void* stream) {
+  Rollout* h = reinterpret_cast<Rollout*>(hh);
+  MOPO_REQUIRE(h && a, "mopo_rollout_run_staged_steps: NULL argument");
+  return run_impl(h, a, p, true, step_begin, step_end, (hipStream_t)stream);
 }

@@ -1,11 +1,13 @@
 """Multi-GPU rollout: shard rollout rows over ranks, RCCL all-gather into replicated device pools.
 
 One process per GPU (torchrun), ``torch.distributed`` backend ``nccl`` (= RCCL over xGMI).  Rank r
-rolls out its own ``B`` rows with ``uid_offset = r*B`` (disjoint Philox sub-streams), staged
-step-major (``mopo_rollout_run_staged``); one ``all_gather_into_tensor`` moves the packed 165-byte
-rows and one moves the per-step counts; every rank then appends all transitions in the global
-order of a single-GPU rollout over the concatenated shards (step-major, then rank-major) to its
-own pool, so the pools stay identical across ranks (SAC samples from them locally).
+rolls out its own ``B`` rows with ``uid_offset = r*B`` (disjoint Philox sub-streams).  The device
+path (``DistributedRollout``) stages each horizon step into its own 165-byte-per-row block and
+all-gathers it asynchronously while the next step computes; every rank then appends all
+transitions in the global order of a single-GPU rollout over the concatenated shards (step-major,
+then rank-major) to its own pool (``mopo_pool_add_blocks``), so the pools stay identical across
+ranks (SAC samples from them locally).  ``pack_rows`` / ``assemble_global`` /
+``allgather_transitions`` are the host-orchestrated form of the same order (CPU gloo tests).
 No reference counterpart (the reference is single-process); see SURVEY §8(e).
 """
 import torch
@@ -46,25 +48,66 @@ def allgather_transitions(staging_fields, steps, horizon, B, O, A, group=None):
     return assemble_global(gathered.view(world, packed.shape[0], -1), counts, horizon, B), counts
 
 
-class DistributedRollout:
-    """Per-rank rollout + all-gather into this rank's replicated ``SimpleReplayPool``."""
+def staged_block_desc(block, B, O, A):
+    """PoolDesc over one staged block (uint8 tensor of mopo_pool_staged_block_bytes): obs | act | rew |
+    next_obs | term (the layout mopo_pool_add_blocks reads)."""
+    from . import _lib as L
+    base = L.ptr(block)
+    obs = base
+    act = obs + 4 * B * O
+    rew = act + 4 * B * A
+    nobs = rew + 4 * B
+    term = nobs + 4 * B * O
+    return L.PoolDesc(d_obs=obs, d_act=act, d_rew=rew, d_term=term, d_next_obs=nobs, d_state=None, max_size=B)
 
-    def __init__(self, model, batch_per_rank, horizon, obs_dim, act_dim, group=None):
+
+class DistributedRollout:
+    """Per-rank rollout + all-gather into this rank's replicated ``SimpleReplayPool``.
+
+    Each horizon step is staged into its own block and all-gathered asynchronously (RCCL runs on its
+    own stream) while the next step computes; the per-step counts are gathered once at the end and
+    ``mopo_pool_add_blocks`` appends every rank's rows in global order (step-major, then rank) with
+    device-side offsets -- no host synchronisation, no packing or re-ordering copies."""
+
+    def __init__(self, model, batch_per_rank, horizon, obs_dim, act_dim, group=None, device=None):
+        import torch
         import torch.distributed as dist
-        from .replay_pool import SimpleReplayPool
+        from . import _lib as L
         from .rollout import ModelRollout
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.group = group
         self.B, self.horizon, self.O, self.A = int(batch_per_rank), int(horizon), obs_dim, act_dim
         self.ro = ModelRollout(model, self.B, self.horizon)
-        self.staging = SimpleReplayPool(obs_dim=obs_dim, act_dim=act_dim, max_size=self.B * self.horizon)
+        self.blk = int(L.lib().mopo_pool_staged_block_bytes(obs_dim, act_dim, self.B))
+        dev = device or torch.device('cuda', torch.cuda.current_device())
+        self.staging = torch.empty((self.horizon, self.blk), dtype=torch.uint8, device=dev)
+        self.gathered = torch.empty((self.horizon, self.world * self.blk), dtype=torch.uint8, device=dev)
+        self.counts = torch.empty((self.world * self.horizon,), dtype=torch.int64, device=dev)
 
     def run(self, env_obs, pi_params, pool, term_kind, penalty_coeff, elites, seed=0, epoch=0, pi_hidden=256):
-        steps = self.ro.run(env_obs, pi_params, self.staging, self.B, self.horizon, term_kind, penalty_coeff, elites,
-                            seed=seed, epoch=epoch, pi_hidden=pi_hidden, staged=True,
-                            uid_offset=self.rank * self.B)
-        rows, counts = allgather_transitions(self.staging.fields, steps, self.horizon, self.B, self.O, self.A,
-                                             self.group)
-        pool.add_samples(unpack_rows(rows, self.O, self.A))
-        return counts.sum(0)
+        import ctypes as C
+        import torch.distributed as dist
+        from . import _lib as L
+        works = []
+
+        def step_desc(i):
+            return staged_block_desc(self.staging[i], self.B, self.O, self.A)
+
+        def step_hook(i, steps):
+            works.append(dist.all_gather_into_tensor(self.gathered[i], self.staging[i], group=self.group,
+                                                     async_op=True))
+
+        steps = self.ro.run(env_obs, pi_params, None, self.B, self.horizon, term_kind, penalty_coeff, elites,
+                            seed=seed, epoch=epoch, pi_hidden=pi_hidden, staged=True, uid_offset=self.rank * self.B,
+                            step_desc=step_desc, step_hook=step_hook)
+        works.append(dist.all_gather_into_tensor(self.counts, steps.contiguous(), group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+        # blocks in memory order (step i, rank r) -> b = i * world + r; counts gathered as [rank][step]
+        cb = self.counts.view(self.world, self.horizon).t().contiguous()
+        desc = pool.desc()
+        L.check(L.lib().mopo_pool_add_blocks(C.byref(desc), self.O, self.A, L.ptr(self.gathered), self.blk,
+                                             self.horizon * self.world, self.B, L.ptr(cb), None))
+        self._keep = cb
+        return self.counts.view(self.world, self.horizon).sum(0)

@@ -65,8 +65,9 @@ class ModelRollout:
 
     def run(self, env_obs, pi_params, pool, batch_size, horizon, term_kind, penalty_coeff, elites,
             seed=0, epoch=0, pi_hidden=256, start_idx=None, eps_act=None, eps_obs=None, model_inds=None,
-            staged=False, uid_offset=0, stream=None):
-        """Returns the device int64[horizon] tensor of rows added per step (steps_added)."""
+            staged=False, uid_offset=0, stream=None, step_desc=None, step_hook=None):
+        """Returns the device int64[horizon] tensor of rows added per step (steps_added).
+        ``step_desc(i)`` / ``step_hook(i, steps)``: per-step staging (see mopo_rollout_run_staged_steps)."""
         import torch
         dev = env_obs.device
         B = int(batch_size)
@@ -88,6 +89,15 @@ class ModelRollout:
             seed=int(seed) & (2 ** 64 - 1), epoch=int(epoch), uid_offset=int(uid_offset),
             d_eps_act=dptr(eps_act, torch.float32), d_eps_obs=dptr(eps_obs, torch.float64),
             d_model_inds=dptr(model_inds, torch.int32), d_steps=L.ptr(steps))
+        if step_hook is not None:
+            # one call per horizon step into the staging block step_hook(i) names; step_hook(i, steps)
+            # is then called after step i is enqueued (multi-GPU: gather step i while i + 1 computes)
+            for i in range(int(horizon)):
+                L.check(L.lib().mopo_rollout_run_staged_steps(self._h, args, step_desc(i), i, i + 1,
+                                                              L.stream_ptr(stream)))
+                step_hook(i, steps)
+            self._keepalive = keep
+            return steps[:horizon]
         desc = pool.desc() if not isinstance(pool, L.PoolDesc) else pool
         fn = L.lib().mopo_rollout_run_staged if staged else L.lib().mopo_rollout_run
         L.check(fn(self._h, args, desc, L.stream_ptr(stream)))
