@@ -42,7 +42,7 @@ int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s) 
   const float* W2 = W1 + O * Hp + Hp;
   const float* Wm = W2 + Hp * Hp + Hp;
   const float* Wl = Wm + Hp * A + A;
-  if (pack_frags(W1, dst, 1, O, Hp, KG0, NB, s)) return -1;
+  if (pack_frags(W1, dst, 1, O, Hp, KG0, NB, s, 1)) return -1;  // obs in slot_feat order
   if (pack_frags(W2, dst + (int64_t)KG0 * NB * 256, 1, Hp, Hp, NB, NB, s)) return -1;
   float* hf = dst + (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256;
   hipLaunchKernelGGL(pack_head_kernel, dim3(ceil_div(NB * 256, 256)), dim3(256), 0, s, Wm, Wl, Hp, A, NB, hf);
@@ -80,7 +80,8 @@ __device__ __forceinline__ void actor_noise(uint64_t seed, uint32_t step, int64_
 
 constexpr int ACT_WAVES = 4;
 
-template <int KG0, int NBP>
+// TQ0: k-steps in the last k-group of the observation (tail_steps(O); 4 = all)
+template <int KG0, int NBP, int TQ0 = 4>
 __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_kernel(const ActorArgs a) {
   constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
@@ -105,15 +106,15 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_kernel(const ActorArg
   for (int kg = 0; kg < KG0; ++kg)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int k = kg * 16 + 4 * g + t;
+      const int k = slot_feat(kg * 16 + 4 * g + t, O);
       float v = 0.f;
-      if (ok && k < O)
+      if (ok && k >= 0)
         v = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
                       : reinterpret_cast<const float*>(a.obs)[row * O + k];
       x0[0][kg][t] = v;
     }
   f32x4 acc[1][NBP], h[1][NBP];
-  layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT>(w1f, x0, acc, lds, wv, lane, b1, lds_bias);  // hidden 1 (:277-278)
+  layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT, NBP * 4, 1, TQ0>(w1f, x0, acc, lds, wv, lane, b1, lds_bias);  // hidden 1 (:277-278)
   bias_relu<NBP>(lds_bias, acc, h, g);
   layer_lds<NBP, NBP, 1, ACT_WAVES, SLOT>(w2f, h, acc, lds, wv, lane, b2, lds_bias);   // hidden 2, relu (:301)
   bias_relu<NBP>(lds_bias, acc, h, g);
@@ -171,7 +172,9 @@ int launch_actor(const ActorArgs& a, hipStream_t s) {
   MOPO_REQUIRE(a.Wpk, "actor: packed weights required");
   dim3 grid(ceil_div((int)a.B, 16 * ACT_WAVES)), block(64 * ACT_WAVES);
   const int KG0 = ceil_div(a.O, 16);
-  if (a.Hp == 256 && KG0 == 2)
+  if (a.Hp == 256 && KG0 == 2 && tail_steps(a.O) == 1)  // halfcheetah / walker2d: 17 = 16 + 1
+    hipLaunchKernelGGL((actor_kernel<2, 16, 1>), grid, block, 0, s, a);
+  else if (a.Hp == 256 && KG0 == 2)
     hipLaunchKernelGGL((actor_kernel<2, 16>), grid, block, 0, s, a);
   else if (a.Hp == 256 && KG0 == 1)
     hipLaunchKernelGGL((actor_kernel<1, 16>), grid, block, 0, s, a);

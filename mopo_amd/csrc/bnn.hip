@@ -25,9 +25,10 @@
 namespace mopo {
 
 // ---------------------------------------------------------------------------------------
-// weight packing:  src W[E][K][N] (TF layout, x @ W)  ->  fragment-major (see internal.h)
+// weight packing:  src W[E][K][N] (TF layout, x @ W)  ->  fragment-major (see internal.h);
+// perm_k / perm_n: that side is a hidden/input width laid out by slot_feat (mlp_tile.h)
 __global__ void pack_frags_kernel(const float* __restrict__ src, float* __restrict__ dst, int E, int K,
-                                  int N, int KG, int NB) {
+                                  int N, int KG, int NB, int perm_k, int perm_n) {
   int64_t total = (int64_t)E * KG * NB * 256;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -37,14 +38,16 @@ __global__ void pack_frags_kernel(const float* __restrict__ src, float* __restri
     int kg = (f / NB) % KG;
     int e = f / ((int64_t)NB * KG);
     int k = kg * 16 + 4 * (lane >> 4) + t, n = nb * 16 + (lane & 15);
-    dst[i] = (k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f;
+    if (perm_k) k = slot_feat(k, K);
+    if (perm_n) n = slot_feat(n, N);
+    dst[i] = (k >= 0 && n >= 0 && k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f;
   }
 }
 
 // bf16 fragments for v_mfma_f32_16x16x32_bf16 (k-group of 32, permuted k order: mlp_tile.h):
 // frag (kg, nb), lane l (n = l&15, g = l>>4), element j = W[e][32 kg + bf16_kperm(g, j)][16 nb + n]
 __global__ void pack_frags_bf16_kernel(const float* __restrict__ src, short* __restrict__ dst, int E, int K, int N,
-                                       int KG, int NB) {
+                                       int KG, int NB, int perm_k, int perm_n) {
   int64_t total = (int64_t)E * KG * NB * 512;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -54,23 +57,26 @@ __global__ void pack_frags_bf16_kernel(const float* __restrict__ src, short* __r
     int kg = (f / NB) % KG;
     int e = f / ((int64_t)NB * KG);
     int k = kg * 32 + bf16_kperm(lane >> 4, j), n = nb * 16 + (lane & 15);
-    dst[i] = to_bf16((k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f);
+    if (perm_k) k = slot_feat(k, K);
+    if (perm_n) n = slot_feat(n, N);
+    dst[i] = to_bf16((k >= 0 && n >= 0 && k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f);
   }
 }
 
+// hidden biases in slot order (slot_feat)
 __global__ void pack_bias_kernel(const float* __restrict__ src, float* __restrict__ dst, int E, int N,
                                  int NP) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= E * NP) return;
-  int e = i / NP, n = i % NP;
-  dst[i] = n < N ? src[e * N + n] : 0.f;
+  int e = i / NP, n = slot_feat(i % NP, N);
+  dst[i] = n >= 0 ? src[e * N + n] : 0.f;
 }
 
 // ---------------------------------------------------------------------------------------
-int pack_frags(const float* src, float* dst, int E, int K, int N, int KG, int NB, hipStream_t s) {
+int pack_frags(const float* src, float* dst, int E, int K, int N, int KG, int NB, hipStream_t s, int perm_k) {
   const int64_t tot = (int64_t)E * KG * NB * 256;
   const int blocks = (int)std::min<int64_t>((tot + 255) / 256, 4096);
-  hipLaunchKernelGGL(pack_frags_kernel, dim3(blocks), dim3(256), 0, s, src, dst, E, K, N, KG, NB);
+  hipLaunchKernelGGL(pack_frags_kernel, dim3(blocks), dim3(256), 0, s, src, dst, E, K, N, KG, NB, perm_k, 0);
   MOPO_HIP(hipGetLastError());
   return 0;
 }
@@ -148,7 +154,8 @@ __device__ __forceinline__ void head_epilogue(const BnnDev& w, const FwdArgs& a,
   }
 }
 
-template <int KG0, int NBH, int NBO, int R, int MODE, int WAVES>
+// TQ0 / TQH: k-steps run in the last k-group of the inputs / hidden width (tail_steps; 4 = all)
+template <int KG0, int NBH, int NBO, int R, int MODE, int WAVES, int TQ0 = 4, int TQH = 4>
 #ifndef BNN_MINB_WIDE
 #define BNN_MINB_WIDE 2  // workgroups per CU the H = 400 variant is compiled for
 #endif
@@ -185,9 +192,9 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
     for (int kg = 0; kg < KG0; ++kg)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const int k = kg * 16 + 4 * g + t;
+        const int k = slot_feat(kg * 16 + 4 * g + t, IN);
         float v = 0.f;
-        if (ok && k < IN) {
+        if (ok && k >= 0) {
           float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
                             : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
           v = (raw - w.mu[k]) / w.sigma[k];
@@ -197,17 +204,17 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
   }
   f32x4 acc[R][NBH], hcur[R][NBH];
   const int64_t hp = w.BS;  // per-member bias stride
-  layer_lds<KG0, NBH, R, WAVES, SLOT>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv, lane, w.b0 + e * hp,
-                                      lds_bias);
+  layer_lds<KG0, NBH, R, WAVES, SLOT, NBH * 4, 1, TQ0>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv, lane,
+                                                     w.b0 + e * hp, lds_bias);
   bias_swish<NBH, R>(lds_bias, acc, hcur, g);
   for (int l = 0; l < 3; ++l) {  // hidden layers 1..3 (constructor.py:31-33)
-    layer_lds<NBH, NBH, R, WAVES, SLOT, NBH * 4, KPB>(w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lds,
+    layer_lds<NBH, NBH, R, WAVES, SLOT, NBH * 4, KPB, TQH>(w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lds,
                                                      wv, lane, w.bh + ((int64_t)l * w.E + e) * hp, lds_bias);
     bias_swish<NBH, R>(lds_bias, acc, hcur, g);
   }
   // ---- heads on the 4th hidden output (bnn.py:661-667): n < D mean, D <= n < 2D log-var
   f32x4 hd[R][NBO];
-  layer_lds<NBH, NBO, R, WAVES, SLOT, 3 * NBO * 4, KPB>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds, wv, lane,
+  layer_lds<NBH, NBO, R, WAVES, SLOT, 3 * NBO * 4, KPB, TQH>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds, wv, lane,
                                                        w.bhd + (int64_t)e * 3 * NBO * 16, lds_bias);
 
 #ifndef BNN_KNOB_NOHEAD
@@ -239,9 +246,9 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_bf16_kernel(const BnnDe
   bf16x8 x0[1];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int k = bf16_kperm(g, j);
+    const int k = slot_feat(bf16_kperm(g, j), IN);
     float v = 0.f;
-    if (ok && k < IN) {
+    if (ok && k >= 0) {
       float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
                         : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
       v = (raw - w.mu[k]) / w.sigma[k];
@@ -282,15 +289,17 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_bf16_kernel(const BnnDe
 #endif
 constexpr int FWD_WAVES = BNN_FWD_WAVES;
 
-template <int KG0, int NBH, int NBO, int R>
+template <int KG0, int NBH, int NBO, int R, int TQ0 = 4, int TQH = 4>
 static int launch_fwd_t(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   a.ntiles = (int)ceil_div((int)a.B, 16 * R);
   if (a.ntiles == 0) return 0;
   dim3 grid(ceil_div(a.ntiles, FWD_WAVES) * h->E), block(64 * FWD_WAVES);
   if (mode == FWD_PREDICT)
-    hipLaunchKernelGGL((bnn_fwd_kernel<KG0, NBH, NBO, R, FWD_PREDICT, FWD_WAVES>), grid, block, 0, s, h->dev, a);
+    hipLaunchKernelGGL((bnn_fwd_kernel<KG0, NBH, NBO, R, FWD_PREDICT, FWD_WAVES, TQ0, TQH>), grid, block, 0, s, h->dev,
+                       a);
   else
-    hipLaunchKernelGGL((bnn_fwd_kernel<KG0, NBH, NBO, R, FWD_ROLLOUT, FWD_WAVES>), grid, block, 0, s, h->dev, a);
+    hipLaunchKernelGGL((bnn_fwd_kernel<KG0, NBH, NBO, R, FWD_ROLLOUT, FWD_WAVES, TQ0, TQH>), grid, block, 0, s, h->dev,
+                       a);
   MOPO_HIP(hipGetLastError());
   return 0;
 }
@@ -300,8 +309,13 @@ static int launch_fwd_h(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s)
   switch (h->dev.NBH) {
     case 2: return launch_fwd_t<KG0, 2, NBO, 2>(h, mode, a, s);
     case 4: return launch_fwd_t<KG0, 4, NBO, 2>(h, mode, a, s);
-    case 13: return launch_fwd_t<KG0, 13, NBO, BNN_R13>(h, mode, a, s);
-    case 25: return launch_fwd_t<KG0, 25, NBO, 1>(h, mode, a, s);
+    case 13:  // H = 200 with 17 + 6 inputs (every halfcheetah / walker2d config): skip the padding k-steps
+      if (KG0 == 2 && NBO == 3 && tail_steps(h->dev.IN) <= 2 && tail_steps(h->H) <= 2)
+        return launch_fwd_t<KG0, 13, NBO, BNN_R13, 2, 2>(h, mode, a, s);
+      return launch_fwd_t<KG0, 13, NBO, BNN_R13>(h, mode, a, s);
+    case 25:
+      if (KG0 == 2 && NBO == 3 && tail_steps(h->dev.IN) <= 2) return launch_fwd_t<KG0, 25, NBO, 1, 2, 4>(h, mode, a, s);
+      return launch_fwd_t<KG0, 25, NBO, 1>(h, mode, a, s);
   }
   return fail("bnn: unsupported hidden size (supported: 32, 64, 200, 400; got H=" +
               std::to_string(h->H) + ")");
@@ -426,11 +440,11 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
   stage_n = std::max(stage_n, (size_t)E * IN * H);
   float* stage = nullptr;
   MOPO_HIP(hipMalloc(&stage, stage_n * sizeof(float)));
-  auto pack = [&](const float* src, size_t nsrc, float* dst, int K, int N, int KG, int NB) -> int {
+  auto pack = [&](const float* src, size_t nsrc, float* dst, int K, int N, int KG, int NB, int perm_n) -> int {
     MOPO_HIP(hipMemcpy(stage, src, nsrc * sizeof(float), hipMemcpyHostToDevice));
     int64_t tot = (int64_t)E * KG * NB * 256;
     int blocks = (int)std::min<int64_t>((tot + 255) / 256, 4096);
-    hipLaunchKernelGGL(pack_frags_kernel, dim3(blocks), dim3(256), 0, 0, stage, dst, E, K, N, KG, NB);
+    hipLaunchKernelGGL(pack_frags_kernel, dim3(blocks), dim3(256), 0, 0, stage, dst, E, K, N, KG, NB, 1, perm_n);
     MOPO_HIP(hipGetLastError());
     MOPO_HIP(hipDeviceSynchronize());
     return 0;
@@ -443,13 +457,13 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
     return 0;
   };
   int rc = 0;
-  rc |= pack(W[0], (size_t)E * IN * H, w0, IN, H, KG0, NBH);
+  rc |= pack(W[0], (size_t)E * IN * H, w0, IN, H, KG0, NBH, 1);
   rc |= packb(Bv[0], b0, H, (int)hp);
   for (int l = 0; l < 3; ++l) {
-    rc |= pack(W[1 + l], (size_t)E * H * H, wh + (int64_t)l * E * NBH * NBH * 256, H, H, NBH, NBH);
+    rc |= pack(W[1 + l], (size_t)E * H * H, wh + (int64_t)l * E * NBH * NBH * 256, H, H, NBH, NBH, 1);
     rc |= packb(Bv[1 + l], bh + l * E * hp, H, (int)hp);
   }
-  rc |= pack(head.data(), head.size(), whd, H, 2 * D, NBH, NBO);
+  rc |= pack(head.data(), head.size(), whd, H, 2 * D, NBH, NBO, 0);  // head outputs: natural order
   {  // head aux [E][bias | max_logvar | min_logvar], NBO*16 each (logvar bounds at columns D..2D-1)
     std::vector<float> aux((size_t)s_bhd, 0.f);
     for (int e = 0; e < E; ++e) {
@@ -470,19 +484,20 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
     float* b0f = reinterpret_cast<float*>(h->bbuf);
     float* bhf = b0f + f0 * 256;
     float* bdf = bhf + fh * 256;
-    auto packh = [&](const float* src, size_t nsrc, float* dst, int K, int N, int KGb, int NB) -> int {
+    auto packh = [&](const float* src, size_t nsrc, float* dst, int K, int N, int KGb, int NB, int perm_n) -> int {
       MOPO_HIP(hipMemcpy(stage, src, nsrc * sizeof(float), hipMemcpyHostToDevice));
       int64_t tot = (int64_t)E * KGb * NB * 512;
       int blocks = (int)std::min<int64_t>((tot + 255) / 256, 4096);
-      hipLaunchKernelGGL(pack_frags_bf16_kernel, dim3(blocks), dim3(256), 0, 0, stage, (short*)dst, E, K, N, KGb, NB);
+      hipLaunchKernelGGL(pack_frags_bf16_kernel, dim3(blocks), dim3(256), 0, 0, stage, (short*)dst, E, K, N, KGb, NB, 1,
+                         perm_n);
       MOPO_HIP(hipGetLastError());
       MOPO_HIP(hipDeviceSynchronize());
       return 0;
     };
-    rc |= packh(W[0], (size_t)E * IN * H, b0f, IN, H, 1, NB2);
+    rc |= packh(W[0], (size_t)E * IN * H, b0f, IN, H, 1, NB2, 1);
     for (int l = 0; l < 3; ++l)
-      rc |= packh(W[1 + l], (size_t)E * H * H, bhf + (int64_t)l * E * KG * NB2 * 256, H, H, KG, NB2);
-    rc |= packh(head.data(), head.size(), bdf, H, 2 * D, KG, NBO);
+      rc |= packh(W[1 + l], (size_t)E * H * H, bhf + (int64_t)l * E * KG * NB2 * 256, H, H, KG, NB2, 1);
+    rc |= packh(head.data(), head.size(), bdf, H, 2 * D, KG, NBO, 0);
     d.w0b = b0f; d.whb = bhf; d.whdb = bdf;
   }
   (void)hipFree(stage);

@@ -67,7 +67,8 @@ struct FwdArgs {
 
 int launch_bnn_fwd(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s);
 // W[E][K][N] (TF layout) -> fragment-major (see BnnDev) on stream s
-int pack_frags(const float* src, float* dst, int E, int K, int N, int KG, int NB, hipStream_t s);
+// perm_k: the K side is an input width in slot_feat order (mlp_tile.h)
+int pack_frags(const float* src, float* dst, int E, int K, int N, int KG, int NB, hipStream_t s, int perm_k = 0);
 
 // termination kinds (mopo/static)
 __device__ __forceinline__ bool term_fn(int kind, const double* nobs, int O) {

@@ -4,6 +4,24 @@
 
 namespace mopo {
 
+// ---- slot -> feature map of a width-F dimension tiled in 16-slot blocks -----------------------
+// Slot s = 4g + t of a block is MFMA lane group g, register (= k-step) t.  Full blocks are the
+// identity.  The last partial block (rem = F mod 16 features) packs its features into the first
+// q = ceil(rem / 4) registers of every lane group -- feature 16 blk + q g + t for t < q -- so its
+// registers t >= q hold only padding and a layer consuming it skips those k-steps (TQ below).
+// Weights (both K and N sides of hidden layers), biases and the layer-0 inputs all use it; the
+// head's outputs keep the natural order.  H = 200: 52 -> 50 k-steps per layer; 23 inputs: 8 -> 6.
+__host__ __device__ __forceinline__ int slot_feat(int slot, int F) {
+  const int blk = slot >> 4, rem = F - 16 * blk;
+  if (rem >= 16) return slot;
+  if (rem <= 0) return -1;
+  const int q = (rem + 3) >> 2, g = (slot >> 2) & 3, t = slot & 3, f = q * g + t;
+  return (t < q && f < rem) ? 16 * blk + f : -1;
+}
+
+// k-steps a consumer must run in the last 16-deep k-group of a width-F input (4: no skip)
+__host__ __device__ constexpr int tail_steps(int F) { return (F & 15) == 0 ? 4 : ((F & 15) + 3) >> 2; }
+
 // ---- LDS-staged weight streaming ------------------------------------------------------------
 // A workgroup of WAVES waves shares one member; every k-group slice of a layer (NB fragments,
 // 1 KiB each, contiguous in HBM) is copied HBM->LDS once per workgroup with global_load_lds
@@ -58,7 +76,8 @@ __device__ __forceinline__ void stage_frags(const float* __restrict__ src, float
   }
 }
 
-template <int KG, int NB, int R, int WAVES, int SLOT, int BQ = NB * 4, int KPB = 1>
+// TQ: k-steps run in the last k-group (slot_feat tail; 4 = all).
+template <int KG, int NB, int R, int WAVES, int SLOT, int BQ = NB * 4, int KPB = 1, int TQ = 4>
 __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f32x4 (&in)[R][KG], f32x4 (&acc)[R][NB],
                                           float* lds, int w, int lane, const float* __restrict__ bias = nullptr,
                                           float* lds_bias = nullptr) {
@@ -102,7 +121,7 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f3
           const f32x4 fr = fr_next;
           if (nb + 1 < NB) fr_next = *reinterpret_cast<const f32x4*>(b + ((nb + 1) * 64 + lane) * 4);
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
+          for (int t = 0; t < (kg + 1 == KG ? TQ : 4); ++t)
 #pragma unroll
             for (int r = 0; r < R; ++r) {
 #ifndef BNN_KNOB_NOMFMA
