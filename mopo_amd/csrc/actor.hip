@@ -84,9 +84,9 @@ constexpr int ACT_WAVES = 4;
 template <int KG0, int NBP, int TQ0 = 4>
 __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_kernel(const ActorArgs a) {
   constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
-  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
   __shared__ float head[ACT_WAVES][16][17];
-  __shared__ __attribute__((aligned(16))) float lds_bias[(NBP * 4 + 63) / 64 * 256];
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + (NBP * 4 + 63) / 64 * 256];  // one array (bnn.hip)
+  float* lds_bias = lds + 2 * SLOT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   if ((int64_t)blockIdx.x * ACT_WAVES * 16 >= count) return;  // whole workgroup past the live rows

@@ -39,7 +39,8 @@ __global__ void pack_frags_kernel(const float* __restrict__ src, float* __restri
     int e = f / ((int64_t)NB * KG);
     int k = kg * 16 + 4 * (lane >> 4) + t, n = nb * 16 + (lane & 15);
     if (perm_k) k = slot_feat(k, K);
-    if (perm_n) n = slot_feat(n, N);
+    if (perm_n == 1) n = slot_feat(n, N);
+    else if (perm_n == 2) n = head_col(n, N / 2);  // fused [mean | log-var] head, N = 2D
     dst[i] = (k >= 0 && n >= 0 && k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f;
   }
 }
@@ -58,7 +59,8 @@ __global__ void pack_frags_bf16_kernel(const float* __restrict__ src, short* __r
     int e = f / ((int64_t)NB * KG);
     int k = kg * 32 + bf16_kperm(lane >> 4, j), n = nb * 16 + (lane & 15);
     if (perm_k) k = slot_feat(k, K);
-    if (perm_n) n = slot_feat(n, N);
+    if (perm_n == 1) n = slot_feat(n, N);
+    else if (perm_n == 2) n = head_col(n, N / 2);
     dst[i] = to_bf16((k >= 0 && n >= 0 && k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f);
   }
 }
@@ -106,12 +108,12 @@ __device__ __forceinline__ void bias_swish(const float* lds_bias, const f32x4 (&
 }
 
 // heads -> outputs for one row per lane group (bnn.py:661-675; rollout mode: fake_env.py:66-81, 110)
-// hx = the member's head aux block [bias | max_logvar | min_logvar] (NBO*16 each, logvar bounds at
-// columns D..2D-1), staged in LDS by the head layer; sel_e = the row's selected member (rollout)
+// hx = the member's head aux block [bias | max_logvar | min_logvar] (NBO*16 each, in head_col slot
+// order), staged in LDS by the head layer; sel_e = the row's selected member (rollout)
 template <int NBO, int MODE>
 __device__ __forceinline__ void head_epilogue(const BnnDev& w, const FwdArgs& a, const f32x4 (&hd)[NBO], int e,
                                               int64_t row, int64_t count, int g, const float* hx, int sel_e) {
-  const int D = w.D;
+  const int D = w.D, Q = (D + 3) >> 2;
   const bool ok = row < count;
   float ss = 0.f;  // sum of std^2 over D (learned-var penalty, fake_env.py:110)
   const bool selected = (MODE == FWD_ROLLOUT) && ok && sel_e == e;
@@ -122,27 +124,31 @@ __device__ __forceinline__ void head_epilogue(const BnnDev& w, const FwdArgs& a,
     const f32x4 bmn = *reinterpret_cast<const f32x4*>(hx + 2 * NBO * 16 + nb * 16 + 4 * g);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int n = nb * 16 + 4 * g + t;
-      float v = hd[nb][t] + bb[t];
-      if (n < D) {
-        if (MODE == FWD_PREDICT) {
-          if (ok) a.mean[((int64_t)e * a.B + row) * D + n] = v;
-        } else if (selected) {
-          a.mean_sel[row * D + n] = v;
-        }
-      } else if (n < 2 * D) {
-        const int d = n - D;
+      const int j = 4 * nb + t;  // wave-uniform kind
+      const float v = hd[nb][t] + bb[t];
+      if (j < Q) {
+        const int d = g + 4 * j;
+        const bool valid = d < D;
         const float mx = bmx[t], mn = bmn[t];
         float lv = mx - softplus_fast(mx - v);  // bnn.py:669
         lv = mn + softplus_fast(lv - mn);       // bnn.py:670
         const float l2 = lv * 1.4426950408889634f;
         if (MODE == FWD_PREDICT) {
           const float var = __builtin_amdgcn_exp2f(l2);         // bnn.py:675
-          if (ok) a.var[((int64_t)e * a.B + row) * D + d] = var;
+          if (ok && valid) a.var[((int64_t)e * a.B + row) * D + d] = var;
         } else {
           const float sd = __builtin_amdgcn_exp2f(0.5f * l2);   // sqrt(exp(lv)), fake_env.py:67
-          ss += sd * sd;
-          if (selected) a.std_sel[row * D + d] = sd;
+          if (valid) ss += sd * sd;
+          if (selected && valid) a.std_sel[row * D + d] = sd;
+        }
+      } else if (j < 2 * Q) {
+        const int d = g + 4 * (j - Q);
+        if (d < D) {
+          if (MODE == FWD_PREDICT) {
+            if (ok) a.mean[((int64_t)e * a.B + row) * D + d] = v;
+          } else if (selected) {
+            a.mean_sel[row * D + d] = v;
+          }
         }
       }
     }
@@ -164,9 +170,12 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
   constexpr int NBMAX = NBH > NBO ? NBH : NBO;
   constexpr int KPB = BNN_KPB;                            // k-groups per barrier (hidden/head layers)
   constexpr int SLOT = KPB == 1 ? Stage<NBMAX, WAVES>::SLOTS * 256 : KPB * NBMAX * 256;  // floats per buffer
-  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
   constexpr int BIASQ = NBH > 3 * NBO ? NBH * 4 : 3 * NBO * 4;  // quads: hidden bias / head aux
-  __shared__ __attribute__((aligned(16))) float lds_bias[(BIASQ + 63) / 64 * 256];
+  // ONE __shared__ array (weight double buffer | bias): a second LDS object beside the
+  // global_load_lds destination makes hipcc wait vmcnt(0) before the first ds_read of a k-group,
+  // draining the next slice's copy instead of overlapping it with the MFMAs
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + (BIASQ + 63) / 64 * 256];
+  float* lds_bias = lds + 2 * SLOT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
@@ -204,6 +213,30 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
   }
   f32x4 acc[R][NBH], hcur[R][NBH];
   const int64_t hp = w.BS;  // per-member bias stride
+#ifndef BNN_KNOB_NOXPRE
+  // each layer's first weight slice is copied during the previous layer's last k-group
+  const float* wh0 = w.wh + (int64_t)e * NBH * NBH * 256;
+  layer_lds<KG0, NBH, R, WAVES, SLOT, NBH * 4, 1, TQ0, NBH>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv,
+                                                          lane, w.b0 + e * hp, lds_bias, 0, wh0);
+  bias_swish<NBH, R>(lds_bias, acc, hcur, g);
+  int par = KG0 & 1;
+  for (int l = 0; l < 2; ++l) {  // hidden layers 1, 2 (constructor.py:31-33)
+    layer_lds<NBH, NBH, R, WAVES, SLOT, NBH * 4, 1, TQH, NBH, true>(
+        w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lds, wv, lane,
+        w.bh + ((int64_t)l * w.E + e) * hp, lds_bias, par, w.wh + ((int64_t)(l + 1) * w.E + e) * NBH * NBH * 256);
+    bias_swish<NBH, R>(lds_bias, acc, hcur, g);
+    par = (par + NBH) & 1;
+  }
+  layer_lds<NBH, NBH, R, WAVES, SLOT, NBH * 4, 1, TQH, NBO, true>(  // hidden layer 3
+      w.wh + ((int64_t)2 * w.E + e) * NBH * NBH * 256, hcur, acc, lds, wv, lane, w.bh + ((int64_t)2 * w.E + e) * hp,
+      lds_bias, par, w.whd + (int64_t)e * NBH * NBO * 256);
+  bias_swish<NBH, R>(lds_bias, acc, hcur, g);
+  par = (par + NBH) & 1;
+  f32x4 hd[R][NBO];
+  layer_lds<NBH, NBO, R, WAVES, SLOT, 3 * NBO * 4, 1, TQH, 0, true>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds,
+                                                                   wv, lane, w.bhd + (int64_t)e * 3 * NBO * 16,
+                                                                   lds_bias, par);
+#else
   layer_lds<KG0, NBH, R, WAVES, SLOT, NBH * 4, 1, TQ0>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv, lane,
                                                      w.b0 + e * hp, lds_bias);
   bias_swish<NBH, R>(lds_bias, acc, hcur, g);
@@ -216,6 +249,8 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
   f32x4 hd[R][NBO];
   layer_lds<NBH, NBO, R, WAVES, SLOT, 3 * NBO * 4, KPB, TQH>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds, wv, lane,
                                                        w.bhd + (int64_t)e * 3 * NBO * 16, lds_bias);
+
+#endif
 
 #ifndef BNN_KNOB_NOHEAD
 #pragma unroll
@@ -463,15 +498,19 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
     rc |= pack(W[1 + l], (size_t)E * H * H, wh + (int64_t)l * E * NBH * NBH * 256, H, H, NBH, NBH, 1);
     rc |= packb(Bv[1 + l], bh + l * E * hp, H, (int)hp);
   }
-  rc |= pack(head.data(), head.size(), whd, H, 2 * D, NBH, NBO, 0);  // head outputs: natural order
-  {  // head aux [E][bias | max_logvar | min_logvar], NBO*16 each (logvar bounds at columns D..2D-1)
+  rc |= pack(head.data(), head.size(), whd, H, 2 * D, NBH, NBO, 2);  // head outputs: head_col slots
+  {  // head aux [E][bias | max_logvar | min_logvar], NBO*16 each, in head_col slot order
     std::vector<float> aux((size_t)s_bhd, 0.f);
     for (int e = 0; e < E; ++e) {
       float* x = aux.data() + (size_t)e * 3 * NBO * 16;
-      for (int j = 0; j < 2 * D; ++j) x[j] = headb[(size_t)e * 2 * D + j];
-      for (int dd = 0; dd < D; ++dd) {
-        x[NBO * 16 + D + dd] = arrs[h->smv ? 14 : 12][dd];
-        x[2 * NBO * 16 + D + dd] = arrs[h->smv ? 15 : 13][dd];
+      for (int sl = 0; sl < NBO * 16; ++sl) {
+        const int c = head_col(sl, D);
+        if (c < 0) continue;
+        x[sl] = headb[(size_t)e * 2 * D + c];
+        if (c >= D) {
+          x[NBO * 16 + sl] = arrs[h->smv ? 14 : 12][c - D];
+          x[2 * NBO * 16 + sl] = arrs[h->smv ? 15 : 13][c - D];
+        }
       }
     }
     MOPO_HIP(hipMemcpy(bhd, aux.data(), aux.size() * sizeof(float), hipMemcpyHostToDevice));
@@ -497,7 +536,7 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
     rc |= packh(W[0], (size_t)E * IN * H, b0f, IN, H, 1, NB2, 1);
     for (int l = 0; l < 3; ++l)
       rc |= packh(W[1 + l], (size_t)E * H * H, bhf + (int64_t)l * E * KG * NB2 * 256, H, H, KG, NB2, 1);
-    rc |= packh(head.data(), head.size(), bdf, H, 2 * D, KG, NBO, 0);
+    rc |= packh(head.data(), head.size(), bdf, H, 2 * D, KG, NBO, 2);
     d.w0b = b0f; d.whb = bhf; d.whdb = bdf;
   }
   (void)hipFree(stage);

@@ -19,6 +19,18 @@ __host__ __device__ __forceinline__ int slot_feat(int slot, int F) {
   return (t < q && f < rem) ? 16 * blk + f : -1;
 }
 
+// Head output slots.  Slot s = 16 nb + 4 g + t of the fused head (lane group g, register t) with
+// j = 4 nb + t and Q = ceil(D / 4): j < Q holds log-var d = g + 4 j, Q <= j < 2Q holds mean
+// d = g + 4 (j - Q), the rest is padding.  The kind of a register is then uniform across the
+// wave (no divergent mean / log-var branches in the epilogue) and each register's 4 lane groups
+// cover 4 consecutive d.  Returns the column of the fused [mean | log-var] head, or -1.
+__host__ __device__ __forceinline__ int head_col(int slot, int D) {
+  const int nb = slot >> 4, g = (slot >> 2) & 3, t = slot & 3, j = 4 * nb + t, Q = (D + 3) >> 2;
+  if (j < Q) return g + 4 * j < D ? D + g + 4 * j : -1;
+  if (j < 2 * Q) return g + 4 * (j - Q) < D ? g + 4 * (j - Q) : -1;
+  return -1;
+}
+
 // k-steps a consumer must run in the last 16-deep k-group of a width-F input (4: no skip)
 __host__ __device__ constexpr int tail_steps(int F) { return (F & 15) == 0 ? 4 : ((F & 15) + 3) >> 2; }
 
@@ -77,24 +89,33 @@ __device__ __forceinline__ void stage_frags(const float* __restrict__ src, float
 }
 
 // TQ: k-steps run in the last k-group (slot_feat tail; 4 = all).
-template <int KG, int NB, int R, int WAVES, int SLOT, int BQ = NB * 4, int KPB = 1, int TQ = 4>
+// Cross-layer prefetch: NBN > 0 stages the NEXT layer's first slice (wf_next, NBN fragments) during
+// this layer's last k-group, and that layer is then called with PRE = true (no initial barrier +
+// exposed copy).  `par` is the buffer of block 0 (block b uses buffer (b + par) & 1).
+template <int KG, int NB, int R, int WAVES, int SLOT, int BQ = NB * 4, int KPB = 1, int TQ = 4, int NBN = 0,
+          bool PRE = false>
 __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f32x4 (&in)[R][KG], f32x4 (&acc)[R][NB],
                                           float* lds, int w, int lane, const float* __restrict__ bias = nullptr,
-                                          float* lds_bias = nullptr) {
+                                          float* lds_bias = nullptr, int par = 0,
+                                          const float* __restrict__ wf_next = nullptr) {
+  static_assert(!(PRE || NBN) || KPB == 1, "cross-layer prefetch needs KPB == 1");
+  static_assert(!PRE || KG >= 2, "a prestaged layer stages its bias with a later slice");
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[r][nb] = zero4();
   constexpr int NBLK = (KG + KPB - 1) / KPB;
   // BNN_KNOB_* (scripts/micro/bnn_knobs.hip): timing-only builds with one part removed
+  if (!PRE) {
 #ifndef BNN_KNOB_NOBARRIER
-  __syncthreads();  // every wave is done reading both buffers (previous layer)
+    __syncthreads();  // every wave is done reading both buffers (previous layer)
 #endif
 #ifndef BNN_KNOB_NOSTAGE
-  if (KPB == 1) stage_slice<NB, WAVES>(wf, lds, w, lane);
-  else stage_frags<KPB * NB, WAVES>(wf, lds, w, lane, KG * NB);
-  if (NBLK == 1 && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
+    if (KPB == 1) stage_slice<NB, WAVES>(wf, lds + par * SLOT, w, lane);
+    else stage_frags<KPB * NB, WAVES>(wf, lds, w, lane, KG * NB);
+    if (NBLK == 1 && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
 #endif
+  }
 #pragma unroll
   for (int blk = 0; blk < NBLK; ++blk) {
 #ifndef BNN_KNOB_NOBARRIER
@@ -103,17 +124,28 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f3
 #ifndef BNN_KNOB_NOSTAGE
     if (blk + 1 < NBLK) {
       const float* src = wf + (blk + 1) * KPB * NB * 256;
-      float* dst = lds + ((blk + 1) & 1) * SLOT;
+      float* dst = lds + ((blk + 1 + par) & 1) * SLOT;
       if (KPB == 1) stage_slice<NB, WAVES>(src, dst, w, lane);
       else stage_frags<KPB * NB, WAVES>(src, dst, w, lane, (KG - (blk + 1) * KPB) * NB);
+    } else if (NBN > 0) {
+      stage_slice<NBN, WAVES>(wf_next, lds + ((blk + 1 + par) & 1) * SLOT, w, lane);
     }
     if (blk + 2 == NBLK && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
+#endif
+#ifndef BNN_KNOB_NOPIN
+    // keep the next slice's copies issued here, ahead of this k-group's MFMAs: left alone, the
+    // scheduler sinks every other k-group's copies to just before the next barrier, whose
+    // vmcnt(0) then exposes their whole latency
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+#ifdef BNN_KNOB_PRIO
+    __builtin_amdgcn_s_setprio(1);
 #endif
 #pragma unroll
     for (int j = 0; j < KPB; ++j) {
       const int kg = blk * KPB + j;
       if (kg < KG) {
-        const float* b = lds + (blk & 1) * SLOT + j * NB * 256;
+        const float* b = lds + ((blk + par) & 1) * SLOT + j * NB * 256;
         // fragment nb + 1 is read before the MFMAs of fragment nb (one LDS read in flight)
         f32x4 fr_next = *reinterpret_cast<const f32x4*>(b + lane * 4);
 #pragma unroll
@@ -133,6 +165,9 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f3
         }
       }
     }
+#ifdef BNN_KNOB_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
   }
 }
 
