@@ -19,13 +19,14 @@ struct ActorArgs {
   // rollout: write the obs/act half of the pool row and clear the penalty accumulator
   float* pool_obs; float* pool_act; const int64_t* pool_state; int64_t pool_max;
   int64_t stage_base;      // >= 0: staged layout, row goes to stage_base + row
+  int64_t pool_off;        // pool layout: row goes to (pool_state[0] + pool_off + row) % pool_max
   uint32_t* pen_zero;
   // rollout: member selection per row (bnn.py:343): injected sel_in or Philox choice over elites
   int32_t* sel_out; const int32_t* sel_in; const int32_t* elites; int n_elites;
 };
 
 int launch_actor(const ActorArgs& a, hipStream_t s);
-int64_t actor_packed_floats(int O, int Hp);
+__host__ __device__ int64_t actor_packed_floats(int O, int Hp);
 int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s);
 
 }  // namespace mopo

@@ -12,46 +12,60 @@
 
 namespace mopo {
 
-// combined head fragments: n < A -> Wmu[:, n], A <= n < 2A -> Wls[:, n - A]
-__global__ void pack_head_kernel(const float* Wm, const float* Wl, int Hp, int A, int KG, float* dst) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= KG * 256) return;
-  const int t = i & 3, lane = (i >> 2) & 63, kg = i >> 8;
-  const int k = kg * 16 + 4 * (lane >> 4) + t, n = lane & 15;
-  float v = 0.f;
-  if (k < Hp) v = n < A ? Wm[k * A + n] : (n < 2 * A ? Wl[k * A + (n - A)] : 0.f);
-  dst[i] = v;
-}
-
 // packed layout: W1 frags | W2 frags | head frags | b1 [NB*16] | b2 [NB*16] | [bmu | bls] [16]
 // (biases zero-padded to whole 16-blocks so the kernel stages them into LDS with global_load_lds)
-int64_t actor_packed_floats(int O, int Hp) {
-  const int KG0 = ceil_div(O, 16), NB = ceil_div(Hp, 16);
+__host__ __device__ int64_t actor_packed_floats(int O, int Hp) {
+  const int KG0 = (O + 15) / 16, NB = (Hp + 15) / 16;
   return (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256 + (int64_t)NB * 256 + 2LL * NB * 16 + 16;
 }
 
-// dst[i] = i < n ? src[i] : 0 for i < np
-__global__ void copy_pad_kernel(const float* src, int n, float* dst, int np) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < np) dst[i] = i < n ? src[i] : 0.f;
-}
-
-int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s) {
+// One launch packs the whole policy (it is repacked at every rollout, after the SAC updates):
+// W1 (observation side in slot_feat order), W2, the combined head (n < A -> Wmu[:, n],
+// A <= n < 2A -> Wls[:, n - A]) fragment-major (mlp_tile.h), then the zero-padded biases.
+__global__ void pack_actor_kernel(const float* __restrict__ P, int O, int A, int Hp, float* __restrict__ dst) {
   const int KG0 = ceil_div(O, 16), NB = ceil_div(Hp, 16);
   const float* W1 = P;
   const float* W2 = W1 + O * Hp + Hp;
   const float* Wm = W2 + Hp * Hp + Hp;
   const float* Wl = Wm + Hp * A + A;
-  if (pack_frags(W1, dst, 1, O, Hp, KG0, NB, s, 1)) return -1;  // obs in slot_feat order
-  if (pack_frags(W2, dst + (int64_t)KG0 * NB * 256, 1, Hp, Hp, NB, NB, s)) return -1;
-  float* hf = dst + (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256;
-  hipLaunchKernelGGL(pack_head_kernel, dim3(ceil_div(NB * 256, 256)), dim3(256), 0, s, Wm, Wl, Hp, A, NB, hf);
-  float* bp = hf + (int64_t)NB * 256;
-  hipLaunchKernelGGL(copy_pad_kernel, dim3(ceil_div(NB * 16, 256)), dim3(256), 0, s, W1 + O * Hp, Hp, bp, NB * 16);
-  hipLaunchKernelGGL(copy_pad_kernel, dim3(ceil_div(NB * 16, 256)), dim3(256), 0, s, W2 + Hp * Hp, Hp, bp + NB * 16,
-                     NB * 16);
-  hipLaunchKernelGGL(copy_pad_kernel, dim3(1), dim3(64), 0, s, Wm + Hp * A, A, bp + 2 * NB * 16, A);
-  hipLaunchKernelGGL(copy_pad_kernel, dim3(1), dim3(64), 0, s, Wl + Hp * A, A, bp + 2 * NB * 16 + A, 16 - A);
+  const int64_t n1 = (int64_t)KG0 * NB * 256, n2 = (int64_t)NB * NB * 256, nh = (int64_t)NB * 256;
+  const int64_t total = actor_packed_floats(O, Hp);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int t = i & 3, lane = (i >> 2) & 63, g = lane >> 4, r = lane & 15;
+    float v = 0.f;
+    if (i < n1 + n2) {  // trunk layers: fragment f = kg * NB + nb
+      const bool l1 = i < n1;
+      const int64_t f = (l1 ? i : i - n1) >> 8;
+      const int kg = (int)(f / NB), nb = (int)(f % NB);
+      int k = kg * 16 + 4 * g + t;
+      const int n = nb * 16 + r;
+      if (l1) {
+        k = slot_feat(k, O);
+        if (k >= 0 && n < Hp) v = W1[k * Hp + n];
+      } else if (k < Hp && n < Hp) {
+        v = W2[k * Hp + n];
+      }
+    } else if (i < n1 + n2 + nh) {
+      const int kg = (int)((i - n1 - n2) >> 8);
+      const int k = kg * 16 + 4 * g + t;
+      if (k < Hp) v = r < A ? Wm[k * A + r] : (r < 2 * A ? Wl[k * A + (r - A)] : 0.f);
+    } else {
+      const int j = (int)(i - n1 - n2 - nh);  // b1 | b2 | [bmu | bls]
+      if (j < NB * 16) v = j < Hp ? W1[O * Hp + j] : 0.f;
+      else if (j < 2 * NB * 16) v = j - NB * 16 < Hp ? W2[Hp * Hp + j - NB * 16] : 0.f;
+      else {
+        const int q = j - 2 * NB * 16;
+        v = q < A ? Wm[Hp * A + q] : (q < 2 * A ? Wl[Hp * A + q - A] : 0.f);
+      }
+    }
+    dst[i] = v;
+  }
+}
+
+int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s) {
+  const int64_t tot = actor_packed_floats(O, Hp);
+  hipLaunchKernelGGL(pack_actor_kernel, dim3((int)std::min<int64_t>((tot + 255) / 256, 1024)), dim3(256), 0, s, P, O,
+                     A, Hp, dst);
   MOPO_HIP(hipGetLastError());
   return 0;
 }
@@ -114,12 +128,16 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_kernel(const ActorArg
       x0[0][kg][t] = v;
     }
   f32x4 acc[1][NBP], h[1][NBP];
-  layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT, NBP * 4, 1, TQ0>(w1f, x0, acc, lds, wv, lane, b1, lds_bias);  // hidden 1 (:277-278)
+  // each layer's first weight slice is copied during the previous layer's last k-group (mlp_tile.h)
+  layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT, NBP * 4, 1, TQ0, NBP>(w1f, x0, acc, lds, wv, lane, b1, lds_bias, 0,
+                                                               w2f);  // hidden 1 (:277-278)
   bias_relu<NBP>(lds_bias, acc, h, g);
-  layer_lds<NBP, NBP, 1, ACT_WAVES, SLOT>(w2f, h, acc, lds, wv, lane, b2, lds_bias);   // hidden 2, relu (:301)
+  constexpr int P2 = KG0 & 1, P3 = (KG0 + NBP) & 1;  // buffer parity of each layer's block 0
+  layer_lds<NBP, NBP, 1, ACT_WAVES, SLOT, NBP * 4, 1, 4, 1, true>(w2f, h, acc, lds, wv, lane, b2, lds_bias, P2,
+                                                                  whf);  // hidden 2, relu (:301)
   bias_relu<NBP>(lds_bias, acc, h, g);
   f32x4 hd[1][1];
-  layer_lds<NBP, 1, 1, ACT_WAVES, SLOT>(whf, h, hd, lds, wv, lane, bh, lds_bias);      // mu | log_std (:302-303)
+  layer_lds<NBP, 1, 1, ACT_WAVES, SLOT, 4, 1, 4, 0, true>(whf, h, hd, lds, wv, lane, bh, lds_bias, P3);  // mu | log_std (:302-303)
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int n = 4 * g + t;
@@ -135,7 +153,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_kernel(const ActorArg
     actor_noise(a.seed, a.step, uid, A, z);
   }
   int64_t pos = -1;
-  if (a.pool_act) pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool_state[0] + row) % a.pool_max;
+  if (a.pool_act) pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool_state[0] + a.pool_off + row) % a.pool_max;
   for (int j = 0; j < A; ++j) {
     const float mu = head[wv][m][j];
     const float ls = fminf(fmaxf(head[wv][m][A + j], -20.f), 2.f);  // mopo.py:304

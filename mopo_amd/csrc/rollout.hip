@@ -100,6 +100,7 @@ struct PostArgs {
   int* blockcnt;
   mopo_pool_desc pool;
   int64_t stage_base;       // >= 0: staged layout
+  int64_t pool_off;         // pool layout: rows go to (state[0] + pool_off + row) % max_size
 };
 
 __global__ __launch_bounds__(PB) void rollout_post_kernel(const PostArgs a) {
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(PB) void rollout_post_kernel(const PostArgs a) {
     const bool term = term_fn(a.term_kind, s + 1, O);               // fake_env.py:91
     const double rew = s[0];
     const double pr = a.coeff != 0.f ? rew - (double)a.coeff * (double)__uint_as_float(a.pen[row]) : rew;
-    const int64_t pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool.d_state[0] + row) % a.pool.max_size;
+    const int64_t pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool.d_state[0] + a.pool_off + row) % a.pool.max_size;
     for (int k = 0; k < O; ++k) {
       a.obs_next[row * O + k] = s[k + 1];
       a.pool.d_next_obs[pos * O + k] = (float)s[k + 1];
@@ -197,6 +198,17 @@ __global__ void step_advance_kernel(int* cnt, int64_t* steps, int i, int compact
   if (compacted) cnt[0] = cnt[1];
 }
 
+// Steps [i0, i1) without compaction (halfcheetah): every step keeps all cnt[0] rows, so step i's
+// rows went to pool_off = (i - i0) * n and one advance covers the whole range.
+__global__ void steps_advance_kernel(const int* cnt, int64_t* steps, int i0, int i1, int64_t* pool_state,
+                                     int64_t max_size) {
+  const int64_t n = cnt[0];
+  for (int i = i0; i < i1; ++i) steps[i] = n;
+  const int64_t tot = n * (i1 - i0);
+  pool_state[0] = (pool_state[0] + tot) % max_size;
+  pool_state[1] = min(pool_state[1] + tot, max_size);
+}
+
 // Horizon steps [i0, i1) of one rollout.  i0 == 0 draws the start states and repacks the policy;
 // later ranges continue from the state the previous call left (obs ping-pong, live counts).  Staged
 // rows of step i go to rows (i - i0) * B of the staging descriptor.
@@ -238,6 +250,8 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     if (pack_actor(a->d_pi_params, O, A, a->pi_hidden, h->wpk, s)) return -1;
   }
   const bool compact = a->term_kind != MOPO_TERM_HALFCHEETAH;
+  // no compaction, pool layout: positions advance by B per step and one launch advances the pool
+  const bool batched_advance = !compact && !staged;
   int oc = h->oc, uc = h->uc;
   for (int i = i0; i < i1; ++i) {
     const uint32_t st = step0 + 1 + i;
@@ -249,6 +263,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     aa.act = h->act;
     aa.pool_obs = p->d_obs; aa.pool_act = p->d_act; aa.pool_state = p->d_state; aa.pool_max = p->max_size;
     aa.stage_base = staged ? (int64_t)(i - i0) * B : -1;
+    aa.pool_off = batched_advance ? (int64_t)(i - i0) * B : 0;
     aa.pen_zero = h->pen;
     aa.sel_out = h->sel;
     aa.sel_in = a->d_model_inds ? a->d_model_inds + (int64_t)i * B : nullptr;
@@ -274,6 +289,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     pa.seed = a->seed; pa.step = st; pa.coeff = a->penalty_coeff; pa.term_kind = a->term_kind;
     pa.obs_next = h->obs[oc ^ 1]; pa.keep = h->keep; pa.blockcnt = h->blockcnt;
     pa.pool = *p; pa.stage_base = staged ? (int64_t)(i - i0) * B : -1;
+    pa.pool_off = batched_advance ? (int64_t)(i - i0) * B : 0;
     {
       KTimer t(h, KC_POST, s);
       hipLaunchKernelGGL(rollout_post_kernel, dim3(nblk), dim3(PB), 0, s, pa);
@@ -288,7 +304,13 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     } else {
       oc ^= 1;
     }
-    {
+    if (batched_advance) {
+      if (i + 1 == i1) {
+        KTimer t(h, KC_ADVANCE, s);
+        hipLaunchKernelGGL(steps_advance_kernel, dim3(1), dim3(1), 0, s, h->cnt, a->d_steps, i0, i1, p->d_state,
+                           p->max_size);
+      }
+    } else {
       KTimer t(h, KC_ADVANCE, s);
       hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, s, h->cnt, a->d_steps, i, compact ? 1 : 0,
                          staged ? nullptr : p->d_state, p->max_size);
