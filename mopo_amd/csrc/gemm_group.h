@@ -29,7 +29,10 @@ enum { MASK_RELU = 0, MASK_DSWISH = 1 };             // GemmProb::mask_kind
 
 struct GemmProb {
   int M, N, K;
-  const float* A; int lda; int ta;   // ta=0: A(i,k)=A[i*lda+k]; ta=1: A(i,k)=A[k*lda+i]
+  const float* A; int lda; int ta;   // ta=0: A(i,k)=A[i*lda+k]; ta=1: A(i,k)=A[k*lda+i]; ta=2: layer-1 recompute
+  // ta == 2: A(i,k) = relu(sum_j X(i,j) W1(j,k) + b1(k)) for j < K1 <= 31, X = A (row stride lda),
+  // W1 = a_u ([K1][K] row-major), b1 = a_v, K1 = a_ldm; tiles with tn == 0 store that 16 x K
+  // slab of the first hidden layer to a_m (row stride K) for the backward pass
   const float* B; int ldb; int tb;   // tb=0: B(k,j)=B[k*ldb+j]; tb=1: B(k,j)=B[j*ldb+k]
   float* C; int ldc;
   const float* bias;                 // C += bias[j]
@@ -268,7 +271,7 @@ static __device__ __forceinline__ void store_panel(const GemmProb& p, int r0, in
 
 // operand modes (A: 0 plain, 1 transposed, 2 rank-1; B: the same, 3 two-segment) as am * 4 + bm
 __host__ static __device__ __forceinline__ int operand_modes(const GemmProb& p) {
-  const int am = p.a_u ? 2 : p.ta, bm = p.b_u ? 2 : p.B2 ? 3 : p.tb;
+  const int am = p.ta == 2 ? 4 : p.a_u ? 2 : p.ta, bm = p.b_u ? 2 : p.B2 ? 3 : p.tb;
   return am * 4 + bm;
 }
 
@@ -284,6 +287,62 @@ static __device__ __forceinline__ void stage_ab(const GemmProb& p, int i0, int j
   store_panel<BM, false, TW>(p, j0, kn, tid, rb, Bs);
 }
 
+// A operand mode 4 (ta == 2): the block's 16 x GKC slab of an MLP's first hidden layer, recomputed
+// here from the K1 <= 32 inputs of its rows instead of being read back from a launch of its own:
+// D(k, r) = W1^T(k, :) X^T(:, r) on f32 MFMA, four 16-wide k tiles per wave (the 256 threads cover
+// one 256-deep chunk), then bias + relu straight into the swizzled A panel.
+template <int BM>
+static __device__ __forceinline__ void stage_mlp1(const GemmProb& p, int i0, int j0, int kc, int kn, int tid,
+                                                  float* As, float* Bs) {
+  PanelRegs rb;
+  load_panel<BM, false>(p, j0, kc, tid, rb);
+  const int lane = tid & 63, w = tid >> 6, r = lane & 15, q = lane >> 4;
+  // the bias rides in the contraction as input column K1 (X = 1, W1 row K1 = b1): K1 <= 31
+  const int k1 = p.a_ldm, ns = (k1 + 4) >> 2, sb = k1 >> 2;
+  const auto dx = rsrc(p.A, (int64_t)(p.M - 1) * p.lda + k1);
+  const auto dw = rsrc(p.a_u, (int64_t)k1 * p.K);
+  const auto db = rsrc(p.a_v, p.K);
+  float xb[8], wa[4][8], bv[4];
+  const int row = i0 + r;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int j = 4 * s + q;
+    const float v = bload(dx, row * p.lda + j);
+    xb[s] = (j < k1 && row < p.M) ? v : (j == k1 ? 1.f : 0.f);
+  }
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    const int k = kc + w * 64 + kt * 16 + r;  // A-operand row of this lane
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int j = 4 * s + q;
+      const float v = bload(dw, j * p.K + k);
+      wa[kt][s] = (j < k1 && k < p.K) ? v : 0.f;
+    }
+    bv[kt] = bload(db, k);
+  }
+  pin_panel<BM, false>(rb);
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s == sb && q == (k1 & 3)) wa[kt][s] = bv[kt];
+  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    if (s < ns)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) acc[kt] = mfma4(wa[kt][s], xb[s], acc[kt]);
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kl = w * 64 + kt * 16 + 4 * q + t;  // D row = k within the chunk; D column = row r
+      As[kl * 16 + (r ^ psw(kl))] = (row < p.M && kl < kn) ? fmaxf(acc[kt][t], 0.f) : 0.f;
+    }
+  store_panel<BM, false>(p, j0, kn, tid, rb, Bs);
+}
+
 template <int TW>
 static __device__ __forceinline__ void stage_dispatch(const GemmProb& p, int i0, int j0, int kc, int kn, int t,
                                                       float* As, float* Bs) {
@@ -293,6 +352,7 @@ static __device__ __forceinline__ void stage_dispatch(const GemmProb& p, int i0,
     case 3: stage_ab<0, 3, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
     case 4: stage_ab<1, 0, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
     case 6: stage_ab<1, 2, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
+    case 16: if (TW == 16) stage_mlp1<0>(p, i0, j0, kc, kn, t, As, Bs); break;
     default: stage_ab<2, 1, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
   }
 }
@@ -349,6 +409,12 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
     // per chunk instead of one per element.
     stage_dispatch<16>(p, i0, j0, kc, kn, t, &As[0][0], &Bs[0][0]);
     __syncthreads();
+    if (p.ta == 2 && tn == 0 && p.a_m && t < kn) {  // first-layer slab for the backward pass (coalesced in k)
+      float* h1 = const_cast<float*>(p.a_m);
+#pragma unroll 4
+      for (int r = 0; r < 16; ++r)
+        if (i0 + r < p.M) h1[(int64_t)(i0 + r) * p.K + kc + t] = As[t][r ^ psw(t)];
+    }
     // the staged panels are zero-padded to GKC rows, so every wave runs exactly 16 k-steps of its
     // quarter with no guards: all 32 LDS reads first, then 16 MFMAs on two accumulators
     float ra[16], rb[16];
@@ -587,10 +653,11 @@ static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const Ad
   for (int i = 0; i < g.n; ++i) {
     const GemmProb& q = ps[i];
     const int c = operand_modes(q);
-    if (!(c == 0 || c == 1 || c == 3 || c == 4 || c == 6 || c == 9)) return fail("unsupported gemm operand modes");
+    if (!(c == 0 || c == 1 || c == 3 || c == 4 || c == 6 || c == 9 || c == 16)) return fail("unsupported gemm operand modes");
+    if (c == 16 && (q.a_ldm < 1 || q.a_ldm > 31 || !q.a_u || !q.a_v)) return fail("gemm layer-1 recompute: 1 <= K1 <= 31");
     if ((int64_t)q.M * q.K >= (1ll << 29) || (int64_t)q.N * q.K >= (1ll << 29)) return fail("gemm operand too large");
     if (q.head && (!hd || q.N > 16 || q.N != 2 * hd->A)) return fail("bad head problem");
-    big = big && q.M >= 32 && q.N >= 32;
+    big = big && q.M >= 32 && q.N >= 32 && c != 16;
     head = head || q.head;
   }
   const int ov = gemm_tile_override();

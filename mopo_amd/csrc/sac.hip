@@ -5,9 +5,10 @@
 // Semantics: every forward and gradient uses the pre-step parameters; then pi, q1, q2
 // and alpha are updated by their own Adam (identical step counts -> one shared lr_t); then Polyak.
 //
-// Structure: 11 launches per step on one stream, captured into hipGraphs of 8 / 2 / 1 steps (no
-// host work per step): 3 grouped-GEMM forward launches for pi(s), pi(s'), Q1/Q2(s,a) (the policy
-// output tile's epilogue runs the squashed-Gaussian head), 2 for Q1/Q2(s,pi) and the target
+// Structure: 9 launches per step on one stream, captured into hipGraphs of 8 / 2 / 1 steps (no
+// host work per step): 2 grouped-GEMM forward launches for pi(s), pi(s'), Q1/Q2(s,a) (both hidden
+// layers in one: the first is recomputed per block from the <= 32 inputs; the policy output tile's
+// epilogue runs the squashed-Gaussian head), 1 for both hidden layers of Q1/Q2(s,pi) and the target
 // critics, sac_qloss_kernel (their 1-wide output layers, the losses and the alpha gradient), then 4
 // grouped-GEMM backward launches and the policy-head backward (which also gathers the next step's
 // batch).  The four TF1 Adams and Polyak run in the weight-gradient GEMM epilogues (gemm_group.h),
@@ -419,23 +420,22 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   const Batch& bt = h->bt[par];
   auto Wq = [&](int qi, int k) { return P + o.q[qi][k]; };
   auto Tq = [&](int qi, int k) { return T + o.q[qi][k]; };
+  // both hidden layers of an MLP instance in one problem: the first is recomputed per block from
+  // the K1 inputs (gemm_group.h, ta == 2) and stored once to h1 for the backward pass
+  auto mlp12 = [&](const float* x, int k1, const float* w1, const float* b1, const float* w2, const float* b2,
+                   float* h1, float* h2) {
+    auto a = mk(n, H, H, x, W, 2, w2, H, 0, h2, H);
+    a.bias = b2; a.act = ACT_RELU;
+    a.a_u = w1; a.a_v = b1; a.a_ldm = k1; a.a_m = h1;
+    return a;
+  };
   // ---- forward stage 1-3: pi(s), pi(s'), Q1(s,a), Q2(s,a)
   {
     std::vector<GemmProb> g;
-    auto a = mk(n, H, O, bt.sa, W, 0, P + o.pW1, H, 0, h->h1[0], H); a.bias = P + o.pb1; a.act = ACT_RELU; g.push_back(a);
-    auto b = mk(n, H, O, bt.xn, W, 0, P + o.pW1, H, 0, h->h1[1], H); b.bias = P + o.pb1; b.act = ACT_RELU; g.push_back(b);
-    for (int qi = 0; qi < 2; ++qi) {
-      auto c = mk(n, H, W, bt.sa, W, 0, Wq(qi, 0), H, 0, h->h1[2 + qi], H); c.bias = Wq(qi, 1); c.act = ACT_RELU; g.push_back(c);
-    }
-    if (launch_group(g, s)) return -1;
-  }
-  {
-    std::vector<GemmProb> g;
-    for (int i = 0; i < 4; ++i) {
-      const float* w2 = i < 2 ? P + o.pW2 : Wq(i - 2, 2);
-      const float* b2 = i < 2 ? P + o.pb2 : Wq(i - 2, 3);
-      auto a = mk(n, H, H, h->h1[i], H, 0, w2, H, 0, h->h2[i], H); a.bias = b2; a.act = ACT_RELU; g.push_back(a);
-    }
+    g.push_back(mlp12(bt.sa, O, P + o.pW1, P + o.pb1, P + o.pW2, P + o.pb2, h->h1[0], h->h2[0]));
+    g.push_back(mlp12(bt.xn, O, P + o.pW1, P + o.pb1, P + o.pW2, P + o.pb2, nullptr, h->h2[1]));  // no gradient
+    for (int qi = 0; qi < 2; ++qi)
+      g.push_back(mlp12(bt.sa, W, Wq(qi, 0), Wq(qi, 1), Wq(qi, 2), Wq(qi, 3), h->h1[2 + qi], h->h2[2 + qi]));
     if (launch_group(g, s)) return -1;
   }
   {
@@ -462,19 +462,8 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     for (int i = 0; i < 4; ++i) {
       const int qi = i & 1;
       const bool tgt = i >= 2;
-      const float* x = tgt ? bt.xn : bt.xpi;
-      auto a = mk(n, H, W, x, W, 0, tgt ? Tq(qi, 0) : Wq(qi, 0), H, 0, h->h1[4 + i], H);
-      a.bias = tgt ? Tq(qi, 1) : Wq(qi, 1); a.act = ACT_RELU; g.push_back(a);
-    }
-    if (launch_group(g, s)) return -1;
-  }
-  {
-    std::vector<GemmProb> g;
-    for (int i = 0; i < 4; ++i) {
-      const int qi = i & 1;
-      const bool tgt = i >= 2;
-      auto a = mk(n, H, H, h->h1[4 + i], H, 0, tgt ? Tq(qi, 2) : Wq(qi, 2), H, 0, h->h2[4 + i], H);
-      a.bias = tgt ? Tq(qi, 3) : Wq(qi, 3); a.act = ACT_RELU; g.push_back(a);
+      auto L = [&](int k) { return tgt ? Tq(qi, k) : Wq(qi, k); };
+      g.push_back(mlp12(tgt ? bt.xn : bt.xpi, W, L(0), L(1), L(2), L(3), tgt ? nullptr : h->h1[4 + i], h->h2[4 + i]));
     }
     if (launch_group(g, s)) return -1;
   }
