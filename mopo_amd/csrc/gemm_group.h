@@ -117,11 +117,29 @@ struct AdamCtx {
   int slot0;                         // this launch's first slot
 };
 
+// SAC log slots (sac.hip, mopo_sac_buffers)
+enum {
+  LOG_Q1_LOSS = 0, LOG_Q2_LOSS, LOG_Q1, LOG_Q2, LOG_ALPHA, LOG_ENTROPY, LOG_LOGP, LOG_PI_GNORM, LOG_Q_GNORM,
+  LOG_PI_LOSS, LOG_PI_GSQ, LOG_Q_GSQ, LOG_N = 16
+};
+
+// Batch-level tail of the SAC losses (mopo.py:361-443): the per-block sums of sac_qloss_kernel
+// (written by the previous launch, so no in-launch hand-off) -> losses / logs, the alpha gradient
+// and its Adam, this step's lr_t, the TF1 beta powers and the step counter.  Run by ONE extra block
+// appended to the first critic-backward launch (none of whose GEMM blocks reads what it writes).
+struct LossTail {
+  const float* part;                 // [nparts][8]
+  int nparts, n;
+  float tent, lr;
+  float* logs; float* beta_pow; int64_t* iter;
+};
+
 struct GemmGroup {
   int n;
   int prefix[MAXP + 1];
   AdamCtx ad;
   HeadCtx hd;
+  LossTail tail;                     // tail.part != NULL: block prefix[n] runs loss_tail_block
   GemmProb p[MAXP];
 };
 
@@ -142,6 +160,36 @@ static __device__ __forceinline__ void adam_apply(const AdamCtx& ad, int64_t i, 
   if (ad.T && i < ad.total) ad.T[i] = (1.f - ad.tau) * a.t + ad.tau * p;   // mopo.py:446-447 (after the updates)
 }
 
+
+// the extra block of a launch carrying a LossTail: sums the per-block partials in block order
+// (deterministic), then one thread applies the batch-level updates.  sh: >= 8 * 64 floats of LDS.
+static __device__ __forceinline__ void loss_tail_block(const LossTail& t, const AdamCtx& ad, float* sh) {
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 8 * t.nparts; i += blockDim.x) sh[i] = t.part[i];
+  __syncthreads();
+  if (tid != 0) return;
+  float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < t.nparts; ++b)
+#pragma unroll
+    for (int i = 0; i < 7; ++i) red[i] += sh[8 * b + i];
+  const AdamIn al = adam_load(ad, ad.total);                       // log_alpha = the last parameter
+  const float fn = (float)t.n;
+  const float l1 = red[0] / fn * 0.5f, l2 = red[1] / fn * 0.5f;   // mopo.py:403-404
+  const float m1 = red[2] / fn, m2 = red[3] / fn, mlp = red[4] / fn, ment = red[5] / fn;
+  const float pil = red[6] / fn;                                  // mopo.py:371-377
+  const float ga = -(mlp + t.tent);                               // d/dlog_alpha of -mean(la*(logp+H))
+  const_cast<float*>(ad.G)[ad.total] = ga;                          // the alpha gradient (logs / tests)
+  float* logs = t.logs;
+  logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;
+  logs[LOG_ALPHA] = expf(al.p); logs[LOG_ENTROPY] = ment; logs[LOG_LOGP] = mlp; logs[LOG_PI_LOSS] = pil;
+  const float b1p = t.beta_pow[0], b2p = t.beta_pow[1];
+  const float lr_t = t.lr * sqrtf(1.f - b2p) / (1.f - b1p);       // TF1 Adam step size (identical step counts)
+  t.beta_pow[2] = lr_t;
+  t.beta_pow[0] = b1p * 0.9f;
+  t.beta_pow[1] = b2p * 0.999f;
+  *t.iter += 1;
+  adam_apply(ad, ad.total, ga, al, lr_t);
+}
 
 constexpr int GKC = 256;  // K chunk staged in LDS
 
@@ -368,6 +416,10 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
   __shared__ float part[4][256];
   __shared__ float csum[16][17];
   __shared__ float hv[16][17];
+  if (g.tail.part && (int)blockIdx.x >= g.prefix[g.n]) {
+    loss_tail_block(g.tail, g.ad, &part[0][0]);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int pi = 0;
   while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
@@ -645,7 +697,7 @@ static inline int gemm_tile_override() {
 }
 
 static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const AdamCtx* ad = nullptr, int* slot = nullptr,
-                               const HeadCtx* hd = nullptr) {
+                               const HeadCtx* hd = nullptr, const LossTail* tail = nullptr) {
   GemmGroup g{};
   g.n = (int)ps.size();
   if (g.n > MAXP) return fail("gemm group too large");
@@ -675,8 +727,12 @@ static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const Ad
     if (slot) *slot += tot;
   }
   if (hd) g.hd = *hd;
+  if (tail) {
+    if (TW != 16 || !ad || tail->nparts > 64) return fail("gemm group: bad loss tail");
+    g.tail = *tail;
+  }
   if (TW == 32) hipLaunchKernelGGL(gemm32_group_kernel, dim3(tot), dim3(256), 0, s, g);
-  else hipLaunchKernelGGL(gemm_group_kernel, dim3(tot), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL(gemm_group_kernel, dim3(tot + (tail ? 1 : 0)), dim3(256), 0, s, g);
   MOPO_HIP(hipGetLastError());
   return 0;
 }

@@ -53,7 +53,9 @@ __device__ __forceinline__ void stage_slice(const float* __restrict__ src, float
 #pragma unroll
   for (int i = 0; i < Stage<NB, WAVES>::PER; ++i) {
     const int f = w + i * WAVES;
-    const int fs = f < NB ? f : NB - 1;  // pad slots re-read a valid fragment (never consumed)
+// pad slots re-read a valid fragment (never consumed); measured: skipping them with a wave-uniform
+    // branch is ~1.5 % slower for H = 200 (13 of 16 slots used)
+    const int fs = f < NB ? f : NB - 1;
     __builtin_amdgcn_global_load_lds((const void*)(src + (fs * 64 + lane) * 4), (lds_void_t)(lds + f * 256), 16, 0, 0);
   }
 }

@@ -47,10 +47,6 @@ static Offs make_offs(int O, int A, int H) {
   return o;
 }
 
-enum {
-  LOG_Q1_LOSS = 0, LOG_Q2_LOSS, LOG_Q1, LOG_Q2, LOG_ALPHA, LOG_ENTROPY, LOG_LOGP, LOG_PI_GNORM, LOG_Q_GNORM,
-  LOG_PI_LOSS, LOG_PI_GSQ, LOG_Q_GSQ, LOG_N = 16
-};
 
 struct Batch {
   float *sa, *xpi, *xn, *rew, *term;  // [s, a], [s, pi(s)], [s', pi(s')], r, done
@@ -66,7 +62,6 @@ struct Sac {
   float* Pb[2];                   // parameter ping-pong: Pb[0] == P is the canonical copy between calls
   float* norm_part = nullptr;     // [nslots][2]
   float* loss_part = nullptr;     // [ceil(n / QL_ROWS)][8] sac_qloss_kernel block partials
-  unsigned* ticket = nullptr;     // its last-block ticket
   int nslots = 0, nslots_cap = 0;
   float* beta_pow;                // [3] f32 beta1_power, beta2_power (TF1 non-slot vars), this step's lr_t
   int64_t* iter;                  // device step counter (Philox)
@@ -178,14 +173,13 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
 // losses, output gradients, alpha gradient and logs (mopo.py:361-404).
 // Block = 16 batch rows; wave w computes instance 4 + w (q = h2 . w3 + b3, 4 lanes per row, K split
 // in 64-wide quarters); then one thread per row forms y, the row-local output gradients and its
-// share of the seven batch means.  Block partials are reduced by the last block to arrive (agent-
-// scope release -> ticket -> acquire, in block order: deterministic), which also applies the alpha
-// Adam, fixes this step's lr_t for the fused optimizer epilogues and advances the TF1 beta powers
-// and the step counter (nothing later in the step reads it).
+// share of the seven batch means.  The block partials are summed (in block order: deterministic) by
+// the LossTail block of the next launch, which also applies the alpha Adam, fixes this step's lr_t
+// for the fused optimizer epilogues and advances the TF1 beta powers and the step counter.
 constexpr int QL_ROWS = 16;
 struct QLossArgs {
   int n, H, A;
-  float gamma, rscale, tent, lr;
+  float gamma, rscale;
   const float* h2[4];               // instances Q1(s,pi) Q2(s,pi) Qt1(s',pi') Qt2(s',pi')
   const float* w3[4];
   const float* b3[4];
@@ -193,17 +187,12 @@ struct QLossArgs {
   const float* q1; const float* q2; // Q1/Q2(s, a) from the forward output stage
   const float* logp_s; const float* logp_n; const float* rew; const float* term; const float* head_s;
   const float* log_alpha;
-  float* dq1; float* dq2; float* dq1p; float* dq2p; float* g_alpha;
-  float* logs; float* beta_pow; int64_t* iter;
-  float* part;                      // [blocks][8]
-  unsigned* ticket;
-  AdamCtx ad;
+  float* dq1; float* dq2; float* dq1p; float* dq2p;
+  float* part;                      // [blocks][8] -> LossTail (gemm_group.h)
 };
 
 __global__ __launch_bounds__(256) void sac_qloss_kernel(const QLossArgs a) {
   __shared__ float qs[4][QL_ROWS];
-  __shared__ float red_s[8];
-  __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r0 = blockIdx.x * QL_ROWS;
   // the loss inputs of this block's rows (wave 0, one lane per row) and the alpha Adam state are
@@ -219,8 +208,6 @@ __global__ __launch_bounds__(256) void sac_qloss_kernel(const QLossArgs a) {
     for (int j = 0; j < 8; ++j) lsr[j] = j < a.A ? a.head_s[lr_row * 2 * a.A + a.A + j] : 0.f;
   }
   const float alpha = expf(*a.log_alpha);                           // mopo.py:361
-  AdamIn al_in{0.f, 0.f, 0.f, 0.f};
-  if (tid == 0) al_in = adam_load(a.ad, a.ad.total);
   {
     const int rr = lane >> 2, part = lane & 3, r = r0 + rr;
     const int rc = min(r, a.n - 1);
@@ -275,43 +262,7 @@ __global__ __launch_bounds__(256) void sac_qloss_kernel(const QLossArgs a) {
       float* pp = a.part + 8 * (int64_t)blockIdx.x;
 #pragma unroll
       for (int i = 0; i < 7; ++i) pp[i] = red[i];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = (t == gridDim.x - 1);
-      if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
-  }
-  __syncthreads();
-  if (!last) return;
-  // after the acquire, plain loads see every block's partials; one load per thread, all in flight
-  // together, then the sums in block order (deterministic)
-  __shared__ float pall[8 * 64];
-  for (int i = tid; i < 8 * (int)gridDim.x; i += 256) pall[i] = a.part[i];
-  __syncthreads();
-  if (tid < 7) {
-    float acc = 0.f;
-    for (int b = 0; b < (int)gridDim.x; ++b) acc += pall[8 * b + tid];
-    red_s[tid] = acc;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    const float fn = (float)a.n;
-    const float l1 = red_s[0] / fn * 0.5f, l2 = red_s[1] / fn * 0.5f; // mopo.py:403-404
-    const float m1 = red_s[2] / fn, m2 = red_s[3] / fn, mlp = red_s[4] / fn, ment = red_s[5] / fn;
-    const float pil = red_s[6] / fn;                                // mopo.py:371-377
-    const float ga = -(mlp + a.tent);                               // d/dlog_alpha of -mean(la*(logp+H))
-    *a.g_alpha = ga;
-    float* logs = a.logs;
-    logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;
-    logs[LOG_ALPHA] = alpha; logs[LOG_ENTROPY] = ment; logs[LOG_LOGP] = mlp; logs[LOG_PI_LOSS] = pil;
-    const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
-    const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-    a.beta_pow[2] = lr_t;
-    a.beta_pow[0] = b1p * 0.9f;
-    a.beta_pow[1] = b2p * 0.999f;
-    *a.iter += 1;
-    adam_apply(a.ad, a.ad.total, ga, al_in, lr_t);
-    *a.ticket = 0u;                                                 // stream order: next launch sees 0
   }
 }
 
@@ -470,7 +421,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   // ---- critic output layers (s, pi) / targets + losses (one launch)
   {
     QLossArgs q{};
-    q.n = n; q.H = H; q.A = A; q.gamma = h->gamma; q.rscale = h->rscale; q.tent = h->tent; q.lr = h->lr;
+    q.n = n; q.H = H; q.A = A; q.gamma = h->gamma; q.rscale = h->rscale;
     for (int i = 0; i < 4; ++i) {
       const int qi = i & 1;
       const bool tgt = i >= 2;
@@ -482,9 +433,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     q.q1 = h->out[2]; q.q2 = h->out[3];
     q.logp_s = h->logp_s; q.logp_n = h->logp_n; q.rew = bt.rew; q.term = bt.term; q.head_s = h->out[0];
     q.log_alpha = P + o.total;
-    q.dq1 = h->dq[0]; q.dq2 = h->dq[1]; q.dq1p = h->dq[2]; q.dq2p = h->dq[3]; q.g_alpha = G + o.total;
-    q.logs = h->logs; q.beta_pow = h->beta_pow; q.iter = h->iter; q.part = h->loss_part; q.ticket = h->ticket;
-    q.ad = ad;
+    q.dq1 = h->dq[0]; q.dq2 = h->dq[1]; q.dq1p = h->dq[2]; q.dq2p = h->dq[3]; q.part = h->loss_part;
     hipLaunchKernelGGL(sac_qloss_kernel, dim3(ceil_div(n, QL_ROWS)), dim3(256), 0, s, q);
     MOPO_HIP(hipGetLastError());
   }
@@ -498,7 +447,8 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       a.a_u = h->dq[i]; a.a_v = Wq(qi, 4); a.a_m = h->h2[2 + i]; a.a_ldm = H;
       g.push_back(a);
     }
-    if (launch_group(g, s, &ad, &slot)) return -1;
+    LossTail lt{h->loss_part, ceil_div(n, QL_ROWS), n, h->tent, h->lr, h->logs, h->beta_pow, h->iter};
+    if (launch_group(g, s, &ad, &slot, nullptr, &lt)) return -1;
   }
   {
     // dW2 / dW3 only need the rank-1 dh2 (not dh1), so they ride with the smaller second launch
@@ -577,7 +527,6 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   auto f = [&](float** p, size_t cnt) { reg.push_back({(void**)p, cnt * 4}); };
   f(&h->Pb[1], tot); f(&h->norm_part, 2 * (size_t)h->nslots_cap);
   f(&h->loss_part, 8 * (size_t)ceil_div(batch, QL_ROWS));
-  reg.push_back({(void**)&h->ticket, 4});
   f(&h->P, tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->T, tot);
   f(&h->beta_pow, 3); f(&h->logs, LOG_N);
   reg.push_back({(void**)&h->iter, 8});
