@@ -17,7 +17,10 @@ int main(int argc, char** argv) {
   const int E = KNOB_E, O = 17, A = 6, H = KNOB_H, D = O + 1, IN = O + A;
   const int64_t B = argc > 1 ? atoll(argv[1]) : 50000;
   mopo_bnn_t hb;
-  if (mopo_bnn_create(&hb, E, O, A, H, 0, 0)) { printf("create: %s\n", mopo_last_error()); return 1; }
+#ifndef KNOB_DTYPE
+#define KNOB_DTYPE 0
+#endif
+  if (mopo_bnn_create(&hb, E, O, A, H, 0, KNOB_DTYPE)) { printf("create: %s\n", mopo_last_error()); return 1; }
   std::mt19937 rng(1);
   std::normal_distribution<float> nd(0.f, 1.f);
   auto arr = [&](size_t n, float sc) { std::vector<float> v(n); for (auto& x : v) x = nd(rng) * sc; return v; };
