@@ -119,6 +119,21 @@ class SAC:
         self._keepalive = keep
         self._num_train_steps += n_steps
 
+    def _training_batch(self, env_pool, model_pool, batch_size=None, as_numpy=False):
+        """mopo.py:801-821 as a host-visible batch (the device step assembles the same batch itself):
+        int(batch_size * real_ratio) env rows, the rest model rows, env-first per shared field."""
+        import torch
+        batch_size = int(batch_size or self.batch_size)
+        env_n = int(batch_size * self._real_ratio)
+        model_n = batch_size - env_n
+        env_batch = env_pool.random_batch(env_n, as_numpy=as_numpy)
+        if model_n <= 0:
+            return env_batch
+        model_batch = model_pool.random_batch(model_n, as_numpy=as_numpy)
+        keys = set(env_batch) & set(model_batch)
+        cat = np.concatenate if as_numpy else torch.cat
+        return {k: cat((env_batch[k], model_batch[k]), 0) for k in keys}
+
     def _update_target(self):
         """Folded into every device step (target_update_interval=1, mopo.py:843-845)."""
 

@@ -157,3 +157,20 @@ def test_sac_graph_replay_matches_eager():
     assert torch.isfinite(pa).all()
     lg = a.logs()
     assert all(np.isfinite(v) for v in lg.values())
+
+
+def test_training_batch_mirror():
+    """SAC._training_batch (mopo.py:801-821): int(256 * 0.05) = 12 env rows then 244 model rows, each
+    drawn with np.random.randint over the pool's size (flexible_replay_pool.py:85-87)."""
+    from mopo_amd.sac import SAC
+    rs = np.random.RandomState(7)
+    (env, env_op), (mod, mod_op) = pools(rs)
+    sac = SAC(O, A, H, batch_size=256, real_ratio=0.05, target_entropy=-3)
+    np.random.seed(11)
+    got = sac._training_batch(env, mod, as_numpy=True)
+    np.random.seed(11)
+    idx = np.concatenate([np.random.randint(0, env.size, 12), np.random.randint(0, mod.size, 244)])
+    ref = host_batch(env_op, mod_op, idx)
+    assert set(got) == set(ref)
+    for k in ref:
+        np.testing.assert_array_equal(np.asarray(got[k], np.float64), ref[k], err_msg=k)
