@@ -96,7 +96,7 @@ constexpr int ACT_WAVES = 4;
 
 // TQ0: k-steps in the last k-group of the observation (tail_steps(O); 4 = all)
 template <int KG0, int NBP, int TQ0 = 4>
-__global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_kernel(const ActorArgs a) {
+__global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? 4 : 2) void actor_kernel(const ActorArgs a) {
   constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
   __shared__ float head[ACT_WAVES][16][17];
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + (NBP * 4 + 63) / 64 * 256];  // one array (bnn.hip)
@@ -127,17 +127,45 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_kernel(const ActorArg
                       : reinterpret_cast<const float*>(a.obs)[row * O + k];
       x0[0][kg][t] = v;
     }
-  f32x4 acc[1][NBP], h[1][NBP];
-  // each layer's first weight slice is copied during the previous layer's last k-group (mlp_tile.h)
-  layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT, NBP * 4, 1, TQ0, NBP>(w1f, x0, acc, lds, wv, lane, b1, lds_bias, 0,
-                                                               w2f);  // hidden 1 (:277-278)
-  bias_relu<NBP>(lds_bias, acc, h, g);
-  constexpr int P2 = KG0 & 1, P3 = (KG0 + NBP) & 1;  // buffer parity of each layer's block 0
-  layer_lds<NBP, NBP, 1, ACT_WAVES, SLOT, NBP * 4, 1, 4, 1, true>(w2f, h, acc, lds, wv, lane, b2, lds_bias, P2,
-                                                                  whf);  // hidden 2, relu (:301)
-  bias_relu<NBP>(lds_bias, acc, h, g);
   f32x4 hd[1][1];
-  layer_lds<NBP, 1, 1, ACT_WAVES, SLOT, 4, 1, 4, 0, true>(whf, h, hd, lds, wv, lane, bh, lds_bias, P3);  // mu | log_std (:302-303)
+  if constexpr (NBP == 16) {
+    // Hp = 256: the second layer runs as two passes of 8 output tiles, each folded into the head
+    // right away, so a wave holds h1 (64 VGPRs) + 8 accumulator tiles (32) instead of 16 + 16:
+    // <= 128 VGPRs = 4 waves/SIMD, and B = 50k (782 workgroups) fits one round of 1,024 slots
+    // instead of spilling 14 workgroups into a second round of 768.  Staged bytes are unchanged
+    // (each pass copies its half of every k-group slice); each layer's first slice is copied
+    // during the previous pass's last k-group (mlp_tile.h).
+    f32x4 h1[1][NBP];  // accumulators, then (in place) the activations
+    layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT, NBP * 4, 1, TQ0, 8>(w1f, x0, h1, lds, wv, lane, b1, lds_bias, 0,
+                                                               w2f);  // hidden 1 (:277-278)
+    bias_relu<NBP>(lds_bias, h1, h1, g);
+    constexpr int P = KG0 & 1;  // buffer parity of block 0 of every later pass (16 and 8 blocks: even)
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      f32x4 h2[1][8];  // accumulators, then (in place) the activations
+      // hidden 2, relu (:301), output tiles [8 half, 8 half + 8); prefetch: this half's head slice
+      layer_lds<NBP, 8, 1, ACT_WAVES, SLOT, 32, 1, 4, 1, true, NBP>(w2f + half * 8 * 256, h1, h2, lds, wv, lane,
+                                                                   b2 + half * 128, lds_bias, P, whf + half * 8 * 256);
+      bias_relu<8>(lds_bias, h2, h2, g);
+      // mu | log_std (:302-303) over k in this half; prefetch: the second half's first slice
+      if (half == 0)
+        layer_lds<8, 1, 1, ACT_WAVES, SLOT, 4, 1, 4, 8, true, 1, false>(whf, h2, hd, lds, wv, lane, nullptr, nullptr, P,
+                                                                       w2f + 8 * 256);
+      else
+        layer_lds<8, 1, 1, ACT_WAVES, SLOT, 4, 1, 4, 0, true, 1, true>(whf + 8 * 256, h2, hd, lds, wv, lane, bh,
+                                                                      lds_bias, P);
+    }
+  } else {
+    f32x4 acc[1][NBP], h[1][NBP];
+    layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT, NBP * 4, 1, TQ0, NBP>(w1f, x0, acc, lds, wv, lane, b1, lds_bias, 0,
+                                                                 w2f);  // hidden 1 (:277-278)
+    bias_relu<NBP>(lds_bias, acc, h, g);
+    constexpr int P2 = KG0 & 1, P3 = (KG0 + NBP) & 1;  // buffer parity of each layer's block 0
+    layer_lds<NBP, NBP, 1, ACT_WAVES, SLOT, NBP * 4, 1, 4, 1, true>(w2f, h, acc, lds, wv, lane, b2, lds_bias, P2,
+                                                                    whf);  // hidden 2, relu (:301)
+    bias_relu<NBP>(lds_bias, acc, h, g);
+    layer_lds<NBP, 1, 1, ACT_WAVES, SLOT, 4, 1, 4, 0, true>(whf, h, hd, lds, wv, lane, bh, lds_bias, P3);  // mu | log_std
+  }
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int n = 4 * g + t;

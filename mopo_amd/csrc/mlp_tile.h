@@ -94,18 +94,22 @@ __device__ __forceinline__ void stage_frags(const float* __restrict__ src, float
 // Cross-layer prefetch: NBN > 0 stages the NEXT layer's first slice (wf_next, NBN fragments) during
 // this layer's last k-group, and that layer is then called with PRE = true (no initial barrier +
 // exposed copy).  `par` is the buffer of block 0 (block b uses buffer (b + par) & 1).
+// NBS: fragments per k-group slice in memory (NB < NBS: this call covers output tiles [0, NB) of a
+// wider layer whose slices start at wf + kg * NBS fragments); ACC: accumulate into acc (no zeroing).
 template <int KG, int NB, int R, int WAVES, int SLOT, int BQ = NB * 4, int KPB = 1, int TQ = 4, int NBN = 0,
-          bool PRE = false>
+          bool PRE = false, int NBS = NB, bool ACC = false>
 __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f32x4 (&in)[R][KG], f32x4 (&acc)[R][NB],
                                           float* lds, int w, int lane, const float* __restrict__ bias = nullptr,
                                           float* lds_bias = nullptr, int par = 0,
                                           const float* __restrict__ wf_next = nullptr) {
   static_assert(!(PRE || NBN) || KPB == 1, "cross-layer prefetch needs KPB == 1");
   static_assert(!PRE || KG >= 2, "a prestaged layer stages its bias with a later slice");
+  static_assert(NBS == NB || KPB == 1, "strided slices need KPB == 1");
+  if (!ACC)
 #pragma unroll
-  for (int r = 0; r < R; ++r)
+    for (int r = 0; r < R; ++r)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[r][nb] = zero4();
+      for (int nb = 0; nb < NB; ++nb) acc[r][nb] = zero4();
   constexpr int NBLK = (KG + KPB - 1) / KPB;
   // BNN_KNOB_* (scripts/micro/bnn_knobs.hip): timing-only builds with one part removed
   if (!PRE) {
@@ -125,7 +129,7 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f3
 #endif
 #ifndef BNN_KNOB_NOSTAGE
     if (blk + 1 < NBLK) {
-      const float* src = wf + (blk + 1) * KPB * NB * 256;
+      const float* src = wf + (blk + 1) * KPB * NBS * 256;
       float* dst = lds + ((blk + 1 + par) & 1) * SLOT;
       if (KPB == 1) stage_slice<NB, WAVES>(src, dst, w, lane);
       else stage_frags<KPB * NB, WAVES>(src, dst, w, lane, (KG - (blk + 1) * KPB) * NB);
