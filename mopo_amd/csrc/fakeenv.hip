@@ -134,12 +134,13 @@ extern "C" int mopo_fakeenv_step(mopo_bnn_t hh, const mopo_fakeenv_args* a, void
   Bnn* h = reinterpret_cast<Bnn*>(hh);
   MOPO_REQUIRE(h && a, "mopo_fakeenv_step: NULL argument");
   MOPO_REQUIRE(h->O + 1 <= MAXD, "mopo_fakeenv_step: obs_dim too large");
+  MOPO_REQUIRE(a->B >= 0, "mopo_fakeenv_step: negative batch");
+  if (a->B == 0) return 0;  // empty batch: nothing to read or write (empty buffers may be NULL)
   MOPO_REQUIRE(a->d_ens_mean && a->d_ens_var, "mopo_fakeenv_step: ensemble workspaces required");
   MOPO_REQUIRE(a->deterministic || (a->d_noise_sel && a->d_model_inds),
                "mopo_fakeenv_step: noise and model_inds required unless deterministic");
   MOPO_REQUIRE(a->d_next_obs && a->d_rewards && a->d_terminals, "mopo_fakeenv_step: NULL output");
   MOPO_REQUIRE(!a->d_info_mean == !a->d_info_std, "mopo_fakeenv_step: info_mean/info_std go together");
-  if (a->B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   FwdArgs f{};
   const size_t es = a->obs_f64 ? 8 : 4;

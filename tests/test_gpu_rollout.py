@@ -148,14 +148,14 @@ def test_pool_vs_reference_trace():
     torch.cuda.synchronize()
 
 
-def _rollout_case(domain, E, H, B, horizon, seed, coeff=1.0, O=17, A=6):
+def _rollout_case(domain, E, H, B, horizon, seed, coeff=1.0, O=17, A=6, height=None):
     """Oracle rollout with every random stream drawn in the reference order; returns inputs,
-    injected streams and the oracle pool."""
+    injected streams and the oracle pool.  ``height``: fixed walker height (50: every row done)."""
     rs = np.random.RandomState(seed)
     env_n = 3000
     env_obs = rs.normal(size=(env_n, O)).astype(np.float32)
     if domain == 'walker2d':
-        env_obs[:, 0] = rs.uniform(0.9, 1.9, env_n)
+        env_obs[:, 0] = rs.uniform(0.9, 1.9, env_n) if height is None else height
         env_obs[:, 1] = rs.uniform(-0.9, 0.9, env_n)
     mats = obnn.to_mat_list(obnn.init_params(E, O, A, hidden=H, seed=seed + 1,
                                              inputs=np.concatenate([env_obs, rs.uniform(-1, 1, (env_n, A))], 1)))
@@ -298,3 +298,54 @@ def test_fused_rollout_bf16_walker_runs():
     exp = ~((h > 0.8) & (h < 2.0) & (a > -1.0) & (a < 1.0))
     near = (np.abs(h - 0.8) < 1e-5) | (np.abs(h - 2.0) < 1e-5) | (np.abs(np.abs(a) - 1.0) < 1e-5)
     assert (f['terminals'][:, 0] == exp)[~near].all()
+
+
+def test_rollout_stops_when_every_row_is_done():
+    """mopo.py:754-756: the horizon loop breaks once all rows are terminal -- walker2d rows at height
+    50 all terminate in step 0, so only step 0's transitions enter the pool and the rest add 0."""
+    import torch
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout
+    from mopo_amd.static import static_fns
+    B, horizon = 300, 4
+    c = _rollout_case('walker2d', 7, 64, B, horizon, seed=5, height=50.0)
+    assert c['steps'] == [B]                                       # the oracle broke after step 0
+    model = make_model(c['mats'], 7, 64)
+    pool = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=B * horizon + 7)
+    ro = ModelRollout(model, B, horizon)
+    dev = torch.device('cuda')
+    steps = ro.run(torch.from_numpy(c['env_obs']).to(dev), torch.from_numpy(c['flat']).to(dev), pool, B, horizon,
+                   static_fns['walker2d'].term_kind, c['coeff'], c['elites'], start_idx=c['start'],
+                   eps_act=c['eps_act'], eps_obs=c['eps_obs'], model_inds=c['inds'])
+    np.testing.assert_array_equal(steps.cpu().numpy(), [B, 0, 0, 0])
+    assert pool.size == B and pool._pointer == B
+    got = pool.return_all_samples(as_numpy=True)
+    assert got['terminals'].all()
+    close(got['next_observations'], c['pool'].return_all_samples()['next_observations'], 5e-5)
+
+
+def test_empty_batches():
+    """Zero rows through every entry point: numpy-shaped empty outputs, pool unchanged (the
+    reference's numpy code returns empty arrays for empty inputs)."""
+    import torch
+    from mopo_amd.fake_env import FakeEnv
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout, init_sac_params
+    from mopo_amd.static import static_fns
+    rs = np.random.RandomState(2)
+    mats = obnn.to_mat_list(obnn.init_params(7, 17, 6, hidden=64, seed=3))
+    model = make_model(mats, 7, 64)
+    mean, var = model.predict(np.zeros((0, 23), np.float32), factored=True)
+    assert mean.shape == (7, 0, 18) and var.shape == (7, 0, 18)
+    env = FakeEnv(model, static_fns['halfcheetah'], penalty_coeff=1.0, penalty_learned_var=True)
+    nobs, rew, term, info = env.step(np.zeros((0, 17), np.float32), np.zeros((0, 6), np.float32))
+    assert nobs.shape == (0, 17) and rew.shape == (0, 1) and term.shape == (0, 1)
+    pool = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=100)
+    pool.add_samples({'observations': np.zeros((0, 17)), 'actions': np.zeros((0, 6)), 'rewards': np.zeros((0, 1)),
+                      'terminals': np.zeros((0, 1), bool), 'next_observations': np.zeros((0, 17))})
+    assert pool.size == 0
+    ro = ModelRollout(model, 64, 3)
+    dev = torch.device('cuda')
+    steps = ro.run(torch.from_numpy(rs.normal(size=(50, 17)).astype(np.float32)).to(dev),
+                   torch.from_numpy(init_sac_params(17, 6)).to(dev), pool, 0, 3, 0, 1.0, [0, 1, 2, 3, 4])
+    assert steps.cpu().numpy().tolist() == [0, 0, 0] and pool.size == 0
