@@ -103,50 +103,68 @@ struct PostArgs {
   int64_t pool_off;         // pool layout: rows go to (state[0] + pool_off + row) % max_size
 };
 
-__global__ __launch_bounds__(PB) void rollout_post_kernel(const PostArgs a) {
-  __shared__ int wcnt[PB / 64];
-  const int64_t row = blockIdx.x * (int64_t)PB + threadIdx.x;
+// FakeEnv post-processing of one horizon step (fake_env.py:66-115) for POST_RPB rows per block, one
+// 32-lane group per row and one lane per output dim d < D = O + 1: every load and store of the row's
+// D values is contiguous across its lanes, and each lane draws only its own normal (Philox block
+// d / 4, Box-Muller pair (d % 4) / 2: the same numbers the per-row order gives).  The row's next
+// observation is assembled in LDS for the termination function.  With compaction, the kept rows of
+// each PB-row chunk are counted into blockcnt (zeroed before the launch).
+constexpr int POST_RPB = 8;
+__global__ __launch_bounds__(256) void rollout_post_kernel(const PostArgs a) {
+  __shared__ double srow[POST_RPB][33];
+  __shared__ int kept[POST_RPB];
+  const int tid = threadIdx.x, sub = tid & 31, rl = tid >> 5;
+  const int64_t row = (int64_t)blockIdx.x * POST_RPB + rl;
   const int O = a.O, D = O + 1;
   const int64_t count = *a.cnt;
-  bool keep = false;
-  if (row < count) {
-    double s[33];
-    float z[36];
-    if (!a.eps) {  // Philox normals for the selected member (perf mode of fake_env.py:72)
+  const bool live = row < count;
+  const bool on = live && sub < D;
+  double s = 0.0;
+  if (on) {
+    float m = a.mean_sel[row * D + sub];
+    if (sub >= 1) m = (float)((double)m + a.obs[row * O + sub - 1]);  // fake_env.py:66
+    double e;
+    if (a.eps) {
+      e = a.eps[row * D + sub];
+    } else {  // Philox normal `sub` of the row's stream (perf mode of fake_env.py:72)
       const int64_t u = a.uid[row];
-      for (int blk = 0; blk * 4 < D; ++blk) {
-        u32x4 c{(uint32_t)u, (uint32_t)((uint64_t)u >> 32) ^ ((uint32_t)blk << 20), a.step, RNG_OBS_NOISE};
-        u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
-        box_muller(r.x, r.y, z[blk * 4 + 0], z[blk * 4 + 1]);
-        box_muller(r.z, r.w, z[blk * 4 + 2], z[blk * 4 + 3]);
-      }
+      u32x4 c{(uint32_t)u, (uint32_t)((uint64_t)u >> 32) ^ ((uint32_t)(sub >> 2) << 20), a.step, RNG_OBS_NOISE};
+      u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+      float z0, z1;
+      if (sub & 2) box_muller(r.z, r.w, z0, z1);
+      else box_muller(r.x, r.y, z0, z1);
+      e = (double)((sub & 1) ? z1 : z0);
     }
-    for (int d = 0; d < D; ++d) {
-      float m = a.mean_sel[row * D + d];
-      if (d >= 1) m = (float)((double)m + a.obs[row * O + d - 1]);  // fake_env.py:66
-      const double e = a.eps ? a.eps[row * D + d] : (double)z[d];
-      s[d] = (double)m + e * (double)a.std_sel[row * D + d];       // fake_env.py:72
-    }
-    const bool term = term_fn(a.term_kind, s + 1, O);               // fake_env.py:91
-    const double rew = s[0];
-    const double pr = a.coeff != 0.f ? rew - (double)a.coeff * (double)__uint_as_float(a.pen[row]) : rew;
-    const int64_t pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool.d_state[0] + a.pool_off + row) % a.pool.max_size;
-    for (int k = 0; k < O; ++k) {
-      a.obs_next[row * O + k] = s[k + 1];
-      a.pool.d_next_obs[pos * O + k] = (float)s[k + 1];
-    }
-    a.pool.d_rew[pos] = (float)pr;
-    a.pool.d_term[pos] = term ? 1 : 0;
-    keep = !term;
-    a.keep[row] = keep ? 1 : 0;
+    s = (double)m + e * (double)a.std_sel[row * D + sub];          // fake_env.py:72
+    srow[rl][sub] = s;
   }
-  const unsigned long long bal = __ballot(keep);
-  if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = __popcll(bal);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int w = 0; w < PB / 64; ++w) t += wcnt[w];
-    a.blockcnt[blockIdx.x] = t;
+  const int64_t pos = a.stage_base >= 0 ? a.stage_base + row
+                                        : (a.pool.d_state[0] + a.pool_off + row) % a.pool.max_size;
+  if (on && sub >= 1) {                                            // next_obs = samples[:, 1:] (:90)
+    a.obs_next[row * O + sub - 1] = s;
+    a.pool.d_next_obs[pos * O + sub - 1] = (float)s;
+  }
+  if (sub == 0) {
+    bool keep = false;
+    if (live) {
+      const bool term = term_fn(a.term_kind, &srow[rl][1], O);     // fake_env.py:91
+      const double pr = a.coeff != 0.f ? s - (double)a.coeff * (double)__uint_as_float(a.pen[row]) : s;
+      a.pool.d_rew[pos] = (float)pr;                               // rewards = samples[:, :1] - c * penalty
+      a.pool.d_term[pos] = term ? 1 : 0;
+      keep = !term;
+      if (a.keep) a.keep[row] = keep ? 1 : 0;
+    }
+    kept[rl] = keep ? 1 : 0;
+  }
+  if (a.blockcnt) {
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+#pragma unroll
+      for (int i = 0; i < POST_RPB; ++i) t += kept[i];
+      if (t) atomicAdd(a.blockcnt + (int64_t)blockIdx.x * POST_RPB / PB, t);  // PB % POST_RPB == 0
+    }
   }
 }
 
@@ -287,12 +305,14 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     pa.mean_sel = h->mean_sel; pa.std_sel = h->std_sel; pa.pen = h->pen;
     pa.eps = a->d_eps_obs ? a->d_eps_obs + (int64_t)i * B * D : nullptr;
     pa.seed = a->seed; pa.step = st; pa.coeff = a->penalty_coeff; pa.term_kind = a->term_kind;
-    pa.obs_next = h->obs[oc ^ 1]; pa.keep = h->keep; pa.blockcnt = h->blockcnt;
+    pa.obs_next = h->obs[oc ^ 1]; pa.keep = compact ? h->keep : nullptr; pa.blockcnt = compact ? h->blockcnt : nullptr;
     pa.pool = *p; pa.stage_base = staged ? (int64_t)(i - i0) * B : -1;
     pa.pool_off = batched_advance ? (int64_t)(i - i0) * B : 0;
     {
       KTimer t(h, KC_POST, s);
-      hipLaunchKernelGGL(rollout_post_kernel, dim3(nblk), dim3(PB), 0, s, pa);
+      // with compaction the post kernel adds each block's kept rows into its PB-row chunk count
+      if (compact) MOPO_HIP(hipMemsetAsync(h->blockcnt, 0, (size_t)nblk * sizeof(int), s));
+      hipLaunchKernelGGL(rollout_post_kernel, dim3(ceil_div((int)B, POST_RPB)), dim3(256), 0, s, pa);
     }
     MOPO_HIP(hipGetLastError());
     if (compact) {
