@@ -135,6 +135,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? 4 : 2) void actor_kerne
     // instead of spilling 14 workgroups into a second round of 768.  Staged bytes are unchanged
     // (each pass copies its half of every k-group slice); each layer's first slice is copied
     // during the previous pass's last k-group (mlp_tile.h).
+    // (measured: staging 2 k-groups per barrier in the 8-tile passes is 3 % slower)
     f32x4 h1[1][NBP];  // accumulators, then (in place) the activations
     layer_lds<KG0, NBP, 1, ACT_WAVES, SLOT, NBP * 4, 1, TQ0, 8>(w1f, x0, h1, lds, wv, lane, b1, lds_bias, 0,
                                                                w2f);  // hidden 1 (:277-278)
@@ -149,8 +150,8 @@ __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? 4 : 2) void actor_kerne
       bias_relu<8>(lds_bias, h2, h2, g);
       // mu | log_std (:302-303) over k in this half; prefetch: the second half's first slice
       if (half == 0)
-        layer_lds<8, 1, 1, ACT_WAVES, SLOT, 4, 1, 4, 8, true, 1, false>(whf, h2, hd, lds, wv, lane, nullptr, nullptr, P,
-                                                                       w2f + 8 * 256);
+        layer_lds<8, 1, 1, ACT_WAVES, SLOT, 4, 1, 4, 8, true, 1, false, 1, NBP>(whf, h2, hd, lds, wv, lane, nullptr,
+                                                                               nullptr, P, w2f + 8 * 256);
       else
         layer_lds<8, 1, 1, ACT_WAVES, SLOT, 4, 1, 4, 0, true, 1, true>(whf + 8 * 256, h2, hd, lds, wv, lane, bh,
                                                                       lds_bias, P);

@@ -169,7 +169,7 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
                                                                                                    const FwdArgs a) {
   constexpr int NBMAX = NBH > NBO ? NBH : NBO;
   constexpr int KPB = BNN_KPB;                            // k-groups per barrier (hidden/head layers)
-  constexpr int SLOT = KPB == 1 ? Stage<NBMAX, WAVES>::SLOTS * 256 : KPB * NBMAX * 256;  // floats per buffer
+  constexpr int SLOT = (KPB * NBMAX + WAVES - 1) / WAVES * WAVES * 256;  // floats per buffer (stage_block)
   constexpr int BIASQ = NBH > 3 * NBO ? NBH * 4 : 3 * NBO * 4;  // quads: hidden bias / head aux
   // ONE __shared__ array (weight double buffer | bias): a second LDS object beside the
   // global_load_lds destination makes hipcc wait vmcnt(0) before the first ds_read of a k-group,

@@ -74,19 +74,20 @@ __device__ __forceinline__ void stage_bias(const float* __restrict__ bias, float
   }
 }
 
-// KPB > 1: KPB consecutive k-groups (contiguous, k-group-major) are staged and consumed per
-// barrier, with the copies spread over the waves without padding slots (the barrier drains every
-// wave's own copies); SLOT must hold KPB * NB fragments.
-template <int NF, int WAVES>
-__device__ __forceinline__ void stage_frags(const float* __restrict__ src, float* lds, int w, int lane, int n_valid) {
+// One pipeline block: KPB k-groups x NB output tiles of a layer whose k-group slices lie NBS
+// fragments apart (NBS > NB: a subset of the output tiles), fragment (j, nb) into LDS slot j*NB + nb.
+// Every wave issues the same number of copies (pad slots re-read a valid fragment, never consumed):
+// measured faster than skipping them with a wave-uniform branch.  kg_valid: k-groups left in the layer.
+template <int NB, int KPB, int NBS, int WAVES>
+__device__ __forceinline__ void stage_block(const float* __restrict__ src, float* lds, int w, int lane, int kg_valid) {
+  constexpr int NF = KPB * NB, PER = (NF + WAVES - 1) / WAVES;
 #pragma unroll
-  for (int i = 0; i < (NF + WAVES - 1) / WAVES; ++i) {
+  for (int i = 0; i < PER; ++i) {
     const int f = w + i * WAVES;
-    if (f < NF) {
-      const int fs = f < n_valid ? f : n_valid - 1;  // past the layer: re-read a valid fragment (unused)
-      __builtin_amdgcn_global_load_lds((const void*)(src + (fs * 64 + lane) * 4), (lds_void_t)(lds + f * 256), 16, 0,
-                                       0);
-    }
+    int j = (f < NF ? f : NF - 1) / NB, nb = (f < NF ? f : NF - 1) % NB;
+    if (j >= kg_valid) j = kg_valid - 1;
+    __builtin_amdgcn_global_load_lds((const void*)(src + ((j * NBS + nb) * 64 + lane) * 4), (lds_void_t)(lds + f * 256),
+                                     16, 0, 0);
   }
 }
 
@@ -96,15 +97,15 @@ __device__ __forceinline__ void stage_frags(const float* __restrict__ src, float
 // exposed copy).  `par` is the buffer of block 0 (block b uses buffer (b + par) & 1).
 // NBS: fragments per k-group slice in memory (NB < NBS: this call covers output tiles [0, NB) of a
 // wider layer whose slices start at wf + kg * NBS fragments); ACC: accumulate into acc (no zeroing).
+// KPBN / NBSN: pipeline-block shape of the next call (its first block is what NBN > 0 prefetches).
 template <int KG, int NB, int R, int WAVES, int SLOT, int BQ = NB * 4, int KPB = 1, int TQ = 4, int NBN = 0,
-          bool PRE = false, int NBS = NB, bool ACC = false>
+          bool PRE = false, int NBS = NB, bool ACC = false, int KPBN = 1, int NBSN = NBN>
 __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f32x4 (&in)[R][KG], f32x4 (&acc)[R][NB],
                                           float* lds, int w, int lane, const float* __restrict__ bias = nullptr,
                                           float* lds_bias = nullptr, int par = 0,
                                           const float* __restrict__ wf_next = nullptr) {
-  static_assert(!(PRE || NBN) || KPB == 1, "cross-layer prefetch needs KPB == 1");
   static_assert(!PRE || KG >= 2, "a prestaged layer stages its bias with a later slice");
-  static_assert(NBS == NB || KPB == 1, "strided slices need KPB == 1");
+  static_assert(((KPB * NB + WAVES - 1) / WAVES) * WAVES * 256 <= SLOT, "pipeline block larger than its buffer");
   if (!ACC)
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -117,8 +118,7 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f3
     __syncthreads();  // every wave is done reading both buffers (previous layer)
 #endif
 #ifndef BNN_KNOB_NOSTAGE
-    if (KPB == 1) stage_slice<NB, WAVES>(wf, lds + par * SLOT, w, lane);
-    else stage_frags<KPB * NB, WAVES>(wf, lds, w, lane, KG * NB);
+    stage_block<NB, KPB, NBS, WAVES>(wf, lds + par * SLOT, w, lane, KG);
     if (NBLK == 1 && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
 #endif
   }
@@ -129,12 +129,11 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ wf, const f3
 #endif
 #ifndef BNN_KNOB_NOSTAGE
     if (blk + 1 < NBLK) {
-      const float* src = wf + (blk + 1) * KPB * NBS * 256;
-      float* dst = lds + ((blk + 1 + par) & 1) * SLOT;
-      if (KPB == 1) stage_slice<NB, WAVES>(src, dst, w, lane);
-      else stage_frags<KPB * NB, WAVES>(src, dst, w, lane, (KG - (blk + 1) * KPB) * NB);
-    } else if (NBN > 0) {
-      stage_slice<NBN, WAVES>(wf_next, lds + ((blk + 1 + par) & 1) * SLOT, w, lane);
+      stage_block<NB, KPB, NBS, WAVES>(wf + (blk + 1) * KPB * NBS * 256, lds + ((blk + 1 + par) & 1) * SLOT, w, lane,
+                                       KG - (blk + 1) * KPB);
+    } else {
+      if constexpr (NBN > 0)
+        stage_block<NBN, KPBN, NBSN, WAVES>(wf_next, lds + ((blk + 1 + par) & 1) * SLOT, w, lane, KPBN);
     }
     if (blk + 2 == NBLK && bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);
 #endif
