@@ -214,28 +214,30 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
   f32x4 acc[R][NBH], hcur[R][NBH];
   const int64_t hp = w.BS;  // per-member bias stride
 #ifndef BNN_KNOB_NOXPRE
-  // each layer's first weight slice is copied during the previous layer's last k-group
+  // each layer's first weight slice (block of KPB k-groups) is copied during the previous layer's
+  // last block; parity: block b of a layer uses buffer (b + par) & 1
+  constexpr int NBLKH = (NBH + KPB - 1) / KPB;
   const float* wh0 = w.wh + (int64_t)e * NBH * NBH * 256;
-  layer_lds<KG0, NBH, R, WAVES, SLOT, NBH * 4, 1, TQ0, NBH>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv,
-                                                          lane, w.b0 + e * hp, lds_bias, 0, wh0);
+  layer_lds<KG0, NBH, R, WAVES, SLOT, NBH * 4, 1, TQ0, NBH, false, NBH, false, KPB, NBH>(
+      w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv, lane, w.b0 + e * hp, lds_bias, 0, wh0);
   bias_swish<NBH, R>(lds_bias, acc, hcur, g);
   int par = KG0 & 1;
   for (int l = 0; l < 2; ++l) {  // hidden layers 1, 2 (constructor.py:31-33)
-    layer_lds<NBH, NBH, R, WAVES, SLOT, NBH * 4, 1, TQH, NBH, true>(
+    layer_lds<NBH, NBH, R, WAVES, SLOT, NBH * 4, KPB, TQH, NBH, true, NBH, false, KPB, NBH>(
         w.wh + ((int64_t)l * w.E + e) * NBH * NBH * 256, hcur, acc, lds, wv, lane,
         w.bh + ((int64_t)l * w.E + e) * hp, lds_bias, par, w.wh + ((int64_t)(l + 1) * w.E + e) * NBH * NBH * 256);
     bias_swish<NBH, R>(lds_bias, acc, hcur, g);
-    par = (par + NBH) & 1;
+    par = (par + NBLKH) & 1;
   }
-  layer_lds<NBH, NBH, R, WAVES, SLOT, NBH * 4, 1, TQH, NBO, true>(  // hidden layer 3
+  layer_lds<NBH, NBH, R, WAVES, SLOT, NBH * 4, KPB, TQH, NBO, true, NBH, false, KPB, NBO>(  // hidden layer 3
       w.wh + ((int64_t)2 * w.E + e) * NBH * NBH * 256, hcur, acc, lds, wv, lane, w.bh + ((int64_t)2 * w.E + e) * hp,
       lds_bias, par, w.whd + (int64_t)e * NBH * NBO * 256);
   bias_swish<NBH, R>(lds_bias, acc, hcur, g);
-  par = (par + NBH) & 1;
+  par = (par + NBLKH) & 1;
   f32x4 hd[R][NBO];
-  layer_lds<NBH, NBO, R, WAVES, SLOT, 3 * NBO * 4, 1, TQH, 0, true>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd, lds,
-                                                                   wv, lane, w.bhd + (int64_t)e * 3 * NBO * 16,
-                                                                   lds_bias, par);
+  layer_lds<NBH, NBO, R, WAVES, SLOT, 3 * NBO * 4, KPB, TQH, 0, true>(w.whd + (int64_t)e * NBH * NBO * 256, hcur, hd,
+                                                                     lds, wv, lane, w.bhd + (int64_t)e * 3 * NBO * 16,
+                                                                     lds_bias, par);
 #else
   layer_lds<KG0, NBH, R, WAVES, SLOT, NBH * 4, 1, TQ0>(w.w0 + (int64_t)e * KG0 * NBH * 256, x0, acc, lds, wv, lane,
                                                      w.b0 + e * hp, lds_bias);

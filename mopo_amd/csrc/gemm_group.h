@@ -67,41 +67,45 @@ struct HeadCtx {
   const int64_t* iter;
 };
 
-static __device__ __forceinline__ void head_fwd_row(const HeadCtx& hc, int nxt, int r, const float* hm, const float* hl) {
+// One action j of row r (8 lanes per row, lanes j >= A idle): its normal (Philox block j / 4,
+// Box-Muller pair (j % 4) / 2 -- the numbers the per-row order draws), the tanh-squashed action,
+// and the row's log-prob as an 8-lane butterfly sum of (gaussian term - squash correction).
+// Called by all 8 lanes of the row's group (the shuffles need them); ok: the row exists.
+static __device__ __forceinline__ void head_fwd_elem(const HeadCtx& hc, int nxt, int r, int j, const float* hm,
+                                                     const float* hl, bool ok) {
   const int A = hc.A;
-  float z[8];
-  const float* ein = hc.eps_in[nxt];
-  if (ein) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) z[j] = j < A ? ein[r * A + j] : 0.f;
-  } else {
-    const int64_t it = *hc.iter;
-#pragma unroll
-    for (int blk = 0; blk < 2; ++blk) {
+  const bool on = ok && j < A;
+  float v = 0.f;
+  if (on) {
+    float z;
+    const float* ein = hc.eps_in[nxt];
+    if (ein) {
+      z = ein[r * A + j];
+    } else {
+      const int64_t it = *hc.iter;
+      const int blk = j >> 2;
       u32x4 c{(uint32_t)r | ((uint32_t)nxt << 31), (uint32_t)it ^ ((uint32_t)blk << 24), (uint32_t)((uint64_t)it >> 32),
               RNG_SAC + 16};
       u32x4 q = philox(c, (uint32_t)hc.seed, (uint32_t)(hc.seed >> 32));
-      box_muller(q.x, q.y, z[4 * blk], z[4 * blk + 1]);
-      box_muller(q.z, q.w, z[4 * blk + 2], z[4 * blk + 3]);
+      float z0, z1;
+      if (j & 2) box_muller(q.z, q.w, z0, z1);
+      else box_muller(q.x, q.y, z0, z1);
+      z = (j & 1) ? z1 : z0;
     }
-  }
-  float logp = 0.f, corr = 0.f;
-  float* x = hc.x[nxt] + r * (hc.O + A) + hc.O;
-  float* eo = hc.eps_out[nxt] + r * A;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (j >= A) break;
     const float mu = hm[j];
-    const float ls = fminf(fmaxf(hl[j], -20.f), 2.f);
+    const float ls = fminf(fmaxf(hl[j], -20.f), 2.f);             // mopo.py:304
     const float sd = expf(ls);
-    const float u = mu + z[j] * sd;
+    const float u = mu + z * sd;                                   // mopo.py:306
     const float zz = (u - mu) / (sd + 1e-8f);
-    logp += -0.5f * (zz * zz + 2.f * ls + 1.8378770664093453f);
-    corr += 2.f * (0.6931471805599453f - u - softplusf(-2.f * u));
-    x[j] = tanhf(u);
-    eo[j] = z[j];
+    v = -0.5f * (zz * zz + 2.f * ls + 1.8378770664093453f)         // gaussian_likelihood (:282-284)
+        - 2.f * (0.6931471805599453f - u - softplusf(-2.f * u));   // squash correction (:292)
+    hc.x[nxt][r * (hc.O + A) + hc.O + j] = tanhf(u);
+    hc.eps_out[nxt][r * A + j] = z;
   }
-  hc.logp[nxt][r] = logp - corr;
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  if (ok && j == 0) hc.logp[nxt][r] = v;
 }
 
 // Fused optimizer (the four TF1 Adams + Polyak, mopo.py:407-447): a weight-gradient tile is final
@@ -523,9 +527,12 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
       }
     }
   }
-  if (p.head) {  // the tile holds all 2A head outputs of its 16 rows: one thread per row
+  if (p.head) {  // the tile holds all 2A head outputs of its 16 rows: 8 lanes per row, one per action
     __syncthreads();
-    if (tid < 16 && i0 + tid < p.M) head_fwd_row(g.hd, p.head - 1, i0 + tid, &hv[tid][0], &hv[tid][g.hd.A]);
+    if (tid < 128) {
+      const int hr = tid >> 3;
+      head_fwd_elem(g.hd, p.head - 1, i0 + hr, tid & 7, &hv[hr][0], &hv[hr][g.hd.A], i0 + hr < p.M);
+    }
   }
   if (ad.norm_part) {  // per-block squared-gradient partial (grad-norm logs; summed by sac_logs_kernel)
 #pragma unroll

@@ -193,19 +193,16 @@ struct QLossArgs {
 
 __global__ __launch_bounds__(256) void sac_qloss_kernel(const QLossArgs a) {
   __shared__ float qs[4][QL_ROWS];
+  __shared__ float ents[QL_ROWS];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r0 = blockIdx.x * QL_ROWS;
   // the loss inputs of this block's rows (wave 0, one lane per row) and the alpha Adam state are
   // fetched first, so their latency hides under the output-layer dot products
   const int lr_row = min(r0 + lane, a.n - 1);
-  float in_q1 = 0.f, in_q2 = 0.f, in_rew = 0.f, in_term = 0.f, in_lps = 0.f, in_lpn = 0.f, lsr[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) lsr[j] = 0.f;
+  float in_q1 = 0.f, in_q2 = 0.f, in_rew = 0.f, in_term = 0.f, in_lps = 0.f, in_lpn = 0.f;
   if (w == 0 && lane < QL_ROWS) {
     in_q1 = a.q1[lr_row]; in_q2 = a.q2[lr_row]; in_rew = a.rew[lr_row]; in_term = a.term[lr_row];
     in_lps = a.logp_s[lr_row]; in_lpn = a.logp_n[lr_row];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) lsr[j] = j < a.A ? a.head_s[lr_row * 2 * a.A + a.A + j] : 0.f;
   }
   const float alpha = expf(*a.log_alpha);                           // mopo.py:361
   {
@@ -227,6 +224,20 @@ __global__ __launch_bounds__(256) void sac_qloss_kernel(const QLossArgs a) {
       qs[w][rr] = qv;
       if (r < a.n) a.q[w][r] = qv;
     }
+    if (w == 1) {  // pi_entropy terms (mopo.py:341) of the 16 rows: 4 lanes per row, 2 actions each
+      float ent = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = part + 4 * jj;
+        if (j < a.A) {
+          const float ls = fminf(fmaxf(a.head_s[(int64_t)rc * 2 * a.A + a.A + j], -20.f), 2.f);
+          ent += logf(expf(ls) + 1e-8f) + 0.5f * logf(2.f * 3.14159265358979f * 2.718281828459045f);
+        }
+      }
+      ent += __shfl_xor(ent, 1);
+      ent += __shfl_xor(ent, 2);
+      if (part == 0) ents[rr] = ent;
+    }
   }
   __syncthreads();
   if (w == 0) {
@@ -244,13 +255,7 @@ __global__ __launch_bounds__(256) void sac_qloss_kernel(const QLossArgs a) {
       const bool sel1 = q1p <= q2p;                                 // tf.minimum grad -> x where x <= y
       a.dq1p[r] = sel1 ? -inv_n : 0.f;
       a.dq2p[r] = sel1 ? 0.f : -inv_n;
-      float ent = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {                                 // pi_entropy (mopo.py:341)
-        if (j >= a.A) break;
-        const float ls = fminf(fmaxf(lsr[j], -20.f), 2.f);
-        ent += logf(expf(ls) + 1e-8f) + 0.5f * logf(2.f * 3.14159265358979f * 2.718281828459045f);
-      }
+      const float ent = ents[lane];
       red[0] = (q1 - y) * (q1 - y); red[1] = (q2 - y) * (q2 - y); red[2] = q1; red[3] = q2;
       red[4] = lps; red[5] = ent; red[6] = alpha * lps - fminf(q1p, q2p);
     }
