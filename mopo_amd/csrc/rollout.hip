@@ -38,7 +38,10 @@ struct Rollout {
   float* std_sel;
   uint8_t* keep;
   int* blockcnt;
-  int* cnt;  // [0] live rows this step, [1] survivors
+  int* cnt;  // [0] live rows this step, [1] survivors, [2 + k] rows of part k (split rollout)
+  static constexpr int MAXSPLIT = 4;
+  hipStream_t sp[MAXSPLIT] = {};        // streams of parts 1.. of the split rollout (run_impl)
+  hipEvent_t ev_fork[MAXSPLIT] = {}, ev_join[MAXSPLIT] = {};
   // horizon state carried between step-range calls (mopo_rollout_run_staged_steps)
   int oc = 0, uc = 0, next_step = 0;
 };
@@ -66,9 +69,13 @@ struct KTimer {
 
 __global__ void rollout_start_kernel(const float* env_obs, int64_t env_size, const int64_t* idx_in, int O,
                                      int64_t B, uint64_t seed, uint32_t step, int64_t uid_offset, double* obs,
-                                     int64_t* uid, int* cnt) {
+                                     int64_t* uid, int* cnt, int nsplit, int64_t bpart) {
   const int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (row == 0) cnt[0] = (int)B;
+  if (row == 0) {
+    cnt[0] = (int)B;
+    for (int k = 0; k < nsplit; ++k)  // split rollout: part k = rows [k bpart, min((k + 1) bpart, B))
+      cnt[2 + k] = (int)(k + 1 < nsplit ? bpart : B - (int64_t)k * bpart);
+  }
   if (row >= B) return;
   int64_t src;
   const int64_t u = uid_offset + row;
@@ -227,6 +234,15 @@ __global__ void steps_advance_kernel(const int* cnt, int64_t* steps, int i0, int
   pool_state[1] = min(pool_state[1] + tot, max_size);
 }
 
+static int split_parts() {  // MOPO_ROLLOUT_SPLIT=<parts> (0 or 1: one stream); default 2
+  static const int v = [] {
+    const char* e = std::getenv("MOPO_ROLLOUT_SPLIT");
+    const int n = e ? std::atoi(e) : 2;
+    return n < 1 ? 1 : (n > Rollout::MAXSPLIT ? Rollout::MAXSPLIT : n);
+  }();
+  return v;
+}
+
 // Horizon steps [i0, i1) of one rollout.  i0 == 0 draws the start states and repacks the policy;
 // later ranges continue from the state the previous call left (obs ping-pong, live counts).  Staged
 // rows of step i go to rows (i - i0) * B of the staging descriptor.
@@ -250,12 +266,23 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
   const int64_t B = a->B;
   const int nblk = ceil_div((int)B, PB);
   const uint32_t step0 = a->epoch * 4096u;
+  const bool compact = a->term_kind != MOPO_TERM_HALFCHEETAH;
+  // no compaction, pool layout: positions advance by B per step and one launch advances the pool
+  const bool batched_advance = !compact && !staged;
+  // Split rollout: with no compaction the rows never interact, so two halves run their own
+  // actor -> ensemble -> post chains on two streams; each half's kernels fill the CUs the other
+  // half's launch tails and small kernels leave idle.  Identical results (rows, Philox streams and
+  // pool positions do not depend on the split).  Off while profiling per kernel.
+  const int nsplit = batched_advance && !h->profile ? std::min<int>(split_parts(), (int)(B / 2048)) : 1;
+  const bool split = nsplit > 1;
+  const int64_t bpart = split ? (B / nsplit + 63) / 64 * 64 : B;
   if (i0 == 0) {
     h->oc = 0;
     h->uc = 0;
     KTimer t(h, KC_START, s);
     hipLaunchKernelGGL(rollout_start_kernel, dim3(nblk), dim3(PB), 0, s, a->d_env_obs, a->env_size,
-                       a->d_start_idx, O, B, a->seed, step0, a->uid_offset, h->obs[0], h->uid[0], h->cnt);
+                       a->d_start_idx, O, B, a->seed, step0, a->uid_offset, h->obs[0], h->uid[0], h->cnt, nsplit,
+                       bpart);
   }
   if (i0 == 0) {
     MOPO_HIP(hipGetLastError());
@@ -267,75 +294,109 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     KTimer t(h, KC_START, s);
     if (pack_actor(a->d_pi_params, O, A, a->pi_hidden, h->wpk, s)) return -1;
   }
-  const bool compact = a->term_kind != MOPO_TERM_HALFCHEETAH;
-  // no compaction, pool layout: positions advance by B per step and one launch advances the pool
-  const bool batched_advance = !compact && !staged;
   int oc = h->oc, uc = h->uc;
-  for (int i = i0; i < i1; ++i) {
+  // one horizon step for rows [off, off + n) of the batch (live count in *cnt) on stream ss
+  auto step_rows = [&](int i, int64_t off, int64_t n, int* cnt, hipStream_t ss, hipEvent_t after_actor) -> int {
     const uint32_t st = step0 + 1 + i;
     ActorArgs aa{};
     aa.P = a->d_pi_params; aa.Wpk = h->wpk; aa.O = O; aa.A = A; aa.Hp = a->pi_hidden;
-    aa.obs = h->obs[oc]; aa.obs_f64 = 1; aa.B = B; aa.d_count = h->cnt;
-    aa.eps = a->d_eps_act ? a->d_eps_act + (int64_t)i * B * A : nullptr;
-    aa.seed = a->seed; aa.step = st; aa.d_uid = h->uid[uc];
-    aa.act = h->act;
+    aa.obs = h->obs[oc] + off * O; aa.obs_f64 = 1; aa.B = n; aa.d_count = cnt;
+    aa.eps = a->d_eps_act ? a->d_eps_act + ((int64_t)i * B + off) * A : nullptr;
+    aa.seed = a->seed; aa.step = st; aa.d_uid = h->uid[uc] + off;
+    aa.act = h->act + off * A;
     aa.pool_obs = p->d_obs; aa.pool_act = p->d_act; aa.pool_state = p->d_state; aa.pool_max = p->max_size;
-    aa.stage_base = staged ? (int64_t)(i - i0) * B : -1;
-    aa.pool_off = batched_advance ? (int64_t)(i - i0) * B : 0;
-    aa.pen_zero = h->pen;
-    aa.sel_out = h->sel;
-    aa.sel_in = a->d_model_inds ? a->d_model_inds + (int64_t)i * B : nullptr;
+    aa.stage_base = staged ? (int64_t)(i - i0) * B + off : -1;
+    aa.pool_off = batched_advance ? (int64_t)(i - i0) * B + off : 0;
+    aa.pen_zero = h->pen + off;
+    aa.sel_out = h->sel + off;
+    aa.sel_in = a->d_model_inds ? a->d_model_inds + (int64_t)i * B + off : nullptr;
     aa.elites = a->d_elites; aa.n_elites = a->n_elites;
     {
-      KTimer t(h, KC_ACTOR, s);
-      if (launch_actor(aa, s)) return -1;
+      KTimer t(h, KC_ACTOR, ss);
+      if (launch_actor(aa, ss)) return -1;
     }
+    if (after_actor) MOPO_HIP(hipEventRecord(after_actor, ss));
 
     FwdArgs f{};
-    f.in = FwdIn{h->obs[oc], 1, O, h->act, 0, A};
-    f.B = B; f.d_count = h->cnt;
-    f.pen_bits = h->pen; f.sel = h->sel; f.mean_sel = h->mean_sel; f.std_sel = h->std_sel;
+    f.in = FwdIn{h->obs[oc] + off * O, 1, O, h->act + off * A, 0, A};
+    f.B = n; f.d_count = cnt;
+    f.pen_bits = h->pen + off; f.sel = h->sel + off; f.mean_sel = h->mean_sel + off * D;
+    f.std_sel = h->std_sel + off * D;
     {
-      KTimer t(h, KC_BNN, s);
-      if (launch_bnn_fwd(bnn, FWD_ROLLOUT, f, s)) return -1;
+      KTimer t(h, KC_BNN, ss);
+      if (launch_bnn_fwd(bnn, FWD_ROLLOUT, f, ss)) return -1;
     }
 
     PostArgs pa{};
-    pa.O = O; pa.cnt = h->cnt; pa.obs = h->obs[oc]; pa.uid = h->uid[uc];
-    pa.mean_sel = h->mean_sel; pa.std_sel = h->std_sel; pa.pen = h->pen;
-    pa.eps = a->d_eps_obs ? a->d_eps_obs + (int64_t)i * B * D : nullptr;
+    pa.O = O; pa.cnt = cnt; pa.obs = h->obs[oc] + off * O; pa.uid = h->uid[uc] + off;
+    pa.mean_sel = h->mean_sel + off * D; pa.std_sel = h->std_sel + off * D; pa.pen = h->pen + off;
+    pa.eps = a->d_eps_obs ? a->d_eps_obs + ((int64_t)i * B + off) * D : nullptr;
     pa.seed = a->seed; pa.step = st; pa.coeff = a->penalty_coeff; pa.term_kind = a->term_kind;
-    pa.obs_next = h->obs[oc ^ 1]; pa.keep = compact ? h->keep : nullptr; pa.blockcnt = compact ? h->blockcnt : nullptr;
-    pa.pool = *p; pa.stage_base = staged ? (int64_t)(i - i0) * B : -1;
-    pa.pool_off = batched_advance ? (int64_t)(i - i0) * B : 0;
+    pa.obs_next = h->obs[oc ^ 1] + off * O; pa.keep = compact ? h->keep : nullptr;
+    pa.blockcnt = compact ? h->blockcnt : nullptr;
+    pa.pool = *p; pa.stage_base = staged ? (int64_t)(i - i0) * B + off : -1;
+    pa.pool_off = batched_advance ? (int64_t)(i - i0) * B + off : 0;
     {
-      KTimer t(h, KC_POST, s);
+      KTimer t(h, KC_POST, ss);
       // with compaction the post kernel adds each block's kept rows into its PB-row chunk count
-      if (compact) MOPO_HIP(hipMemsetAsync(h->blockcnt, 0, (size_t)nblk * sizeof(int), s));
-      hipLaunchKernelGGL(rollout_post_kernel, dim3(ceil_div((int)B, POST_RPB)), dim3(256), 0, s, pa);
+      if (compact) MOPO_HIP(hipMemsetAsync(h->blockcnt, 0, (size_t)nblk * sizeof(int), ss));
+      hipLaunchKernelGGL(rollout_post_kernel, dim3(ceil_div((int)n, POST_RPB)), dim3(256), 0, ss, pa);
     }
     MOPO_HIP(hipGetLastError());
-    if (compact) {
-      KTimer t(h, KC_COMPACT, s);
-      hipLaunchKernelGGL(rollout_compact_kernel, dim3(nblk), dim3(PB), 0, s, O, h->blockcnt, h->keep, h->cnt,
-                         h->obs[oc ^ 1], h->obs[oc], h->uid[uc], h->uid[uc ^ 1], h->cnt + 1);
-      MOPO_HIP(hipGetLastError());
-      uc ^= 1;
-    } else {
+    return 0;
+  };
+  if (split) {
+    for (int k = 1; k < nsplit; ++k)
+      if (!h->sp[k]) {
+        MOPO_HIP(hipStreamCreateWithFlags(&h->sp[k], hipStreamNonBlocking));
+        MOPO_HIP(hipEventCreateWithFlags(&h->ev_fork[k], hipEventDisableTiming));
+        MOPO_HIP(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
+      }
+    // part k starts once part k - 1's first actor is done: the chains run offset by about one actor
+    // launch instead of in lockstep, so their ensemble tails do not coincide
+    for (int i = i0; i < i1; ++i) {
+      for (int k = 0; k < nsplit; ++k) {
+        hipStream_t ss = k == 0 ? s : h->sp[k];
+        if (i == i0 && k > 0) MOPO_HIP(hipStreamWaitEvent(ss, h->ev_fork[k], 0));
+        const int64_t off = k * bpart, n = k + 1 < nsplit ? bpart : B - off;
+        if (step_rows(i, off, n, h->cnt + 2 + k, ss, i == i0 && k + 1 < nsplit ? h->ev_fork[k + 1] : nullptr))
+          return -1;
+      }
       oc ^= 1;
     }
-    if (batched_advance) {
-      if (i + 1 == i1) {
-        KTimer t(h, KC_ADVANCE, s);
-        hipLaunchKernelGGL(steps_advance_kernel, dim3(1), dim3(1), 0, s, h->cnt, a->d_steps, i0, i1, p->d_state,
-                           p->max_size);
-      }
-    } else {
-      KTimer t(h, KC_ADVANCE, s);
-      hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, s, h->cnt, a->d_steps, i, compact ? 1 : 0,
-                         staged ? nullptr : p->d_state, p->max_size);
+    for (int k = 1; k < nsplit; ++k) {
+      MOPO_HIP(hipEventRecord(h->ev_join[k], h->sp[k]));
+      MOPO_HIP(hipStreamWaitEvent(s, h->ev_join[k], 0));
     }
+    KTimer t(h, KC_ADVANCE, s);
+    hipLaunchKernelGGL(steps_advance_kernel, dim3(1), dim3(1), 0, s, h->cnt, a->d_steps, i0, i1, p->d_state,
+                       p->max_size);
     MOPO_HIP(hipGetLastError());
+  } else {
+    for (int i = i0; i < i1; ++i) {
+      if (step_rows(i, 0, B, h->cnt, s, nullptr)) return -1;
+      if (compact) {
+        KTimer t(h, KC_COMPACT, s);
+        hipLaunchKernelGGL(rollout_compact_kernel, dim3(nblk), dim3(PB), 0, s, O, h->blockcnt, h->keep, h->cnt,
+                           h->obs[oc ^ 1], h->obs[oc], h->uid[uc], h->uid[uc ^ 1], h->cnt + 1);
+        MOPO_HIP(hipGetLastError());
+        uc ^= 1;
+      } else {
+        oc ^= 1;
+      }
+      if (batched_advance) {
+        if (i + 1 == i1) {
+          KTimer t(h, KC_ADVANCE, s);
+          hipLaunchKernelGGL(steps_advance_kernel, dim3(1), dim3(1), 0, s, h->cnt, a->d_steps, i0, i1, p->d_state,
+                             p->max_size);
+        }
+      } else {
+        KTimer t(h, KC_ADVANCE, s);
+        hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, s, h->cnt, a->d_steps, i, compact ? 1 : 0,
+                           staged ? nullptr : p->d_state, p->max_size);
+      }
+      MOPO_HIP(hipGetLastError());
+    }
   }
   h->oc = oc;
   h->uc = uc;
@@ -359,7 +420,7 @@ extern "C" int mopo_rollout_create(mopo_rollout_t* out, mopo_bnn_t bnn, int64_t 
   const int nblk = ceil_div((int)B, PB);
   size_t sz[] = {(size_t)B * O * 8, (size_t)B * O * 8, (size_t)B * 8, (size_t)B * 8, (size_t)B * A * 4,
                  (size_t)B * 4,     (size_t)B * 4,     (size_t)B * D * 4, (size_t)B * D * 4, (size_t)B,
-                 (size_t)nblk * 4,  16};
+                 (size_t)nblk * 4,  32};
   size_t off[12], tot = 0;
   for (int i = 0; i < 12; ++i) { off[i] = tot; tot += (sz[i] + 255) & ~(size_t)255; }
   if (hipMalloc(&h->mem, tot) != hipSuccess) { delete h; return fail("mopo_rollout_create: out of device memory"); }
@@ -400,6 +461,11 @@ extern "C" int mopo_rollout_destroy(mopo_rollout_t hh) {
   Rollout* h = reinterpret_cast<Rollout*>(hh);
   if (!h) return 0;
   for (auto& e : h->ev) { (void)hipEventDestroy(e.second.first); (void)hipEventDestroy(e.second.second); }
+  for (int k = 0; k < Rollout::MAXSPLIT; ++k) {
+    if (h->ev_fork[k]) (void)hipEventDestroy(h->ev_fork[k]);
+    if (h->ev_join[k]) (void)hipEventDestroy(h->ev_join[k]);
+    if (h->sp[k]) (void)hipStreamDestroy(h->sp[k]);
+  }
   if (h->mem) (void)hipFree(h->mem);
   if (h->wpk) (void)hipFree(h->wpk);
   delete h;
