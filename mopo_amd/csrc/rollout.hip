@@ -224,11 +224,12 @@ __global__ void step_advance_kernel(int* cnt, int64_t* steps, int i, int compact
 }
 
 // Steps [i0, i1) without compaction (halfcheetah): every step keeps all cnt[0] rows, so step i's
-// rows went to pool_off = (i - i0) * n and one advance covers the whole range.
+// rows went to pool_off = (i - i0) * n and one advance covers the whole range (staged: no pool).
 __global__ void steps_advance_kernel(const int* cnt, int64_t* steps, int i0, int i1, int64_t* pool_state,
                                      int64_t max_size) {
   const int64_t n = cnt[0];
   for (int i = i0; i < i1; ++i) steps[i] = n;
+  if (!pool_state) return;
   const int64_t tot = n * (i1 - i0);
   pool_state[0] = (pool_state[0] + tot) % max_size;
   pool_state[1] = min(pool_state[1] + tot, max_size);
@@ -269,11 +270,11 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
   const bool compact = a->term_kind != MOPO_TERM_HALFCHEETAH;
   // no compaction, pool layout: positions advance by B per step and one launch advances the pool
   const bool batched_advance = !compact && !staged;
-  // Split rollout: with no compaction the rows never interact, so two halves run their own
+  // Split rollout (pool or staged layout): with no compaction the rows never interact, so two halves run their own
   // actor -> ensemble -> post chains on two streams; each half's kernels fill the CUs the other
   // half's launch tails and small kernels leave idle.  Identical results (rows, Philox streams and
   // pool positions do not depend on the split).  Off while profiling per kernel.
-  const int nsplit = batched_advance && !h->profile ? std::min<int>(split_parts(), (int)(B / 2048)) : 1;
+  const int nsplit = !compact && !h->profile ? std::min<int>(split_parts(), (int)(B / 2048)) : 1;
   const bool split = nsplit > 1;
   const int64_t bpart = split ? (B / nsplit + 63) / 64 * 64 : B;
   if (i0 == 0) {
@@ -369,8 +370,8 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
       MOPO_HIP(hipStreamWaitEvent(s, h->ev_join[k], 0));
     }
     KTimer t(h, KC_ADVANCE, s);
-    hipLaunchKernelGGL(steps_advance_kernel, dim3(1), dim3(1), 0, s, h->cnt, a->d_steps, i0, i1, p->d_state,
-                       p->max_size);
+    hipLaunchKernelGGL(steps_advance_kernel, dim3(1), dim3(1), 0, s, h->cnt, a->d_steps, i0, i1,
+                       staged ? nullptr : p->d_state, p->max_size);
     MOPO_HIP(hipGetLastError());
   } else {
     for (int i = i0; i < i1; ++i) {

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
-O, A, B, HZ = 17, 6, 700, 3
+O, A, HZ = 17, 6, 3
 
 
 def _setup():
@@ -32,7 +32,7 @@ def _fields(pool):
     return {k: v[:n].cpu().numpy() for k, v in pool.fields.items()}
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, B):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY='0')
@@ -52,7 +52,8 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_overlapped_allgather_matches_single_process():
+@pytest.mark.parametrize('B', [700, 4500])  # 4500 rows per rank: the split (two-stream) staged rollout
+def test_overlapped_allgather_matches_single_process(B):
     import torch
     import torch.multiprocessing as mp
     from mopo_amd.replay_pool import SimpleReplayPool
@@ -60,7 +61,7 @@ def test_overlapped_allgather_matches_single_process():
     world = 2
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, 'r0.npz')
-        mp.start_processes(_worker, args=(world, 29600 + os.getpid() % 1000, out), nprocs=world, join=True,
+        mp.start_processes(_worker, args=(world, 29600 + os.getpid() % 1000 + B % 7, out, B), nprocs=world, join=True,
                            start_method='spawn')
         got = dict(np.load(out))
     m, env, pi = _setup()
