@@ -13,7 +13,7 @@ brc=$?
 cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err
 if [ $brc -ne 0 ]; then echo "bench rc=$brc: stopping"; exit $brc; fi
 [ -n "$NO_PROF" ] && exit $rc
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof" -o run -- python "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof_bench.json" 2> "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof.err"
+cd /tmp && MOPO_ROLLOUT_SPLIT=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof" -o run -- python "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof_bench.json" 2> "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/prof.err"
 prc=$?
 echo "rocprof rc=$prc"
 exit $rc

@@ -6,6 +6,8 @@ R=$PWD
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 ARGS="--steps 3 --warmup 1 --no-cpu-baseline --sac-steps 50"
+# one stream: every ensemble launch is the 50k-row launch bench.py prices (roofline.avg_launch_ms)
+export MOPO_ROLLOUT_SPLIT=1
 cd /tmp
 i=0
 for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" "SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY"; do
