@@ -267,14 +267,17 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
   const int64_t B = a->B;
   const int nblk = ceil_div((int)B, PB);
   const uint32_t step0 = a->epoch * 4096u;
-  const bool compact = a->term_kind != MOPO_TERM_HALFCHEETAH;
+  // live rows are compacted between steps (mopo.py:758); a one-step rollout never needs it: its
+  // rows, terminal or not, all enter the pool (mopo.py:750-751) and no next step reads them
+  const bool compact = a->term_kind != MOPO_TERM_HALFCHEETAH && a->horizon > 1;
   // no compaction, pool layout: positions advance by B per step and one launch advances the pool
   const bool batched_advance = !compact && !staged;
   // Split rollout (pool or staged layout): with no compaction the rows never interact, so two halves run their own
   // actor -> ensemble -> post chains on two streams; each half's kernels fill the CUs the other
   // half's launch tails and small kernels leave idle.  Identical results (rows, Philox streams and
   // pool positions do not depend on the split).  Off while profiling per kernel.
-  const int nsplit = !compact && !h->profile ? std::min<int>(split_parts(), (int)(B / 2048)) : 1;
+  // (a one-step rollout gains nothing from it: measured 150 -> 137M transitions/s for C3)
+  const int nsplit = !compact && !h->profile && a->horizon > 1 ? std::min<int>(split_parts(), (int)(B / 2048)) : 1;
   const bool split = nsplit > 1;
   const int64_t bpart = split ? (B / nsplit + 63) / 64 * 64 : B;
   if (i0 == 0) {

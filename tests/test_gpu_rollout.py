@@ -201,7 +201,8 @@ def _rollout_case(domain, E, H, B, horizon, seed, coeff=1.0, O=17, A=6, height=N
 
 @pytest.mark.parametrize('domain,E,H,B,horizon', [('halfcheetah', 7, 200, 1000, 5), ('walker2d', 7, 200, 777, 5),
                                                   ('hopper', 7, 64, 300, 4), ('halfcheetah', 32, 32, 64, 3),
-                                                  ('halfcheetah', 7, 200, 5000, 3)])  # B >= 4096: split rollout
+                                                  ('halfcheetah', 7, 200, 5000, 3),   # B >= 4096: split rollout
+                                                  ('walker2d', 7, 200, 4500, 1)])     # one step: no compaction
 def test_fused_rollout_parity(domain, E, H, B, horizon):
     import torch
     from mopo_amd.replay_pool import SimpleReplayPool
