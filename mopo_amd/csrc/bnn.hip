@@ -301,8 +301,16 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_bf16_kernel(const BnnDe
       const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), b1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
+#if defined(BNN_KNOB_CHEAPSWISH)
+        hin[c][t] = to_bf16(acc[2 * c][t] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[2 * c][t])));
+        hin[c][4 + t] = to_bf16(acc[2 * c + 1][t] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[2 * c + 1][t])));
+#elif !defined(BNN_KNOB_NOSWISH)
         hin[c][t] = to_bf16(swish_fast(acc[2 * c][t] + b0[t]));
         hin[c][4 + t] = to_bf16(swish_fast(acc[2 * c + 1][t] + b1[t]));
+#else
+        hin[c][t] = to_bf16(acc[2 * c][t] + b0[t]);
+        hin[c][4 + t] = to_bf16(acc[2 * c + 1][t] + b1[t]);
+#endif
       }
     }
   };

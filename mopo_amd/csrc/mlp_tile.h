@@ -197,17 +197,29 @@ __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, con
                                                float* lds, int w, int lane) {
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) acc[nb] = zero4();
+#ifndef BNN_KNOB_NOBARRIER
   __syncthreads();
+#endif
+#ifndef BNN_KNOB_NOSTAGE
   stage_slice<NB, WAVES>(wf, lds, w, lane);
+#endif
 #pragma unroll
   for (int kg = 0; kg < KG; ++kg) {
+#ifndef BNN_KNOB_NOBARRIER
     __syncthreads();
+#endif
+#ifndef BNN_KNOB_NOSTAGE
     if (kg + 1 < KG) stage_slice<NB, WAVES>(wf + (kg + 1) * NB * 256, lds + ((kg + 1) & 1) * SLOT, w, lane);
+#endif
     const float* b = lds + (kg & 1) * SLOT;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const bf16x8 fr = *reinterpret_cast<const bf16x8*>(b + (nb * 64 + lane) * 4);
+#ifndef BNN_KNOB_NOMFMA
       acc[nb] = mfma_bf16(fr, in[kg], acc[nb]);
+#else
+      acc[nb][0] += (float)fr[0];
+#endif
     }
   }
 }

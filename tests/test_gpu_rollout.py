@@ -351,3 +351,73 @@ def test_empty_batches():
     steps = ro.run(torch.from_numpy(rs.normal(size=(50, 17)).astype(np.float32)).to(dev),
                    torch.from_numpy(init_sac_params(17, 6)).to(dev), pool, 0, 3, 0, 1.0, [0, 1, 2, 3, 4])
     assert steps.cpu().numpy().tolist() == [0, 0, 0] and pool.size == 0
+
+
+@pytest.mark.parametrize('domain', ['halfcheetah', 'walker2d'])
+def test_full_size_perf_mode_rows_vs_oracle(domain):
+    """The headline workload at full size (E=7, H=200, B=50,000, h=5, learned-var penalty, perf-mode
+    Philox streams; halfcheetah: split rollout, walker2d: order-preserving compaction between steps):
+    192 sampled rows are recomputed end to end by the oracle from the restated Philox streams
+    (oracle/rng.py) and compared at their pool positions.  Start rows bit-exact, terminals
+    bit-exact, floats at the parity tolerance.  Under compaction a row's position at step i+1 is its
+    rank among step i's survivors (mopo.py:758), taken from the device's own terminal flags of the
+    other rows (the sampled rows' flags are checked against the oracle)."""
+    import torch
+    from oracle import rng as orng
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout, init_sac_params, split_params
+    from mopo_amd.static import static_fns
+    E, H, B, h, O, A = 7, 200, 50000, 5, 17, 6
+    seed, epoch = 0x1234567890ab, 3
+    rs = np.random.RandomState(21)
+    env_n = 40000
+    env_obs = rs.normal(size=(env_n, O)).astype(np.float32)
+    if domain == 'walker2d':
+        env_obs[:, 0] = rs.uniform(0.9, 1.9, env_n)
+        env_obs[:, 1] = rs.uniform(-0.9, 0.9, env_n)
+    mats = obnn.to_mat_list(obnn.init_params(E, O, A, hidden=H, seed=22,
+                                             inputs=np.concatenate([env_obs[:2000], rs.uniform(-1, 1, (2000, A))], 1)))
+    p = obnn.from_mat_list(mats)
+    flat = init_sac_params(O, A, 256, seed=23)
+    P = [q.astype(np.float64) for q in split_params(flat, O, A)[:8]]
+    elites = [4, 1, 0, 6, 2]
+    model = make_model(mats, E, H)
+    pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=B * h)
+    ro = ModelRollout(model, B, h)
+    steps = ro.run(torch.from_numpy(env_obs).cuda(), torch.from_numpy(flat).cuda(), pool, B, h,
+                   static_fns[domain].term_kind, 1.0, elites, seed=seed, epoch=epoch).cpu().numpy()
+    assert steps[0] == B and pool.size == steps.sum()
+    if domain == 'halfcheetah':
+        assert steps.tolist() == [B] * h
+    term_dev = pool.fields['terminals'][:pool.size, 0].cpu().numpy()
+    rows = np.sort(rs.choice(B, 192, replace=False))   # uids (global row ids) of the sampled rows
+    idx = rows.copy()                                   # their positions within the current step
+    obs = env_obs[orng.start_rows(rows, seed, epoch * 4096, env_n)].astype(np.float64)
+    base, checked = 0, 0
+    for i in range(h):
+        if len(rows) == 0:
+            break
+        st = epoch * 4096 + 1 + i
+        ea = orng.act_noise(rows, seed, st, A).astype(np.float64)
+        act, _ = osac.actor_act(P, obs.astype(np.float32).astype(np.float64), ea)
+        act = act.astype(np.float32)
+        sel = orng.model_choice(rows, seed, st, elites)
+        noise = np.broadcast_to(orng.obs_noise(rows, seed, st, O + 1).astype(np.float64), (E, len(rows), O + 1))
+        nobs, rew, term, _ = ofe.step(p, elites, obs, act, ofe.TERMINATION[domain], penalty_coeff=1.0,
+                                      penalty_learned_var=True, noise=noise, model_inds=sel)
+        pos = torch.from_numpy(base + idx).cuda()
+        got = {k: v[pos].cpu().numpy() for k, v in pool.fields.items()}
+        if i == 0:   # the start rows: an exact copy of the Philox-chosen env rows
+            np.testing.assert_array_equal(got['observations'], obs.astype(np.float32))
+        close(got['observations'], obs, 5e-5)
+        close(got['actions'], act, 5e-5)
+        close(got['next_observations'], nobs, 5e-5)
+        close(got['rewards'], rew, 5e-5)
+        np.testing.assert_array_equal(got['terminals'], term)
+        checked += len(rows)
+        live = ~term[:, 0]
+        keep = ~term_dev[base:base + steps[i]]
+        rank = np.cumsum(keep) - keep
+        base += steps[i]
+        rows, idx, obs = rows[live], rank[idx[live]], nobs[live]
+    assert checked >= (192 * h if domain == 'halfcheetah' else 192 + 64)   # walker: >= 1 compacted step

@@ -153,3 +153,26 @@ def test_sac_oracle_matches_torch_autograd():
     for p0, p1, gt in zip(params[14:20], st.params[14:20], gq2):
         g = gt.numpy()
         np.testing.assert_allclose(p1, p0 - lr_t * 0.1 * g / (np.sqrt(0.001 * g * g) + 1e-8), rtol=1e-9, atol=1e-15)
+
+
+def test_philox_known_answers():
+    """oracle/rng.py Philox4x32-10 against the Random123 known-answer vectors (counter, key -> out)."""
+    from oracle.rng import philox4x32_10
+    kat = [((0, 0, 0, 0, 0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 6, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344, 0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for inp, out in kat:
+        assert tuple(int(x) for x in philox4x32_10(*inp)) == out
+
+
+def test_perf_streams_shape_and_range():
+    from oracle import rng
+    uid = np.arange(5000)
+    idx = rng.start_rows(uid, 7, 0, 333)
+    assert idx.min() >= 0 and idx.max() < 333 and len(np.unique(idx)) == 333
+    z = rng.obs_noise(uid, 7, 1, 18)
+    assert z.shape == (5000, 18) and abs(z.mean()) < 0.02 and abs(z.std() - 1) < 0.02
+    assert (rng.act_noise(uid, 7, 1, 6) != rng.act_noise(uid, 7, 2, 6)).all()   # step is in the counter
+    sel = rng.model_choice(uid, 7, 1, [4, 1, 0, 6, 2])
+    assert set(np.unique(sel)) == {0, 1, 2, 4, 6}
