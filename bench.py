@@ -206,9 +206,9 @@ def c3_leg(args, dev):
             'bf16_peak_tflops': BF16_PEAK_TFLOPS}
 
 
-def c5_leg(args, dev):
+def c5_leg(args, dev, dtype='fp32'):
     """BASELINE config C5 (stress), one GPU's share: E=32, H=400, 1M rows / 8 GPUs = 125k rows per GPU,
-    horizon 5, fp32 (synthetic weights; halfcheetah dims)."""
+    horizon 5, fp32 or bf16 ensemble (synthetic weights; halfcheetah dims)."""
     import torch
     from mopo_amd.bnn import construct_model
     from mopo_amd.replay_pool import SimpleReplayPool
@@ -217,7 +217,7 @@ def c5_leg(args, dev):
     rs = np.random.RandomState(4)
     env_obs = rs.normal(size=(ENV_ROWS, O)).astype(np.float32)
     model = construct_model(obs_dim=O, act_dim=A, hidden_dim=H5, num_networks=E5, num_elites=5,
-                            separate_mean_var=True, seed=1)
+                            separate_mean_var=True, seed=1, dtype=dtype)
     mats = model.get_params()
     x = np.concatenate([env_obs, rs.uniform(-1, 1, (ENV_ROWS, A))], 1)
     mats[0] = x.mean(0, keepdims=True).astype(np.float32)
@@ -238,12 +238,17 @@ def c5_leg(args, dev):
     n = int(sum(int(t.sum().item()) for t in tot))
     flop_row = 2 * E5 * ((O + A) * H5 + 3 * H5 * H5 + 2 * H5 * (O + 1))
     v = n / dt
-    return {'metric': 'model-rollout transitions/s (C5 stress, one GPU of eight)', 'value': v,
-            'unit': 'transitions/s', 'dtype': 'fp32', 'ms_per_rollout': dt / reps * 1e3,
-            'config': {'workload': 'E=32, H=400, obs=17, act=6, rollout_batch=125000 per GPU (1M / 8), horizon=5',
-                       'rollout_batch_per_gpu': B, 'horizon': h},
-            'bnn_flop_per_row': flop_row, 'ensemble_tflops_lower_bound': v * flop_row / 1e12,
-            'f32_peak_tflops': MFMA_F32_PEAK_TFLOPS}
+    out = {'metric': 'model-rollout transitions/s (C5 stress, one GPU of eight%s)' % (', bf16 ensemble' if dtype == 'bf16' else ''),
+           'value': v, 'unit': 'transitions/s', 'dtype': 'fp32' if dtype == 'fp32' else 'bf16 (f32 accumulate)',
+           'ms_per_rollout': dt / reps * 1e3,
+           'config': {'workload': 'E=32, H=400, obs=17, act=6, rollout_batch=125000 per GPU (1M / 8), horizon=5',
+                      'rollout_batch_per_gpu': B, 'horizon': h},
+           'bnn_flop_per_row': flop_row, 'ensemble_tflops_lower_bound': v * flop_row / 1e12}
+    if dtype == 'bf16':
+        out['bf16_peak_tflops'] = BF16_PEAK_TFLOPS
+    else:
+        out['f32_peak_tflops'] = MFMA_F32_PEAK_TFLOPS
+    return out
 
 
 def train_leg(args, env):
@@ -393,6 +398,7 @@ def main():
     sac_rate = sac_leg(args, pool, env, dev, world)
     c3 = c3_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None
     c5 = c5_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None
+    c5b = c5_leg(args, dev, 'bf16') if (rank == 0 and world == 1 and not args.no_c3) else None
     tr = train_leg(args, env) if (rank == 0 and world == 1 and args.train_epochs > 0) else None
     if rank != 0:
         if world > 1:
@@ -427,7 +433,7 @@ def main():
                 'us_per_step': 1e6 / sac_rate, **SAC_DIAG, 'parallelism': 'replicas only (one independent learner per GPU)'},
     }
     if c3 is not None:
-        out['extra_configs'] = {'C3': c3, 'C5_per_gpu': c5}
+        out['extra_configs'] = {'C3': c3, 'C5_per_gpu': c5, 'C5_bf16_per_gpu': c5b}
     if tr is not None:
         out['model_train'] = tr
     if not args.no_cpu_baseline and world == 1:

@@ -259,7 +259,7 @@ def test_fused_rollout_perf_mode_runs():
     np.testing.assert_array_equal(p2.fields['next_observations'].cpu().numpy(), f['next_observations'][:B * h])
 
 
-@pytest.mark.parametrize('E,H,B', [(7, 200, 3000), (7, 64, 257), (32, 32, 100)])
+@pytest.mark.parametrize('E,H,B', [(7, 200, 3000), (7, 64, 257), (32, 32, 100), (32, 400, 300)])
 def test_bnn_predict_bf16_vs_oracle(E, H, B):
     """bf16 weights/activations, f32 accumulate: |d| <= 3e-2 * (1 + |ref|) against the f32 oracle."""
     from mopo_amd.bnn import BNN
