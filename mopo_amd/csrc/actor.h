@@ -23,6 +23,9 @@ struct ActorArgs {
   uint32_t* pen_zero;
   // rollout: member selection per row (bnn.py:343): injected sel_in or Philox choice over elites
   int32_t* sel_out; const int32_t* sel_in; const int32_t* elites; int n_elites;
+  // rollout: the ensemble's scaled input row (utils.py:96) [B][32] in slot_feat(., xs_in) order,
+  // (concat(obs, act) - mu) / sigma, so the ensemble reads 128 contiguous bytes per row and member
+  float* xs; const float* xs_mu; const float* xs_sigma; int xs_in;
 };
 
 int launch_actor(const ActorArgs& a, hipStream_t s);

@@ -98,7 +98,7 @@ constexpr int ACT_WAVES = 4;
 template <int KG0, int NBP, int TQ0 = 4>
 __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? 4 : 2) void actor_kernel(const ActorArgs a) {
   constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
-  __shared__ float head[ACT_WAVES][16][17];
+  __shared__ float head[ACT_WAVES][16][25];  // head outputs [0, 16), then the actions [16, 16 + A)
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + (NBP * 4 + 63) / 64 * 256];  // one array (bnn.hip)
   float* lds_bias = lds + 2 * SLOT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
@@ -173,47 +173,73 @@ __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? 4 : 2) void actor_kerne
     head[wv][m][n] = hd[0][0][t] + lds_bias[n];
   }
   __syncthreads();
-  if (g != 0 || !ok) return;
-  float z[16];
-  const int64_t uid = a.d_uid ? a.d_uid[row] : row + a.uid_offset;
-  if (a.eps) {
-    for (int j = 0; j < A; ++j) z[j] = a.eps[row * A + j];
-  } else {
-    actor_noise(a.seed, a.step, uid, A, z);
-  }
-  int64_t pos = -1;
-  if (a.pool_act) pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool_state[0] + a.pool_off + row) % a.pool_max;
-  for (int j = 0; j < A; ++j) {
-    const float mu = head[wv][m][j];
-    const float ls = fminf(fmaxf(head[wv][m][A + j], -20.f), 2.f);  // mopo.py:304
-    const float sd = expf(ls);                                      // mopo.py:305
-    const float u = mu + z[j] * sd;                                 // mopo.py:306
-    const float act = tanhf(u);                                     // mopo.py:295
-    if (a.act) a.act[row * A + j] = act;
-    if (a.mu) a.mu[row * A + j] = tanhf(mu);                        // mopo.py:294
-    if (pos >= 0) a.pool_act[pos * A + j] = act;
-  }
-  if (pos >= 0) {  // the observation half of the pool row (mopo.py:750), stored f32
-    for (int k = 0; k < O; ++k)
-      a.pool_obs[pos * O + k] = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
-                                          : reinterpret_cast<const float*>(a.obs)[row * O + k];
-  }
-  if (a.pen_zero) a.pen_zero[row] = 0u;
-  if (a.sel_out) {
-    int32_t sel;
-    if (a.sel_in) {
-      sel = a.sel_in[row];
-    } else {  // perf mode of np.random.choice(elites, B) (bnn.py:343)
-      u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32), a.step, RNG_MODEL};
-      u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
-      sel = a.elites[(int)(((uint64_t)r.x * (uint64_t)a.n_elites) >> 32)];
+  if (g == 0 && ok) {
+    float z[16];
+    const int64_t uid = a.d_uid ? a.d_uid[row] : row + a.uid_offset;
+    if (a.eps) {
+      for (int j = 0; j < A; ++j) z[j] = a.eps[row * A + j];
+    } else {
+      actor_noise(a.seed, a.step, uid, A, z);
     }
-    a.sel_out[row] = sel;
+    int64_t pos = -1;
+    if (a.pool_act) pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool_state[0] + a.pool_off + row) % a.pool_max;
+    for (int j = 0; j < A; ++j) {
+      const float mu = head[wv][m][j];
+      const float ls = fminf(fmaxf(head[wv][m][A + j], -20.f), 2.f);  // mopo.py:304
+      const float sd = expf(ls);                                      // mopo.py:305
+      const float u = mu + z[j] * sd;                                 // mopo.py:306
+      const float act = tanhf(u);                                     // mopo.py:295
+      head[wv][m][16 + j] = act;
+      if (a.act) a.act[row * A + j] = act;
+      if (a.mu) a.mu[row * A + j] = tanhf(mu);                        // mopo.py:294
+      if (pos >= 0) a.pool_act[pos * A + j] = act;
+    }
+    if (pos >= 0) {  // the observation half of the pool row (mopo.py:750), stored f32
+      for (int k = 0; k < O; ++k)
+        a.pool_obs[pos * O + k] = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
+                                            : reinterpret_cast<const float*>(a.obs)[row * O + k];
+    }
+    if (a.pen_zero) a.pen_zero[row] = 0u;
+    if (a.sel_out) {
+      int32_t sel;
+      if (a.sel_in) {
+        sel = a.sel_in[row];
+      } else {  // perf mode of np.random.choice(elites, B) (bnn.py:343)
+        u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32), a.step, RNG_MODEL};
+        u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+        sel = a.elites[(int)(((uint64_t)r.x * (uint64_t)a.n_elites) >> 32)];
+      }
+      a.sel_out[row] = sel;
+    }
+  }
+  if (a.xs) {  // the ensemble's layer-0 input, scaled exactly as bnn_fwd_kernel would; lane g: 8 slots
+    __syncthreads();
+    if (ok) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        f32x4 v;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int k = slot_feat(8 * g + 4 * q + t, a.xs_in);
+          float x = 0.f;
+          if (k >= 0) {
+            const float raw = k < O ? (a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
+                                                  : reinterpret_cast<const float*>(a.obs)[row * O + k])
+                                    : head[wv][m][16 + k - O];
+            x = (raw - a.xs_mu[k]) / a.xs_sigma[k];
+          }
+          v[t] = x;
+        }
+        *reinterpret_cast<f32x4*>(a.xs + row * XS_STRIDE + 8 * g + 4 * q) = v;
+      }
+    }
   }
 }
 
 int launch_actor(const ActorArgs& a, hipStream_t s) {
   if (a.B == 0) return 0;
+  MOPO_REQUIRE(!a.xs || (a.xs_mu && a.xs_sigma && a.xs_in == a.O + a.A && a.xs_in <= XS_STRIDE),
+               "actor: scaled-input rows need the scaler and obs_dim + act_dim <= 32");
   MOPO_REQUIRE(a.A >= 1 && 2 * a.A <= 16, "actor: act_dim must be in [1, 8]");
   MOPO_REQUIRE(a.O >= 1 && a.O <= 32, "actor: obs_dim must be in [1, 32]");
   MOPO_REQUIRE(a.Wpk, "actor: packed weights required");

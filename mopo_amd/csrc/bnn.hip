@@ -193,6 +193,14 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
 
   // ---- layer-0 input: scaler transform (utils.py:96), f64 inputs cast to f32 as TF's feed does
   f32x4 x0[R][KG0];
+  if (a.xs) {  // rollout: the actor already wrote the scaled row in slot order
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t row = row0 + r * 16 + m;
+#pragma unroll
+      for (int kg = 0; kg < KG0; ++kg) x0[r][kg] = row < count ? ld4(a.xs + row * XS_STRIDE + kg * 16 + 4 * g) : zero4();
+    }
+  } else
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int64_t row = row0 + r * 16 + m;
@@ -203,11 +211,15 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
       for (int t = 0; t < 4; ++t) {
         const int k = slot_feat(kg * 16 + 4 * g + t, IN);
         float v = 0.f;
+#ifndef BNN_KNOB_NOX0
         if (ok && k >= 0) {
           float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
                             : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
           v = (raw - w.mu[k]) / w.sigma[k];
         }
+#else
+        v = ok && k >= 0 ? 0.01f * (float)(k + m) : 0.f;
+#endif
         x0[r][kg][t] = v;
       }
   }
@@ -281,6 +293,15 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_bf16_kernel(const BnnDe
   const int IN = w.IN, O = w.O;
   const bool ok = row < count;
   bf16x8 x0[1];
+  if (a.xs) {  // rollout: the actor already wrote the scaled row in slot order (bf16_kperm)
+    const f32x4 lo = ok ? ld4(a.xs + row * XS_STRIDE + 4 * g) : zero4();
+    const f32x4 hi = ok ? ld4(a.xs + row * XS_STRIDE + 16 + 4 * g) : zero4();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      x0[0][t] = to_bf16(lo[t]);
+      x0[0][4 + t] = to_bf16(hi[t]);
+    }
+  } else
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int k = slot_feat(bf16_kperm(g, j), IN);

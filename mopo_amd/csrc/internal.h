@@ -49,11 +49,15 @@ struct FwdIn {
 };
 
 enum { FWD_PREDICT = 0, FWD_ROLLOUT = 1 };
+constexpr int XS_STRIDE = 32;  // floats per pre-scaled input row (FwdArgs::xs): 2 k-groups of slots
 
 struct FwdArgs {
   FwdIn in;
   int64_t B;              // launch rows (grid sized for this)
   const int* d_count;     // optional device row count (<= B)
+  // optional pre-scaled input rows [B][32] f32 in slot_feat order (written once per row by the
+  // rollout's actor): replaces the per-member f64 obs / act loads and scaler transform
+  const float* xs;
   int ntiles;             // tiles per member in the grid
   // predict outputs
   float* mean;            // [E][B][D]

@@ -34,6 +34,7 @@ struct Rollout {
   int wpk_hp = 0;
   uint32_t* pen;
   int32_t* sel;
+  float* xs;        // [B][32] the ensemble's scaled input rows (written by the actor)
   float* mean_sel;
   float* std_sel;
   uint8_t* keep;
@@ -315,6 +316,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     aa.sel_out = h->sel + off;
     aa.sel_in = a->d_model_inds ? a->d_model_inds + (int64_t)i * B + off : nullptr;
     aa.elites = a->d_elites; aa.n_elites = a->n_elites;
+    aa.xs = h->xs + off * XS_STRIDE; aa.xs_mu = bnn->dev.mu; aa.xs_sigma = bnn->dev.sigma; aa.xs_in = bnn->dev.IN;
     {
       KTimer t(h, KC_ACTOR, ss);
       if (launch_actor(aa, ss)) return -1;
@@ -323,7 +325,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
 
     FwdArgs f{};
     f.in = FwdIn{h->obs[oc] + off * O, 1, O, h->act + off * A, 0, A};
-    f.B = n; f.d_count = cnt;
+    f.B = n; f.d_count = cnt; f.xs = h->xs + off * XS_STRIDE;
     f.pen_bits = h->pen + off; f.sel = h->sel + off; f.mean_sel = h->mean_sel + off * D;
     f.std_sel = h->std_sel + off * D;
     {
@@ -424,16 +426,16 @@ extern "C" int mopo_rollout_create(mopo_rollout_t* out, mopo_bnn_t bnn, int64_t 
   const int nblk = ceil_div((int)B, PB);
   size_t sz[] = {(size_t)B * O * 8, (size_t)B * O * 8, (size_t)B * 8, (size_t)B * 8, (size_t)B * A * 4,
                  (size_t)B * 4,     (size_t)B * 4,     (size_t)B * D * 4, (size_t)B * D * 4, (size_t)B,
-                 (size_t)nblk * 4,  32};
-  size_t off[12], tot = 0;
-  for (int i = 0; i < 12; ++i) { off[i] = tot; tot += (sz[i] + 255) & ~(size_t)255; }
+                 (size_t)nblk * 4,  32,                (size_t)B * XS_STRIDE * 4};
+  size_t off[13], tot = 0;
+  for (int i = 0; i < 13; ++i) { off[i] = tot; tot += (sz[i] + 255) & ~(size_t)255; }
   if (hipMalloc(&h->mem, tot) != hipSuccess) { delete h; return fail("mopo_rollout_create: out of device memory"); }
   char* m = (char*)h->mem;
   h->obs[0] = (double*)(m + off[0]); h->obs[1] = (double*)(m + off[1]);
   h->uid[0] = (int64_t*)(m + off[2]); h->uid[1] = (int64_t*)(m + off[3]);
   h->act = (float*)(m + off[4]); h->pen = (uint32_t*)(m + off[5]); h->sel = (int32_t*)(m + off[6]);
   h->mean_sel = (float*)(m + off[7]); h->std_sel = (float*)(m + off[8]); h->keep = (uint8_t*)(m + off[9]);
-  h->blockcnt = (int*)(m + off[10]); h->cnt = (int*)(m + off[11]);
+  h->blockcnt = (int*)(m + off[10]); h->cnt = (int*)(m + off[11]); h->xs = (float*)(m + off[12]);
   *out = reinterpret_cast<mopo_rollout_t>(h);
   return 0;
 }
