@@ -92,7 +92,10 @@ __device__ __forceinline__ void actor_noise(uint64_t seed, uint32_t step, int64_
   }
 }
 
-constexpr int ACT_WAVES = 4;
+#ifndef ACT_WAVES_CFG
+#define ACT_WAVES_CFG 4  // waves (16-row tiles) per workgroup
+#endif
+constexpr int ACT_WAVES = ACT_WAVES_CFG;
 
 // TQ0: k-steps in the last k-group of the observation (tail_steps(O); 4 = all)
 template <int KG0, int NBP, int TQ0 = 4>
