@@ -30,6 +30,13 @@ FLOP_BNN_ROW = 2 * E * ((O + A) * H + 3 * H * H + 2 * H * (O + 1))       # 1,845
 FLOP_ACTOR_ROW = 2 * (O * HP + HP * HP + HP * 2 * A)                      # 145,920
 PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01_v9_pmc_summary.json')
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
+# ensemble dtype -> (bf16 parts per operand, bf16 products per f32 product); fp32 runs f32 MFMA
+SPLIT = {'bf16': (1, 1), 'bf16x3': (2, 3), 'bf16x6': (3, 6)}
+DTYPE_DESC = {'fp32': 'fp32 (f32 MFMA 16x16x4)',
+              'bf16x6': 'f32 (f32 operands split into 3 bf16 parts, 6 bf16 MFMA products, f32 accumulate: '
+                        'f32-accurate, held to the fp32 parity tolerances)',
+              'bf16x3': 'f32 operands as 2 bf16 parts (3 bf16 MFMA products, ~17 significand bits, f32 accumulate)',
+              'bf16': 'bf16 (f32 accumulate)'}
 
 
 def parse():
@@ -46,6 +53,11 @@ def parse():
     p.add_argument('--no-c3', action='store_true', help='skip the secondary C3 (bf16 walker2d) line')
     p.add_argument('--train-epochs', type=int, default=2, help='timed BNN.train epochs (0: skip)')
     p.add_argument('--cpu-train-steps', type=int, default=10)
+    p.add_argument('--ensemble-dtype', default='bf16x6', choices=['fp32', 'bf16x6', 'bf16x3', 'bf16'],
+                   help='headline ensemble-forward arithmetic (mopo_amd.bnn._DTYPES); bf16x6 = f32 operands '
+                        'as 3 bf16 parts, f32-accurate (held to the fp32 parity tolerances)')
+    p.add_argument('--no-alt-dtypes', action='store_true',
+                   help='skip the extra headline-workload lines with the other ensemble dtypes')
     p.add_argument('--prof-steps', type=int, default=3, help='untimed rollouts timed per kernel with HIP events')
     return p.parse_args()
 
@@ -71,7 +83,7 @@ def dist_setup(args):
     return rank, world, torch.device('cuda', 0)
 
 
-def build(args, dev, rank):
+def build(args, dev, rank, world=None):
     import torch
     from mopo_amd.bnn import construct_model
     from mopo_amd.replay_pool import SimpleReplayPool
@@ -80,14 +92,14 @@ def build(args, dev, rank):
     env_obs = rs.normal(size=(ENV_ROWS, O)).astype(np.float32)
     env_act = rs.uniform(-1, 1, size=(ENV_ROWS, A)).astype(np.float32)
     model = construct_model(obs_dim=O, act_dim=A, hidden_dim=H, num_networks=E, num_elites=ELITES,
-                            separate_mean_var=True, seed=1)
+                            separate_mean_var=True, seed=1, dtype=args.ensemble_dtype)
     mats = model.get_params()
     x = np.concatenate([env_obs, env_act], 1)
     mats[0] = x.mean(0, keepdims=True).astype(np.float32)                 # scaler.fit (utils.py:79-81)
     mats[1] = x.std(0, keepdims=True).astype(np.float32)
     model.set_params(mats)
     model.set_elites([0, 1, 2, 3, 4])
-    world = int(os.environ.get('WORLD_SIZE', '1'))
+    world = int(os.environ.get('WORLD_SIZE', '1')) if world is None else world
     pool_rows = 5 * args.horizon * args.batch * world                       # mopo.py:693-695 (x ranks)
     pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=pool_rows)
     pi = torch.from_numpy(init_sac_params(O, A, HP, seed=2)).to(dev)
@@ -159,6 +171,43 @@ def cpu_baseline_1core(args):
 
 
 BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense MFMA
+
+
+def roofline_of(dtype, rows, ms):
+    """Roofline of the ensemble-forward launch: f32 MFMA for fp32; executed bf16 MFMA flops (products x
+    the algorithmic f32 flops) against the bf16 dense peak for the split / bf16 kernels."""
+    alg = rows * FLOP_BNN_ROW / (ms * 1e-3) / 1e12
+    if dtype == 'fp32':
+        return {'bound': 'mfma', 'kernel': 'bnn_fwd_kernel (ensemble forward, f32 MFMA 16x16x4)',
+                'achieved': alg, 'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': alg / MFMA_F32_PEAK_TFLOPS,
+                'flop_per_launch': rows * FLOP_BNN_ROW, 'avg_launch_ms': ms}
+    parts, prods = SPLIT[dtype]
+    return {'bound': 'mfma', 'kernel': 'bnn_fwd_bf16_kernel<P=%d> (ensemble forward, bf16 MFMA 16x16x32, %d '
+                                       'products per f32 product)' % (parts, prods),
+            'achieved': alg * prods, 'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': alg * prods / BF16_PEAK_TFLOPS, 'achieved_note': 'executed bf16 MFMA TFLOP/s = %d x the '
+            'algorithmic f32 rate' % prods, 'algorithmic_f32_tflops': alg,
+            'flop_per_launch': rows * FLOP_BNN_ROW, 'bf16_flop_per_launch': prods * rows * FLOP_BNN_ROW,
+            'avg_launch_ms': ms}
+
+
+def alt_headline_leg(args, dev, dtype, reps=10):
+    """The headline workload (same synthetic model / env pool / seeds as build()) with another ensemble
+    dtype; one rank, rollouts timed back to back like the headline."""
+    import torch
+    a2 = argparse.Namespace(**vars(args))
+    a2.ensemble_dtype = dtype
+    _, pool, ro, pi, env, _ = build(a2, dev, 0, world=1)
+    for w in range(2):
+        rollout_step(a2, ro, pool, pi, env, None, w, 0, 1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = [rollout_step(a2, ro, pool, pi, env, None, 2 + i, 0, 1) for i in range(reps)]
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n = int(sum(int(x.sum().item()) for x in st))
+    return {'metric': 'model-rollout transitions/s (halfcheetah-mixed, %s ensemble)' % dtype, 'value': n / dt,
+            'unit': 'transitions/s', 'dtype': DTYPE_DESC[dtype], 'ms_per_rollout': dt / reps * 1e3}
 
 
 def c3_leg(args, dev):
@@ -400,13 +449,17 @@ def main():
     c5 = c5_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None
     c5b = c5_leg(args, dev, 'bf16') if (rank == 0 and world == 1 and not args.no_c3) else None
     tr = train_leg(args, env) if (rank == 0 and world == 1 and args.train_epochs > 0) else None
+    alts = {}
+    if rank == 0 and world == 1 and not args.no_alt_dtypes:
+        for dt_alt in ('fp32', 'bf16x6', 'bf16x3'):
+            if dt_alt != args.ensemble_dtype:
+                alts[dt_alt] = alt_headline_leg(args, dev, dt_alt)
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
         return
     bnn_ms = ms[2] / max(nl[2], 1)
     rows_per_launch = args.batch  # halfcheetah: no terminations, every step runs all rows
-    achieved = rows_per_launch * FLOP_BNN_ROW / (bnn_ms * 1e-3) / 1e12
     kernel_ms = {k: ms[i] / max(nl[i], 1) for i, k in enumerate(['start', 'actor', 'ensemble_fwd', 'fakeenv_post',
                                                                   'compact', 'advance'])}
     value = total / dt
@@ -415,18 +468,15 @@ def main():
         'metric': 'model-rollout transitions/s (halfcheetah-mixed)',
         'value': value, 'unit': 'transitions/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'fp32', 'data': 'synthetic (random-init weights, N(0,1) env pool; D4RL/.mat unavailable offline)',
+        'dtype': DTYPE_DESC[args.ensemble_dtype], 'data': 'synthetic (random-init weights, N(0,1) env pool; D4RL/.mat unavailable offline)',
         'config': {'workload': 'halfcheetah_mixed rollout: E=7 (5 elites), H=200 smv, obs=17, act=6, '
                                'rollout_batch=%d per GPU, horizon=%d, penalty_coeff=1.0, learned-var penalty'
                                % (args.batch, args.horizon),
                    'rollout_batch_per_gpu': args.batch, 'horizon': args.horizon, 'parallelism': 'dp%d' % world},
-        'roofline': {'bound': 'mfma', 'kernel': 'bnn_fwd_kernel (ensemble forward, f32 MFMA 16x16x4)',
-                     'achieved': achieved, 'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                     'frac': achieved / MFMA_F32_PEAK_TFLOPS, 'traffic': traffic,
+        'roofline': {**roofline_of(args.ensemble_dtype, rows_per_launch, bnn_ms), 'traffic': traffic,
                      'traffic_note': 'HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction, '
                                      'MI355X_MICROARCH.md HBM) from the committed --pmc passes, '
-                                     + os.path.relpath(PMC_SUMMARY, ROOT) + ' (same workload)',
-                     'flop_per_launch': rows_per_launch * FLOP_BNN_ROW, 'avg_launch_ms': bnn_ms},
+                                     + os.path.relpath(PMC_SUMMARY, ROOT) + ' (same workload)'},
         'kernel_ms_avg': kernel_ms,
         'sac': {'metric': 'SAC grad-steps/s (batch 256 = 12 env + 244 model rows, mopo.py:801-850)',
                 'per_gpu': sac_rate, 'aggregate_replicas': sac_rate * world, 'steps_timed': args.sac_steps,
@@ -434,6 +484,8 @@ def main():
     }
     if c3 is not None:
         out['extra_configs'] = {'C3': c3, 'C5_per_gpu': c5, 'C5_bf16_per_gpu': c5b}
+    if alts:
+        out['headline_other_dtypes'] = alts
     if tr is not None:
         out['model_train'] = tr
     if not args.no_cpu_baseline and world == 1:
@@ -452,8 +504,11 @@ def pmc_traffic(args):
     if (args.batch, args.horizon) != (50000, 5) or not os.path.exists(PMC_SUMMARY):
         return None
     ks = json.load(open(PMC_SUMMARY))['kernels']
+    P = SPLIT.get(args.ensemble_dtype, (0, 0))[0]
+    want = 'mopo::bnn_fwd_kernel' if P == 0 else \
+        'mopo::bnn_fwd_bf16_kernel<14, 3, 1, %d, %d, %d>' % (4 if P == 1 else 8, P, 1 if P == 1 else P)
     for k, v in ks.items():
-        if k.startswith('mopo::bnn_fwd_kernel') and 'hbm_bytes' in v:
+        if k.startswith(want) and 'hbm_bytes' in v:
             return v['hbm_bytes']
     return None
 

@@ -21,6 +21,11 @@ import numpy as np
 
 from . import _lib as L
 
+# ensemble-forward arithmetic (mopo_bnn_create dtype): 'fp32' f32 MFMA; 'bf16' bf16 operands;
+# 'bf16x3' / 'bf16x6' f32 operands split into 2 / 3 bf16 parts (3 / 6 bf16 MFMAs per product,
+# f32 accumulate; bf16x6 is f32-accurate, bf16x3 keeps ~17 significand bits).
+_DTYPES = {'fp32': 0, 'bf16': 1, 'bf16x3': 2, 'bf16x6': 3}
+
 N_HIDDEN = 4
 
 
@@ -67,12 +72,14 @@ class BNN:
         self.act_dim = int(params['act_dim'])
         self.hidden_dim = int(params.get('hidden_dim', 200))
         self.dtype = params.get('dtype', 'fp32')
+        if self.dtype not in _DTYPES:
+            raise ValueError('dtype must be one of %s, got %r' % (sorted(_DTYPES), self.dtype))
         self.model_loaded = False
         self._model_inds = list(range(min(self.num_elites, self.num_nets)))   # set by _end_train
         self._mats = None
         h = C.c_void_p()
         L.check(L.lib().mopo_bnn_create(C.byref(h), self.num_nets, self.obs_dim, self.act_dim, self.hidden_dim,
-                                        int(self.separate_mean_var), 0 if self.dtype == 'fp32' else 1))
+                                        int(self.separate_mean_var), _DTYPES[self.dtype]))
         self._h = h
 
     def __del__(self):

@@ -47,21 +47,30 @@ __global__ void pack_frags_kernel(const float* __restrict__ src, float* __restri
 
 // bf16 fragments for v_mfma_f32_16x16x32_bf16 (k-group of 32, permuted k order: mlp_tile.h):
 // frag (kg, nb), lane l (n = l&15, g = l>>4), element j = W[e][32 kg + bf16_kperm(g, j)][16 nb + n]
+// P > 1: fragment (kg, p, nb) holds part p of the split (split_bf16), laid out [e][kg][p][nb].
+template <int P>
 __global__ void pack_frags_bf16_kernel(const float* __restrict__ src, short* __restrict__ dst, int E, int K, int N,
                                        int KG, int NB, int perm_k, int perm_n) {
-  int64_t total = (int64_t)E * KG * NB * 512;
+  int64_t total = (int64_t)E * KG * P * NB * 512;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     int j = i & 7, lane = (i >> 3) & 63;
     int64_t f = i >> 9;
     int nb = f % NB;
-    int kg = (f / NB) % KG;
-    int e = f / ((int64_t)NB * KG);
+    int p = (f / NB) % P;
+    int kg = (f / ((int64_t)NB * P)) % KG;
+    int e = f / ((int64_t)NB * P * KG);
     int k = kg * 32 + bf16_kperm(lane >> 4, j), n = nb * 16 + (lane & 15);
     if (perm_k) k = slot_feat(k, K);
     if (perm_n == 1) n = slot_feat(n, N);
     else if (perm_n == 2) n = head_col(n, N / 2);
-    dst[i] = to_bf16((k >= 0 && n >= 0 && k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f);
+    short parts[P];
+    split_bf16<P>((k >= 0 && n >= 0 && k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f, parts);
+    short v = parts[0];
+#pragma unroll
+    for (int q = 1; q < P; ++q)
+      if (q == p) v = parts[q];
+    dst[i] = v;
   }
 }
 
@@ -276,13 +285,19 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
   (void)D;
 }
 
-// ---- bf16 forward (dtype 1): bf16 weights/activations, f32 accumulate and f32 epilogues.
+// ---- bf16 forward: weights/activations as P bf16 parts, f32 accumulate and f32 epilogues.
+// P = 1 (dtype 1): bf16.  P = 2 (dtype 2, "bf16x3"): 3 products per k-group, ~17 significand bits.
+// P = 3 (dtype 3, "bf16x6"): 6 products, f32-accurate (mlp_tile.h split_bf16 / layer_lds_split).
 // NB2 = hidden blocks rounded up to even (k-groups of 32 pair two accumulator blocks).
-template <int NB2, int NBO, int MODE, int WAVES>
-__global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_bf16_kernel(const BnnDev w, const FwdArgs a) {
+#ifndef BNN_SPLIT_MINB
+#define BNN_SPLIT_MINB 3  // split kernels (P > 1): 4-wave workgroups per CU (3: 168 VGPRs; P = 3 spills 15, still 4 % faster than 2)
+#endif
+template <int NB2, int NBO, int MODE, int WAVES, int P = 1, int PS = 1>
+__global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB * 4 / WAVES) : 512 / (WAVES * 64)) void bnn_fwd_bf16_kernel(
+    const BnnDev w, const FwdArgs a) {
   constexpr int KG = NB2 / 2;
   constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
-  constexpr int SLOT = Stage<NBMAX, WAVES>::SLOTS * 256;
+  constexpr int SLOT = Stage<PS * NBMAX, WAVES>::SLOTS * 256;
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
@@ -292,14 +307,27 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_bf16_kernel(const BnnDe
   if ((int64_t)grp * WAVES * 16 >= count) return;
   const int IN = w.IN, O = w.O;
   const bool ok = row < count;
-  bf16x8 x0[1];
+  bf16x8 x0[P][1];
+  auto put = [&](bf16x8 (&dst)[P][KG], int c, int j, float v) {
+    short parts[P];
+    split_bf16<P>(v, parts);
+#pragma unroll
+    for (int p = 0; p < P; ++p) dst[p][c][j] = parts[p];
+  };
+  (void)put;
+  auto put0 = [&](int j, float v) {
+    short parts[P];
+    split_bf16<P>(v, parts);
+#pragma unroll
+    for (int p = 0; p < P; ++p) x0[p][0][j] = parts[p];
+  };
   if (a.xs) {  // rollout: the actor already wrote the scaled row in slot order (bf16_kperm)
     const f32x4 lo = ok ? ld4(a.xs + row * XS_STRIDE + 4 * g) : zero4();
     const f32x4 hi = ok ? ld4(a.xs + row * XS_STRIDE + 16 + 4 * g) : zero4();
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      x0[0][t] = to_bf16(lo[t]);
-      x0[0][4 + t] = to_bf16(hi[t]);
+      put0(t, lo[t]);
+      put0(4 + t, hi[t]);
     }
   } else
 #pragma unroll
@@ -311,38 +339,53 @@ __global__ __launch_bounds__(WAVES * 64, 2) void bnn_fwd_bf16_kernel(const BnnDe
                         : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
       v = (raw - w.mu[k]) / w.sigma[k];
     }
-    x0[0][j] = to_bf16(v);
+    put0(j, v);
   }
   const int64_t bs = w.BS;
   f32x4 acc[NB2];
-  bf16x8 hin[KG];
-  auto to_input = [&](const float* b) {  // bias + swish in f32, then the bf16 B operand
+  bf16x8 hin[P][KG];
+  auto to_input = [&](const float* b) {  // bias + swish in f32, then the bf16 B operand parts
 #pragma unroll
     for (int c = 0; c < KG; ++c) {
       const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), b1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
+        if constexpr (P > 1) {
+          put(hin, c, t, swish_fast(acc[2 * c][t] + b0[t]));
+          put(hin, c, 4 + t, swish_fast(acc[2 * c + 1][t] + b1[t]));
+          continue;
+        }
 #if defined(BNN_KNOB_CHEAPSWISH)
-        hin[c][t] = to_bf16(acc[2 * c][t] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[2 * c][t])));
-        hin[c][4 + t] = to_bf16(acc[2 * c + 1][t] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[2 * c + 1][t])));
+        hin[0][c][t] = to_bf16(acc[2 * c][t] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[2 * c][t])));
+        hin[0][c][4 + t] = to_bf16(acc[2 * c + 1][t] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[2 * c + 1][t])));
 #elif !defined(BNN_KNOB_NOSWISH)
-        hin[c][t] = to_bf16(swish_fast(acc[2 * c][t] + b0[t]));
-        hin[c][4 + t] = to_bf16(swish_fast(acc[2 * c + 1][t] + b1[t]));
+        hin[0][c][t] = to_bf16(swish_fast(acc[2 * c][t] + b0[t]));
+        hin[0][c][4 + t] = to_bf16(swish_fast(acc[2 * c + 1][t] + b1[t]));
 #else
-        hin[c][t] = to_bf16(acc[2 * c][t] + b0[t]);
-        hin[c][4 + t] = to_bf16(acc[2 * c + 1][t] + b1[t]);
+        hin[0][c][t] = to_bf16(acc[2 * c][t] + b0[t]);
+        hin[0][c][4 + t] = to_bf16(acc[2 * c + 1][t] + b1[t]);
 #endif
       }
     }
   };
-  layer_lds_bf16<1, NB2, WAVES, SLOT>(w.w0b + (int64_t)e * NB2 * 256, x0, acc, lds, wv, lane);
+  if constexpr (P == 1) {
+    layer_lds_bf16<1, NB2, WAVES, SLOT>(w.w0b + (int64_t)e * NB2 * 256, x0[0], acc, lds, wv, lane);
+  } else {
+    layer_lds_split<1, NB2, WAVES, SLOT, P, PS>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane);
+  }
   to_input(w.b0 + e * bs);
   for (int l = 0; l < 3; ++l) {
-    layer_lds_bf16<KG, NB2, WAVES, SLOT>(w.whb + ((int64_t)l * w.E + e) * KG * NB2 * 256, hin, acc, lds, wv, lane);
+    const float* wl = w.whb + ((int64_t)l * w.E + e) * KG * P * NB2 * 256;
+    if constexpr (P == 1) layer_lds_bf16<KG, NB2, WAVES, SLOT>(wl, hin[0], acc, lds, wv, lane);
+    else layer_lds_split<KG, NB2, WAVES, SLOT, P, PS>(wl, hin, acc, lds, wv, lane);
     to_input(w.bh + ((int64_t)l * w.E + e) * bs);
   }
   f32x4 hd[NBO];
-  layer_lds_bf16<KG, NBO, WAVES, SLOT>(w.whdb + (int64_t)e * KG * NBO * 256, hin, hd, lds, wv, lane);
+  if constexpr (P == 1) {
+    layer_lds_bf16<KG, NBO, WAVES, SLOT>(w.whdb + (int64_t)e * KG * NBO * 256, hin[0], hd, lds, wv, lane);
+  } else {
+    layer_lds_split<KG, NBO, WAVES, SLOT, P, PS>(w.whdb + (int64_t)e * KG * P * NBO * 256, hin, hd, lds, wv, lane);
+  }
   head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
                            (MODE == FWD_ROLLOUT && ok) ? a.sel[row] : -1);
 }
@@ -387,17 +430,38 @@ static int launch_fwd_h(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s)
               std::to_string(h->H) + ")");
 }
 
-template <int NB2, int NBO>
-static int launch_bf16_t(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
+// split kernels (P > 1): one slice per k-group holding all P weight parts (every slice then feeds
+// P (P + 1) / 2 MFMAs per block, so the copy of the next slice hides behind uniform work), 8 waves
+// per workgroup sharing the 2 x P * NB KiB of LDS
+#ifndef BNN_SPLIT_WAVES
+#define BNN_SPLIT_WAVES 4
+#endif
+#ifndef BNN_SPLIT_PS
+#define BNN_SPLIT_PS 1  // parts per slice; 0: all P
+#endif
+
+template <int NB2, int NBO, int P>
+static int launch_bf16_p(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
+  constexpr int WV = P == 1 ? FWD_WAVES : BNN_SPLIT_WAVES;
+  constexpr int PS = P == 1 ? 1 : (BNN_SPLIT_PS == 0 ? P : BNN_SPLIT_PS);
   a.ntiles = (int)ceil_div((int)a.B, 16);
   if (a.ntiles == 0) return 0;
-  dim3 grid(ceil_div(a.ntiles, FWD_WAVES) * h->E), block(64 * FWD_WAVES);
+  dim3 grid(ceil_div(a.ntiles, WV) * h->E), block(64 * WV);
   if (mode == FWD_PREDICT)
-    hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_PREDICT, FWD_WAVES>), grid, block, 0, s, h->dev, a);
+    hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_PREDICT, WV, P, PS>), grid, block, 0, s, h->dev, a);
   else
-    hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_ROLLOUT, FWD_WAVES>), grid, block, 0, s, h->dev, a);
+    hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, PS>), grid, block, 0, s, h->dev, a);
   MOPO_HIP(hipGetLastError());
   return 0;
+}
+
+template <int NB2, int NBO>
+static int launch_bf16_t(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) {
+  switch (bf16_parts(h->dtype)) {
+    case 2: return launch_bf16_p<NB2, NBO, 2>(h, mode, a, s);
+    case 3: return launch_bf16_p<NB2, NBO, 3>(h, mode, a, s);
+  }
+  return launch_bf16_p<NB2, NBO, 1>(h, mode, a, s);
 }
 
 static int launch_bf16(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) {
@@ -411,6 +475,7 @@ static int launch_bf16(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) 
     }
   } else if (h->dev.NBO == 2) {
     switch (h->dev.NB2) {
+      case 4: return launch_bf16_t<4, 2>(h, mode, a, s);
       case 14: return launch_bf16_t<14, 2>(h, mode, a, s);
     }
   }
@@ -419,7 +484,7 @@ static int launch_bf16(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) 
 
 int launch_bnn_fwd(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) {
   if (!h->has_params) return fail("bnn: parameters not set (mopo_bnn_set_params)");
-  if (h->dtype == 1) return launch_bf16(h, mode, a, s);
+  if (h->dtype != 0) return launch_bf16(h, mode, a, s);
   if (h->dev.KG0 != 1 && h->dev.KG0 != 2) return fail("bnn: obs_dim + act_dim must be <= 32");
   const bool k1 = h->dev.KG0 == 1;  // hopper: 11 + 3 inputs
   switch (h->dev.NBO) {
@@ -439,7 +504,8 @@ extern "C" int mopo_bnn_create(mopo_bnn_t* out, int E, int obs_dim, int act_dim,
   MOPO_REQUIRE(out != nullptr, "mopo_bnn_create: out is NULL");
   MOPO_REQUIRE(E >= 1 && E <= 256, "mopo_bnn_create: num_networks must be in [1, 256]");
   MOPO_REQUIRE(obs_dim >= 1 && act_dim >= 1, "mopo_bnn_create: bad obs/act dims");
-  MOPO_REQUIRE(dtype == 0 || dtype == 1, "mopo_bnn_create: dtype must be 0 (fp32) or 1 (bf16)");
+  MOPO_REQUIRE(dtype >= 0 && dtype <= 3,
+               "mopo_bnn_create: dtype must be 0 (fp32), 1 (bf16), 2 (bf16x3) or 3 (bf16x6)");
   Bnn* h = new Bnn();
   h->E = E; h->O = obs_dim; h->A = act_dim; h->H = hidden; h->smv = smv; h->dtype = dtype;
   BnnDev& d = h->dev;
@@ -546,27 +612,34 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
     }
     MOPO_HIP(hipMemcpy(bhd, aux.data(), aux.size() * sizeof(float), hipMemcpyHostToDevice));
   }
-  if (h->dtype == 1 && rc == 0) {
-    // bf16 fragments: [E][1][NB2] | [3][E][KG][NB2] | [E][KG][NBO], 256 floats (= 512 bf16) each
-    const int NB2 = d.NB2, KG = NB2 / 2;
-    const int64_t f0 = (int64_t)E * NB2, fh = 3LL * E * KG * NB2, fd = (int64_t)E * KG * NBO;
+  if (h->dtype != 0 && rc == 0) {
+    // bf16 fragments: [E][1][P][NB2] | [3][E][KG][P][NB2] | [E][KG][P][NBO], 256 floats (= 512 bf16) each
+    const int NB2 = d.NB2, KG = NB2 / 2, P = bf16_parts(h->dtype);
+    const int64_t f0 = (int64_t)E * P * NB2, fh = 3LL * E * KG * P * NB2, fd = (int64_t)E * KG * P * NBO;
     if (!h->bbuf) MOPO_HIP(hipMalloc(&h->bbuf, (f0 + fh + fd) * 256 * sizeof(float)));
     float* b0f = reinterpret_cast<float*>(h->bbuf);
     float* bhf = b0f + f0 * 256;
     float* bdf = bhf + fh * 256;
     auto packh = [&](const float* src, size_t nsrc, float* dst, int K, int N, int KGb, int NB, int perm_n) -> int {
       MOPO_HIP(hipMemcpy(stage, src, nsrc * sizeof(float), hipMemcpyHostToDevice));
-      int64_t tot = (int64_t)E * KGb * NB * 512;
+      int64_t tot = (int64_t)E * KGb * P * NB * 512;
       int blocks = (int)std::min<int64_t>((tot + 255) / 256, 4096);
-      hipLaunchKernelGGL(pack_frags_bf16_kernel, dim3(blocks), dim3(256), 0, 0, stage, (short*)dst, E, K, N, KGb, NB, 1,
-                         perm_n);
+      if (P == 3)
+        hipLaunchKernelGGL(pack_frags_bf16_kernel<3>, dim3(blocks), dim3(256), 0, 0, stage, (short*)dst, E, K, N, KGb,
+                           NB, 1, perm_n);
+      else if (P == 2)
+        hipLaunchKernelGGL(pack_frags_bf16_kernel<2>, dim3(blocks), dim3(256), 0, 0, stage, (short*)dst, E, K, N, KGb,
+                           NB, 1, perm_n);
+      else
+        hipLaunchKernelGGL(pack_frags_bf16_kernel<1>, dim3(blocks), dim3(256), 0, 0, stage, (short*)dst, E, K, N, KGb,
+                           NB, 1, perm_n);
       MOPO_HIP(hipGetLastError());
       MOPO_HIP(hipDeviceSynchronize());
       return 0;
     };
     rc |= packh(W[0], (size_t)E * IN * H, b0f, IN, H, 1, NB2, 1);
     for (int l = 0; l < 3; ++l)
-      rc |= packh(W[1 + l], (size_t)E * H * H, bhf + (int64_t)l * E * KG * NB2 * 256, H, H, KG, NB2, 1);
+      rc |= packh(W[1 + l], (size_t)E * H * H, bhf + (int64_t)l * E * KG * P * NB2 * 256, H, H, KG, NB2, 1);
     rc |= packh(head.data(), head.size(), bdf, H, 2 * D, KG, NBO, 2);
     d.w0b = b0f; d.whb = bhf; d.whdb = bdf;
   }

@@ -26,13 +26,16 @@ struct BnnDev {
   const float* maxlv; // [D]
   const float* minlv; // [D]
   int BS;             // per-member bias stride (floats): even(NBH) * 16
-  // bf16 fragments (dtype 1): 1 KiB = 64 lanes x 8 bf16 per (32-deep k-group, 16-wide block),
+  // bf16 fragments (dtype 1..3): 1 KiB = 64 lanes x 8 bf16 per (32-deep k-group, 16-wide block),
   // addressed in float units like the f32 fragments; hidden width padded to NB2 = even(NBH)
   int NB2;
   const float* w0b;   // [E][1][NB2]
   const float* whb;   // [3][E][NB2/2][NB2]
   const float* whdb;  // [E][NB2/2][NBO]
 };
+
+// bf16 parts per operand of a dtype (1 bf16, 2 bf16x3, 3 bf16x6; split_bf16 in mlp_tile.h)
+__host__ __device__ constexpr int bf16_parts(int dtype) { return dtype < 1 ? 1 : dtype; }
 
 struct Bnn {
   int E, O, A, H, smv, dtype;

@@ -224,4 +224,61 @@ __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, con
   }
 }
 
+// ---- split-bf16 variant: f32 operands as P bf16 parts (x = x0 + x1 [+ x2]) ---------------------
+// Part p of a value is its residual after parts 0..p-1, truncated to bf16 (the last part rounded),
+// so P = 3 carries 8 + 8 + 8 significand bits plus the rounding of the last: f32-accurate.  The
+// layer runs the products W_p x X_q with p + q < P (P = 2: 3 MFMAs, P = 3: 6 MFMAs per k-group
+// and block) on v_mfma_f32_16x16x32_bf16 with f32 accumulate.  Weight fragments are packed
+// [kg][p][nb] (pack_frags_bf16_kernel with P parts), so the pipeline streams KG * P slices of NB
+// fragments through the same double-buffered LDS slot as the bf16 layer: slice (kg, p) feeds the
+// (P - p) activation parts of k-group kg.
+template <int P>
+__device__ __forceinline__ void split_bf16(float v, short (&out)[P]) {
+  float r = v;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, r);
+    const short s = p + 1 < P ? (short)(u >> 16) : to_bf16(r);
+    out[p] = s;
+    if (p + 1 < P) r -= __builtin_bit_cast(float, (uint32_t)(uint16_t)s << 16);
+  }
+}
+
+// PS: parts staged per slice (P: one slice of P * NB fragments per k-group; 1: P slices of NB).
+template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P>
+__device__ __forceinline__ void layer_lds_split(const float* __restrict__ wf, const bf16x8 (&in)[P][KG],
+                                                f32x4 (&acc)[NB], float* lds, int w, int lane) {
+  static_assert(P % PS == 0, "parts per slice must divide the parts");
+  constexpr int SPK = P / PS, S = KG * SPK, NF = PS * NB;
+  static_assert(Stage<NF, WAVES>::SLOTS * 256 <= SLOT, "slice larger than its buffer");
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = zero4();
+  __syncthreads();
+  stage_slice<NF, WAVES>(wf, lds, w, lane);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    __syncthreads();
+    if (s + 1 < S) stage_slice<NF, WAVES>(wf + (s + 1) * NF * 256, lds + ((s + 1) & 1) * SLOT, w, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    const int kg = s / SPK;
+    const float* b = lds + (s & 1) * SLOT;
+#ifndef BNN_SPLIT_NOPF
+    // fragment i + 1 is read before the MFMAs of fragment i (one LDS read in flight)
+    bf16x8 fr_next = *reinterpret_cast<const bf16x8*>(b + lane * 4);
+#endif
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int pp = i / NB, nb = i % NB, p = (s % SPK) * PS + pp;
+#ifndef BNN_SPLIT_NOPF
+      const bf16x8 fr = fr_next;
+      if (i + 1 < NF) fr_next = *reinterpret_cast<const bf16x8*>(b + ((i + 1) * 64 + lane) * 4);
+#else
+      const bf16x8 fr = *reinterpret_cast<const bf16x8*>(b + (i * 64 + lane) * 4);
+#endif
+#pragma unroll
+      for (int q = P - 1 - p; q >= 0; --q) acc[nb] = mfma_bf16(fr, in[q][kg], acc[nb]);
+    }
+  }
+}
+
 }  // namespace mopo

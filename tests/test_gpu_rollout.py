@@ -36,10 +36,10 @@ def golden_params(E, H):
     return [z['w%d' % i] for i in range(16)]
 
 
-def make_model(mats, E, H, O=17, A=6):
+def make_model(mats, E, H, O=17, A=6, dtype='fp32'):
     from mopo_amd.bnn import BNN
     m = BNN({'name': 't', 'num_networks': E, 'num_elites': 5, 'separate_mean_var': True, 'obs_dim': O,
-             'act_dim': A, 'hidden_dim': H})
+             'act_dim': A, 'hidden_dim': H, 'dtype': dtype})
     return m.set_params(mats)
 
 
@@ -199,17 +199,24 @@ def _rollout_case(domain, E, H, B, horizon, seed, coeff=1.0, O=17, A=6, height=N
                 eps_obs=eps_obs, inds=inds_all, steps=steps, pool=model_pool, coeff=coeff)
 
 
-@pytest.mark.parametrize('domain,E,H,B,horizon', [('halfcheetah', 7, 200, 1000, 5), ('walker2d', 7, 200, 777, 5),
+@pytest.mark.parametrize('domain,E,H,B,horizon,dtype', [
+    c if len(c) == 6 else c + ('fp32',) for c in [
+                                                  ('halfcheetah', 7, 200, 1000, 5), ('walker2d', 7, 200, 777, 5),
                                                   ('hopper', 7, 64, 300, 4), ('halfcheetah', 32, 32, 64, 3),
                                                   ('halfcheetah', 7, 200, 5000, 3),   # B >= 4096: split rollout
-                                                  ('walker2d', 7, 200, 4500, 1)])     # one step: no compaction
-def test_fused_rollout_parity(domain, E, H, B, horizon):
+                                                  ('walker2d', 7, 200, 4500, 1),      # one step: no compaction
+                                                  # f32 via 3 bf16 parts (f32-accurate), same tolerances
+                                                  ('halfcheetah', 7, 200, 1000, 5, 'bf16x6'),
+                                                  ('walker2d', 7, 200, 777, 5, 'bf16x6'),
+                                                  ('hopper', 7, 64, 300, 4, 'bf16x6'),
+                                                  ('halfcheetah', 7, 200, 5000, 3, 'bf16x6')]])
+def test_fused_rollout_parity(domain, E, H, B, horizon, dtype):
     import torch
     from mopo_amd.replay_pool import SimpleReplayPool
     from mopo_amd.rollout import ModelRollout
     from mopo_amd.static import static_fns
     c = _rollout_case(domain, E, H, B, horizon, seed=11)
-    model = make_model(c['mats'], E, H)
+    model = make_model(c['mats'], E, H, dtype=dtype)
     dev = torch.device('cuda')
     pool = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=B * horizon + 7)
     ro = ModelRollout(model, B, horizon)
@@ -276,6 +283,27 @@ def test_bnn_predict_bf16_vs_oracle(E, H, B):
     # and it is genuinely a different (reduced-precision) path: not bit-identical to fp32
     m32 = make_model(mats, E, H)
     assert not np.array_equal(mean, m32.predict(x)[0])
+
+
+@pytest.mark.parametrize('dtype,tol', [('bf16x6', 2e-5), ('bf16x3', 1e-4)])
+@pytest.mark.parametrize('E,H,B', [(7, 200, 4099), (7, 64, 257), (32, 32, 100), (32, 400, 300), (7, 200, 1)])
+def test_bnn_predict_split_vs_oracle(E, H, B, dtype, tol):
+    """f32 operands split into bf16 parts, f32 accumulate.  bf16x6 (3 parts, 6 products) holds the
+    fp32 path's tolerance, 2e-5 * (1 + |ref|) against the f64 oracle; bf16x3 (2 parts, 3 products,
+    ~17 significand bits) is held to 1e-4 * (1 + |ref|)."""
+    rs = np.random.RandomState(E + H + B)
+    mats = obnn.to_mat_list(obnn.init_params(E, 17, 6, hidden=H, seed=3, inputs=rs.normal(size=(300, 23)) * 3))
+    p = obnn.from_mat_list(mats)
+    x = (rs.normal(size=(B, 23)) * 2).astype(np.float32)
+    mean, var = make_model(mats, E, H, dtype=dtype).predict(x)
+    rm, rv = obnn.forward(p, x, dtype=np.float64)
+    close(mean, rm, tol)
+    close(var, rv, tol)
+    if dtype == 'bf16x6':   # f32-accurate: no worse than the f32-MFMA path's own rounding (x2, floor 2e-6)
+        m32, v32 = make_model(mats, E, H).predict(x)
+        err = lambda a, b: float(np.max(np.abs(np.float64(a) - b) / (1 + np.abs(b))))
+        assert err(mean, rm) <= max(2 * err(m32, rm), 2e-6), (err(mean, rm), err(m32, rm))
+        assert err(var, rv) <= max(2 * err(v32, rv), 2e-6), (err(var, rv), err(v32, rv))
 
 
 def test_fused_rollout_bf16_walker_runs():
@@ -353,8 +381,9 @@ def test_empty_batches():
     assert steps.cpu().numpy().tolist() == [0, 0, 0] and pool.size == 0
 
 
-@pytest.mark.parametrize('domain', ['halfcheetah', 'walker2d'])
-def test_full_size_perf_mode_rows_vs_oracle(domain):
+@pytest.mark.parametrize('domain,dtype', [('halfcheetah', 'fp32'), ('walker2d', 'fp32'), ('halfcheetah', 'bf16x6'),
+                                          ('walker2d', 'bf16x6')])
+def test_full_size_perf_mode_rows_vs_oracle(domain, dtype):
     """The headline workload at full size (E=7, H=200, B=50,000, h=5, learned-var penalty, perf-mode
     Philox streams; halfcheetah: split rollout, walker2d: order-preserving compaction between steps):
     192 sampled rows are recomputed end to end by the oracle from the restated Philox streams
@@ -381,7 +410,7 @@ def test_full_size_perf_mode_rows_vs_oracle(domain):
     flat = init_sac_params(O, A, 256, seed=23)
     P = [q.astype(np.float64) for q in split_params(flat, O, A)[:8]]
     elites = [4, 1, 0, 6, 2]
-    model = make_model(mats, E, H)
+    model = make_model(mats, E, H, dtype=dtype)
     pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=B * h)
     ro = ModelRollout(model, B, h)
     steps = ro.run(torch.from_numpy(env_obs).cuda(), torch.from_numpy(flat).cuda(), pool, B, h,
