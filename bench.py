@@ -28,7 +28,7 @@ O, A, E, ELITES, H, HP = 17, 6, 7, 5, 200, 256
 ENV_ROWS = 101000
 FLOP_BNN_ROW = 2 * E * ((O + A) * H + 3 * H * H + 2 * H * (O + 1))       # 1,845,200
 FLOP_ACTOR_ROW = 2 * (O * HP + HP * HP + HP * 2 * A)                      # 145,920
-PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01_v9_pmc_summary.json')
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01_v10_pmc_summary.json')
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
 # ensemble dtype -> (bf16 parts per operand, bf16 products per f32 product); fp32 runs f32 MFMA
 SPLIT = {'bf16': (1, 1), 'bf16x3': (2, 3), 'bf16x6': (3, 6)}
@@ -505,11 +505,16 @@ def pmc_traffic(args):
         return None
     ks = json.load(open(PMC_SUMMARY))['kernels']
     P = SPLIT.get(args.ensemble_dtype, (0, 0))[0]
-    want = 'mopo::bnn_fwd_kernel' if P == 0 else \
-        'mopo::bnn_fwd_bf16_kernel<14, 3, 1, %d, %d, %d>' % (4 if P == 1 else 8, P, 1 if P == 1 else P)
     for k, v in ks.items():
-        if k.startswith(want) and 'hbm_bytes' in v:
+        if 'hbm_bytes' not in v:
+            continue
+        if P == 0 and k.startswith('mopo::bnn_fwd_kernel<2, 13,'):
             return v['hbm_bytes']
+        # bnn_fwd_bf16_kernel<hidden tiles, ..., parts, ...>: H=200 -> 14 tiles; 5th argument = bf16 parts
+        if P > 0 and k.startswith('mopo::bnn_fwd_bf16_kernel<14,'):
+            targs = [a.strip() for a in k.split('<', 1)[1].rstrip('>').split(',')]
+            if len(targs) >= 5 and targs[4] == str(P):
+                return v['hbm_bytes']
     return None
 
 
