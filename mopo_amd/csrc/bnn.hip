@@ -289,6 +289,9 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
 // P = 1 (dtype 1): bf16.  P = 2 (dtype 2, "bf16x3"): 3 products per k-group, ~17 significand bits.
 // P = 3 (dtype 3, "bf16x6"): 6 products, f32-accurate (mlp_tile.h split_bf16 / layer_lds_split).
 // NB2 = hidden blocks rounded up to even (k-groups of 32 pair two accumulator blocks).
+#ifndef BNN_SPLIT_HOLD_F32
+#define BNN_SPLIT_HOLD_F32 1  // hold split activations in f32 (P = 3 scratch spill 64 -> 20 B/lane)
+#endif
 #ifndef BNN_SPLIT_MINB
 #define BNN_SPLIT_MINB 3  // split kernels (P > 1): 4-wave workgroups per CU (3: 168 VGPRs; P = 3 spills 15, still 4 % faster than 2)
 #endif
@@ -344,6 +347,10 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
   const int64_t bs = w.BS;
   f32x4 acc[NB2];
   bf16x8 hin[P][KG];
+  // P = 3: split activations held in f32, parts made per k-group (P = 2's parts take no more VGPRs)
+  constexpr bool HOLD = BNN_SPLIT_HOLD_F32 && P >= 3;
+  float hf[KG][8];
+  (void)hf;
   auto to_input = [&](const float* b) {  // bias + swish in f32, then the bf16 B operand parts
 #pragma unroll
     for (int c = 0; c < KG; ++c) {
@@ -351,8 +358,13 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if constexpr (P > 1) {
-          put(hin, c, t, swish_fast(acc[2 * c][t] + b0[t]));
-          put(hin, c, 4 + t, swish_fast(acc[2 * c + 1][t] + b1[t]));
+          if constexpr (HOLD) {
+            hf[c][t] = swish_fast(acc[2 * c][t] + b0[t]);
+            hf[c][4 + t] = swish_fast(acc[2 * c + 1][t] + b1[t]);
+          } else {
+            put(hin, c, t, swish_fast(acc[2 * c][t] + b0[t]));
+            put(hin, c, 4 + t, swish_fast(acc[2 * c + 1][t] + b1[t]));
+          }
           continue;
         }
 #if defined(BNN_KNOB_CHEAPSWISH)
@@ -377,6 +389,7 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
   for (int l = 0; l < 3; ++l) {
     const float* wl = w.whb + ((int64_t)l * w.E + e) * KG * P * NB2 * 256;
     if constexpr (P == 1) layer_lds_bf16<KG, NB2, WAVES, SLOT>(wl, hin[0], acc, lds, wv, lane);
+    else if constexpr (HOLD) layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS>(wl, hf, acc, lds, wv, lane);
     else layer_lds_split<KG, NB2, WAVES, SLOT, P, PS>(wl, hin, acc, lds, wv, lane);
     to_input(w.bh + ((int64_t)l * w.E + e) * bs);
   }
@@ -384,7 +397,10 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
   if constexpr (P == 1) {
     layer_lds_bf16<KG, NBO, WAVES, SLOT>(w.whdb + (int64_t)e * KG * NBO * 256, hin[0], hd, lds, wv, lane);
   } else {
-    layer_lds_split<KG, NBO, WAVES, SLOT, P, PS>(w.whdb + (int64_t)e * KG * P * NBO * 256, hin, hd, lds, wv, lane);
+    if constexpr (HOLD)
+      layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, PS>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd, lds, wv, lane);
+    else
+      layer_lds_split<KG, NBO, WAVES, SLOT, P, PS>(w.whdb + (int64_t)e * KG * P * NBO * 256, hin, hd, lds, wv, lane);
   }
   head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
                            (MODE == FWD_ROLLOUT && ok) ? a.sel[row] : -1);

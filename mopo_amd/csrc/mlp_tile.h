@@ -281,4 +281,45 @@ __device__ __forceinline__ void layer_lds_split(const float* __restrict__ wf, co
   }
 }
 
+// layer_lds_split with f32 activations held (8 VGPRs per k-group instead of 4 * P): each k-group's P
+// bf16 parts are split when its first slice is consumed, so only one k-group's parts are live.
+template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P>
+__device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf, const float (&in)[KG][8],
+                                                    f32x4 (&acc)[NB], float* lds, int w, int lane) {
+  static_assert(P % PS == 0, "parts per slice must divide the parts");
+  constexpr int SPK = P / PS, S = KG * SPK, NF = PS * NB;
+  static_assert(Stage<NF, WAVES>::SLOTS * 256 <= SLOT, "slice larger than its buffer");
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = zero4();
+  bf16x8 cur[P];
+  __syncthreads();
+  stage_slice<NF, WAVES>(wf, lds, w, lane);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int kg = s / SPK;
+    if (s % SPK == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        short parts[P];
+        split_bf16<P>(in[kg][j], parts);
+#pragma unroll
+        for (int p = 0; p < P; ++p) cur[p][j] = parts[p];
+      }
+    }
+    __syncthreads();
+    if (s + 1 < S) stage_slice<NF, WAVES>(wf + (s + 1) * NF * 256, lds + ((s + 1) & 1) * SLOT, w, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    const float* b = lds + (s & 1) * SLOT;
+    bf16x8 fr_next = *reinterpret_cast<const bf16x8*>(b + lane * 4);
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int pp = i / NB, nb = i % NB, p = (s % SPK) * PS + pp;
+      const bf16x8 fr = fr_next;
+      if (i + 1 < NF) fr_next = *reinterpret_cast<const bf16x8*>(b + ((i + 1) * 64 + lane) * 4);
+#pragma unroll
+      for (int q = P - 1 - p; q >= 0; --q) acc[nb] = mfma_bf16(fr, cur[q], acc[nb]);
+    }
+  }
+}
+
 }  // namespace mopo
