@@ -28,7 +28,7 @@ O, A, E, ELITES, H, HP = 17, 6, 7, 5, 200, 256
 ENV_ROWS = 101000
 FLOP_BNN_ROW = 2 * E * ((O + A) * H + 3 * H * H + 2 * H * (O + 1))       # 1,845,200
 FLOP_ACTOR_ROW = 2 * (O * HP + HP * HP + HP * 2 * A)                      # 145,920
-PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01_v10_pmc_summary.json')
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01_v11_pmc_summary.json')
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
 # ensemble dtype -> (bf16 parts per operand, bf16 products per f32 product); fp32 runs f32 MFMA
 SPLIT = {'bf16': (1, 1), 'bf16x3': (2, 3), 'bf16x6': (3, 6)}
