@@ -52,18 +52,22 @@ def get_logprob(x, means, variances):
 
 
 def step(params, elites, obs, act, termination_fn, penalty_coeff=0.0, penalty_learned_var=False,
-         deterministic=False, noise=None, model_inds=None):
+         deterministic=False, noise=None, model_inds=None, predicted=None):
     """FakeEnv.step (fake_env.py:37-131) with the ensemble forward of ``oracle.bnn``.
 
     RNG order follows the reference: ``np.random.normal(size=[E,B,D])`` (fake_env.py:72)
     then ``np.random.choice(elites, B)`` (bnn.py:343).  Either stream may be injected.
     Returns next_obs, penalized_rewards, terminals, info (same keys as fake_env.py:129-130).
+    ``predicted=(mean, var)`` replaces the forward (e.g. the reference graph's own f32 outputs).
     """
     return_single = obs.ndim == 1
     if return_single:
         obs, act = obs[None], act[None]
     inputs = np.concatenate((obs, act), axis=-1)                       # fake_env.py:46
-    means, variances = obnn.forward(params, inputs)                    # fake_env.py:50-64 (chunking is row-independent)
+    if predicted is None:
+        means, variances = obnn.forward(params, inputs)                # fake_env.py:50-64 (chunking is row-independent)
+    else:
+        means, variances = (np.array(a, np.float32) for a in predicted)
     means[:, :, 1:] += obs                                             # fake_env.py:66 (in-place, stays f32)
     stds = np.sqrt(variances)                                          # fake_env.py:67
     E, B, _ = means.shape

@@ -156,8 +156,9 @@ class SACState:
         self.opt_a = Adam([self.log_alpha], lr)
 
 
-def sac_step(st, batch, eps_s, eps_s2, gamma=0.99, tau=5e-3, reward_scale=1.0, target_entropy=-3.0):
-    """One ``_do_training`` + ``_update_target`` (mopo.py:834-853). Mutates ``st``; returns logs."""
+def sac_step(st, batch, eps_s, eps_s2, gamma=0.99, tau=5e-3, reward_scale=1.0, target_entropy=-3.0, grads_out=None):
+    """One ``_do_training`` + ``_update_target`` (mopo.py:834-853). Mutates ``st``; returns logs.
+    ``grads_out`` (dict): receives the pre-step gradients 'pi', 'q1', 'q2' (lists) and 'alpha'."""
     s, a, s2 = batch['observations'], batch['actions'], batch['next_observations']
     r, d = batch['rewards'][:, 0], batch['terminals'][:, 0].astype(np.float64)
     n = s.shape[0]
@@ -187,6 +188,8 @@ def sac_step(st, batch, eps_s, eps_s2, gamma=0.99, tau=5e-3, reward_scale=1.0, t
     da = dx1[:, O:] + dx2[:, O:]
     g_pi = pi_backward(P, cpi, np.full(n, alpha / n), da)
     g_alpha = -np.mean(logp_pi + target_entropy)                    # d/dlog_alpha of :437-438
+    if grads_out is not None:
+        grads_out.update(pi=g_pi, q1=g_q1, q2=g_q2, alpha=g_alpha)
     pi_gnorm = np.sqrt(sum(np.sum(g * g) for g in g_pi))
     q_gnorm = np.sqrt(sum(np.sum((0.5 * g) ** 2) for g in g_q1))     # grads of Q_loss wrt q1 vars (:431-432)
     # updates

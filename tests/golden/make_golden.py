@@ -11,9 +11,10 @@ functions):
   * mopo/models/bnn.py       ``BNN.random_inds``                         (bnn.py:342-344)
   * mopo/static/{halfcheetah,walker2d,hopper}.py ``termination_fn``
   * softlearning/replay_pools/flexible_replay_pool.py ``FlexibleReplayPool``
-The TF-only ensemble forward (bnn.py:631-675) is supplied by ``oracle.bnn.forward``
-(restatement), so rollout fixtures pin FakeEnv's numpy post-processing and RNG order
-exactly and the forward as a restatement.
+The TF-only ensemble forward (bnn.py:631-675) is the reference's own ``BNN._compile_outputs``
+executed in f32 under the torch-backed TF stand-in (make_ref_vectors.py / tfstub.py), so every
+float in the rollout fixtures comes from reference code; for B <= 64 the forward's mean/var are
+stored too (``ref_mean`` / ``ref_var``) so the oracle's post-processing can be pinned bit-exactly.
 Outputs: tests/golden/*.npz (inputs + expected outputs only; no reference source).
 """
 import importlib.util
@@ -27,16 +28,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 REF = '/root/reference'
 sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
 
 from oracle import bnn as obnn  # noqa: E402
-
-
-def _stub(name, **attrs):
-    m = types.ModuleType(name)
-    for k, v in attrs.items():
-        setattr(m, k, v)
-    sys.modules[name] = m
-    return m
 
 
 def _load(modname, path):
@@ -47,51 +41,41 @@ def _load(modname, path):
     return m
 
 
-class _Anything:
-    """Attribute/call sink standing in for the TF1 API at import time only."""
-
-    def __getattr__(self, name):
-        return _Anything()
-
-    def __call__(self, *a, **k):
-        return _Anything()
-
-
 def load_reference():
-    tf = _stub('tensorflow')
-    tf.__getattr__ = lambda name: _Anything()
-    _stub('RLA'); _stub('RLA.easy_log'); _stub('RLA.easy_log.logger', logger=None)
-    _stub('RLA.easy_log.tester', tester=None)
-    sys.modules['RLA.easy_log'].logger = None
-    # package skeletons so bnn.py's relative-absolute imports resolve to file-path loads
-    for pkg in ('mopo', 'mopo.models', 'mopo.utils', 'softlearning', 'softlearning.replay_pools'):
-        _stub(pkg)
-    _load('mopo.models.utils', os.path.join(REF, 'mopo/models/utils.py'))
-    _load('mopo.models.fc', os.path.join(REF, 'mopo/models/fc.py'))
-    _load('mopo.utils.logging', os.path.join(REF, 'mopo/utils/logging.py'))
-    bnn = _load('mopo.models.bnn', os.path.join(REF, 'mopo/models/bnn.py'))
+    from make_ref_vectors import load_reference as load_graph_code
+    refs = load_graph_code()                 # tfstub as ``tensorflow``; fc / utils / bnn / mopo
+    bnn = refs[2]
     fe = _load('mopo.models.fake_env', os.path.join(REF, 'mopo/models/fake_env.py'))
     static = {d: _load('ref_static_' + d, os.path.join(REF, 'mopo/static/%s.py' % d)).StaticFns
               for d in ('halfcheetah', 'walker2d', 'hopper')}
     _load('softlearning.replay_pools.replay_pool', os.path.join(REF, 'softlearning/replay_pools/replay_pool.py'))
     frp = _load('softlearning.replay_pools.flexible_replay_pool',
                 os.path.join(REF, 'softlearning/replay_pools/flexible_replay_pool.py'))
-    return bnn, fe, static, frp
+    return refs, bnn, fe, static, frp
 
 
 class _Model:
-    """Stand-in for the TF BNN: reference ``random_inds`` + restated ``predict``."""
+    """Stand-in for the TF BNN: reference ``random_inds`` + the reference graph's forward (f32)."""
 
-    def __init__(self, bnn_mod, params, E, elites):
-        self._p, self.num_nets, self._model_inds = params, E, list(elites)
+    def __init__(self, refs, bnn_mod, params, E, elites):
+        import torch
+        from make_ref_vectors import build_bnn
+        self._refs, self._p, self.num_nets, self._model_inds = refs, params, E, list(elites)
         self.random_inds = types.MethodType(bnn_mod.BNN.random_inds, self)
+        self._obj = build_bnn(refs, params, E, 17, 6, params['W'][1].shape[1], True, torch.float32)
+        self.last = None
 
     def predict(self, inputs, factored=True):
+        import torch
+        import tfstub
         assert factored
-        return obnn.forward(self._p, inputs)
+        x = tfstub.w(torch.as_tensor(np.asarray(inputs, np.float32)))       # the f32 placeholder feed
+        mean, var = self._refs[2].BNN._compile_outputs(self._obj, x)
+        self.last = (mean.detach().numpy().copy(), var.detach().numpy().copy())
+        return self.last
 
 
-def make_fakeenv_cases(bnn_mod, fe_mod, static):
+def make_fakeenv_cases(refs, bnn_mod, fe_mod, static):
     cases = []
     rs = np.random.RandomState(1234)
     cid = 0
@@ -122,7 +106,7 @@ def make_fakeenv_cases(bnn_mod, fe_mod, static):
                         act = rs.uniform(-1, 1, size=(B, A)).astype(np.float32)
                         coeff = 1.0 if cid % 2 == 0 else 5.0
                         seed = 1000 + cid
-                        model = _Model(bnn_mod, params, E, elites)
+                        model = _Model(refs, bnn_mod, params, E, elites)
                         env = fe_mod.FakeEnv(model, static[domain], penalty_coeff=coeff,
                                              penalty_learned_var=learned_var)
                         np.random.seed(seed)
@@ -142,6 +126,8 @@ def make_fakeenv_cases(bnn_mod, fe_mod, static):
                                     info_mean=info['mean'], info_std=info['std'],
                                     log_prob=info['log_prob'], dev=info['dev'],
                                     unpenalized=info['unpenalized_rewards'], penalty=info['penalty'])
+                        if B <= 64:
+                            case['ref_mean'], case['ref_var'] = model.last
                         cases.append(case)
                         cid += 1
     return cases
@@ -201,8 +187,8 @@ def make_pool_trace(frp):
 
 
 def main():
-    bnn_mod, fe_mod, static, frp = load_reference()
-    cases = make_fakeenv_cases(bnn_mod, fe_mod, static)
+    refs, bnn_mod, fe_mod, static, frp = load_reference()
+    cases = make_fakeenv_cases(refs, bnn_mod, fe_mod, static)
     for i, c in enumerate(cases):
         np.savez_compressed(os.path.join(HERE, 'fakeenv_%03d.npz' % i), **c)
     np.savez_compressed(os.path.join(HERE, 'termination.npz'), **make_termination_cases(static))
