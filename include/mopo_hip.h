@@ -42,7 +42,15 @@ typedef struct mopo_bnn_s* mopo_bnn_t;
 
 /* E members, obs_dim O, act_dim A, hidden H (4 swish layers), D = O+1 outputs.
  * smv=1: separate mean / var heads (bnn.py:656-675); smv=0: joint 2D head (bnn.py:644-655).
- * dtype: 0 = fp32 (exact-f32 MFMA), 1 = bf16 weights/activations with fp32 accumulate. */
+ * dtype: 0 = fp32 (exact-f32 MFMA 16x16x4);
+ *        1 = bf16 weights/activations, f32 accumulate (~8 significand bits; the C3 config);
+ *        2 = "bf16x3": every f32 operand split into 2 bf16 parts, 3 bf16 products per f32 product
+ *            (~17 significand bits), f32 accumulate;
+ *        3 = "bf16x6": 3 bf16 parts, 6 bf16 products per f32 product, f32 accumulate: f32-accurate
+ *            (held to the fp32 parity tolerances; the headline configuration).
+ * Limits: obs_dim + act_dim <= 32 (one or two 16-wide input k-groups); hidden 32, 64, 200 or 400 (any
+ * width with the same number of 16-wide blocks); the bf16 kinds need 2 (obs_dim + 1) <= 48 head
+ * slots; E <= 256. */
 int mopo_bnn_create(mopo_bnn_t* out, int E, int obs_dim, int act_dim, int hidden, int smv, int dtype);
 int mopo_bnn_destroy(mopo_bnn_t h);
 /* The reference .mat layout, keys '0'..'15' (bnn.py:224-225, 588-592): mu[1,IN], sigma[1,IN],
@@ -194,6 +202,13 @@ typedef struct {
   const int32_t* d_model_inds; /* [horizon, B] member per row */
   /* outputs */
   int64_t* d_steps;         /* [horizon] rows added per step (mopo.py:748) */
+  /* FakeEnv / rollout modes (fake_env.py:37-131, mopo.py:734-738) */
+  int penalty_learned_var;  /* 1: max_e ||std_e|| over all D dims (every D4RL config, fake_env.py:110)
+                               0: max_e ||mean_e - mean over members|| over the obs dims (fake_env.py:98-108) */
+  int deterministic;        /* 1: no sampling; next state = mean over ALL members of the means (fake_env.py:69-70,
+                               84-86); the selection streams are unused */
+  int rollout_random;       /* 1: actions ~ U(-1, 1) instead of the policy's (mopo.py:736-738) */
+  const float* d_act_uniform; /* parity mode with rollout_random: [horizon, B, A] injected uniforms, or NULL */
 } mopo_rollout_args;
 
 int mopo_rollout_create(mopo_rollout_t* out, mopo_bnn_t bnn, int64_t max_batch, int max_horizon);

@@ -35,7 +35,8 @@ class RolloutArgs(C.Structure):
                 ('n_elites', c_int), ('B', c_i64), ('horizon', c_int), ('penalty_coeff', c_float),
                 ('term_kind', c_int), ('seed', c_u64), ('epoch', c_u32), ('uid_offset', c_i64),
                 ('d_eps_act', c_void_p), ('d_eps_obs', c_void_p), ('d_model_inds', c_void_p),
-                ('d_steps', c_void_p)]
+                ('d_steps', c_void_p), ('penalty_learned_var', c_int), ('deterministic', c_int),
+                ('rollout_random', c_int), ('d_act_uniform', c_void_p)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/mopo_hip.h

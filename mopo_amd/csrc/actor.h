@@ -26,6 +26,9 @@ struct ActorArgs {
   // rollout: the ensemble's scaled input row (utils.py:96) [B][32] in slot_feat(., xs_in) order,
   // (concat(obs, act) - mu) / sigma, so the ensemble reads 128 contiguous bytes per row and member
   float* xs; const float* xs_mu; const float* xs_sigma; int xs_in;
+  // rollout_random (mopo.py:736-738): the actions are U(-1, 1) draws -- injected act_uni [B, A] or
+  // Philox -- and replace the policy's (still computed, as the reference calls get_action_meta first)
+  int rand_act; const float* act_uni;
 };
 
 int launch_actor(const ActorArgs& a, hipStream_t s);

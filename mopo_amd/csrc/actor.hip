@@ -186,12 +186,26 @@ __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? 4 : 2) void actor_kerne
     }
     int64_t pos = -1;
     if (a.pool_act) pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool_state[0] + a.pool_off + row) % a.pool_max;
+    float uni[16];
+    if (a.rand_act) {  // np.random.uniform(low=-1, high=1, size=act.shape) (mopo.py:738)
+      if (a.act_uni) {
+        for (int j = 0; j < A; ++j) uni[j] = a.act_uni[row * A + j];
+      } else {
+        for (int blk = 0; blk * 4 < A; ++blk) {
+          u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32) ^ ((uint32_t)blk << 20), a.step, RNG_ACT_UNIFORM};
+          const u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+          const uint32_t ws[4] = {r.x, r.y, r.z, r.w};
+          for (int i = 0; i < 4 && blk * 4 + i < A; ++i)
+            uni[blk * 4 + i] = -1.0f + 2.0f * ((float)(ws[i] >> 8) * 5.9604645e-8f);  // [-1, 1), 24-bit uniform
+        }
+      }
+    }
     for (int j = 0; j < A; ++j) {
       const float mu = head[wv][m][j];
       const float ls = fminf(fmaxf(head[wv][m][A + j], -20.f), 2.f);  // mopo.py:304
       const float sd = expf(ls);                                      // mopo.py:305
       const float u = mu + z[j] * sd;                                 // mopo.py:306
-      const float act = tanhf(u);                                     // mopo.py:295
+      const float act = a.rand_act ? uni[j] : tanhf(u);               // mopo.py:295 / 738
       head[wv][m][16 + j] = act;
       if (a.act) a.act[row * A + j] = act;
       if (a.mu) a.mu[row * A + j] = tanhf(mu);                        // mopo.py:294

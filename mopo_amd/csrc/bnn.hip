@@ -149,14 +149,16 @@ __device__ __forceinline__ void head_epilogue(const BnnDev& w, const FwdArgs& a,
           const float sd = __builtin_amdgcn_exp2f(0.5f * l2);   // sqrt(exp(lv)), fake_env.py:67
           if (valid) ss += sd * sd;
           if (selected && valid) a.std_sel[row * D + d] = sd;
+          if (a.std_all && ok && valid) a.std_all[((int64_t)e * a.all_stride + row) * D + d] = sd;
         }
       } else if (j < 2 * Q) {
         const int d = g + 4 * (j - Q);
         if (d < D) {
           if (MODE == FWD_PREDICT) {
             if (ok) a.mean[((int64_t)e * a.B + row) * D + d] = v;
-          } else if (selected) {
-            a.mean_sel[row * D + d] = v;
+          } else {
+            if (selected) a.mean_sel[row * D + d] = v;
+            if (a.mean_all && ok) a.mean_all[((int64_t)e * a.all_stride + row) * D + d] = v;
           }
         }
       }
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int64_t row = row0 + r * 16 + m;
-    sel_e[r] = (MODE == FWD_ROLLOUT && row < count) ? a.sel[row] : -1;
+    sel_e[r] = (MODE == FWD_ROLLOUT && a.sel && row < count) ? a.sel[row] : -1;
   }
 
   // ---- layer-0 input: scaler transform (utils.py:96), f64 inputs cast to f32 as TF's feed does
@@ -403,7 +405,7 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
       layer_lds_split<KG, NBO, WAVES, SLOT, P, PS>(w.whdb + (int64_t)e * KG * P * NBO * 256, hin, hd, lds, wv, lane);
   }
   head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
-                           (MODE == FWD_ROLLOUT && ok) ? a.sel[row] : -1);
+                           (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
 }
 
 #ifndef BNN_R13

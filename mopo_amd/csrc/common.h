@@ -94,7 +94,7 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, fl
 }
 
 // stream ids for the Philox counter (counter = {row_uid, step, stream, block})
-enum : uint32_t { RNG_START = 1, RNG_ACT = 2, RNG_OBS_NOISE = 3, RNG_MODEL = 4, RNG_SAC = 5 };
+enum : uint32_t { RNG_START = 1, RNG_ACT = 2, RNG_OBS_NOISE = 3, RNG_MODEL = 4, RNG_SAC = 5, RNG_ACT_UNIFORM = 6 };
 
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 

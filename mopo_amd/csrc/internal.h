@@ -70,6 +70,11 @@ struct FwdArgs {
   const int32_t* sel;     // [B] selected member per row
   float* mean_sel;        // [B][D]
   float* std_sel;         // [B][D]
+  // rollout, optional: every member's mean / std (mean-distance penalty and deterministic mode,
+  // fake_env.py:84-86, 98-108): [E][all_stride][D], row r of this launch at all_stride rows apart
+  float* mean_all;
+  float* std_all;
+  int64_t all_stride;
 };
 
 int launch_bnn_fwd(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s);

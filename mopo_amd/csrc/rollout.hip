@@ -37,6 +37,7 @@ struct Rollout {
   float* xs;        // [B][32] the ensemble's scaled input rows (written by the actor)
   float* mean_sel;
   float* std_sel;
+  float* mean_all = nullptr;  // [E][Bmax][D], allocated on first use (mean-distance penalty / deterministic)
   uint8_t* keep;
   int* blockcnt;
   int* cnt;  // [0] live rows this step, [1] survivors, [2 + k] rows of part k (split rollout)
@@ -109,6 +110,12 @@ struct PostArgs {
   mopo_pool_desc pool;
   int64_t stage_base;       // >= 0: staged layout
   int64_t pool_off;         // pool layout: rows go to (state[0] + pool_off + row) % max_size
+  // every member's mean [E][all_stride][D] (the ensemble's mean_all), for the mean-distance penalty
+  // (pen_dist, fake_env.py:98-108) and deterministic steps (det, fake_env.py:69-70, 84-86)
+  const float* mean_all;
+  int E;
+  int64_t all_stride;
+  int pen_dist, det;
 };
 
 // FakeEnv post-processing of one horizon step (fake_env.py:66-115) for POST_RPB rows per block, one
@@ -128,9 +135,35 @@ __global__ __launch_bounds__(256) void rollout_post_kernel(const PostArgs a) {
   const bool live = row < count;
   const bool on = live && sub < D;
   double s = 0.0;
-  if (on) {
+  // member e's mean of this lane's dim after the residual add, in f32 as the reference's in-place
+  // ensemble_model_means[:, :, 1:] += obs (fake_env.py:66)
+  const double ob = on && sub >= 1 ? a.obs[row * O + sub - 1] : 0.0;
+  auto member_mean = [&](int e) {
+    const float m = a.mean_all[((int64_t)e * a.all_stride + row) * D + sub];
+    return sub >= 1 ? (float)((double)m + ob) : m;
+  };
+  float pen_d = 0.f;
+  if (a.pen_dist) {  // max_e || mean_e - mean_e' mean_e' || over the obs dims (fake_env.py:98-108)
+    float sum = 0.f;
+    if (on && sub >= 1)
+      for (int e = 0; e < a.E; ++e) sum += member_mean(e);
+    const float avg = sum / (float)a.E;                           // np.mean(axis=0), f32
+    for (int e = 0; e < a.E; ++e) {
+      const float dd = on && sub >= 1 ? member_mean(e) - avg : 0.f;
+      float q = dd * dd;
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) q += __shfl_xor(q, o);       // the row's 32-lane group
+      pen_d = fmaxf(pen_d, sqrtf(q));
+    }
+  }
+  if (on && a.det) {  // samples = mean over ALL members of the means (fake_env.py:69-70, 84-86)
+    float acc = 0.f;
+    for (int e = 0; e < a.E; ++e) acc += member_mean(e);
+    s = (double)(acc / (float)a.E);
+    srow[rl][sub] = s;
+  } else if (on) {
     float m = a.mean_sel[row * D + sub];
-    if (sub >= 1) m = (float)((double)m + a.obs[row * O + sub - 1]);  // fake_env.py:66
+    if (sub >= 1) m = (float)((double)m + ob);                      // fake_env.py:66
     double e;
     if (a.eps) {
       e = a.eps[row * D + sub];
@@ -157,7 +190,8 @@ __global__ __launch_bounds__(256) void rollout_post_kernel(const PostArgs a) {
     bool keep = false;
     if (live) {
       const bool term = term_fn(a.term_kind, &srow[rl][1], O);     // fake_env.py:91
-      const double pr = a.coeff != 0.f ? s - (double)a.coeff * (double)__uint_as_float(a.pen[row]) : s;
+      const float pen = a.pen_dist ? pen_d : __uint_as_float(a.pen[row]);
+      const double pr = a.coeff != 0.f ? s - (double)a.coeff * (double)pen : s;   // fake_env.py:115
       a.pool.d_rew[pos] = (float)pr;                               // rewards = samples[:, :1] - c * penalty
       a.pool.d_term[pos] = term ? 1 : 0;
       keep = !term;
@@ -299,6 +333,14 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     KTimer t(h, KC_START, s);
     if (pack_actor(a->d_pi_params, O, A, a->pi_hidden, h->wpk, s)) return -1;
   }
+  // every member's mean per row is needed by the mean-distance penalty and by deterministic steps
+  const bool det = a->deterministic != 0;
+  const bool pen_dist = a->penalty_learned_var == 0 && a->penalty_coeff != 0.f;
+  const bool need_all = det || pen_dist;
+  if (need_all && !h->mean_all)
+    MOPO_HIP(hipMalloc(&h->mean_all, (size_t)bnn->E * h->Bmax * D * sizeof(float)));
+  MOPO_REQUIRE(!a->rollout_random || a->d_act_uniform || !a->d_eps_act,
+               "rollout: parity mode with rollout_random needs the injected uniforms (d_act_uniform)");
   int oc = h->oc, uc = h->uc;
   // one horizon step for rows [off, off + n) of the batch (live count in *cnt) on stream ss
   auto step_rows = [&](int i, int64_t off, int64_t n, int* cnt, hipStream_t ss, hipEvent_t after_actor) -> int {
@@ -313,8 +355,10 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     aa.stage_base = staged ? (int64_t)(i - i0) * B + off : -1;
     aa.pool_off = batched_advance ? (int64_t)(i - i0) * B + off : 0;
     aa.pen_zero = h->pen + off;
-    aa.sel_out = h->sel + off;
+    aa.sel_out = det ? nullptr : h->sel + off;
     aa.sel_in = a->d_model_inds ? a->d_model_inds + (int64_t)i * B + off : nullptr;
+    aa.rand_act = a->rollout_random;
+    aa.act_uni = a->d_act_uniform ? a->d_act_uniform + ((int64_t)i * B + off) * A : nullptr;
     aa.elites = a->d_elites; aa.n_elites = a->n_elites;
     aa.xs = h->xs + off * XS_STRIDE; aa.xs_mu = bnn->dev.mu; aa.xs_sigma = bnn->dev.sigma; aa.xs_in = bnn->dev.IN;
     {
@@ -326,8 +370,10 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     FwdArgs f{};
     f.in = FwdIn{h->obs[oc] + off * O, 1, O, h->act + off * A, 0, A};
     f.B = n; f.d_count = cnt; f.xs = h->xs + off * XS_STRIDE;
-    f.pen_bits = h->pen + off; f.sel = h->sel + off; f.mean_sel = h->mean_sel + off * D;
+    f.pen_bits = h->pen + off; f.sel = det ? nullptr : h->sel + off; f.mean_sel = h->mean_sel + off * D;
     f.std_sel = h->std_sel + off * D;
+    f.mean_all = need_all ? h->mean_all + off * D : nullptr;
+    f.all_stride = h->Bmax;
     {
       KTimer t(h, KC_BNN, ss);
       if (launch_bnn_fwd(bnn, FWD_ROLLOUT, f, ss)) return -1;
@@ -342,6 +388,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     pa.blockcnt = compact ? h->blockcnt : nullptr;
     pa.pool = *p; pa.stage_base = staged ? (int64_t)(i - i0) * B + off : -1;
     pa.pool_off = batched_advance ? (int64_t)(i - i0) * B + off : 0;
+    pa.mean_all = f.mean_all; pa.E = bnn->E; pa.all_stride = h->Bmax; pa.pen_dist = pen_dist; pa.det = det;
     {
       KTimer t(h, KC_POST, ss);
       // with compaction the post kernel adds each block's kept rows into its PB-row chunk count
@@ -474,6 +521,7 @@ extern "C" int mopo_rollout_destroy(mopo_rollout_t hh) {
   }
   if (h->mem) (void)hipFree(h->mem);
   if (h->wpk) (void)hipFree(h->wpk);
+  if (h->mean_all) (void)hipFree(h->mean_all);
   delete h;
   return 0;
 }

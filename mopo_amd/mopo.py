@@ -32,7 +32,7 @@ class MOPO:
                  hidden_dim=200, separate_mean_var=False, penalty_coeff=0., penalty_learned_var=False,
                  model_name=None, model_load_dir=None, deterministic=False, network_kwargs=None, epoch_length=1000,
                  n_epochs=1000, n_train_repeat=1, batch_size=256, seed=88, reparameterize=True, max_model_t=None,
-                 **kwargs):
+                 rollout_random=False, **kwargs):
         if target_update_interval != 1:
             raise NotImplementedError('target_update_interval != 1 (all D4RL configs use 1)')
         self._pool = pool                                   # device SimpleReplayPool of env data
@@ -49,6 +49,7 @@ class MOPO:
         self._model_train_freq = model_train_freq
         self._rollout_batch_size = int(rollout_batch_size)
         self._deterministic = deterministic
+        self._rollout_random = rollout_random
         self._real_ratio = real_ratio
         self._epoch_length, self._n_epochs, self._n_train_repeat = epoch_length, n_epochs, n_train_repeat
         self._epoch = 0
@@ -105,8 +106,8 @@ class MOPO:
                                                 L.ptr(y), None))
         return self._model.train(x, y, permuted=True, **kwargs)
 
-    # -- mopo.py:723-765 (device-resident, perf-mode RNG)
-    def _rollout_model(self, rollout_batch_size, **kwargs):
+    # -- mopo.py:723-765 (device-resident, perf-mode RNG); ``deterministic`` as mopo.py:558-559 passes it
+    def _rollout_model(self, rollout_batch_size, deterministic=None, **kwargs):
         if self._rollout is None or self._rollout.max_batch < rollout_batch_size or \
                 self._rollout.max_horizon < self._rollout_length:
             self._rollout = ModelRollout(self._model, rollout_batch_size, max(self._rollout_length, 1))
@@ -114,7 +115,9 @@ class MOPO:
         steps = self._rollout.run(env_obs, self._sac.policy_params_ptr, self._model_pool, rollout_batch_size,
                                   self._rollout_length, self.fake_env.term_kind, self.fake_env.penalty_coeff,
                                   self._model._model_inds, seed=self._seed, epoch=self._epoch,
-                                  pi_hidden=self._pi_hidden)
+                                  pi_hidden=self._pi_hidden, penalty_learned_var=self.fake_env.penalty_learned_var,
+                                  deterministic=self._deterministic if deterministic is None else deterministic,
+                                  rollout_random=self._rollout_random)
         added = int(steps.sum().item())
         return {'mean_rollout_length': added / rollout_batch_size}
 

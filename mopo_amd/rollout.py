@@ -65,9 +65,13 @@ class ModelRollout:
 
     def run(self, env_obs, pi_params, pool, batch_size, horizon, term_kind, penalty_coeff, elites,
             seed=0, epoch=0, pi_hidden=256, start_idx=None, eps_act=None, eps_obs=None, model_inds=None,
-            staged=False, uid_offset=0, stream=None, step_desc=None, step_hook=None):
+            staged=False, uid_offset=0, stream=None, step_desc=None, step_hook=None, penalty_learned_var=True,
+            deterministic=False, rollout_random=False, act_uniform=None):
         """Returns the device int64[horizon] tensor of rows added per step (steps_added).
-        ``step_desc(i)`` / ``step_hook(i, steps)``: per-step staging (see mopo_rollout_run_staged_steps)."""
+        ``step_desc(i)`` / ``step_hook(i, steps)``: per-step staging (see mopo_rollout_run_staged_steps).
+        ``penalty_learned_var`` / ``deterministic``: FakeEnv's modes (fake_env.py:69-110; every D4RL
+        config uses the learned-var penalty, not deterministic); ``rollout_random``: uniform actions
+        (mopo.py:736-738), ``act_uniform`` [horizon, B, A] injects them in parity mode."""
         import torch
         dev = env_obs.device
         B = int(batch_size)
@@ -88,7 +92,9 @@ class ModelRollout:
             B=B, horizon=int(horizon), penalty_coeff=float(penalty_coeff), term_kind=int(term_kind),
             seed=int(seed) & (2 ** 64 - 1), epoch=int(epoch), uid_offset=int(uid_offset),
             d_eps_act=dptr(eps_act, torch.float32), d_eps_obs=dptr(eps_obs, torch.float64),
-            d_model_inds=dptr(model_inds, torch.int32), d_steps=L.ptr(steps))
+            d_model_inds=dptr(model_inds, torch.int32), d_steps=L.ptr(steps),
+            penalty_learned_var=int(bool(penalty_learned_var)), deterministic=int(bool(deterministic)),
+            rollout_random=int(bool(rollout_random)), d_act_uniform=dptr(act_uniform, torch.float32))
         if step_hook is not None:
             # one call per horizon step into the staging block step_hook(i) names; step_hook(i, steps)
             # is then called after step i is enqueued (multi-GPU: gather step i while i + 1 computes)

@@ -41,8 +41,6 @@ def test_bnn_predict_vs_reference_graph(path, dtype):
     from mopo_amd.bnn import BNN
     z = dict(np.load(path))
     E, H, smv = int(z['E']), int(z['H']), bool(z['smv'])
-    if dtype != 'fp32' and not smv:
-        pytest.skip('the bf16 kernels implement the smv head only (every D4RL config, base_mopo.py:5-8)')
     p = ref_bnn_params(z)
     m = BNN({'name': 'ref', 'num_networks': E, 'num_elites': min(5, E), 'separate_mean_var': smv, 'obs_dim': 17,
              'act_dim': 6, 'hidden_dim': H, 'dtype': dtype}).set_params(obnn.to_mat_list(p))

@@ -148,9 +148,12 @@ def test_pool_vs_reference_trace():
     torch.cuda.synchronize()
 
 
-def _rollout_case(domain, E, H, B, horizon, seed, coeff=1.0, O=17, A=6, height=None):
+def _rollout_case(domain, E, H, B, horizon, seed, coeff=1.0, O=17, A=6, height=None, learned_var=True, det=False,
+                  rand_act=False):
     """Oracle rollout with every random stream drawn in the reference order; returns inputs,
-    injected streams and the oracle pool.  ``height``: fixed walker height (50: every row done)."""
+    injected streams and the oracle pool.  ``height``: fixed walker height (50: every row done).
+    ``learned_var`` / ``det``: FakeEnv's penalty and deterministic modes (fake_env.py:69-110);
+    ``rand_act``: rollout_random (mopo.py:736-738: uniform actions drawn after get_action_meta)."""
     rs = np.random.RandomState(seed)
     env_n = 3000
     env_obs = rs.normal(size=(env_n, O)).astype(np.float32)
@@ -175,19 +178,27 @@ def _rollout_case(domain, E, H, B, horizon, seed, coeff=1.0, O=17, A=6, height=N
     eps_act = np.zeros((horizon, B, A), np.float32)
     eps_obs = np.zeros((horizon, B, O + 1))
     inds_all = np.zeros((horizon, B), np.int32)
+    act_uni = np.zeros((horizon, B, A), np.float32)
     steps = []
     for i in range(horizon):
         Bi = len(obs)
         ea = act_rs.normal(size=(Bi, A)).astype(np.float32)
         act, _ = osac.actor_act(P, obs.astype(np.float32).astype(np.float64), ea.astype(np.float64))
         act = act.astype(np.float32)
-        noise = np.random.normal(size=(E, Bi, O + 1))
-        inds = np.random.choice(elites, size=Bi)
-        nobs, rew, term, info = ofe.step(p, elites, obs, act, ofe.TERMINATION[domain], penalty_coeff=coeff,
-                                         penalty_learned_var=True, noise=noise, model_inds=inds)
+        if rand_act:
+            act = np.random.uniform(low=-1, high=1, size=act.shape).astype(np.float32)    # mopo.py:738
+            act_uni[i, :Bi] = act
+        if det:
+            nobs, rew, term, info = ofe.step(p, elites, obs, act, ofe.TERMINATION[domain], penalty_coeff=coeff,
+                                             penalty_learned_var=learned_var, deterministic=True)
+        else:
+            noise = np.random.normal(size=(E, Bi, O + 1))
+            inds = np.random.choice(elites, size=Bi)
+            nobs, rew, term, info = ofe.step(p, elites, obs, act, ofe.TERMINATION[domain], penalty_coeff=coeff,
+                                             penalty_learned_var=learned_var, noise=noise, model_inds=inds)
+            eps_obs[i, :Bi] = noise[inds, np.arange(Bi)]
+            inds_all[i, :Bi] = inds
         eps_act[i, :Bi] = ea
-        eps_obs[i, :Bi] = noise[inds, np.arange(Bi)]
-        inds_all[i, :Bi] = inds
         steps.append(Bi)
         model_pool.add_samples({'observations': obs, 'actions': act, 'next_observations': nobs,
                                 'rewards': rew, 'terminals': term})
@@ -196,7 +207,8 @@ def _rollout_case(domain, E, H, B, horizon, seed, coeff=1.0, O=17, A=6, height=N
             break
         obs = nobs[nt]
     return dict(env_obs=env_obs, mats=mats, flat=flat, elites=elites, start=start, eps_act=eps_act,
-                eps_obs=eps_obs, inds=inds_all, steps=steps, pool=model_pool, coeff=coeff)
+                eps_obs=eps_obs, inds=inds_all, steps=steps, pool=model_pool, coeff=coeff, act_uni=act_uni,
+                learned_var=learned_var, det=det, rand_act=rand_act)
 
 
 @pytest.mark.parametrize('domain,E,H,B,horizon,dtype', [
@@ -237,6 +249,60 @@ def test_fused_rollout_parity(domain, E, H, B, horizon, dtype):
     close(got['actions'], ref['actions'], 5e-5)
     close(got['next_observations'], ref['next_observations'], 5e-5)
     close(got['rewards'], ref['rewards'], 5e-5)
+
+
+@pytest.mark.parametrize('domain,E,H,B,horizon,dtype,learned_var,det,rand_act', [
+    ('walker2d', 7, 200, 777, 5, 'fp32', False, False, False),     # mean-distance penalty (fake_env.py:98-108)
+    ('halfcheetah', 7, 200, 5000, 3, 'bf16x6', False, False, False),  # ... through the split rollout
+    ('hopper', 7, 64, 300, 4, 'fp32', True, True, False),           # deterministic (fake_env.py:69-70, 84-86)
+    ('walker2d', 7, 200, 777, 4, 'bf16x6', False, True, False),     # deterministic + mean-distance
+    ('halfcheetah', 7, 200, 1000, 3, 'fp32', True, False, True),    # rollout_random (mopo.py:736-738)
+    ('walker2d', 32, 32, 300, 3, 'fp32', False, False, True)])
+def test_fused_rollout_modes_parity(domain, E, H, B, horizon, dtype, learned_var, det, rand_act):
+    """The fused rollout's FakeEnv modes vs the oracle (which follows the reference FakeEnv.step,
+    pinned by the golden fixtures covering both penalty modes and deterministic)."""
+    import torch
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout
+    from mopo_amd.static import static_fns
+    c = _rollout_case(domain, E, H, B, horizon, seed=13, coeff=2.0, learned_var=learned_var, det=det,
+                      rand_act=rand_act)
+    model = make_model(c['mats'], E, H, dtype=dtype)
+    dev = torch.device('cuda')
+    pool = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=B * horizon + 7)
+    ro = ModelRollout(model, B, horizon)
+    steps = ro.run(torch.from_numpy(c['env_obs']).to(dev), torch.from_numpy(c['flat']).to(dev), pool, B, horizon,
+                   static_fns[domain].term_kind, c['coeff'], c['elites'], start_idx=c['start'], eps_act=c['eps_act'],
+                   eps_obs=c['eps_obs'], model_inds=c['inds'], penalty_learned_var=learned_var, deterministic=det,
+                   rollout_random=rand_act, act_uniform=c['act_uni'] if rand_act else None)
+    exp = np.zeros(horizon, np.int64)
+    exp[:len(c['steps'])] = c['steps']
+    np.testing.assert_array_equal(steps.cpu().numpy(), exp)
+    op = c['pool']
+    assert pool.size == op.size and pool._pointer == op._pointer
+    got, ref = pool.return_all_samples(as_numpy=True), op.return_all_samples()
+    np.testing.assert_array_equal(got['terminals'], ref['terminals'])
+    for k in ('observations', 'actions', 'next_observations', 'rewards'):
+        close(got[k], ref[k], 5e-5)
+
+
+def test_fused_rollout_random_actions_perf_mode():
+    """rollout_random with Philox uniforms: actions in [-1, 1), roughly uniform, deterministic per seed."""
+    import torch
+    from mopo_amd.bnn import construct_model
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout, init_sac_params
+    dev = torch.device('cuda')
+    model = construct_model(obs_dim=17, act_dim=6, hidden_dim=200, num_networks=7, num_elites=5,
+                            separate_mean_var=True, seed=0)
+    B, h = 4000, 2
+    pool = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=B * h)
+    ro = ModelRollout(model, B, h)
+    env = torch.randn(10000, 17, device=dev)
+    pi = torch.from_numpy(init_sac_params(17, 6)).to(dev)
+    ro.run(env, pi, pool, B, h, 0, 1.0, [0, 1, 2, 3, 4], seed=3, rollout_random=True)
+    a = pool.return_all_samples(as_numpy=True)['actions']
+    assert a.min() >= -1 and a.max() < 1 and abs(a.mean()) < 0.02 and abs(a.std() - 1 / np.sqrt(3)) < 0.01
 
 
 def test_fused_rollout_perf_mode_runs():
