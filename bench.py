@@ -31,12 +31,14 @@ FLOP_ACTOR_ROW = 2 * (O * HP + HP * HP + HP * 2 * A)                      # 145,
 PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01_v11_pmc_summary.json')
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
 # ensemble dtype -> (bf16 parts per operand, bf16 products per f32 product); fp32 runs f32 MFMA
-SPLIT = {'bf16': (1, 1), 'bf16x3': (2, 3), 'bf16x6': (3, 6)}
+SPLIT = {'bf16': (1, 1), 'bf16x3': (2, 3), 'bf16x6': (3, 6), 'f16x3': (2, 3)}
 DTYPE_DESC = {'fp32': 'fp32 (f32 MFMA 16x16x4)',
               'bf16x6': 'f32 (f32 operands split into 3 bf16 parts, 6 bf16 MFMA products, f32 accumulate: '
                         'f32-accurate, held to the fp32 parity tolerances)',
               'bf16x3': 'f32 operands as 2 bf16 parts (3 bf16 MFMA products, ~17 significand bits, f32 accumulate)',
-              'bf16': 'bf16 (f32 accumulate)'}
+              'bf16': 'bf16 (f32 accumulate)',
+              'f16x3': 'f32 (f32 operands as 2 fp16 parts under power-of-two scales, 3 f16 MFMA products, f32 '
+                       'accumulate: ~22-bit operands like bf16x6, held to the fp32 parity tolerances)'}
 
 
 def parse():
@@ -53,7 +55,7 @@ def parse():
     p.add_argument('--no-c3', action='store_true', help='skip the secondary C3 (bf16 walker2d) line')
     p.add_argument('--train-epochs', type=int, default=2, help='timed BNN.train epochs (0: skip)')
     p.add_argument('--cpu-train-steps', type=int, default=10)
-    p.add_argument('--ensemble-dtype', default='bf16x6', choices=['fp32', 'bf16x6', 'bf16x3', 'bf16'],
+    p.add_argument('--ensemble-dtype', default='f16x3', choices=['fp32', 'bf16x6', 'f16x3', 'bf16x3', 'bf16'],
                    help='headline ensemble-forward arithmetic (mopo_amd.bnn._DTYPES); bf16x6 = f32 operands '
                         'as 3 bf16 parts, f32-accurate (held to the fp32 parity tolerances)')
     p.add_argument('--no-alt-dtypes', action='store_true',
@@ -182,11 +184,15 @@ def roofline_of(dtype, rows, ms):
                 'achieved': alg, 'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': alg / MFMA_F32_PEAK_TFLOPS,
                 'flop_per_launch': rows * FLOP_BNN_ROW, 'avg_launch_ms': ms}
     parts, prods = SPLIT[dtype]
-    return {'bound': 'mfma', 'kernel': 'bnn_fwd_bf16_kernel<P=%d> (ensemble forward, bf16 MFMA 16x16x32, %d '
-                                       'products per f32 product)' % (parts, prods),
+    if dtype == 'f16x3':
+        kern = 'bnn_fwd_f16s_kernel (ensemble forward, f16 MFMA 16x16x32, 3 products per f32 product)'
+    else:
+        kern = 'bnn_fwd_bf16_kernel<P=%d> (ensemble forward, bf16 MFMA 16x16x32, %d products per f32 product)' % (
+            parts, prods)
+    return {'bound': 'mfma', 'kernel': kern,
             'achieved': alg * prods, 'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-            'frac': alg * prods / BF16_PEAK_TFLOPS, 'achieved_note': 'executed bf16 MFMA TFLOP/s = %d x the '
-            'algorithmic f32 rate' % prods, 'algorithmic_f32_tflops': alg,
+            'frac': alg * prods / BF16_PEAK_TFLOPS, 'achieved_note': 'executed 16-bit MFMA TFLOP/s = %d x the '
+            'algorithmic f32 rate (bf16 and f16 share the 2.5 PF dense peak)' % prods, 'algorithmic_f32_tflops': alg,
             'flop_per_launch': rows * FLOP_BNN_ROW, 'bf16_flop_per_launch': prods * rows * FLOP_BNN_ROW,
             'avg_launch_ms': ms}
 
@@ -451,7 +457,7 @@ def main():
     tr = train_leg(args, env) if (rank == 0 and world == 1 and args.train_epochs > 0) else None
     alts = {}
     if rank == 0 and world == 1 and not args.no_alt_dtypes:
-        for dt_alt in ('fp32', 'bf16x6', 'bf16x3'):
+        for dt_alt in ('fp32', 'bf16x6', 'f16x3', 'bf16x3'):
             if dt_alt != args.ensemble_dtype:
                 alts[dt_alt] = alt_headline_leg(args, dev, dt_alt)
     if rank != 0:

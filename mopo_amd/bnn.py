@@ -23,8 +23,9 @@ from . import _lib as L
 
 # ensemble-forward arithmetic (mopo_bnn_create dtype): 'fp32' f32 MFMA; 'bf16' bf16 operands;
 # 'bf16x3' / 'bf16x6' f32 operands split into 2 / 3 bf16 parts (3 / 6 bf16 MFMAs per product,
-# f32 accumulate; bf16x6 is f32-accurate, bf16x3 keeps ~17 significand bits).
-_DTYPES = {'fp32': 0, 'bf16': 1, 'bf16x3': 2, 'bf16x6': 3}
+# f32 accumulate; bf16x6 ~22-bit operands, bf16x3 ~17 significand bits); 'f16x3' f32 operands as
+# 2 fp16 parts under power-of-two scales (3 f16 MFMAs per product, ~22-bit operands like bf16x6).
+_DTYPES = {'fp32': 0, 'bf16': 1, 'bf16x3': 2, 'bf16x6': 3, 'f16x3': 4}
 
 N_HIDDEN = 4
 

@@ -21,6 +21,7 @@
 
 #include <vector>
 #include <cstring>
+#include <cmath>
 
 namespace mopo {
 
@@ -71,6 +72,30 @@ __global__ void pack_frags_bf16_kernel(const float* __restrict__ src, short* __r
     for (int q = 1; q < P; ++q)
       if (q == p) v = parts[q];
     dst[i] = v;
+  }
+}
+
+// f16x3 fragments: the bf16 fragment layout with P = 2 fp16 parts of W * 2^k_e (split_f16_scaled);
+// scale[e] = 2^k_e puts member e's max |W| of this layer in [2^14, 2^15)
+__global__ void pack_frags_f16s_kernel(const float* __restrict__ src, short* __restrict__ dst, int E, int K, int N,
+                                       int KG, int NB, int perm_k, int perm_n, const float* __restrict__ scale) {
+  constexpr int P = 2;
+  int64_t total = (int64_t)E * KG * P * NB * 512;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int j = i & 7, lane = (i >> 3) & 63;
+    int64_t f = i >> 9;
+    int nb = f % NB;
+    int p = (f / NB) % P;
+    int kg = (f / ((int64_t)NB * P)) % KG;
+    int e = f / ((int64_t)NB * P * KG);
+    int k = kg * 32 + bf16_kperm(lane >> 4, j), n = nb * 16 + (lane & 15);
+    if (perm_k) k = slot_feat(k, K);
+    if (perm_n == 1) n = slot_feat(n, N);
+    else if (perm_n == 2) n = head_col(n, N / 2);
+    const F16Parts q = split_f16_scaled((k >= 0 && n >= 0 && k < K && n < N) ? src[((int64_t)e * K + k) * N + n] : 0.f,
+                                        scale[e]);
+    dst[i] = p == 0 ? q.hi : q.lo;
   }
 }
 
@@ -408,6 +433,108 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
                            (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
 }
 
+// ---- f16x3 forward: f32 operands as 2 fp16 parts under power-of-two scales (mlp_tile.h
+// split_f16_scaled / row_scale), 3 products per k-group on v_mfma_f32_16x16x32_f16, f32 accumulate and
+// f32 epilogues.  Each layer's output is acc * (2^-k_w / s_row): the weight scale of the layer and
+// member, the row scale of the layer's input (both exact powers of two), folded into the bias add.
+template <int NB2, int NBO, int MODE, int WAVES, int PS = 1>
+__global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_SPLIT_MINB * 4 / WAVES) void bnn_fwd_f16s_kernel(
+    const BnnDev w, const FwdArgs a) {
+  constexpr int P = 2, KG = NB2 / 2;
+  constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
+  constexpr int SLOT = Stage<PS * NBMAX, WAVES>::SLOTS * 256;
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
+  const int groups = ceil_div(a.ntiles, WAVES);
+  const int e = blockIdx.x / groups, grp = blockIdx.x % groups;
+  const int64_t row = (int64_t)(grp * WAVES + wv) * 16 + m;
+  if ((int64_t)grp * WAVES * 16 >= count) return;
+  const int IN = w.IN, O = w.O, E = w.E;
+  const bool ok = row < count;
+  // the row's max |v| over the lane group's 8-per-k-group values -> the 4 lanes of row m (g = 0..3)
+  auto row_max = [&](float mx) {
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    return fmaxf(mx, __shfl_xor(mx, 32));
+  };
+
+  float xv[8];
+  if (a.xs) {  // rollout: the actor already wrote the scaled row in slot order (bf16_kperm)
+    const f32x4 lo = ok ? ld4(a.xs + row * XS_STRIDE + 4 * g) : zero4();
+    const f32x4 hi = ok ? ld4(a.xs + row * XS_STRIDE + 16 + 4 * g) : zero4();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      xv[t] = lo[t];
+      xv[4 + t] = hi[t];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = slot_feat(bf16_kperm(g, j), IN);
+      float v = 0.f;
+      if (ok && k >= 0) {
+        float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
+                          : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
+        v = (raw - w.mu[k]) / w.sigma[k];
+      }
+      xv[j] = v;
+    }
+  }
+  float mx = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(xv[j]));
+  float sc, inv_row;
+  row_scale(row_max(mx), sc, inv_row);
+  bf16x8 x0[P][1];
+  {
+    u32x4v h4, l4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const F16Pair pr = split_f16_pair(xv[2 * q], xv[2 * q + 1], sc);
+      h4[q] = pr.hi;
+      l4[q] = pr.lo;
+    }
+    x0[0][0] = __builtin_bit_cast(bf16x8, h4);
+    x0[1][0] = __builtin_bit_cast(bf16x8, l4);
+  }
+  const int64_t bs = w.BS;
+  f32x4 acc[NB2];
+  // the activations are held in f32 and each k-group's fp16 parts made when it is consumed
+  // (layer_lds_split_f32): holding both parts would take 168 VGPRs and spill at H = 200
+  float hf[KG][8];
+  float s_in = 1.f;  // the held activations' row scale
+  // acc * f + bias, swish (fc.py:21), and the row scale of the result (the next layer's input)
+  auto to_input = [&](const float* b, float f) {
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < KG; ++c) {
+      const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), b1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        hf[c][t] = swish_fast(fmaf(acc[2 * c][t], f, b0[t]));
+        hf[c][4 + t] = swish_fast(fmaf(acc[2 * c + 1][t], f, b1[t]));
+        mx = fmaxf(mx, fmaxf(fabsf(hf[c][t]), fabsf(hf[c][4 + t])));
+      }
+    }
+    row_scale(row_max(mx), s_in, inv_row);
+  };
+  layer_lds_split<1, NB2, WAVES, SLOT, P, PS, true>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane);
+  to_input(w.b0 + e * bs, inv_row * w.wscale[e]);
+  for (int l = 0; l < 3; ++l) {
+    layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, true>(w.whb + ((int64_t)l * E + e) * KG * P * NB2 * 256, hf, acc,
+                                                           lds, wv, lane, s_in);
+    to_input(w.bh + ((int64_t)l * E + e) * bs, inv_row * w.wscale[(1 + l) * E + e]);
+  }
+  f32x4 hd[NBO];
+  layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, PS, true>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd, lds, wv,
+                                                         lane, s_in);
+  const float f = inv_row * w.wscale[4 * E + e];
+#pragma unroll
+  for (int nb = 0; nb < NBO; ++nb) hd[nb] *= f;
+  head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
+                           (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
+}
+
 #ifndef BNN_R13
 #define BNN_R13 1  // row blocks per wave at H = 200
 #endif
@@ -474,7 +601,22 @@ static int launch_bf16_p(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
 }
 
 template <int NB2, int NBO>
+static int launch_f16s(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
+  constexpr int WV = BNN_SPLIT_WAVES, PS = BNN_SPLIT_PS == 0 ? 2 : BNN_SPLIT_PS;
+  a.ntiles = (int)ceil_div((int)a.B, 16);
+  if (a.ntiles == 0) return 0;
+  dim3 grid(ceil_div(a.ntiles, WV) * h->E), block(64 * WV);
+  if (mode == FWD_PREDICT)
+    hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_PREDICT, WV, PS>), grid, block, 0, s, h->dev, a);
+  else
+    hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_ROLLOUT, WV, PS>), grid, block, 0, s, h->dev, a);
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+template <int NB2, int NBO>
 static int launch_bf16_t(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s) {
+  if (h->dtype == DT_F16X3) return launch_f16s<NB2, NBO>(h, mode, a, s);
   switch (bf16_parts(h->dtype)) {
     case 2: return launch_bf16_p<NB2, NBO, 2>(h, mode, a, s);
     case 3: return launch_bf16_p<NB2, NBO, 3>(h, mode, a, s);
@@ -522,8 +664,8 @@ extern "C" int mopo_bnn_create(mopo_bnn_t* out, int E, int obs_dim, int act_dim,
   MOPO_REQUIRE(out != nullptr, "mopo_bnn_create: out is NULL");
   MOPO_REQUIRE(E >= 1 && E <= 256, "mopo_bnn_create: num_networks must be in [1, 256]");
   MOPO_REQUIRE(obs_dim >= 1 && act_dim >= 1, "mopo_bnn_create: bad obs/act dims");
-  MOPO_REQUIRE(dtype >= 0 && dtype <= 3,
-               "mopo_bnn_create: dtype must be 0 (fp32), 1 (bf16), 2 (bf16x3) or 3 (bf16x6)");
+  MOPO_REQUIRE(dtype >= 0 && dtype <= 4,
+               "mopo_bnn_create: dtype must be 0 (fp32), 1 (bf16), 2 (bf16x3), 3 (bf16x6) or 4 (f16x3)");
   Bnn* h = new Bnn();
   h->E = E; h->O = obs_dim; h->A = act_dim; h->H = hidden; h->smv = smv; h->dtype = dtype;
   BnnDev& d = h->dev;
@@ -558,12 +700,14 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
   const int64_t s_w0 = (int64_t)E * KG0 * NBH * 256, s_wh = 3LL * E * NBH * NBH * 256,
                 s_whd = (int64_t)E * NBH * NBO * 256, s_b0 = E * hp, s_bh = 3 * E * hp,
                 s_bhd = (int64_t)E * 3 * NBO * 16;
-  const int64_t total = s_w0 + s_wh + s_whd + s_b0 + s_bh + s_bhd + 2 * 64 + 2 * 64;
+  const int64_t s_ws = (5LL * E + 63) / 64 * 64;  // f16x3 inverse weight scales [5][E]
+  const int64_t total = s_w0 + s_wh + s_whd + s_b0 + s_bh + s_bhd + 2 * 64 + 2 * 64 + s_ws;
   if (!h->buf) MOPO_HIP(hipMalloc(&h->buf, total * sizeof(float)));
   float* base = h->buf;
   float* w0 = base; float* wh = w0 + s_w0; float* whd = wh + s_wh;
   float* b0 = whd + s_whd; float* bh = b0 + s_b0; float* bhd = bh + s_bh;
   float* mu = bhd + s_bhd; float* sg = mu + 64; float* mx = sg + 64; float* mn = mx + 64;
+  float* wsc = mn + 64;
 
   // stage raw arrays on the device, then pack there (same code path as on-device repacking)
   const int n_layers = 5;
@@ -590,6 +734,10 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
   stage_n = std::max(stage_n, (size_t)E * IN * H);
   float* stage = nullptr;
   MOPO_HIP(hipMalloc(&stage, stage_n * sizeof(float)));
+  struct DevFree {  // frees the staging buffers on every return path
+    float*& p;
+    ~DevFree() { if (p) (void)hipFree(p); }
+  } stage_guard{stage};
   auto pack = [&](const float* src, size_t nsrc, float* dst, int K, int N, int KG, int NB, int perm_n) -> int {
     MOPO_HIP(hipMemcpy(stage, src, nsrc * sizeof(float), hipMemcpyHostToDevice));
     int64_t tot = (int64_t)E * KG * NB * 256;
@@ -606,14 +754,14 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
     MOPO_HIP(hipDeviceSynchronize());
     return 0;
   };
-  int rc = 0;
-  rc |= pack(W[0], (size_t)E * IN * H, w0, IN, H, KG0, NBH, 1);
-  rc |= packb(Bv[0], b0, H, (int)hp);
-  for (int l = 0; l < 3; ++l) {
-    rc |= pack(W[1 + l], (size_t)E * H * H, wh + (int64_t)l * E * NBH * NBH * 256, H, H, NBH, NBH, 1);
-    rc |= packb(Bv[1 + l], bh + l * E * hp, H, (int)hp);
+  int rc = pack(W[0], (size_t)E * IN * H, w0, IN, H, KG0, NBH, 1);  // each step runs only if all before succeeded
+  if (rc == 0) rc = packb(Bv[0], b0, H, (int)hp);
+  for (int l = 0; l < 3 && rc == 0; ++l) {
+    rc = pack(W[1 + l], (size_t)E * H * H, wh + (int64_t)l * E * NBH * NBH * 256, H, H, NBH, NBH, 1);
+    if (rc == 0) rc = packb(Bv[1 + l], bh + l * E * hp, H, (int)hp);
   }
-  rc |= pack(head.data(), head.size(), whd, H, 2 * D, NBH, NBO, 2);  // head outputs: head_col slots
+  if (rc == 0) rc = pack(head.data(), head.size(), whd, H, 2 * D, NBH, NBO, 2);  // head outputs: head_col slots
+  if (rc) return rc;
   {  // head aux [E][bias | max_logvar | min_logvar], NBO*16 each, in head_col slot order
     std::vector<float> aux((size_t)s_bhd, 0.f);
     for (int e = 0; e < E; ++e) {
@@ -638,11 +786,33 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
     float* b0f = reinterpret_cast<float*>(h->bbuf);
     float* bhf = b0f + f0 * 256;
     float* bdf = bhf + fh * 256;
+    // f16x3: per layer and member, 2^k with max |W| 2^k in [2^14, 2^15) (mlp_tile.h split_f16_scaled)
+    std::vector<float> scale_h(5 * E), inv_h(5 * E, 1.f);
+    float* scale_d = nullptr;
+    DevFree scale_guard{scale_d};
+    if (h->dtype == DT_F16X3) MOPO_HIP(hipMalloc(&scale_d, E * sizeof(float)));
+    auto member_scales = [&](const float* src, int K, int N, int layer) {
+      for (int e = 0; e < E; ++e) {
+        float m = 0.f;
+        for (int64_t i = 0; i < (int64_t)K * N; ++i) m = std::max(m, std::fabs(src[(int64_t)e * K * N + i]));
+        int ex = 0;
+        if (m > 0.f && std::isfinite(m)) std::frexp(m, &ex);  // m in [2^(ex-1), 2^ex)
+        const int k = m > 0.f && std::isfinite(m) ? 15 - ex : 0;
+        scale_h[layer * E + e] = std::ldexp(1.f, k);
+        inv_h[layer * E + e] = std::ldexp(1.f, -k);
+      }
+    };
+    int layer_idx = 0;
     auto packh = [&](const float* src, size_t nsrc, float* dst, int K, int N, int KGb, int NB, int perm_n) -> int {
       MOPO_HIP(hipMemcpy(stage, src, nsrc * sizeof(float), hipMemcpyHostToDevice));
       int64_t tot = (int64_t)E * KGb * P * NB * 512;
       int blocks = (int)std::min<int64_t>((tot + 255) / 256, 4096);
-      if (P == 3)
+      if (h->dtype == DT_F16X3) {
+        member_scales(src, K, N, layer_idx);
+        MOPO_HIP(hipMemcpy(scale_d, scale_h.data() + layer_idx * E, E * sizeof(float), hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(pack_frags_f16s_kernel, dim3(blocks), dim3(256), 0, 0, stage, (short*)dst, E, K, N, KGb, NB,
+                           1, perm_n, (const float*)scale_d);
+      } else if (P == 3)
         hipLaunchKernelGGL(pack_frags_bf16_kernel<3>, dim3(blocks), dim3(256), 0, 0, stage, (short*)dst, E, K, N, KGb,
                            NB, 1, perm_n);
       else if (P == 2)
@@ -653,15 +823,18 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
                            NB, 1, perm_n);
       MOPO_HIP(hipGetLastError());
       MOPO_HIP(hipDeviceSynchronize());
+      ++layer_idx;
       return 0;
     };
-    rc |= packh(W[0], (size_t)E * IN * H, b0f, IN, H, 1, NB2, 1);
-    for (int l = 0; l < 3; ++l)
-      rc |= packh(W[1 + l], (size_t)E * H * H, bhf + (int64_t)l * E * KG * P * NB2 * 256, H, H, KG, NB2, 1);
-    rc |= packh(head.data(), head.size(), bdf, H, 2 * D, KG, NBO, 2);
-    d.w0b = b0f; d.whb = bhf; d.whdb = bdf;
+    if (rc == 0) rc = packh(W[0], (size_t)E * IN * H, b0f, IN, H, 1, NB2, 1);
+    for (int l = 0; l < 3 && rc == 0; ++l)
+      rc = packh(W[1 + l], (size_t)E * H * H, bhf + (int64_t)l * E * KG * P * NB2 * 256, H, H, KG, NB2, 1);
+    if (rc == 0) rc = packh(head.data(), head.size(), bdf, H, 2 * D, KG, NBO, 2);
+    if (rc == 0 && h->dtype == DT_F16X3)
+      rc = hipMemcpy(wsc, inv_h.data(), 5 * E * sizeof(float), hipMemcpyHostToDevice) == hipSuccess ? 0
+                                                                                                 : fail("bnn: scale copy");
+    d.w0b = b0f; d.whb = bhf; d.whdb = bdf; d.wscale = wsc;
   }
-  (void)hipFree(stage);
   if (rc) return -1;
   MOPO_HIP(hipMemcpy(mu, arrs[0], IN * sizeof(float), hipMemcpyHostToDevice));
   MOPO_HIP(hipMemcpy(sg, arrs[1], IN * sizeof(float), hipMemcpyHostToDevice));

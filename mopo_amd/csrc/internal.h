@@ -32,10 +32,12 @@ struct BnnDev {
   const float* w0b;   // [E][1][NB2]
   const float* whb;   // [3][E][NB2/2][NB2]
   const float* whdb;  // [E][NB2/2][NBO]
+  const float* wscale;  // f16x3: [5][E] inverse power-of-two weight scales (layer 0, hidden 1..3, head)
 };
 
-// bf16 parts per operand of a dtype (1 bf16, 2 bf16x3, 3 bf16x6; split_bf16 in mlp_tile.h)
-__host__ __device__ constexpr int bf16_parts(int dtype) { return dtype < 1 ? 1 : dtype; }
+enum { DT_FP32 = 0, DT_BF16 = 1, DT_BF16X3 = 2, DT_BF16X6 = 3, DT_F16X3 = 4 };
+// 16-bit parts per operand of a dtype (1 bf16, 2 bf16x3, 3 bf16x6, 2 f16x3; mlp_tile.h split_*)
+__host__ __device__ constexpr int bf16_parts(int dtype) { return dtype < 1 ? 1 : (dtype == DT_F16X3 ? 2 : dtype); }
 
 struct Bnn {
   int E, O, A, H, smv, dtype;

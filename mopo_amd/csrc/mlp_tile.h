@@ -188,6 +188,18 @@ __device__ __forceinline__ f32x4 mfma_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// the same 16x16x32 shape on f16 operands (the "f16x3" split: fp16 parts, stored as their bits)
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mfma_f16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma_16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
+  if constexpr (F16) return mfma_f16(a, b, c);
+  else return mfma_bf16(a, b, c);
+}
+
 __host__ __device__ __forceinline__ int bf16_kperm(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
 
 __device__ __forceinline__ short to_bf16(float x) { return __builtin_bit_cast(short, (__bf16)x); }
@@ -245,7 +257,8 @@ __device__ __forceinline__ void split_bf16(float v, short (&out)[P]) {
 }
 
 // PS: parts staged per slice (P: one slice of P * NB fragments per k-group; 1: P slices of NB).
-template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P>
+// F16: the parts are fp16 ("f16x3", split_f16_scaled) and the products run on the f16 MFMA.
+template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false>
 __device__ __forceinline__ void layer_lds_split(const float* __restrict__ wf, const bf16x8 (&in)[P][KG],
                                                 f32x4 (&acc)[NB], float* lds, int w, int lane) {
   static_assert(P % PS == 0, "parts per slice must divide the parts");
@@ -276,16 +289,63 @@ __device__ __forceinline__ void layer_lds_split(const float* __restrict__ wf, co
       const bf16x8 fr = *reinterpret_cast<const bf16x8*>(b + (i * 64 + lane) * 4);
 #endif
 #pragma unroll
-      for (int q = P - 1 - p; q >= 0; --q) acc[nb] = mfma_bf16(fr, in[q][kg], acc[nb]);
+      for (int q = P - 1 - p; q >= 0; --q) acc[nb] = mfma_16x16x32<F16>(fr, in[q][kg], acc[nb]);
     }
   }
 }
 
+// ---- "f16x3": f32 operands as 2 fp16 parts under a power-of-two scale ---------------------------
+// v ~ (x0 + x1) / s with x0 = RN_f16(v s), x1 = RN_f16(v s - x0): |v - (x0 + x1)/s| <= 2^-22 |v| (fp16
+// unit roundoff 2^-11, squared), and the products x0 w0 + x0 w1 + x1 w0 drop x1 w1 <= 2^-22 |v w|:
+// the same ~22-bit class as the 3-part bf16 split (whose truncated parts leave 2^-22 and whose dropped
+// products x1 w2, x2 w1 are 2^-21 each) at half its MFMAs.  The scale keeps fp16's range out of the
+// way: weights carry one 2^k per layer and member (packed on the device), activations one per row
+// (row_scale: the row's max |v| lands in [2^14, 2^15), so nothing overflows and an element far below
+// the row max loses at most 2^-38 of it, below f32 rounding of the sums); acc * (2^-k / s) undoes it.
+struct F16Parts {
+  short hi, lo;
+};
+__device__ __forceinline__ F16Parts split_f16_scaled(float v, float s) {
+  const float vs = v * s;
+  const _Float16 h = (_Float16)vs;
+  const _Float16 l = (_Float16)(vs - (float)h);
+  return {__builtin_bit_cast(short, h), __builtin_bit_cast(short, l)};
+}
+
+// Two elements at once into whole dwords (hi parts, lo parts) with v_cvt_pk_f16_f32 (round to nearest):
+// every write of an MFMA operand register is a full 32-bit write.  Left to itself the compiler folds the
+// split into v_fma_mix{lo,hi}_f16 half-register writes, and an MFMA issued right after a mixhi write
+// of its B operand was measured to read a stale half (nondeterministic 2^-11 errors).
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+struct F16Pair {
+  uint32_t hi, lo;
+};
+__device__ __forceinline__ F16Pair split_f16_pair(float a, float b, float s) {
+  const float as = a * s, bs = b * s;
+  uint32_t h;
+  asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h) : "v"(as), "v"(bs));
+  const float ah = (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
+  const float bh = (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16));
+  uint32_t l;
+  asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(l) : "v"(as - ah), "v"(bs - bh));
+  return {h, l};
+}
+
+// power-of-two scale s with max |v| * s in [2^14, 2^15) (mx >= 0; zero / tiny rows clamp, inf / NaN
+// stay inf / NaN as in f32) and its exact inverse
+__device__ __forceinline__ void row_scale(float mx, float& s, float& inv) {
+  uint32_t eb = (__float_as_uint(mx) >> 23) & 0xffu;
+  eb = eb < 15u ? 15u : (eb > 254u ? 254u : eb);
+  s = __uint_as_float((268u - eb) << 23);
+  inv = __uint_as_float((eb - 14u) << 23);
+}
+
 // layer_lds_split with f32 activations held (8 VGPRs per k-group instead of 4 * P): each k-group's P
 // bf16 parts are split when its first slice is consumed, so only one k-group's parts are live.
-template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P>
+// F16: the 2 fp16 parts of in * s (split_f16_scaled; s = the row scale) on the f16 MFMA.
+template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false>
 __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf, const float (&in)[KG][8],
-                                                    f32x4 (&acc)[NB], float* lds, int w, int lane) {
+                                                    f32x4 (&acc)[NB], float* lds, int w, int lane, float sc = 1.f) {
   static_assert(P % PS == 0, "parts per slice must divide the parts");
   constexpr int SPK = P / PS, S = KG * SPK, NF = PS * NB;
   static_assert(Stage<NF, WAVES>::SLOTS * 256 <= SLOT, "slice larger than its buffer");
@@ -298,12 +358,26 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
   for (int s = 0; s < S; ++s) {
     const int kg = s / SPK;
     if (s % SPK == 0) {
+      if constexpr (F16) {
+        static_assert(!F16 || P == 2, "f16 split has 2 parts");
+        u32x4v h4, l4;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        short parts[P];
-        split_bf16<P>(in[kg][j], parts);
+        for (int q = 0; q < 4; ++q) {
+          const F16Pair pr = split_f16_pair(in[kg][2 * q], in[kg][2 * q + 1], sc);
+          h4[q] = pr.hi;
+          l4[q] = pr.lo;
+        }
+        cur[0] = __builtin_bit_cast(bf16x8, h4);
+        cur[P - 1] = __builtin_bit_cast(bf16x8, l4);
+      }
+      if constexpr (!F16) {
 #pragma unroll
-        for (int p = 0; p < P; ++p) cur[p][j] = parts[p];
+        for (int j = 0; j < 8; ++j) {
+          short parts[P];
+          split_bf16<P>(in[kg][j], parts);
+#pragma unroll
+          for (int p = 0; p < P; ++p) cur[p][j] = parts[p];
+        }
       }
     }
     __syncthreads();
@@ -317,7 +391,7 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
       const bf16x8 fr = fr_next;
       if (i + 1 < NF) fr_next = *reinterpret_cast<const bf16x8*>(b + ((i + 1) * 64 + lane) * 4);
 #pragma unroll
-      for (int q = P - 1 - p; q >= 0; --q) acc[nb] = mfma_bf16(fr, cur[q], acc[nb]);
+      for (int q = P - 1 - p; q >= 0; --q) acc[nb] = mfma_16x16x32<F16>(fr, cur[q], acc[nb]);
     }
   }
 }

@@ -221,7 +221,10 @@ def _rollout_case(domain, E, H, B, horizon, seed, coeff=1.0, O=17, A=6, height=N
                                                   ('halfcheetah', 7, 200, 1000, 5, 'bf16x6'),
                                                   ('walker2d', 7, 200, 777, 5, 'bf16x6'),
                                                   ('hopper', 7, 64, 300, 4, 'bf16x6'),
-                                                  ('halfcheetah', 7, 200, 5000, 3, 'bf16x6')]])
+                                                  ('halfcheetah', 7, 200, 5000, 3, 'bf16x6'),
+                                                  ('halfcheetah', 7, 200, 1000, 5, 'f16x3'),
+                                                  ('walker2d', 7, 200, 777, 5, 'f16x3'),
+                                                  ('halfcheetah', 7, 200, 5000, 3, 'f16x3')]])
 def test_fused_rollout_parity(domain, E, H, B, horizon, dtype):
     import torch
     from mopo_amd.replay_pool import SimpleReplayPool
@@ -351,7 +354,7 @@ def test_bnn_predict_bf16_vs_oracle(E, H, B):
     assert not np.array_equal(mean, m32.predict(x)[0])
 
 
-@pytest.mark.parametrize('dtype,tol', [('bf16x6', 2e-5), ('bf16x3', 1e-4)])
+@pytest.mark.parametrize('dtype,tol', [('bf16x6', 2e-5), ('f16x3', 2e-5), ('bf16x3', 1e-4)])
 @pytest.mark.parametrize('E,H,B', [(7, 200, 4099), (7, 64, 257), (32, 32, 100), (32, 400, 300), (7, 200, 1)])
 def test_bnn_predict_split_vs_oracle(E, H, B, dtype, tol):
     """f32 operands split into bf16 parts, f32 accumulate.  bf16x6 (3 parts, 6 products) holds the
@@ -365,11 +368,36 @@ def test_bnn_predict_split_vs_oracle(E, H, B, dtype, tol):
     rm, rv = obnn.forward(p, x, dtype=np.float64)
     close(mean, rm, tol)
     close(var, rv, tol)
-    if dtype == 'bf16x6':   # f32-accurate: no worse than the f32-MFMA path's own rounding (x2, floor 2e-6)
+    if dtype in ('bf16x6', 'f16x3'):   # f32-class: no worse than the f32-MFMA path's own rounding (x2, floor 2e-6)
         m32, v32 = make_model(mats, E, H).predict(x)
         err = lambda a, b: float(np.max(np.abs(np.float64(a) - b) / (1 + np.abs(b))))
         assert err(mean, rm) <= max(2 * err(m32, rm), 2e-6), (err(mean, rm), err(m32, rm))
         assert err(var, rv) <= max(2 * err(v32, rv), 2e-6), (err(var, rv), err(v32, rv))
+
+
+@pytest.mark.parametrize('scale', [1e-6, 1.0, 1e3, 1e5])
+def test_f16x3_dynamic_range(scale):
+    """f16x3 carries fp16 parts under power-of-two scales (per row for activations, per layer and member
+    for weights): inputs and weights far outside fp16's range give the f32 kernel's answer, no inf/NaN."""
+    rs = np.random.RandomState(17)
+    E, H, B = 7, 200, 640
+    p = obnn.init_params(E, 17, 6, hidden=H, seed=4, inputs=rs.normal(size=(300, 23)))
+    p['W'] = [w * np.float32(scale if i == 0 else 1.0) for i, w in enumerate(p['W'])]   # layer-0 weights x scale
+    mats = obnn.to_mat_list(p)
+    x = (rs.normal(size=(B, 23)) * 3).astype(np.float32)
+    x[::7] *= np.float32(1e4)                                                              # far-out rows
+    mean, var = make_model(mats, E, H, dtype='f16x3').predict(x)
+    rm, rv = obnn.forward(p, x, dtype=np.float64)
+    assert np.isfinite(mean).all() and np.isfinite(var).all()
+    # the same ~22-bit operand class as bf16x6: within 2x the worse of the fp32 and bf16x6 kernels' own
+    # errors (adversarial scales make cancellations that amplify every kernel's rounding alike)
+    err = lambda a, b: float(np.max(np.abs(np.float64(a) - b) / (1 + np.abs(b))))
+    ref_m, ref_v = 2e-6, 2e-6
+    for dt in ('fp32', 'bf16x6'):
+        mo, vo = make_model(mats, E, H, dtype=dt).predict(x)
+        ref_m, ref_v = max(ref_m, 2 * err(mo, rm)), max(ref_v, 2 * err(vo, rv))
+    assert err(mean, rm) <= ref_m, (err(mean, rm), ref_m)
+    assert err(var, rv) <= ref_v, (err(var, rv), ref_v)
 
 
 def test_fused_rollout_bf16_walker_runs():
