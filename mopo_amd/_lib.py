@@ -36,7 +36,7 @@ class RolloutArgs(C.Structure):
                 ('term_kind', c_int), ('seed', c_u64), ('epoch', c_u32), ('uid_offset', c_i64),
                 ('d_eps_act', c_void_p), ('d_eps_obs', c_void_p), ('d_model_inds', c_void_p),
                 ('d_steps', c_void_p), ('penalty_learned_var', c_int), ('deterministic', c_int),
-                ('rollout_random', c_int), ('d_act_uniform', c_void_p)]
+                ('rollout_random', c_int), ('d_act_uniform', c_void_p), ('actor_dtype', c_int)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/mopo_hip.h
@@ -51,6 +51,8 @@ SIGNATURES = {
     'mopo_sac_param_count': (c_i64, [c_int, c_int, c_int]),
     'mopo_actor_forward': (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_i64, c_void_p,
                                    c_u64, c_u32, c_void_p, c_void_p, c_void_p]),
+    'mopo_actor_forward_dtype': (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_i64, c_void_p,
+                                         c_u64, c_u32, c_void_p, c_void_p, c_int, c_void_p]),
     'mopo_pool_add': (c_int, [C.POINTER(PoolDesc), c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_i64, c_void_p]),
     'mopo_pool_gather': (c_int, [C.POINTER(PoolDesc), c_int, c_int, c_void_p, c_i64, c_void_p, c_void_p,

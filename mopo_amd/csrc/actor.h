@@ -29,10 +29,13 @@ struct ActorArgs {
   // rollout_random (mopo.py:736-738): the actions are U(-1, 1) draws -- injected act_uni [B, A] or
   // Philox -- and replace the policy's (still computed, as the reference calls get_action_meta first)
   int rand_act; const float* act_uni;
+  // 0: f32 MFMA on the fragment-major f32 packing; 4 (DT_F16X3): the f16x3 split (mlp_tile.h) on the
+  // f16 packing (pack_actor with f16 = 1)
+  int dtype;
 };
 
 int launch_actor(const ActorArgs& a, hipStream_t s);
-__host__ __device__ int64_t actor_packed_floats(int O, int Hp);
-int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s);
+__host__ __device__ int64_t actor_packed_floats(int O, int Hp, int f16 = 0);
+int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s, int f16 = 0);
 
 }  // namespace mopo

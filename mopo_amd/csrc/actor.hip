@@ -14,9 +14,90 @@ namespace mopo {
 
 // packed layout: W1 frags | W2 frags | head frags | b1 [NB*16] | b2 [NB*16] | [bmu | bls] [16]
 // (biases zero-padded to whole 16-blocks so the kernel stages them into LDS with global_load_lds)
-__host__ __device__ int64_t actor_packed_floats(int O, int Hp) {
+// f16 (f16x3): W1 [1][2][NB] | W2 [NB/2][2][NB] | head [NB/2][2][1] fragments of 64 lanes x 8 fp16
+// (256 floats each, the ensemble's bf16 fragment layout with its k permutation), then the same biases,
+// then 3 inverse weight scales and 3 max-|W| words (actor_wmax_kernel)
+__host__ __device__ int64_t actor_packed_floats(int O, int Hp, int f16) {
   const int KG0 = (O + 15) / 16, NB = (Hp + 15) / 16;
+  if (f16) return (int64_t)(2 * NB + NB * NB + NB) * 256 + 2LL * NB * 16 + 16 + 8;
   return (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256 + (int64_t)NB * 256 + 2LL * NB * 16 + 16;
+}
+
+// max |W| of the three weight matrices (W1, W2, [Wmu | Wls]) as ordered uint bits -> wmax[3]
+__global__ void actor_wmax_kernel(const float* __restrict__ P, int O, int A, int Hp, uint32_t* __restrict__ wmax) {
+  const float* W1 = P;
+  const float* W2 = W1 + O * Hp + Hp;
+  const float* Wm = W2 + Hp * Hp + Hp;
+  const float* Wl = Wm + Hp * A + A;
+  const int64_t n1 = (int64_t)O * Hp, n2 = (int64_t)Hp * Hp, nh = 2LL * Hp * A;
+  float m[3] = {0.f, 0.f, 0.f};
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n1 + n2 + nh; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n1) m[0] = fmaxf(m[0], fabsf(W1[i]));
+    else if (i < n1 + n2) m[1] = fmaxf(m[1], fabsf(W2[i - n1]));
+    else {
+      const int64_t j = i - n1 - n2;
+      m[2] = fmaxf(m[2], fabsf(j < (int64_t)Hp * A ? Wm[j] : Wl[j - (int64_t)Hp * A]));
+    }
+  }
+  for (int q = 0; q < 3; ++q) {
+    float v = m[q];
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0 && v > 0.f) atomicMax(wmax + q, __float_as_uint(v));
+  }
+}
+
+// f16x3 packing: fp16 parts of W * 2^k (k per matrix from wmax: max |W| 2^k in [2^14, 2^15)), the
+// biases as in the f32 packing, and the 3 inverse scales
+__global__ void pack_actor_f16_kernel(const float* __restrict__ P, int O, int A, int Hp, float* __restrict__ dst,
+                                      const uint32_t* __restrict__ wmax) {
+  const int NB = ceil_div(Hp, 16), KG = NB / 2;
+  const float* W1 = P;
+  const float* W2 = W1 + O * Hp + Hp;
+  const float* Wm = W2 + Hp * Hp + Hp;
+  const float* Wl = Wm + Hp * A + A;
+  float sc[3], inv[3];
+  for (int q = 0; q < 3; ++q) row_scale(__uint_as_float(wmax[q]), sc[q], inv[q]);
+  const int64_t f1 = 2LL * NB, f2 = (int64_t)KG * 2 * NB, fh = (int64_t)KG * 2;
+  const int64_t nfrag = (f1 + f2 + fh) * 512;  // fp16 elements
+  short* d16 = reinterpret_cast<short*>(dst);
+  float* tail = dst + (f1 + f2 + fh) * 256;
+  const int64_t total = nfrag + 2LL * NB * 16 + 16 + 3;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < nfrag) {
+      const int j = i & 7, lane = (int)((i >> 3) & 63), g = lane >> 4, r = lane & 15;
+      int64_t f = i >> 9;
+      int which, nbs;
+      if (f < f1) { which = 0; nbs = NB; }
+      else if (f < f1 + f2) { which = 1; f -= f1; nbs = NB; }
+      else { which = 2; f -= f1 + f2; nbs = 1; }
+      const int nb = (int)(f % nbs), p = (int)((f / nbs) % 2), kg = (int)(f / (2 * nbs));
+      int k = kg * 32 + bf16_kperm(g, j);
+      const int n = nb * 16 + r;
+      float v = 0.f;
+      if (which == 0) {
+        k = slot_feat(k, O);
+        if (k >= 0 && n < Hp) v = W1[k * Hp + n];
+      } else if (which == 1) {
+        if (k < Hp && n < Hp) v = W2[k * Hp + n];
+      } else if (k < Hp) {
+        v = r < A ? Wm[k * A + r] : (r < 2 * A ? Wl[k * A + (r - A)] : 0.f);
+      }
+      const F16Parts q = split_f16_scaled(v, sc[which]);
+      d16[i] = p == 0 ? q.hi : q.lo;
+    } else {
+      const int j = (int)(i - nfrag);  // b1 | b2 | [bmu | bls] | inverse scales
+      float v;
+      if (j < NB * 16) v = j < Hp ? W1[O * Hp + j] : 0.f;
+      else if (j < 2 * NB * 16) v = j - NB * 16 < Hp ? W2[Hp * Hp + j - NB * 16] : 0.f;
+      else if (j < 2 * NB * 16 + 16) {
+        const int q = j - 2 * NB * 16;
+        v = q < A ? Wm[Hp * A + q] : (q < 2 * A ? Wl[Hp * A + q - A] : 0.f);
+      } else {
+        v = inv[j - 2 * NB * 16 - 16];
+      }
+      tail[j] = v;
+    }
+  }
 }
 
 // One launch packs the whole policy (it is repacked at every rollout, after the SAC updates):
@@ -62,7 +143,21 @@ __global__ void pack_actor_kernel(const float* __restrict__ P, int O, int A, int
   }
 }
 
-int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s) {
+int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s, int f16) {
+  if (f16) {
+    MOPO_REQUIRE(Hp % 32 == 0, "actor f16x3: hidden width must be a multiple of 32");
+    MOPO_REQUIRE(O <= 32 && 2 * A <= 16, "actor f16x3: obs_dim <= 32, act_dim <= 8");
+    const int NB = Hp / 16;
+    uint32_t* wmax = reinterpret_cast<uint32_t*>(dst + (2LL * NB + NB * NB + NB) * 256 + 2LL * NB * 16 + 16 + 3);
+    MOPO_HIP(hipMemsetAsync(wmax, 0, 3 * sizeof(uint32_t), s));
+    hipLaunchKernelGGL(actor_wmax_kernel, dim3(64), dim3(256), 0, s, P, O, A, Hp, wmax);
+    MOPO_HIP(hipGetLastError());
+    const int64_t tot = (2LL * NB + NB * NB + NB) * 512 + 2LL * NB * 16 + 16 + 3;
+    hipLaunchKernelGGL(pack_actor_f16_kernel, dim3((int)std::min<int64_t>((tot + 255) / 256, 1024)), dim3(256), 0, s,
+                       P, O, A, Hp, dst, (const uint32_t*)wmax);
+    MOPO_HIP(hipGetLastError());
+    return 0;
+  }
   const int64_t tot = actor_packed_floats(O, Hp);
   hipLaunchKernelGGL(pack_actor_kernel, dim3((int)std::min<int64_t>((tot + 255) / 256, 1024)), dim3(256), 0, s, P, O,
                      A, Hp, dst);
@@ -96,6 +191,88 @@ __device__ __forceinline__ void actor_noise(uint64_t seed, uint32_t step, int64_
 #define ACT_WAVES_CFG 4  // waves (16-row tiles) per workgroup
 #endif
 constexpr int ACT_WAVES = ACT_WAVES_CFG;
+
+// Actions from the head outputs head[wv][m][0, 16) (mu | log_std) of the wave's 16 rows: noise or
+// uniform actions, tanh squash, pool row / member pick (lane group 0), the ensemble's scaled input row.
+__device__ __forceinline__ void actor_finish(const ActorArgs& a, float (&head)[ACT_WAVES][16][25], int wv, int m,
+                                             int g, int64_t row, bool ok) {
+  const int O = a.O, A = a.A;
+  if (g == 0 && ok) {
+    float z[16];
+    const int64_t uid = a.d_uid ? a.d_uid[row] : row + a.uid_offset;
+    if (a.eps) {
+      for (int j = 0; j < A; ++j) z[j] = a.eps[row * A + j];
+    } else {
+      actor_noise(a.seed, a.step, uid, A, z);
+    }
+    int64_t pos = -1;
+    if (a.pool_act) pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool_state[0] + a.pool_off + row) % a.pool_max;
+    float uni[16];
+    if (a.rand_act) {  // np.random.uniform(low=-1, high=1, size=act.shape) (mopo.py:738)
+      if (a.act_uni) {
+        for (int j = 0; j < A; ++j) uni[j] = a.act_uni[row * A + j];
+      } else {
+        for (int blk = 0; blk * 4 < A; ++blk) {
+          u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32) ^ ((uint32_t)blk << 20), a.step, RNG_ACT_UNIFORM};
+          const u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+          const uint32_t ws[4] = {r.x, r.y, r.z, r.w};
+          for (int i = 0; i < 4 && blk * 4 + i < A; ++i)
+            uni[blk * 4 + i] = -1.0f + 2.0f * ((float)(ws[i] >> 8) * 5.9604645e-8f);  // [-1, 1), 24-bit uniform
+        }
+      }
+    }
+    for (int j = 0; j < A; ++j) {
+      const float mu = head[wv][m][j];
+      const float ls = fminf(fmaxf(head[wv][m][A + j], -20.f), 2.f);  // mopo.py:304
+      const float sd = expf(ls);                                      // mopo.py:305
+      const float u = mu + z[j] * sd;                                 // mopo.py:306
+      const float act = a.rand_act ? uni[j] : tanhf(u);               // mopo.py:295 / 738
+      head[wv][m][16 + j] = act;
+      if (a.act) a.act[row * A + j] = act;
+      if (a.mu) a.mu[row * A + j] = tanhf(mu);                        // mopo.py:294
+      if (pos >= 0) a.pool_act[pos * A + j] = act;
+    }
+    if (pos >= 0) {  // the observation half of the pool row (mopo.py:750), stored f32
+      for (int k = 0; k < O; ++k)
+        a.pool_obs[pos * O + k] = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
+                                            : reinterpret_cast<const float*>(a.obs)[row * O + k];
+    }
+    if (a.pen_zero) a.pen_zero[row] = 0u;
+    if (a.sel_out) {
+      int32_t sel;
+      if (a.sel_in) {
+        sel = a.sel_in[row];
+      } else {  // perf mode of np.random.choice(elites, B) (bnn.py:343)
+        u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32), a.step, RNG_MODEL};
+        u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+        sel = a.elites[(int)(((uint64_t)r.x * (uint64_t)a.n_elites) >> 32)];
+      }
+      a.sel_out[row] = sel;
+    }
+  }
+  if (a.xs) {  // the ensemble's layer-0 input, scaled exactly as bnn_fwd_kernel would; lane g: 8 slots
+    __syncthreads();
+    if (ok) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        f32x4 v;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int k = slot_feat(8 * g + 4 * q + t, a.xs_in);
+          float x = 0.f;
+          if (k >= 0) {
+            const float raw = k < O ? (a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
+                                                  : reinterpret_cast<const float*>(a.obs)[row * O + k])
+                                    : head[wv][m][16 + k - O];
+            x = (raw - a.xs_mu[k]) / a.xs_sigma[k];
+          }
+          v[t] = x;
+        }
+        *reinterpret_cast<f32x4*>(a.xs + row * XS_STRIDE + 8 * g + 4 * q) = v;
+      }
+    }
+  }
+}
 
 // TQ0: k-steps in the last k-group of the observation (tail_steps(O); 4 = all)
 template <int KG0, int NBP, int TQ0 = 4>
@@ -176,81 +353,89 @@ __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? 4 : 2) void actor_kerne
     head[wv][m][n] = hd[0][0][t] + lds_bias[n];
   }
   __syncthreads();
-  if (g == 0 && ok) {
-    float z[16];
-    const int64_t uid = a.d_uid ? a.d_uid[row] : row + a.uid_offset;
-    if (a.eps) {
-      for (int j = 0; j < A; ++j) z[j] = a.eps[row * A + j];
-    } else {
-      actor_noise(a.seed, a.step, uid, A, z);
-    }
-    int64_t pos = -1;
-    if (a.pool_act) pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool_state[0] + a.pool_off + row) % a.pool_max;
-    float uni[16];
-    if (a.rand_act) {  // np.random.uniform(low=-1, high=1, size=act.shape) (mopo.py:738)
-      if (a.act_uni) {
-        for (int j = 0; j < A; ++j) uni[j] = a.act_uni[row * A + j];
-      } else {
-        for (int blk = 0; blk * 4 < A; ++blk) {
-          u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32) ^ ((uint32_t)blk << 20), a.step, RNG_ACT_UNIFORM};
-          const u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
-          const uint32_t ws[4] = {r.x, r.y, r.z, r.w};
-          for (int i = 0; i < 4 && blk * 4 + i < A; ++i)
-            uni[blk * 4 + i] = -1.0f + 2.0f * ((float)(ws[i] >> 8) * 5.9604645e-8f);  // [-1, 1), 24-bit uniform
-        }
-      }
-    }
-    for (int j = 0; j < A; ++j) {
-      const float mu = head[wv][m][j];
-      const float ls = fminf(fmaxf(head[wv][m][A + j], -20.f), 2.f);  // mopo.py:304
-      const float sd = expf(ls);                                      // mopo.py:305
-      const float u = mu + z[j] * sd;                                 // mopo.py:306
-      const float act = a.rand_act ? uni[j] : tanhf(u);               // mopo.py:295 / 738
-      head[wv][m][16 + j] = act;
-      if (a.act) a.act[row * A + j] = act;
-      if (a.mu) a.mu[row * A + j] = tanhf(mu);                        // mopo.py:294
-      if (pos >= 0) a.pool_act[pos * A + j] = act;
-    }
-    if (pos >= 0) {  // the observation half of the pool row (mopo.py:750), stored f32
-      for (int k = 0; k < O; ++k)
-        a.pool_obs[pos * O + k] = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
-                                            : reinterpret_cast<const float*>(a.obs)[row * O + k];
-    }
-    if (a.pen_zero) a.pen_zero[row] = 0u;
-    if (a.sel_out) {
-      int32_t sel;
-      if (a.sel_in) {
-        sel = a.sel_in[row];
-      } else {  // perf mode of np.random.choice(elites, B) (bnn.py:343)
-        u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32), a.step, RNG_MODEL};
-        u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
-        sel = a.elites[(int)(((uint64_t)r.x * (uint64_t)a.n_elites) >> 32)];
-      }
-      a.sel_out[row] = sel;
-    }
-  }
-  if (a.xs) {  // the ensemble's layer-0 input, scaled exactly as bnn_fwd_kernel would; lane g: 8 slots
-    __syncthreads();
-    if (ok) {
+  actor_finish(a, head, wv, m, g, row, ok);
+}
+
+// f16x3 policy forward (mlp_tile.h split_f16_pair / row_scale): observation row scaled per row, each
+// layer's output acc * (2^-k_W / s_row) + bias, relu; 16x16x32 f16 MFMAs, 3 products per k-group.
+template <int NBP>
+__global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16_kernel(const ActorArgs a) {
+  constexpr int P = 2, KG = NBP / 2;
+  constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
+  __shared__ float head[ACT_WAVES][16][25];
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
+  if ((int64_t)blockIdx.x * ACT_WAVES * 16 >= count) return;  // whole workgroup past the live rows
+  const int64_t row = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16 + m;
+  const bool ok = row < count;
+  const int O = a.O;
+  const float* w1f = a.Wpk;
+  const float* w2f = w1f + 2 * NBP * 256;
+  const float* whf = w2f + KG * 2 * NBP * 256;
+  const float* b1 = whf + KG * 2 * 256;
+  const float* b2 = b1 + NBP * 16;
+  const float* bh = b2 + NBP * 16;
+  const float* inv_w = bh + 16;
+  auto row_max = [&](float mx) {
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    return fmaxf(mx, __shfl_xor(mx, 32));
+  };
+  float xv[8], mx = 0.f;
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        f32x4 v;
+  for (int j = 0; j < 8; ++j) {
+    const int k = slot_feat(bf16_kperm(g, j), O);
+    float v = 0.f;
+    if (ok && k >= 0)
+      v = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
+                    : reinterpret_cast<const float*>(a.obs)[row * O + k];
+    xv[j] = v;
+    mx = fmaxf(mx, fabsf(v));
+  }
+  float s_in, inv_row;
+  row_scale(row_max(mx), s_in, inv_row);
+  bf16x8 x0[P][1];
+  {
+    u32x4v h4, l4;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int k = slot_feat(8 * g + 4 * q + t, a.xs_in);
-          float x = 0.f;
-          if (k >= 0) {
-            const float raw = k < O ? (a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
-                                                  : reinterpret_cast<const float*>(a.obs)[row * O + k])
-                                    : head[wv][m][16 + k - O];
-            x = (raw - a.xs_mu[k]) / a.xs_sigma[k];
-          }
-          v[t] = x;
-        }
-        *reinterpret_cast<f32x4*>(a.xs + row * XS_STRIDE + 8 * g + 4 * q) = v;
+    for (int q = 0; q < 4; ++q) {
+      const F16Pair pr = split_f16_pair(xv[2 * q], xv[2 * q + 1], s_in);
+      h4[q] = pr.hi;
+      l4[q] = pr.lo;
+    }
+    x0[0][0] = __builtin_bit_cast(bf16x8, h4);
+    x0[1][0] = __builtin_bit_cast(bf16x8, l4);
+  }
+  f32x4 acc[NBP];
+  float hf[KG][8];
+  auto to_input = [&](const float* b, float f) {  // acc * f + bias, relu (mopo.py:277-278, 301), row scale
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < KG; ++c) {
+      const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), bb1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        hf[c][t] = fmaxf(fmaf(acc[2 * c][t], f, b0[t]), 0.f);
+        hf[c][4 + t] = fmaxf(fmaf(acc[2 * c + 1][t], f, bb1[t]), 0.f);
+        mx = fmaxf(mx, fmaxf(hf[c][t], hf[c][4 + t]));
       }
     }
+    row_scale(row_max(mx), s_in, inv_row);
+  };
+  layer_lds_split<1, NBP, ACT_WAVES, SLOT, P, 1, true>(w1f, x0, acc, lds, wv, lane);
+  to_input(b1, inv_row * inv_w[0]);
+  layer_lds_split_f32<KG, NBP, ACT_WAVES, SLOT, P, 1, true>(w2f, hf, acc, lds, wv, lane, s_in);
+  to_input(b2, inv_row * inv_w[1]);
+  f32x4 hd[1];
+  layer_lds_split_f32<KG, 1, ACT_WAVES, SLOT, P, 1, true>(whf, hf, hd, lds, wv, lane, s_in);
+  const float f = inv_row * inv_w[2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n = 4 * g + t;
+    head[wv][m][n] = fmaf(hd[0][t], f, bh[n]);   // mu | log_std (mopo.py:302-303)
   }
+  __syncthreads();
+  actor_finish(a, head, wv, m, g, row, ok);
 }
 
 int launch_actor(const ActorArgs& a, hipStream_t s) {
@@ -261,6 +446,13 @@ int launch_actor(const ActorArgs& a, hipStream_t s) {
   MOPO_REQUIRE(a.O >= 1 && a.O <= 32, "actor: obs_dim must be in [1, 32]");
   MOPO_REQUIRE(a.Wpk, "actor: packed weights required");
   dim3 grid(ceil_div((int)a.B, 16 * ACT_WAVES)), block(64 * ACT_WAVES);
+  if (a.dtype == DT_F16X3) {
+    if (a.Hp == 256) hipLaunchKernelGGL(actor_f16_kernel<16>, grid, block, 0, s, a);
+    else if (a.Hp == 32) hipLaunchKernelGGL(actor_f16_kernel<2>, grid, block, 0, s, a);
+    else return fail("actor f16x3: unsupported hidden size (256 or 32)");
+    MOPO_HIP(hipGetLastError());
+    return 0;
+  }
   const int KG0 = ceil_div(a.O, 16);
   if (a.Hp == 256 && KG0 == 2 && tail_steps(a.O) == 1)  // halfcheetah / walker2d: 17 = 16 + 1
     hipLaunchKernelGGL((actor_kernel<2, 16, 1>), grid, block, 0, s, a);
@@ -288,18 +480,20 @@ extern "C" int64_t mopo_sac_param_count(int O, int A, int H) {
   return pi + 2 * q;
 }
 
-extern "C" int mopo_actor_forward(const float* P, int O, int A, int H, const void* obs, int obs_f64, int64_t B,
-                                  const float* eps, uint64_t seed, uint32_t step, float* act, float* mu,
-                                  void* stream) {
+extern "C" int mopo_actor_forward_dtype(const float* P, int O, int A, int H, const void* obs, int obs_f64, int64_t B,
+                                        const float* eps, uint64_t seed, uint32_t step, float* act, float* mu,
+                                        int dtype, void* stream) {
   MOPO_REQUIRE(P && obs, "mopo_actor_forward: NULL pointer");
+  MOPO_REQUIRE(dtype == DT_FP32 || dtype == DT_F16X3, "mopo_actor_forward: dtype must be 0 (fp32) or 4 (f16x3)");
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  const int f16 = dtype == DT_F16X3;
   float* wpk = nullptr;
-  MOPO_HIP(hipMallocAsync((void**)&wpk, actor_packed_floats(O, H) * sizeof(float), s));
-  int rc = pack_actor(P, O, A, H, wpk, s);
+  MOPO_HIP(hipMallocAsync((void**)&wpk, actor_packed_floats(O, H, f16) * sizeof(float), s));
+  int rc = pack_actor(P, O, A, H, wpk, s, f16);
   if (rc == 0) {
     ActorArgs a{};
-    a.P = P; a.Wpk = wpk; a.O = O; a.A = A; a.Hp = H;
+    a.P = P; a.Wpk = wpk; a.O = O; a.A = A; a.Hp = H; a.dtype = dtype;
     a.obs = obs; a.obs_f64 = obs_f64; a.B = B;
     a.eps = eps; a.seed = seed; a.step = step;
     a.act = act; a.mu = mu;
@@ -308,4 +502,10 @@ extern "C" int mopo_actor_forward(const float* P, int O, int A, int H, const voi
   }
   (void)hipFreeAsync(wpk, s);
   return rc;
+}
+
+extern "C" int mopo_actor_forward(const float* P, int O, int A, int H, const void* obs, int obs_f64, int64_t B,
+                                  const float* eps, uint64_t seed, uint32_t step, float* act, float* mu,
+                                  void* stream) {
+  return mopo_actor_forward_dtype(P, O, A, H, obs, obs_f64, B, eps, seed, step, act, mu, DT_FP32, stream);
 }

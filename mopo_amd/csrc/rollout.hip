@@ -31,7 +31,7 @@ struct Rollout {
   int64_t* uid[2];
   float* act;
   float* wpk = nullptr;  // policy weights, fragment-major (pack_actor), repacked every run
-  int wpk_hp = 0;
+  int wpk_hp = 0, wpk_f16 = 0;
   uint32_t* pen;
   int32_t* sel;
   float* xs;        // [B][32] the ensemble's scaled input rows (written by the actor)
@@ -325,13 +325,16 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
   }
   if (i0 == 0) {
     MOPO_HIP(hipGetLastError());
-    if (!h->wpk || h->wpk_hp != a->pi_hidden) {
+    MOPO_REQUIRE(a->actor_dtype == DT_FP32 || a->actor_dtype == DT_F16X3, "rollout: actor_dtype must be 0 or 4");
+    const int f16 = a->actor_dtype == DT_F16X3;
+    if (!h->wpk || h->wpk_hp != a->pi_hidden || h->wpk_f16 != f16) {
       if (h->wpk) (void)hipFree(h->wpk);
-      MOPO_HIP(hipMalloc(&h->wpk, actor_packed_floats(O, a->pi_hidden) * sizeof(float)));
+      MOPO_HIP(hipMalloc(&h->wpk, actor_packed_floats(O, a->pi_hidden, f16) * sizeof(float)));
       h->wpk_hp = a->pi_hidden;
+      h->wpk_f16 = f16;
     }
     KTimer t(h, KC_START, s);
-    if (pack_actor(a->d_pi_params, O, A, a->pi_hidden, h->wpk, s)) return -1;
+    if (pack_actor(a->d_pi_params, O, A, a->pi_hidden, h->wpk, s, f16)) return -1;
   }
   // every member's mean per row is needed by the mean-distance penalty and by deterministic steps
   const bool det = a->deterministic != 0;
@@ -358,6 +361,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     aa.sel_out = det ? nullptr : h->sel + off;
     aa.sel_in = a->d_model_inds ? a->d_model_inds + (int64_t)i * B + off : nullptr;
     aa.rand_act = a->rollout_random;
+    aa.dtype = a->actor_dtype;
     aa.act_uni = a->d_act_uniform ? a->d_act_uniform + ((int64_t)i * B + off) * A : nullptr;
     aa.elites = a->d_elites; aa.n_elites = a->n_elites;
     aa.xs = h->xs + off * XS_STRIDE; aa.xs_mu = bnn->dev.mu; aa.xs_sigma = bnn->dev.sigma; aa.xs_in = bnn->dev.IN;

@@ -47,6 +47,9 @@ def split_params(flat, O, A, H=256):
     return out
 
 
+_ACTOR_DTYPES = {'fp32': 0, 'f16x3': 4}
+
+
 class ModelRollout:
     """Owns the rollout workspace for up to ``max_batch`` rows x ``max_horizon`` steps."""
 
@@ -66,12 +69,13 @@ class ModelRollout:
     def run(self, env_obs, pi_params, pool, batch_size, horizon, term_kind, penalty_coeff, elites,
             seed=0, epoch=0, pi_hidden=256, start_idx=None, eps_act=None, eps_obs=None, model_inds=None,
             staged=False, uid_offset=0, stream=None, step_desc=None, step_hook=None, penalty_learned_var=True,
-            deterministic=False, rollout_random=False, act_uniform=None):
+            deterministic=False, rollout_random=False, act_uniform=None, actor_dtype=None):
         """Returns the device int64[horizon] tensor of rows added per step (steps_added).
         ``step_desc(i)`` / ``step_hook(i, steps)``: per-step staging (see mopo_rollout_run_staged_steps).
         ``penalty_learned_var`` / ``deterministic``: FakeEnv's modes (fake_env.py:69-110; every D4RL
         config uses the learned-var penalty, not deterministic); ``rollout_random``: uniform actions
-        (mopo.py:736-738), ``act_uniform`` [horizon, B, A] injects them in parity mode."""
+        (mopo.py:736-738), ``act_uniform`` [horizon, B, A] injects them in parity mode.
+        ``actor_dtype``: 'fp32' or 'f16x3' policy forward (default: f16x3 with an f16x3 ensemble)."""
         import torch
         dev = env_obs.device
         B = int(batch_size)
@@ -94,7 +98,8 @@ class ModelRollout:
             d_eps_act=dptr(eps_act, torch.float32), d_eps_obs=dptr(eps_obs, torch.float64),
             d_model_inds=dptr(model_inds, torch.int32), d_steps=L.ptr(steps),
             penalty_learned_var=int(bool(penalty_learned_var)), deterministic=int(bool(deterministic)),
-            rollout_random=int(bool(rollout_random)), d_act_uniform=dptr(act_uniform, torch.float32))
+            rollout_random=int(bool(rollout_random)), d_act_uniform=dptr(act_uniform, torch.float32),
+            actor_dtype=_ACTOR_DTYPES[actor_dtype or ('f16x3' if self.model.dtype == 'f16x3' else 'fp32')])
         if step_hook is not None:
             # one call per horizon step into the staging block step_hook(i) names; step_hook(i, steps)
             # is then called after step i is enqueued (multi-GPU: gather step i while i + 1 computes)

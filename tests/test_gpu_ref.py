@@ -112,8 +112,9 @@ def test_sac_steps_vs_reference_graph(path):
             assert np.abs(tgt - t_ref).max() <= 2e-6 + 5e-3 * 2 * sum(lr_t[:k + 1])
 
 
+@pytest.mark.parametrize('dtype', [0, 4])   # fp32, f16x3
 @pytest.mark.parametrize('path', SAC, ids=[os.path.basename(p)[8:-4] for p in SAC])
-def test_actor_vs_reference_graph(path):
+def test_actor_vs_reference_graph(path, dtype):
     """get_action_meta (mopo.py:468-485): pi and the deterministic mu for the step-0 batch."""
     import torch
     from mopo_amd import _lib as L
@@ -126,7 +127,7 @@ def test_actor_vs_reference_graph(path):
     te = torch.from_numpy(np.ascontiguousarray(z['b0_noise0'][0])).to(dev)
     act = torch.empty((n, A), device=dev)
     mu = torch.empty((n, A), device=dev)
-    L.check(L.lib().mopo_actor_forward(L.ptr(tp), O, A, H, L.ptr(to), 0, n, L.ptr(te), 0, 0, L.ptr(act),
-                                       L.ptr(mu), L.stream_ptr()))
+    L.check(L.lib().mopo_actor_forward_dtype(L.ptr(tp), O, A, H, L.ptr(to), 0, n, L.ptr(te), 0, 0, L.ptr(act),
+                                             L.ptr(mu), dtype, L.stream_ptr()))
     assert np.abs(act.cpu().numpy() - z['actor_pi_f32']).max() < 2e-5
     assert np.abs(mu.cpu().numpy() - z['actor_mu_f32']).max() < 2e-5

@@ -98,7 +98,8 @@ def test_fakeenv_step_vs_reference_golden(path):
         assert near.all()
 
 
-def test_actor_forward_vs_oracle():
+@pytest.mark.parametrize('dtype', [0, 4])   # fp32, f16x3
+def test_actor_forward_vs_oracle(dtype):
     import torch
     from mopo_amd import _lib as L
     from mopo_amd.rollout import init_sac_params, split_params
@@ -113,8 +114,8 @@ def test_actor_forward_vs_oracle():
     tp, to, te = (torch.from_numpy(x).to(dev) for x in (flat, obs, eps))
     act = torch.empty((B, A), device=dev)
     mu = torch.empty((B, A), device=dev)
-    L.check(L.lib().mopo_actor_forward(L.ptr(tp), O, A, H, L.ptr(to), 1, B, L.ptr(te), 0, 0, L.ptr(act),
-                                       L.ptr(mu), L.stream_ptr()))
+    L.check(L.lib().mopo_actor_forward_dtype(L.ptr(tp), O, A, H, L.ptr(to), 1, B, L.ptr(te), 0, 0, L.ptr(act),
+                                             L.ptr(mu), dtype, L.stream_ptr()))
     ra, rmu = osac.actor_act(P, obs.astype(np.float32).astype(np.float64), eps.astype(np.float64))
     close(act.cpu().numpy(), ra, 2e-5)
     close(mu.cpu().numpy(), rmu, 2e-5)
