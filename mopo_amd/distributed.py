@@ -85,7 +85,10 @@ class DistributedRollout:
         self.gathered = torch.empty((self.horizon, self.world * self.blk), dtype=torch.uint8, device=dev)
         self.counts = torch.empty((self.world * self.horizon,), dtype=torch.int64, device=dev)
 
-    def run(self, env_obs, pi_params, pool, term_kind, penalty_coeff, elites, seed=0, epoch=0, pi_hidden=256):
+    def run(self, env_obs, pi_params, pool, term_kind, penalty_coeff, elites, seed=0, epoch=0, pi_hidden=256,
+            **modes):
+        """``modes``: the FakeEnv / rollout modes of ModelRollout.run (penalty_learned_var, deterministic,
+        rollout_random, actor_dtype).  Returns the global rows per step (sum over ranks)."""
         import ctypes as C
         import torch.distributed as dist
         from . import _lib as L
@@ -100,7 +103,7 @@ class DistributedRollout:
 
         steps = self.ro.run(env_obs, pi_params, None, self.B, self.horizon, term_kind, penalty_coeff, elites,
                             seed=seed, epoch=epoch, pi_hidden=pi_hidden, staged=True, uid_offset=self.rank * self.B,
-                            step_desc=step_desc, step_hook=step_hook)
+                            step_desc=step_desc, step_hook=step_hook, **modes)
         works.append(dist.all_gather_into_tensor(self.counts, steps.contiguous(), group=self.group, async_op=True))
         for w in works:
             w.wait()
@@ -111,3 +114,51 @@ class DistributedRollout:
                                              self.horizon * self.world, self.B, L.ptr(cb), None))
         self._keep = cb
         return self.counts.view(self.world, self.horizon).sum(0)
+
+
+# ---------------------------------------------------------------------------------------------------
+# State sync for the multi-GPU training loop (MOPO with torch.distributed initialised).  Rank 0 is
+# authoritative: before every rollout it broadcasts the ensemble (the .mat arrays + elites, ~3.7 MB at
+# E=7, H=200) and the whole SAC state (parameters, targets, Adam moments: ~3.5 MB at 256-256), so every
+# rank rolls out its shard with the same policy and model, and the replicated learners
+# stay identical even if some float reduction on the device were not bit-reproducible.
+
+def world_info(group=None):
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def broadcast_model(model, src=0, group=None):
+    """BNN parameters and elites from ``src`` to every rank (repacked on each rank's device)."""
+    import numpy as np
+    import torch.distributed as dist
+    mats = model.get_params()
+    shapes = [m.shape for m in mats]
+    dev = torch.device('cuda', torch.cuda.current_device())
+    flat = torch.from_numpy(np.concatenate([m.ravel() for m in mats]).astype(np.float32)).to(dev)
+    el = torch.tensor(list(model._model_inds), dtype=torch.int64, device=dev)
+    dist.broadcast(flat, src, group=group)
+    dist.broadcast(el, src, group=group)
+    h, off = flat.cpu().numpy(), 0
+    out = []
+    for shp in shapes:
+        n = int(np.prod(shp))
+        out.append(h[off:off + n].reshape(shp))
+        off += n
+    model.set_params(out)
+    model.set_elites(el.cpu().tolist())
+
+
+def broadcast_sac(sac, src=0, group=None):
+    """The SAC state (params + log_alpha, targets, Adam m / v) from ``src`` to every rank."""
+    import torch.distributed as dist
+    n = sac.n_params
+    parts = [(0, n + 1), (1, n), (2, n + 1), (3, n + 1)]
+    buf = torch.cat([sac._copy(w, c) for w, c in parts])
+    dist.broadcast(buf, src, group=group)
+    off = 0
+    for w, c in parts:
+        sac._copy(w, c, buf[off:off + c].contiguous(), to_handle=True)
+        off += c

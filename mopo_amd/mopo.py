@@ -41,7 +41,8 @@ class MOPO:
         self._model = construct_model(obs_dim=obs_dim, act_dim=act_dim, hidden_dim=hidden_dim,
                                       num_networks=num_networks, num_elites=num_elites,
                                       separate_mean_var=separate_mean_var, name=model_name,
-                                      load_dir=model_load_dir, deterministic=deterministic)
+                                      load_dir=model_load_dir, deterministic=deterministic,
+                                      seed=seed)   # the run seed (simple_run/main.py:180 set_seed) fixes the init
         self.fake_env = FakeEnv(self._model, static_fns, penalty_coeff=penalty_coeff,
                                 penalty_learned_var=penalty_learned_var)
         self._rollout_schedule = [20, 100, rollout_length, rollout_length]                 # mopo.py:137
@@ -64,6 +65,12 @@ class MOPO:
         self._pi_hidden = hs[0]
         self._rollout = None
         self._rollout_length = rollout_length
+        # multi-GPU (torch.distributed initialised, one process per GPU): the rollout rows are sharded
+        # over the ranks and all-gathered into every rank's model pool; SAC runs replicated
+        from .distributed import world_info
+        self._rank, self._world = world_info()
+        if self._rollout_batch_size % self._world:
+            raise ValueError('rollout_batch_size must be a multiple of the world size')
         self._max_model_t = max_model_t
         self._model_train_metrics = None
 
@@ -108,16 +115,36 @@ class MOPO:
 
     # -- mopo.py:723-765 (device-resident, perf-mode RNG); ``deterministic`` as mopo.py:558-559 passes it
     def _rollout_model(self, rollout_batch_size, deterministic=None, **kwargs):
+        modes = dict(penalty_learned_var=self.fake_env.penalty_learned_var,
+                     deterministic=self._deterministic if deterministic is None else deterministic,
+                     rollout_random=self._rollout_random)
+        env_obs = self._pool.fields['observations'][:self._pool.size]
+        if self._world > 1:
+            return self._rollout_model_sharded(rollout_batch_size, env_obs, modes)
         if self._rollout is None or self._rollout.max_batch < rollout_batch_size or \
                 self._rollout.max_horizon < self._rollout_length:
             self._rollout = ModelRollout(self._model, rollout_batch_size, max(self._rollout_length, 1))
-        env_obs = self._pool.fields['observations'][:self._pool.size]
         steps = self._rollout.run(env_obs, self._sac.policy_params_ptr, self._model_pool, rollout_batch_size,
                                   self._rollout_length, self.fake_env.term_kind, self.fake_env.penalty_coeff,
                                   self._model._model_inds, seed=self._seed, epoch=self._epoch,
-                                  pi_hidden=self._pi_hidden, penalty_learned_var=self.fake_env.penalty_learned_var,
-                                  deterministic=self._deterministic if deterministic is None else deterministic,
-                                  rollout_random=self._rollout_random)
+                                  pi_hidden=self._pi_hidden, **modes)
+        added = int(steps.sum().item())
+        return {'mean_rollout_length': added / rollout_batch_size}
+
+    def _rollout_model_sharded(self, rollout_batch_size, env_obs, modes):
+        """Rank r rolls out rows [r B/N, (r + 1) B/N) of the batch (Philox streams keyed by the global
+        row id, so the N shards are exactly the single-GPU rollout's rows) after rank 0's model and SAC
+        state are broadcast; every rank's model pool receives all transitions in the single-GPU order."""
+        from .distributed import DistributedRollout, broadcast_model, broadcast_sac
+        broadcast_model(self._model)
+        broadcast_sac(self._sac)
+        b = rollout_batch_size // self._world
+        h = max(self._rollout_length, 1)
+        if self._rollout is None or self._rollout.B != b or self._rollout.horizon != h:
+            self._rollout = DistributedRollout(self._model, b, h, self._obs_dim, self._act_dim)
+        steps = self._rollout.run(env_obs, self._sac.policy_params_ptr, self._model_pool, self.fake_env.term_kind,
+                                  self.fake_env.penalty_coeff, self._model._model_inds, seed=self._seed,
+                                  epoch=self._epoch, pi_hidden=self._pi_hidden, **modes)
         added = int(steps.sum().item())
         return {'mean_rollout_length': added / rollout_batch_size}
 

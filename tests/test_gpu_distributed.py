@@ -74,3 +74,72 @@ def test_overlapped_allgather_matches_single_process(B):
     np.testing.assert_array_equal(got['counts'], steps.cpu().numpy())
     for k in ref:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+# ---- the training loop itself sharded: MOPO.train with torch.distributed initialised ---------------
+def _mopo(data_path, B):
+    from mopo_amd.config import get_params
+    from mopo_amd.loader import restore_pool
+    from mopo_amd.mopo import from_config
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.static import static_fns
+    pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=int(1e5))
+    restore_pool(pool, data_path)
+    np.random.seed(0)   # numpy's global stream drives the model training loop (bnn.py:369-503)
+    return from_config(get_params('examples.config.d4rl.halfcheetah_mixed'), pool, static_fns['halfcheetah'],
+                       rollout_batch_size=B, epoch_length=40, model_train_freq=40)
+
+
+def _state(algo):
+    p, la = algo._sac.get_params()
+    mp_ = algo._model_pool
+    return dict(sac=p.cpu().numpy(), log_alpha=np.float32(la.item()), target=algo._sac.get_target().cpu().numpy(),
+                bnn=np.concatenate([m.ravel() for m in algo._model.get_params()]),
+                **{'pool_' + k: v[:mp_.size].cpu().numpy() for k, v in mp_.fields.items()})
+
+
+def _mopo_worker(rank, world, port, data_path, out, B):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY='0')
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    algo = _mopo(data_path, B)
+    assert algo._world == world
+    diags = list(algo.train(2))
+    torch.cuda.synchronize()
+    st = _state(algo)
+    st['mean_rollout_length'] = np.array([d['model/mean_rollout_length'] for d in diags])
+    np.savez(out % rank, **st)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_mopo_train_sharded_matches_single_process(tmp_path):
+    """Two ranks (gloo on the one GPU; RCCL on a real node) run MOPO.train(2) with the rollout rows
+    sharded: both ranks end with identical model pools, SAC states and ensembles, and those equal a
+    single-process MOPO.train(2) of the same config bit for bit."""
+    import torch
+    import torch.multiprocessing as mp
+    rs = np.random.RandomState(0)
+    n = 3000
+    obs = rs.normal(size=(n, O)).astype(np.float32)
+    data = str(tmp_path / 'd.npz')
+    np.savez(data, observations=obs, actions=rs.uniform(-1, 1, (n, A)).astype(np.float32),
+             next_observations=obs + 0.1 * rs.normal(size=(n, O)).astype(np.float32),
+             rewards=rs.normal(size=n).astype(np.float32), terminals=np.zeros(n, bool))
+    B, world = 2400, 2
+    out = str(tmp_path / 'r%d.npz')
+    mp.start_processes(_mopo_worker, args=(world, 29700 + os.getpid() % 1000, data, out, B), nprocs=world, join=True,
+                       start_method='spawn')
+    r0, r1 = dict(np.load(out % 0)), dict(np.load(out % 1))
+    for k in r0:
+        np.testing.assert_array_equal(r0[k], r1[k], err_msg='ranks differ: ' + k)
+    algo = _mopo(data, B)
+    diags = list(algo.train(2))
+    torch.cuda.synchronize()
+    single = _state(algo)
+    np.testing.assert_array_equal(r0['mean_rollout_length'], [d['model/mean_rollout_length'] for d in diags])
+    bad = {k: float(np.max(np.abs(r0[k].astype(np.float64) - single[k]))) for k in single
+           if not np.array_equal(r0[k], single[k])}
+    assert not bad, 'sharded != single process: %s' % bad
