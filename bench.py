@@ -28,7 +28,7 @@ O, A, E, ELITES, H, HP = 17, 6, 7, 5, 200, 256
 ENV_ROWS = 101000
 FLOP_BNN_ROW = 2 * E * ((O + A) * H + 3 * H * H + 2 * H * (O + 1))       # 1,845,200
 FLOP_ACTOR_ROW = 2 * (O * HP + HP * HP + HP * 2 * A)                      # 145,920
-PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01_v11_pmc_summary.json')
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r02_pmc_summary.json')
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
 # ensemble dtype -> (bf16 parts per operand, bf16 products per f32 product); fp32 runs f32 MFMA
 SPLIT = {'bf16': (1, 1), 'bf16x3': (2, 3), 'bf16x6': (3, 6), 'f16x3': (2, 3)}
@@ -41,6 +41,20 @@ DTYPE_DESC = {'fp32': 'fp32 (f32 MFMA 16x16x4)',
                        'accumulate: ~22-bit operands like bf16x6, held to the fp32 parity tolerances)'}
 
 
+# BASELINE.json configs.  B_total = the config's rollout_batch; 'sharded': the batch is
+# split over the ranks (C4, C5: 400k / 1M over 8 GPUs), otherwise every GPU runs B_total rows (weak scaling).
+CONFIGS = {
+    'C2': dict(name='halfcheetah-mixed (examples.config.d4rl.halfcheetah_mixed)', E=7, H=200, B_total=50000, h=5,
+               domain='halfcheetah', penalty=1.0, env_rows=101000),
+    'C3': dict(name='walker2d-medium-replay, bf16 ensemble', E=7, H=200, B_total=100000, h=1, domain='walker2d',
+               penalty=1.0, env_rows=101000, dtype='bf16'),
+    'C4': dict(name='halfcheetah-medium-expert, 400k rows sharded over the GPUs', E=7, H=200, B_total=400000, h=5,
+               domain='halfcheetah', penalty=5.0, env_rows=1000000, sharded=True),
+    'C5': dict(name='halfcheetah-mixed stress, E=32, H=400, 1M rows sharded over the GPUs', E=32, H=400,
+               B_total=1000000, h=5, domain='halfcheetah', penalty=1.0, env_rows=101000, sharded=True),
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
@@ -49,7 +63,8 @@ def parse():
     p.add_argument('--batch', type=int, default=50000)
     p.add_argument('--horizon', type=int, default=5)
     p.add_argument('--no-cpu-baseline', action='store_true')
-    p.add_argument('--cpu-batch', type=int, default=30000)
+    p.add_argument('--cpu-batch', type=int, default=50000,
+                   help='rows of the CPU baseline rollout (default: the headline batch, same workload)')
     p.add_argument('--sac-steps', type=int, default=1000)
     p.add_argument('--cpu-sac-steps', type=int, default=500)
     p.add_argument('--no-c3', action='store_true', help='skip the secondary C3 (bf16 walker2d) line')
@@ -61,7 +76,17 @@ def parse():
     p.add_argument('--no-alt-dtypes', action='store_true',
                    help='skip the extra headline-workload lines with the other ensemble dtypes')
     p.add_argument('--prof-steps', type=int, default=3, help='untimed rollouts timed per kernel with HIP events')
-    return p.parse_args()
+    p.add_argument('--config', default='C2', choices=sorted(CONFIGS),
+                   help='BASELINE.json workload of the main line (C2 = the headline); the per-rank batch is the '
+                        "config's total rollout_batch / world for C4 / C5")
+    a = p.parse_args()
+    spec = CONFIGS[a.config]
+    if a.config != 'C2':   # the config fixes the workload; --batch / --horizon apply to C2 only
+        world = int(os.environ.get('WORLD_SIZE', '1'))
+        a.batch, a.horizon = spec['B_total'] // world if spec.get('sharded') else spec['B_total'], spec['h']
+        if a.ensemble_dtype == 'f16x3' and spec.get('dtype'):
+            a.ensemble_dtype = spec['dtype']
+    return a
 
 
 def dist_setup(args):
@@ -85,15 +110,31 @@ def dist_setup(args):
     return rank, world, torch.device('cuda', 0)
 
 
+def spec_flop_row(spec):
+    return 2 * spec['E'] * ((O + A) * spec['H'] + 3 * spec['H'] ** 2 + 2 * spec['H'] * (O + 1))
+
+
+def make_env(spec, seed=0):
+    """Synthetic env pool of the config's size: obs ~ N(0, 1), actions ~ U(-1, 1); walker2d
+    heights / angles spread over the termination bounds so rows terminate at a moderate rate."""
+    rs = np.random.RandomState(seed)
+    n = spec['env_rows']
+    env_obs = rs.normal(size=(n, O)).astype(np.float32)
+    if spec['domain'] == 'walker2d':
+        env_obs[:, 0] = rs.uniform(0.7, 2.1, n)
+        env_obs[:, 1] = rs.uniform(-1.1, 1.1, n)
+    env_act = rs.uniform(-1, 1, size=(n, A)).astype(np.float32)
+    return env_obs, env_act
+
+
 def build(args, dev, rank, world=None):
     import torch
     from mopo_amd.bnn import construct_model
     from mopo_amd.replay_pool import SimpleReplayPool
     from mopo_amd.rollout import ModelRollout, init_sac_params
-    rs = np.random.RandomState(0)  # identical synthetic env pool on every rank (replicated D4RL data)
-    env_obs = rs.normal(size=(ENV_ROWS, O)).astype(np.float32)
-    env_act = rs.uniform(-1, 1, size=(ENV_ROWS, A)).astype(np.float32)
-    model = construct_model(obs_dim=O, act_dim=A, hidden_dim=H, num_networks=E, num_elites=ELITES,
+    spec = CONFIGS[args.config]
+    env_obs, env_act = make_env(spec)   # identical on every rank (replicated D4RL data)
+    model = construct_model(obs_dim=O, act_dim=A, hidden_dim=spec['H'], num_networks=spec['E'], num_elites=ELITES,
                             separate_mean_var=True, seed=1, dtype=args.ensemble_dtype)
     mats = model.get_params()
     x = np.concatenate([env_obs, env_act], 1)
@@ -118,11 +159,22 @@ def build(args, dev, rank, world=None):
 
 def rollout_step(args, ro, pool, pi, env, staging, epoch, rank, world):
     """One MOPO._rollout_model; returns transitions added (device tensor)."""
-    import torch
+    from mopo_amd.static import static_fns
+    spec = CONFIGS[args.config]
+    tk, pen = static_fns[spec['domain']].term_kind, spec['penalty']
     if world == 1:
-        return ro.run(env, pi, pool, args.batch, args.horizon, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=epoch)
+        return ro.run(env, pi, pool, args.batch, args.horizon, tk, pen, [0, 1, 2, 3, 4], seed=88, epoch=epoch)
     # RCCL all-gather of each step's staged transitions (overlapping the next step) into every rank's pool
-    return staging.run(env, pi, pool, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=epoch)
+    return staging.run(env, pi, pool, tk, pen, [0, 1, 2, 3, 4], seed=88, epoch=epoch)
+
+
+def blas_threads():
+    """Threads the numpy oracle actually runs on (the BLAS pool; 1 if it cannot be read)."""
+    try:
+        from threadpoolctl import threadpool_info
+        return int(max([i.get('num_threads', 1) for i in threadpool_info() if i.get('user_api') == 'blas'] or [1]))
+    except Exception:
+        return 1
 
 
 def cpu_baseline(args):
@@ -175,14 +227,14 @@ def cpu_baseline_1core(args):
 BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense MFMA
 
 
-def roofline_of(dtype, rows, ms):
+def roofline_of(dtype, rows, ms, flop_row=FLOP_BNN_ROW):
     """Roofline of the ensemble-forward launch: f32 MFMA for fp32; executed bf16 MFMA flops (products x
     the algorithmic f32 flops) against the bf16 dense peak for the split / bf16 kernels."""
-    alg = rows * FLOP_BNN_ROW / (ms * 1e-3) / 1e12
+    alg = rows * flop_row / (ms * 1e-3) / 1e12
     if dtype == 'fp32':
         return {'bound': 'mfma', 'kernel': 'bnn_fwd_kernel (ensemble forward, f32 MFMA 16x16x4)',
                 'achieved': alg, 'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': alg / MFMA_F32_PEAK_TFLOPS,
-                'flop_per_launch': rows * FLOP_BNN_ROW, 'avg_launch_ms': ms}
+                'flop_per_launch': rows * flop_row, 'avg_launch_ms': ms}
     parts, prods = SPLIT[dtype]
     if dtype == 'f16x3':
         kern = 'bnn_fwd_f16s_kernel (ensemble forward, f16 MFMA 16x16x32, 3 products per f32 product)'
@@ -193,7 +245,7 @@ def roofline_of(dtype, rows, ms):
             'achieved': alg * prods, 'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
             'frac': alg * prods / BF16_PEAK_TFLOPS, 'achieved_note': 'executed 16-bit MFMA TFLOP/s = %d x the '
             'algorithmic f32 rate (bf16 and f16 share the 2.5 PF dense peak)' % prods, 'algorithmic_f32_tflops': alg,
-            'flop_per_launch': rows * FLOP_BNN_ROW, 'bf16_flop_per_launch': prods * rows * FLOP_BNN_ROW,
+            'flop_per_launch': rows * flop_row, 'bf16_flop_per_launch': prods * rows * flop_row,
             'avg_launch_ms': ms}
 
 
@@ -216,93 +268,35 @@ def alt_headline_leg(args, dev, dtype, reps=10):
             'unit': 'transitions/s', 'dtype': DTYPE_DESC[dtype], 'ms_per_rollout': dt / reps * 1e3}
 
 
-def c3_leg(args, dev):
-    """BASELINE config C3: walker2d-style rollout, bf16 ensemble (f32 accumulate / post-processing),
-    E=7, H=200, B=100,000, horizon 1, live walker2d terminations, penalty 1.0 (synthetic weights)."""
+def config_leg(args, dev, name, dtype, reps=3):
+    """Another BASELINE config on this GPU (one rank's share of a sharded config): same synthetic
+    construction and timing as the main line."""
     import torch
-    from mopo_amd.bnn import construct_model
-    from mopo_amd.replay_pool import SimpleReplayPool
-    from mopo_amd.rollout import ModelRollout, init_sac_params
-    from mopo_amd.static import TERM_WALKER2D
-    B, h = 100000, 1
-    rs = np.random.RandomState(3)
-    env_obs = rs.normal(size=(ENV_ROWS, O)).astype(np.float32)
-    env_obs[:, 0] = rs.uniform(0.7, 2.1, ENV_ROWS)                          # walker height
-    env_obs[:, 1] = rs.uniform(-1.1, 1.1, ENV_ROWS)                         # walker angle
-    model = construct_model(obs_dim=O, act_dim=A, hidden_dim=H, num_networks=E, num_elites=ELITES,
-                            separate_mean_var=True, seed=1, dtype='bf16')
-    mats = model.get_params()
-    x = np.concatenate([env_obs, rs.uniform(-1, 1, (ENV_ROWS, A))], 1)
-    mats[0] = x.mean(0, keepdims=True).astype(np.float32)
-    mats[1] = x.std(0, keepdims=True).astype(np.float32)
-    model.set_params(mats)
-    model.set_elites([0, 1, 2, 3, 4])
-    pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=5 * B)
-    ro = ModelRollout(model, B, h)
-    pi = torch.from_numpy(init_sac_params(O, A, HP, seed=2)).to(dev)
-    env = torch.from_numpy(env_obs).to(dev)
-    tk = TERM_WALKER2D
-    ro.run(env, pi, pool, B, h, tk, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=0)
+    spec = CONFIGS[name]
+    a2 = argparse.Namespace(**vars(args))
+    a2.config, a2.ensemble_dtype, a2.horizon = name, dtype, spec['h']
+    a2.batch = spec['B_total'] // 8 if spec.get('sharded') else spec['B_total']
+    _, pool, ro, pi, env, _ = build(a2, dev, 0, world=1)
+    rollout_step(a2, ro, pool, pi, env, None, 0, 0, 1)
     torch.cuda.synchronize()
-    reps = 5
     t0 = time.perf_counter()
-    tot = [ro.run(env, pi, pool, B, h, tk, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=1 + i) for i in range(reps)]
+    st = [rollout_step(a2, ro, pool, pi, env, None, 1 + i, 0, 1) for i in range(reps)]
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    n = int(sum(int(t.sum().item()) for t in tot))
+    n = int(sum(int(x.sum().item()) for x in st))
+    fr = spec_flop_row(spec)
     v = n / dt
-    flop_row = FLOP_BNN_ROW
-    return {'metric': 'model-rollout transitions/s (C3: walker2d-style, bf16 ensemble)', 'value': v,
-            'unit': 'transitions/s', 'dtype': 'bf16 (f32 accumulate)', 'ms_per_rollout': dt / reps * 1e3,
-            'config': {'workload': 'E=7, H=200, obs=17, act=6, rollout_batch=100000, horizon=1, walker2d '
-                                   'terminations, penalty_coeff=1.0', 'rollout_batch_per_gpu': B, 'horizon': h},
-            'bnn_flop_per_row': flop_row,
-            'ensemble_tflops_upper_bound': v * flop_row / 1e12,
-            'bf16_peak_tflops': BF16_PEAK_TFLOPS}
-
-
-def c5_leg(args, dev, dtype='fp32'):
-    """BASELINE config C5 (stress), one GPU's share: E=32, H=400, 1M rows / 8 GPUs = 125k rows per GPU,
-    horizon 5, fp32 or bf16 ensemble (synthetic weights; halfcheetah dims)."""
-    import torch
-    from mopo_amd.bnn import construct_model
-    from mopo_amd.replay_pool import SimpleReplayPool
-    from mopo_amd.rollout import ModelRollout, init_sac_params
-    E5, H5, B, h = 32, 400, 125000, 5
-    rs = np.random.RandomState(4)
-    env_obs = rs.normal(size=(ENV_ROWS, O)).astype(np.float32)
-    model = construct_model(obs_dim=O, act_dim=A, hidden_dim=H5, num_networks=E5, num_elites=5,
-                            separate_mean_var=True, seed=1, dtype=dtype)
-    mats = model.get_params()
-    x = np.concatenate([env_obs, rs.uniform(-1, 1, (ENV_ROWS, A))], 1)
-    mats[0] = x.mean(0, keepdims=True).astype(np.float32)
-    mats[1] = x.std(0, keepdims=True).astype(np.float32)
-    model.set_params(mats)
-    model.set_elites([0, 1, 2, 3, 4])
-    pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=2 * h * B)
-    ro = ModelRollout(model, B, h)
-    pi = torch.from_numpy(init_sac_params(O, A, HP, seed=2)).to(dev)
-    env = torch.from_numpy(env_obs).to(dev)
-    ro.run(env, pi, pool, B, h, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=0)
-    torch.cuda.synchronize()
-    reps = 2
-    t0 = time.perf_counter()
-    tot = [ro.run(env, pi, pool, B, h, 0, 1.0, [0, 1, 2, 3, 4], seed=88, epoch=1 + i) for i in range(reps)]
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    n = int(sum(int(t.sum().item()) for t in tot))
-    flop_row = 2 * E5 * ((O + A) * H5 + 3 * H5 * H5 + 2 * H5 * (O + 1))
-    v = n / dt
-    out = {'metric': 'model-rollout transitions/s (C5 stress, one GPU of eight%s)' % (', bf16 ensemble' if dtype == 'bf16' else ''),
-           'value': v, 'unit': 'transitions/s', 'dtype': 'fp32' if dtype == 'fp32' else 'bf16 (f32 accumulate)',
-           'ms_per_rollout': dt / reps * 1e3,
-           'config': {'workload': 'E=32, H=400, obs=17, act=6, rollout_batch=125000 per GPU (1M / 8), horizon=5',
-                      'rollout_batch_per_gpu': B, 'horizon': h},
-           'bnn_flop_per_row': flop_row, 'ensemble_tflops_lower_bound': v * flop_row / 1e12}
-    if dtype == 'bf16':
-        out['bf16_peak_tflops'] = BF16_PEAK_TFLOPS
-    else:
-        out['f32_peak_tflops'] = MFMA_F32_PEAK_TFLOPS
+    share = ' (one GPU of eight: %d of %d rows)' % (a2.batch, spec['B_total']) if spec.get('sharded') else ''
+    out = {'metric': 'model-rollout transitions/s (%s: %s%s)' % (name, spec['name'], share), 'value': v,
+           'unit': 'transitions/s', 'dtype': DTYPE_DESC[dtype], 'ms_per_rollout': dt / reps * 1e3,
+           'config': {'workload': 'E=%d, H=%d, obs=17, act=6, rollout_batch=%d per GPU, horizon=%d, %s terminations, '
+                                  'penalty_coeff=%g, env pool %d rows' % (spec['E'], spec['H'], a2.batch, spec['h'],
+                                                                           spec['domain'], spec['penalty'],
+                                                                           spec['env_rows']),
+                      'rollout_batch_per_gpu': a2.batch, 'horizon': spec['h']},
+           'bnn_flop_per_row': fr,
+           # rows per step shrink under terminations: transitions x flop/row bounds the ensemble rate from above
+           'ensemble_algorithmic_tflops': v * fr / 1e12}
     return out
 
 
@@ -351,12 +345,30 @@ def cpu_baseline_train(args):
     for _ in range(n):
         st.step(X, Y, np.float32)
     dt = time.perf_counter() - t0
-    return {'value': n / dt, 'unit': 'grad-steps/s', 'cores': 16, 'kind': 'port',
+    return {'value': n / dt, 'unit': 'grad-steps/s', 'cores': blas_threads(), 'kind': 'port',
             'sample': 'oracle numpy BNN train step (bnn.py:241-249 loss, hand backward, TF1 Adam), E=7, H=200, '
                       'batch 256: %d steps in %.2f s' % (n, dt)}
 
 
 SAC_DIAG = {}
+
+
+def sac_roofline(rate):
+    """one step is 0.59 GFLOP of GEMM work (forward + backward of the 8 MLP instances,
+    oracle.sac.flops_per_step) and ~9.6 MB of parameter / Adam / target traffic; the floor is the larger
+    of FLOP / f32 MFMA peak and bytes / HBM peak."""
+    n, H_ = 256, HP
+    pi_f, q_f = O * H_ + H_ * H_ + 2 * H_ * A, (O + A) * H_ + H_ * H_ + H_          # MACs per sample
+    fwd = 2 * pi_f + 6 * q_f                       # pi(s), pi(s'), Q1/Q2 at (s, a), (s, pi(s)), target (s', pi')
+    bwd = 2 * pi_f + 2 * (2 * q_f) + 2 * q_f      # pi params + input; Q1, Q2 params + input; Q*(s, pi) input
+    fl = 2 * n * (fwd + bwd)
+    n_par = (O * H_ + H_ + H_ * H_ + H_ + 2 * (H_ * A + A)) + 2 * ((O + A) * H_ + H_ + H_ * H_ + H_ + H_ + 1)
+    by = n_par * 4 * 11     # params read + write, grads, Adam m / v read + write, target read + write
+    floor_us = max(fl / (MFMA_F32_PEAK_TFLOPS * 1e12), by / 8e12) * 1e6
+    us = 1e6 / rate
+    return {'bound': 'latency (launch / dependency chain)', 'flop_per_step': fl, 'bytes_per_step': by,
+            'floor_us': floor_us, 'achieved_us': us, 'frac': floor_us / us,
+            'note': 'frac = max(FLOP / 157.3 TF f32 MFMA, bytes / 8 TB/s HBM) floor over the measured step time'}
 
 
 def sac_leg(args, pool, env, dev, world):
@@ -451,12 +463,14 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     sac_rate = sac_leg(args, pool, env, dev, world)
-    c3 = c3_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None
-    c5 = c5_leg(args, dev) if (rank == 0 and world == 1 and not args.no_c3) else None
-    c5b = c5_leg(args, dev, 'bf16') if (rank == 0 and world == 1 and not args.no_c3) else None
-    tr = train_leg(args, env) if (rank == 0 and world == 1 and args.train_epochs > 0) else None
+    extra = {}
+    if rank == 0 and world == 1 and not args.no_c3 and args.config == 'C2':
+        for key, name, dt in (('C3', 'C3', 'bf16'), ('C4_per_gpu', 'C4', 'f16x3'), ('C5_per_gpu', 'C5', 'fp32'),
+                              ('C5_f16x3_per_gpu', 'C5', 'f16x3'), ('C5_bf16_per_gpu', 'C5', 'bf16')):
+            extra[key] = config_leg(args, dev, name, dt)
+    tr = train_leg(args, env) if (rank == 0 and world == 1 and args.train_epochs > 0 and args.config == 'C2') else None
     alts = {}
-    if rank == 0 and world == 1 and not args.no_alt_dtypes:
+    if rank == 0 and world == 1 and not args.no_alt_dtypes and args.config == 'C2':
         for dt_alt in ('fp32', 'bf16x6', 'f16x3', 'bf16x3'):
             if dt_alt != args.ensemble_dtype:
                 alts[dt_alt] = alt_headline_leg(args, dev, dt_alt)
@@ -470,26 +484,31 @@ def main():
                                                                   'compact', 'advance'])}
     value = total / dt
     traffic = pmc_traffic(args)
+    spec = CONFIGS[args.config]
     out = {
-        'metric': 'model-rollout transitions/s (halfcheetah-mixed)',
+        'metric': 'model-rollout transitions/s (halfcheetah-mixed)' if args.config == 'C2' else
+                  'model-rollout transitions/s (%s: %s)' % (args.config, spec['name']),
         'value': value, 'unit': 'transitions/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
         'dtype': DTYPE_DESC[args.ensemble_dtype], 'data': 'synthetic (random-init weights, N(0,1) env pool; D4RL/.mat unavailable offline)',
-        'config': {'workload': 'halfcheetah_mixed rollout: E=7 (5 elites), H=200 smv, obs=17, act=6, '
-                               'rollout_batch=%d per GPU, horizon=%d, penalty_coeff=1.0, learned-var penalty'
-                               % (args.batch, args.horizon),
+        'config': {'workload': '%s rollout: E=%d (5 elites), H=%d smv, obs=17, act=6, rollout_batch=%d per GPU, '
+                               'horizon=%d, penalty_coeff=%g, learned-var penalty, env pool %d rows'
+                               % (args.config, spec['E'], spec['H'], args.batch, args.horizon, spec['penalty'],
+                                  spec['env_rows']),
                    'rollout_batch_per_gpu': args.batch, 'horizon': args.horizon, 'parallelism': 'dp%d' % world},
-        'roofline': {**roofline_of(args.ensemble_dtype, rows_per_launch, bnn_ms), 'traffic': traffic,
+        'roofline': {**roofline_of(args.ensemble_dtype, rows_per_launch, bnn_ms, spec_flop_row(spec)),
+                     'traffic': traffic,
                      'traffic_note': 'HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction, '
                                      'MI355X_MICROARCH.md HBM) from the committed --pmc passes, '
                                      + os.path.relpath(PMC_SUMMARY, ROOT) + ' (same workload)'},
         'kernel_ms_avg': kernel_ms,
         'sac': {'metric': 'SAC grad-steps/s (batch 256 = 12 env + 244 model rows, mopo.py:801-850)',
                 'per_gpu': sac_rate, 'aggregate_replicas': sac_rate * world, 'steps_timed': args.sac_steps,
-                'us_per_step': 1e6 / sac_rate, **SAC_DIAG, 'parallelism': 'replicas only (one independent learner per GPU)'},
+                'us_per_step': 1e6 / sac_rate, **SAC_DIAG, 'parallelism': 'replicas only (one independent learner per GPU)',
+                'roofline': sac_roofline(sac_rate)},
     }
-    if c3 is not None:
-        out['extra_configs'] = {'C3': c3, 'C5_per_gpu': c5, 'C5_bf16_per_gpu': c5b}
+    if extra:
+        out['extra_configs'] = extra
     if alts:
         out['headline_other_dtypes'] = alts
     if tr is not None:
@@ -505,23 +524,28 @@ def main():
         torch.distributed.destroy_process_group()
 
 
+# the ensemble-forward launch of each dtype at the C2 shapes (E=7, H=200, obs 17 + act 6), rollout mode
+ENSEMBLE_KERNEL = {'fp32': 'mopo::bnn_fwd_kernel<2, 13, 3, 1, 1, 4, 2, 2>',
+                   'f16x3': 'mopo::bnn_fwd_f16s_kernel<14, 3, 1, 4, 1>',
+                   'bf16x6': 'mopo::bnn_fwd_bf16_kernel<14, 3, 1, 4, 3, 1>',
+                   'bf16x3': 'mopo::bnn_fwd_bf16_kernel<14, 3, 1, 4, 2, 1>',
+                   'bf16': 'mopo::bnn_fwd_bf16_kernel<14, 3, 1, 4, 1, 1>'}
+
+
+def workload_key(args):
+    return '%s B=%d h=%d dtype=%s' % (args.config, args.batch, args.horizon, args.ensemble_dtype)
+
+
 def pmc_traffic(args):
-    """HBM bytes per bnn_fwd launch from the committed PMC summary (scripts/pmc.sh, default workload)."""
-    if (args.batch, args.horizon) != (50000, 5) or not os.path.exists(PMC_SUMMARY):
+    """HBM bytes per ensemble launch from the committed PMC summary (scripts/pmc.sh): only when that
+    summary was collected on this exact workload and names this dtype's kernel; else None."""
+    if not os.path.exists(PMC_SUMMARY):
         return None
-    ks = json.load(open(PMC_SUMMARY))['kernels']
-    P = SPLIT.get(args.ensemble_dtype, (0, 0))[0]
-    for k, v in ks.items():
-        if 'hbm_bytes' not in v:
-            continue
-        if P == 0 and k.startswith('mopo::bnn_fwd_kernel<2, 13,'):
-            return v['hbm_bytes']
-        # bnn_fwd_bf16_kernel<hidden tiles, ..., parts, ...>: H=200 -> 14 tiles; 5th argument = bf16 parts
-        if P > 0 and k.startswith('mopo::bnn_fwd_bf16_kernel<14,'):
-            targs = [a.strip() for a in k.split('<', 1)[1].rstrip('>').split(',')]
-            if len(targs) >= 5 and targs[4] == str(P):
-                return v['hbm_bytes']
-    return None
+    d = json.load(open(PMC_SUMMARY))
+    if d.get('workload') != workload_key(args):
+        return None
+    v = d['kernels'].get(ENSEMBLE_KERNEL.get(args.ensemble_dtype, ''), {})
+    return v.get('hbm_bytes')
 
 
 from ctypes import c_double as C_double, c_int64 as C_int64  # noqa: E402

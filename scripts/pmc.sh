@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --sac-steps 50"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --sac-steps 50 --no-c3 --no-alt-dtypes --train-epochs 0"
 # one stream: every ensemble launch is the 50k-row launch bench.py prices (roofline.avg_launch_ms)
 export MOPO_ROLLOUT_SPLIT=1
 cd /tmp
@@ -17,3 +17,5 @@ for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_
   echo "pass $i ($C) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$R/gpurun_out/pmc$i.log"; exit $rc; fi
 done
+cd "$R" && python scripts/pmc_summary.py gpurun_out/pmc_summary.json gpurun_out \
+  "$(python -c 'import sys; sys.argv=["bench.py"]; import bench; print(bench.workload_key(bench.parse()))')"

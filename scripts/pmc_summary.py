@@ -52,9 +52,13 @@ def summarize(agg):
 if __name__ == '__main__':
     dst = sys.argv[1]
     src = sys.argv[2] if len(sys.argv) > 2 else 'gpurun_out'
+    # the workload the passes ran (bench.py workload_key of that run): bench.py reports a kernel's
+    # traffic only for the same workload
+    workload = sys.argv[3] if len(sys.argv) > 3 else None
     s = summarize(load(src))
     s = {k: v for k, v in s.items() if 'mopo::' in k}
     json.dump({'source': 'rocprofv3 --pmc passes of scripts/pmc.sh (bench.py --steps 3 --warmup 1 '
-                         '--sac-steps 50, default workload)', 'kernels': s}, open(dst, 'w'), indent=1)
+                         '--sac-steps 50, default workload)', 'workload': workload, 'kernels': s}, open(dst, 'w'),
+              indent=1)
     for k, v in s.items():
         print(k, {a: round(b, 4) if isinstance(b, float) else b for a, b in v.items()})

@@ -476,22 +476,29 @@ def test_empty_batches():
     assert steps.cpu().numpy().tolist() == [0, 0, 0] and pool.size == 0
 
 
-@pytest.mark.parametrize('domain,dtype', [('halfcheetah', 'fp32'), ('walker2d', 'fp32'), ('halfcheetah', 'bf16x6'),
-                                          ('walker2d', 'bf16x6')])
-def test_full_size_perf_mode_rows_vs_oracle(domain, dtype):
-    """The headline workload at full size (E=7, H=200, B=50,000, h=5, learned-var penalty, perf-mode
-    Philox streams; halfcheetah: split rollout, walker2d: order-preserving compaction between steps):
-    192 sampled rows are recomputed end to end by the oracle from the restated Philox streams
-    (oracle/rng.py) and compared at their pool positions.  Start rows bit-exact, terminals
-    bit-exact, floats at the parity tolerance.  Under compaction a row's position at step i+1 is its
-    rank among step i's survivors (mopo.py:758), taken from the device's own terminal flags of the
-    other rows (the sampled rows' flags are checked against the oracle)."""
+@pytest.mark.parametrize('domain,dtype,E,H,B,h', [
+    ('halfcheetah', 'fp32', 7, 200, 50000, 5), ('walker2d', 'fp32', 7, 200, 50000, 5),
+    ('halfcheetah', 'bf16x6', 7, 200, 50000, 5), ('walker2d', 'bf16x6', 7, 200, 50000, 5),
+    ('halfcheetah', 'f16x3', 7, 200, 50000, 5), ('walker2d', 'f16x3', 7, 200, 50000, 5),   # C2 (headline)
+    ('walker2d', 'bf16', 7, 200, 100000, 1),                                               # C3
+    ('halfcheetah', 'fp32', 32, 400, 125000, 5), ('halfcheetah', 'f16x3', 32, 400, 125000, 5)])  # C5 per GPU
+def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h):
+    """BASELINE workloads at full size (C2: E=7, H=200, B=50,000, h=5; C3: walker2d, bf16, B=100,000, h=1;
+    C5: one GPU's share, E=32, H=400, B=125,000, h=5), learned-var penalty, perf-mode Philox streams
+    (halfcheetah: split rollout, walker2d: order-preserving compaction between steps): 192 sampled rows
+    are recomputed end to end by the oracle from the restated Philox streams (oracle/rng.py) and
+    compared at their pool positions.  Start rows bit-exact, terminals bit-exact (bf16: except where the
+    oracle's next state is within the bf16 tolerance of a walker bound), floats at the parity tolerance
+    (5e-5; bf16 3e-2).  Under compaction a row's position at step i+1 is its rank among step i's
+    survivors (mopo.py:758), taken from the device's own terminal flags of the other rows (the sampled
+    rows' flags are checked against the oracle)."""
     import torch
     from oracle import rng as orng
     from mopo_amd.replay_pool import SimpleReplayPool
     from mopo_amd.rollout import ModelRollout, init_sac_params, split_params
     from mopo_amd.static import static_fns
-    E, H, B, h, O, A = 7, 200, 50000, 5, 17, 6
+    O, A = 17, 6
+    tol = 3e-2 if dtype == 'bf16' else 5e-5
     seed, epoch = 0x1234567890ab, 3
     rs = np.random.RandomState(21)
     env_n = 40000
@@ -533,15 +540,22 @@ def test_full_size_perf_mode_rows_vs_oracle(domain, dtype):
         got = {k: v[pos].cpu().numpy() for k, v in pool.fields.items()}
         if i == 0:   # the start rows: an exact copy of the Philox-chosen env rows
             np.testing.assert_array_equal(got['observations'], obs.astype(np.float32))
-        close(got['observations'], obs, 5e-5)
-        close(got['actions'], act, 5e-5)
-        close(got['next_observations'], nobs, 5e-5)
-        close(got['rewards'], rew, 5e-5)
-        np.testing.assert_array_equal(got['terminals'], term)
+        close(got['observations'], obs, tol)
+        close(got['actions'], act, 5e-5 if i == 0 else tol)
+        close(got['next_observations'], nobs, tol)
+        close(got['rewards'], rew, tol)
+        bad = got['terminals'][:, 0] != term[:, 0]
+        if dtype == 'bf16' and bad.any():   # a bf16 next state may land on the other side of a bound
+            hh, an = nobs[bad, 0], nobs[bad, 1]
+            near = (np.abs(hh[:, None] - np.array([0.8, 2.0])).min(1) < tol * (1 + np.abs(hh))) | \
+                   (np.abs(np.abs(an) - 1.0) < tol * (1 + np.abs(an)))
+            assert near.all()
+        else:
+            np.testing.assert_array_equal(got['terminals'], term)
         checked += len(rows)
         live = ~term[:, 0]
         keep = ~term_dev[base:base + steps[i]]
         rank = np.cumsum(keep) - keep
         base += steps[i]
         rows, idx, obs = rows[live], rank[idx[live]], nobs[live]
-    assert checked >= (192 * h if domain == 'halfcheetah' else 192 + 64)   # walker: >= 1 compacted step
+    assert checked >= (192 * h if domain == 'halfcheetah' else min(192 * h, 192 + 64))   # walker: >= 1 compacted step
