@@ -58,8 +58,8 @@ CONFIGS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=10)
-    p.add_argument('--warmup', type=int, default=2)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=10, help='untimed rollouts first (the clocks ramp up over ~20 ms)')
     p.add_argument('--batch', type=int, default=50000)
     p.add_argument('--horizon', type=int, default=5)
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -268,7 +268,7 @@ def alt_headline_leg(args, dev, dtype, reps=10):
             'unit': 'transitions/s', 'dtype': DTYPE_DESC[dtype], 'ms_per_rollout': dt / reps * 1e3}
 
 
-def config_leg(args, dev, name, dtype, reps=3):
+def config_leg(args, dev, name, dtype, reps=5, warm=3):
     """Another BASELINE config on this GPU (one rank's share of a sharded config): same synthetic
     construction and timing as the main line."""
     import torch
@@ -277,10 +277,11 @@ def config_leg(args, dev, name, dtype, reps=3):
     a2.config, a2.ensemble_dtype, a2.horizon = name, dtype, spec['h']
     a2.batch = spec['B_total'] // 8 if spec.get('sharded') else spec['B_total']
     _, pool, ro, pi, env, _ = build(a2, dev, 0, world=1)
-    rollout_step(a2, ro, pool, pi, env, None, 0, 0, 1)
+    for w in range(warm):
+        rollout_step(a2, ro, pool, pi, env, None, w, 0, 1)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    st = [rollout_step(a2, ro, pool, pi, env, None, 1 + i, 0, 1) for i in range(reps)]
+    st = [rollout_step(a2, ro, pool, pi, env, None, warm + i, 0, 1) for i in range(reps)]
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     n = int(sum(int(x.sum().item()) for x in st))
@@ -465,9 +466,9 @@ def main():
     sac_rate = sac_leg(args, pool, env, dev, world)
     extra = {}
     if rank == 0 and world == 1 and not args.no_c3 and args.config == 'C2':
-        for key, name, dt in (('C3', 'C3', 'bf16'), ('C4_per_gpu', 'C4', 'f16x3'), ('C5_per_gpu', 'C5', 'fp32'),
-                              ('C5_f16x3_per_gpu', 'C5', 'f16x3'), ('C5_bf16_per_gpu', 'C5', 'bf16')):
-            extra[key] = config_leg(args, dev, name, dt)
+        for key, name, dty in (('C3', 'C3', 'bf16'), ('C4_per_gpu', 'C4', 'f16x3'), ('C5_per_gpu', 'C5', 'fp32'),
+                               ('C5_f16x3_per_gpu', 'C5', 'f16x3'), ('C5_bf16_per_gpu', 'C5', 'bf16')):
+            extra[key] = config_leg(args, dev, name, dty)
     tr = train_leg(args, env) if (rank == 0 and world == 1 and args.train_epochs > 0 and args.config == 'C2') else None
     alts = {}
     if rank == 0 and world == 1 and not args.no_alt_dtypes and args.config == 'C2':
