@@ -437,8 +437,11 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
 // split_f16_scaled / row_scale), 3 products per k-group on v_mfma_f32_16x16x32_f16, f32 accumulate and
 // f32 epilogues.  Each layer's output is acc * (2^-k_w / s_row): the weight scale of the layer and
 // member, the row scale of the layer's input (both exact powers of two), folded into the bias add.
+#ifndef BNN_F16_MINB
+#define BNN_F16_MINB 2  // 4-wave workgroups per CU: 2 (170 VGPRs, no scratch) measured 0.5 % faster than 3 (28 B/lane spill)
+#endif
 template <int NB2, int NBO, int MODE, int WAVES, int PS = 1>
-__global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_SPLIT_MINB * 4 / WAVES) void bnn_fwd_f16s_kernel(
+__global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES) void bnn_fwd_f16s_kernel(
     const BnnDev w, const FwdArgs a) {
   constexpr int P = 2, KG = NB2 / 2;
   constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
