@@ -59,12 +59,54 @@ def tf_init_params(E, obs_dim, act_dim, hidden, separate_mean_var=True, rng=None
     return arrs
 
 
+# ---- structure files ('<name>.nns', bnn.py:559-582 / 594-625): one repr(FC) per line, fc.py:47-51
+WEIGHT_DECAYS = (0.000025, 0.00005, 0.000075, 0.000075, 0.0001)   # constructor.py:30-34
+VAR_WEIGHT_DECAY = 0.0001                                         # constructor.py:36
+
+
+def fc_repr(output_dim, input_dim, activation, weight_decay, ensemble_size):
+    """FC.__repr__ (fc.py:47-51)."""
+    return 'FC(output_dim={!r}, input_dim={!r}, activation={!r}, weight_decay={!r}, ensemble_size={!r})'.format(
+        output_dim, input_dim, activation, weight_decay, ensemble_size)
+
+
+def structure_lines(E, obs_dim, act_dim, hidden):
+    """The smv structure construct_model builds (constructor.py:28-36): (mean-layer lines, var-layer lines)."""
+    IN, D = obs_dim + act_dim, obs_dim + 1
+    dims = [IN] + [hidden] * N_HIDDEN
+    mean = [fc_repr(hidden, dims[i], 'swish', WEIGHT_DECAYS[i], E) for i in range(N_HIDDEN)]
+    mean.append(fc_repr(D, hidden, None, WEIGHT_DECAYS[N_HIDDEN], E))
+    return mean, [fc_repr(D, hidden, None, VAR_WEIGHT_DECAY, E)]
+
+
+def parse_structure(path):
+    """BNN._load_structure's line parser (bnn.py:594-625): a list of FC keyword dicts."""
+    layers = []
+    with open(path) as f:
+        for line in f:
+            kw = dict(a.split('=') for a in line[3:-2].split(', '))
+            layers.append({'input_dim': int(kw['input_dim']), 'output_dim': int(kw['output_dim']),
+                           'weight_decay': None if kw['weight_decay'] == 'None' else float(kw['weight_decay']),
+                           'activation': None if kw['activation'] == 'None' else kw['activation'][1:-1],
+                           'ensemble_size': int(kw['ensemble_size'])})
+    return layers
+
+
 class BNN:
     """Device-resident probabilistic ensemble (smv or joint head), fp32 or bf16 forward."""
 
     def __init__(self, params):
         self.name = params.get('name', 'BNN')
         self.model_dir = params.get('model_dir', None)
+        if params.get('load_model', False):   # bnn.py:72-80: the structure file fixes the shapes
+            if self.model_dir is None:
+                raise ValueError('Cannot load model without providing model directory.')
+            layers = parse_structure(os.path.join(self.model_dir, '%s.nns' % self.name))
+            if len(layers) != N_HIDDEN + 1 or layers[0]['activation'] != 'swish':
+                raise ValueError('unsupported structure in %s.nns (expected 4 swish FC layers + a head)' % self.name)
+            D, IN = layers[-1]['output_dim'], layers[0]['input_dim']
+            params = dict(params, num_networks=layers[0]['ensemble_size'], hidden_dim=layers[0]['output_dim'],
+                          obs_dim=D - 1, act_dim=IN - (D - 1))
         self.num_nets = int(params.get('num_networks', 1))
         self.num_elites = int(params['num_elites'])
         self.separate_mean_var = bool(params.get('separate_mean_var', False))
@@ -82,6 +124,8 @@ class BNN:
         L.check(L.lib().mopo_bnn_create(C.byref(h), self.num_nets, self.obs_dim, self.act_dim, self.hidden_dim,
                                         int(self.separate_mean_var), _DTYPES[self.dtype]))
         self._h = h
+        if params.get('load_model', False):
+            self.load_params()                                                     # finalize: bnn.py:266-267
 
     def __del__(self):
         t = getattr(self, '_train_h', None)
@@ -138,8 +182,18 @@ class BNN:
         self.model_loaded = True
 
     def save(self, savedir, timestep):
-        """bnn.py:588-592 parameter file ('<name>_<timestep>.mat', keys '0'..'15')."""
+        """BNN.save (bnn.py:559-592): '<name>_<t>.nns' + '<name>_<t>_var.nns' (the structure, one
+        repr(FC) per line) and '<name>_<t>.mat' (keys '0'..'15' = nonoptvars + optvars)."""
         from scipy.io import savemat
+        if not self.separate_mean_var:
+            # the reference's joint-head branch (bnn.py:571-576) writes the halved last layer once per
+            # hidden layer, a file its own _load_structure cannot read back; only smv is written here
+            raise NotImplementedError('BNN.save: structure files are written for separate_mean_var=True only')
+        savedir = self.model_dir if savedir is None else savedir
+        mean, var = structure_lines(self.num_nets, self.obs_dim, self.act_dim, self.hidden_dim)
+        for suffix, lines in (('', mean), ('_var', var)):
+            with open(os.path.join(savedir, '{}_{}{}.nns'.format(self.name, timestep, suffix)), 'w+') as f:
+                f.write(''.join('%s\n' % ln for ln in lines))
         savemat(os.path.join(savedir, '{}_{}.mat'.format(self.name, timestep)),
                 {str(i): m for i, m in enumerate(self._mats)})
 

@@ -22,13 +22,67 @@ LOG_KEYS = ['Q/q1_loss', 'sac_Q/q2_loss', 'sac_Q/q1', 'sac_Q/q2', 'sac_pi/alpha'
             'sac_pi/logp_pi', 'sac_pi/pi_global_norm', 'sac_Q/q_global_norm', 'policy_loss']
 
 
+def _space_dim(space):
+    shp = getattr(space, 'shape', None)
+    if shp is None or len(shp) != 1:
+        raise ValueError('expected a flat Box space with a 1-D shape, got %r' % (space,))
+    return int(shp[0])
+
+
 class SAC:
-    def __init__(self, obs_dim, act_dim, hidden=256, batch_size=256, real_ratio=0.05, lr=3e-4, discount=0.99,
-                 tau=5e-3, reward_scale=1.0, target_entropy='auto', params=None, log_alpha=0.0, seed=2,
-                 reparameterize=True, use_graph=True):
+    """Two constructor forms:
+
+    * ``SAC(obs_dim, act_dim, hidden=256, ...)`` -- the dims directly;
+    * ``SAC(training_environment, evaluation_environment, policy, Qs, pool, plotter=None,
+      tf_summaries=False, lr=3e-4, reward_scale=1.0, target_entropy='auto', discount=0.99, tau=5e-3,
+      target_update_interval=1, action_prior='uniform', reparameterize=False, store_extra_policy_info=False,
+      save_full_state=False, **kwargs)`` -- softlearning/algorithms/sac.py:26-47: the dims come from the
+      environment's spaces, the hidden width from the policy / Qs (``hidden_layer_sizes`` or
+      ``hidden_sizes``, default 256 x 2); ``pool`` becomes the default env pool of ``_do_training``.
+    """
+
+    def __init__(self, obs_dim, act_dim=None, *args, **kwargs):
+        if not isinstance(obs_dim, (int, np.integer)):
+            self._init_softlearning(obs_dim, act_dim, *args, **kwargs)
+        else:
+            self._init(obs_dim, act_dim, *args, **kwargs)
+
+    def _init_softlearning(self, training_environment, evaluation_environment, policy=None, Qs=(), pool=None,
+                           plotter=None, tf_summaries=False, lr=3e-4, reward_scale=1.0, target_entropy='auto',
+                           discount=0.99, tau=5e-3, target_update_interval=1, action_prior='uniform',
+                           reparameterize=False, store_extra_policy_info=False, save_full_state=False,
+                           batch_size=256, real_ratio=1.0, **kwargs):
+        if action_prior != 'uniform':
+            raise NotImplementedError("action_prior must be 'uniform' (sac.py:255-262 normal prior not on this path)")
+        if target_update_interval != 1:
+            raise NotImplementedError('target_update_interval != 1')
+        if store_extra_policy_info:
+            raise NotImplementedError('store_extra_policy_info')
+        env = training_environment
+        obs_space = getattr(env, 'active_observation_shape', None)
+        obs_dim = int(obs_space[0]) if obs_space is not None else _space_dim(env.observation_space)
+        act_dim = _space_dim(env.action_space)
+        hs = None
+        for src in (policy, *(Qs or ())):
+            hs = hs or getattr(src, 'hidden_layer_sizes', None) or getattr(src, '_hidden_layer_sizes', None) or \
+                getattr(src, 'hidden_sizes', None)
+        hs = list(hs or [256, 256])
+        if len(hs) != 2 or hs[0] != hs[1]:
+            raise NotImplementedError('policy / Q hidden sizes must be [H, H]')
+        self._training_environment, self._evaluation_environment = training_environment, evaluation_environment
+        self._policy, self._Qs, self._pool, self._plotter = policy, Qs, pool, plotter
+        self._init(obs_dim, act_dim, hidden=hs[0], batch_size=batch_size, real_ratio=real_ratio, lr=lr,
+                   discount=discount, tau=tau, reward_scale=reward_scale, target_entropy=target_entropy,
+                   reparameterize=reparameterize, **kwargs)
+
+    def _init(self, obs_dim, act_dim, hidden=256, batch_size=256, real_ratio=0.05, lr=3e-4, discount=0.99,
+              tau=5e-3, reward_scale=1.0, target_entropy='auto', params=None, log_alpha=0.0, seed=2,
+              reparameterize=True, use_graph=True):
         if not reparameterize:
-            raise NotImplementedError('MOPO only implements the reparameterized policy loss (mopo.py:370-374)')
+            raise NotImplementedError('only the reparameterized policy loss is implemented (mopo.py:370-374; '
+                                      'every config sets reparameterize=True, examples/config/d4rl/base.py)')
         self.obs_dim, self.act_dim, self.hidden = obs_dim, act_dim, hidden
+        self._pool = getattr(self, '_pool', None)
         self.batch_size = int(batch_size)
         self._real_ratio = real_ratio
         self.n_env = int(self.batch_size * real_ratio)                       # mopo.py:803
@@ -99,11 +153,19 @@ class SAC:
         d['sac_pi/std'] = d['sac_pi/logp_pi']   # the reference logs logp_pi under this key (mopo.py:463)
         return d
 
-    def _do_training(self, iteration, env_pool, model_pool, n_steps=1, seed=0, idx=None, eps_s=None, eps_n=None,
-                     stream=None):
+    def _do_training(self, iteration, env_pool=None, model_pool=None, n_steps=1, seed=0, idx=None, eps_s=None,
+                     eps_n=None, stream=None):
         """``n_steps`` x (_training_batch + _do_training + _update_target) on the device.  With
-        injected ``idx`` ([batch] rows: first n_env index the env pool) and policy noise, one step."""
+        injected ``idx`` ([batch] rows: first n_env index the env pool) and policy noise, one step.
+        ``_do_training(iteration, batch)`` with a batch dict (sac.py:340-349 / mopo.py:834-850): one step
+        on exactly those rows (host or device arrays, ``batch_size`` rows)."""
         import torch
+        if isinstance(env_pool, dict):
+            return self._do_training_batch(iteration, env_pool, eps_s=eps_s, eps_n=eps_n, stream=stream)
+        if env_pool is None:
+            env_pool = self._pool
+        if model_pool is None:
+            model_pool = env_pool
         keep = []
 
         def dp(x, dt):
@@ -118,6 +180,39 @@ class SAC:
                                       dp(eps_n, torch.float32), L.stream_ptr(stream)))
         self._keepalive = keep
         self._num_train_steps += n_steps
+
+    def _do_training_batch(self, iteration, batch, eps_s=None, eps_n=None, stream=None):
+        """One step on the given batch: its rows are staged in two scratch pools (env part first,
+        mopo.py:815-816 order) and drawn back by index, so the device step sees exactly this batch."""
+        import torch
+        from .replay_pool import SimpleReplayPool
+        n = int(np.asarray(batch['observations']).shape[0] if not torch.is_tensor(batch['observations'])
+                else batch['observations'].shape[0])
+        if n != self.batch_size:
+            raise ValueError('batch has %d rows, the step was built for %d' % (n, self.batch_size))
+        cut = self.n_env
+        pools = []
+        for lo, hi in ((0, cut), (cut, n)):
+            p = SimpleReplayPool(obs_dim=self.obs_dim, act_dim=self.act_dim, max_size=max(hi - lo, 1))
+            p.add_samples({k: v[lo:hi] for k, v in batch.items() if k in p.fields})
+            pools.append(p)
+        idx = np.concatenate([np.arange(cut), np.arange(n - cut)]).astype(np.int64)
+        self._do_training(iteration, pools[0], pools[1], idx=idx, seed=iteration,
+                          eps_s=eps_s if eps_s is not None else np.random.normal(size=(n, self.act_dim)),
+                          eps_n=eps_n if eps_n is not None else np.random.normal(size=(n, self.act_dim)),
+                          stream=stream)
+        return self.logs()
+
+    def state_dict(self):
+        """Device copies of everything a step reads (the saveables of sac.py:418-427 and the targets)."""
+        n = self.n_params
+        return {'params': self._copy(0, n + 1), 'target': self._copy(1, n), 'adam_m': self._copy(2, n + 1),
+                'adam_v': self._copy(3, n + 1)}
+
+    def load_state_dict(self, state):
+        n = self.n_params
+        for w, (k, c) in enumerate((('params', n + 1), ('target', n), ('adam_m', n + 1), ('adam_v', n + 1))):
+            self._copy(w, c, state[k].contiguous(), to_handle=True)
 
     def _training_batch(self, env_pool, model_pool, batch_size=None, as_numpy=False):
         """mopo.py:801-821 as a host-visible batch (the device step assembles the same batch itself):
@@ -137,6 +232,7 @@ class SAC:
     def _update_target(self):
         """Folded into every device step (target_update_interval=1, mopo.py:843-845)."""
 
-    def get_diagnostics(self):
+    def get_diagnostics(self, *args, **kwargs):
+        """mopo.py:900-905 keys (the arguments of sac.py's get_diagnostics are accepted and unused)."""
         lg = self.logs()
         return OrderedDict({'Q_loss': (lg['Q/q1_loss'] + lg['sac_Q/q2_loss']) / 2, 'alpha': lg['sac_pi/alpha']})

@@ -327,8 +327,36 @@ def sac_case(refs, name, O, A, H, n, seed, steps=3, term_frac=0.2, compact=False
     np.savez_compressed(os.path.join(HERE, 'ref_sac_%s.npz' % name), **out)
 
 
+def bnn_save_case(refs, E=3, H=32, seed=41):
+    """BNN.save (bnn.py:559-592) executed from the reference on a stand-in model: the structure files
+    ('<name>_<t>.nns', '<name>_<t>_var.nns': one repr(FC) per line) and the '.mat' of nonoptvars +
+    optvars, written to tests/golden/ref_save/."""
+    utils, fc, bnn, _ = refs
+    O, A = 17, 6
+    rs = np.random.RandomState(seed)
+    p = obnn.init_params(E, O, A, hidden=H, seed=seed, smv=True, inputs=rs.normal(size=(200, O + A)))
+    obj = build_bnn(refs, p, E, O, A, H, True, torch.float32)
+    obj.finalized, obj.name, obj.model_dir = True, 'BNN', None
+    obj.nonoptvars = obj.scaler.get_vars()
+    obj.optvars = []
+    for layer in obj.layers + obj.var_layers:
+        obj.optvars.extend(layer.get_vars())
+    obj.optvars += [obj.max_logvar, obj.min_logvar]
+    obj._sess = tfstub.Session()   # BNN.sess is a property over _sess
+    out = os.path.join(HERE, 'ref_save')
+    os.makedirs(out, exist_ok=True)
+    bnn.BNN.save(obj, out, 0)
+    # the inputs / outputs of one predict with these weights, for the load test
+    x = rs.normal(size=(32, O + A)).astype(np.float32)
+    xin = tfstub.w(torch.as_tensor(x))
+    mean, var = bnn.BNN._compile_outputs(obj, xin)
+    np.savez_compressed(os.path.join(out, 'predict.npz'), x=x, mean=tfstub.u(mean).detach().numpy(),
+                        var=tfstub.u(var).detach().numpy())
+
+
 def main():
     refs = load_reference()
+    bnn_save_case(refs)
     # ensemble forward: the headline shapes and the stress shape (weights regenerated from the seed
     # for the large ones), the joint-head branch, f64 inputs (the rollout feeds f64 next_obs)
     bnn_forward_case(refs, 'E7_H200', 7, 200, 96, True, 11, store_weights=False)

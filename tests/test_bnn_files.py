@@ -1,0 +1,66 @@
+"""BNN on-disk format (bnn.py:559-625): the structure files and the .mat written by the reference's own
+BNN.save (tests/golden/ref_save, made by make_ref_vectors.py) against this package's writer / parser.
+CPU: text and keys; GPU: load -> predict vs the reference graph's outputs, save -> reload round trip."""
+import os
+
+import numpy as np
+import pytest
+
+REF = os.path.join(os.path.dirname(__file__), 'golden', 'ref_save')
+
+
+def _lines(path):
+    with open(path) as f:
+        return f.read()
+
+
+def test_structure_text_matches_reference_save():
+    from mopo_amd.bnn import structure_lines
+    mean, var = structure_lines(3, 17, 6, 32)
+    assert _lines(os.path.join(REF, 'BNN_0.nns')) == ''.join(l + '\n' for l in mean)
+    assert _lines(os.path.join(REF, 'BNN_0_var.nns')) == ''.join(l + '\n' for l in var)
+
+
+def test_parse_reference_structure():
+    from mopo_amd.bnn import parse_structure
+    layers = parse_structure(os.path.join(REF, 'BNN_0.nns'))
+    assert [l['output_dim'] for l in layers] == [32, 32, 32, 32, 18]
+    assert [l['input_dim'] for l in layers] == [23, 32, 32, 32, 32]
+    assert [l['activation'] for l in layers] == ['swish'] * 4 + [None]
+    assert [l['weight_decay'] for l in layers] == [2.5e-05, 5e-05, 7.5e-05, 7.5e-05, 0.0001]
+    assert all(l['ensemble_size'] == 3 for l in layers)
+    var = parse_structure(os.path.join(REF, 'BNN_0_var.nns'))
+    assert len(var) == 1 and var[0]['output_dim'] == 18 and var[0]['input_dim'] == 32
+
+
+def test_reference_mat_keys():
+    from scipy.io import loadmat
+    d = loadmat(os.path.join(REF, 'BNN_0.mat'))
+    shapes = [d[str(i)].shape for i in range(16)]
+    assert shapes[:2] == [(1, 23), (1, 23)]                                       # scaler mu, sigma
+    assert shapes[2:12:2] == [(3, 23, 32), (3, 32, 32), (3, 32, 32), (3, 32, 32), (3, 32, 18)]
+    assert shapes[12:] == [(3, 32, 18), (3, 1, 18), (1, 18), (1, 18)]
+
+
+@pytest.mark.gpu
+def test_load_reference_save_and_round_trip(tmp_path):
+    from mopo_amd.bnn import BNN
+    m = BNN({'name': 'BNN_0', 'model_dir': REF, 'load_model': True, 'num_elites': 3, 'separate_mean_var': True})
+    assert (m.num_nets, m.hidden_dim, m.obs_dim, m.act_dim, m.model_loaded) == (3, 32, 17, 6, True)
+    z = np.load(os.path.join(REF, 'predict.npz'))
+    mean, var = m.predict(z['x'])
+    assert np.max(np.abs(mean - z['mean']) / (1 + np.abs(z['mean']))) < 2e-5
+    assert np.max(np.abs(var - z['var']) / z['var']) < 5e-5
+    m.save(str(tmp_path), 7)
+    for suffix in ('.nns', '_var.nns'):
+        assert _lines(str(tmp_path / ('BNN_0_7' + suffix))) == _lines(os.path.join(REF, 'BNN_0' + suffix))
+    from scipy.io import loadmat
+    a, b = loadmat(str(tmp_path / 'BNN_0_7.mat')), loadmat(os.path.join(REF, 'BNN_0.mat'))
+    for i in range(16):
+        np.testing.assert_array_equal(a[str(i)], b[str(i)])
+    os.rename(str(tmp_path / 'BNN_0_7.nns'), str(tmp_path / 'again.nns'))
+    os.rename(str(tmp_path / 'BNN_0_7.mat'), str(tmp_path / 'again.mat'))
+    m2 = BNN({'name': 'again', 'model_dir': str(tmp_path), 'load_model': True, 'num_elites': 3, 'separate_mean_var': True})
+    mean2, var2 = m2.predict(z['x'])
+    np.testing.assert_array_equal(mean2, mean)
+    np.testing.assert_array_equal(var2, var)

@@ -50,3 +50,16 @@ def test_module_entry_point():
                        timeout=120)
     assert r.returncode == 0, r.stderr
     assert '"penalty_coeff": 1.0' in r.stdout
+
+
+def test_console_command_entry_points():
+    """setup.py maps the `mopo` console command to mopo_amd.__main__:main (reference setup.py:14-18);
+    bin/mopo runs it from a checkout."""
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, 'setup.py')).read()
+    assert "'mopo=mopo_amd.__main__:main'" in src
+    out = subprocess.run([sys.executable, os.path.join(root, 'bin', 'mopo'), 'run_example_dry', 'examples.development',
+                          '--config=examples.config.d4rl.walker2d_mixed'], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert '"domain": "walker2d"' in out.stdout

@@ -131,3 +131,26 @@ def test_actor_vs_reference_graph(path, dtype):
                                              L.ptr(mu), dtype, L.stream_ptr()))
     assert np.abs(act.cpu().numpy() - z['actor_pi_f32']).max() < 2e-5
     assert np.abs(mu.cpu().numpy() - z['actor_mu_f32']).max() < 2e-5
+
+
+def test_softlearning_sac_api_vs_reference_graph():
+    """softlearning/algorithms/sac.py:26-47's constructor form (environment spaces, policy / Qs, pool) and
+    _do_training(iteration, batch) with a batch dict: step 0 of the reference-executed H=256 case."""
+    import types
+    from mopo_amd.sac import SAC
+    z = dict(np.load(os.path.join(GOLD, 'ref_sac_H256.npz')))
+    O, A, H, n = int(z['O']), int(z['A']), int(z['H']), int(z['n'])
+    env = types.SimpleNamespace(observation_space=types.SimpleNamespace(shape=(O,)),
+                                action_space=types.SimpleNamespace(shape=(A,)))
+    policy = types.SimpleNamespace(hidden_layer_sizes=(H, H))
+    init = np.concatenate([z['init%d' % i].ravel() for i in range(20)]).astype(np.float32)
+    sac = SAC(env, env, policy, (policy, policy), None, lr=3e-4, target_entropy=-3, reparameterize=True,
+              real_ratio=0.05, params=init)
+    assert (sac.obs_dim, sac.act_dim, sac.hidden, sac.n_env) == (O, A, H, 12)
+    b = {k: z['b0_%s' % k] for k in ('observations', 'actions', 'next_observations', 'rewards', 'terminals')}
+    lg = sac._do_training(0, b, eps_s=z['b0_noise0'][0], eps_n=z['b0_noise2'][0])
+    for key in ('Q/q1_loss', 'sac_Q/q2_loss', 'sac_pi/alpha', 'sac_pi/logp_pi', 'sac_Q/q_global_norm'):
+        ref = float(z['b0_log_%s_f32' % key.replace('/', '.')])
+        assert abs(lg[key] - ref) <= 2e-4 * abs(ref) + 1e-6, (key, lg[key], ref)
+    with pytest.raises(NotImplementedError):
+        SAC(env, env, policy, (policy,), None, reparameterize=False)
