@@ -8,8 +8,9 @@ Reference: mopo/algorithms/mopo.py — ``__init__`` (46-201), ``_train`` (490-64
 Differences that are deliberate: the rollout and the SAC steps run on the device
 (csrc/rollout.hip, csrc/sac.hip); the epoch's 1000 SAC steps are issued as one replayed hipGraph
 batch (the reference runs them one ``session.run`` at a time, with the same batch rule per step);
-MuJoCo evaluation (``_evaluation_paths``) is out of scope -- no simulator in this image -- so
-``evaluation/*`` diagnostics are absent.  The dynamics model is trained once before the epoch loop
+Evaluation rollouts (``_evaluation_paths`` / ``_evaluate_rollouts``, mopo.py:575-629) run when an
+``evaluation_environment`` (gym API) is passed -- MuJoCo is not in this image, so the caller supplies
+it; without one the ``evaluation/*`` and ``perf/*`` keys are absent.  The dynamics model is trained once before the epoch loop
 (mopo.py:526-531): one epoch when it was loaded from ``model_load_dir``, else to early stopping,
 on the device (``_train_model`` formats the env pool on the device in the holdout-permutation order).
 """
@@ -32,7 +33,8 @@ class MOPO:
                  hidden_dim=200, separate_mean_var=False, penalty_coeff=0., penalty_learned_var=False,
                  model_name=None, model_load_dir=None, deterministic=False, network_kwargs=None, epoch_length=1000,
                  n_epochs=1000, n_train_repeat=1, batch_size=256, seed=88, reparameterize=True, max_model_t=None,
-                 rollout_random=False, **kwargs):
+                 rollout_random=False, evaluation_environment=None, eval_n_episodes=10, eval_deterministic=True,
+                 max_path_length=1000, **kwargs):
         if target_update_interval != 1:
             raise NotImplementedError('target_update_interval != 1 (all D4RL configs use 1)')
         self._pool = pool                                   # device SimpleReplayPool of env data
@@ -72,6 +74,11 @@ class MOPO:
         if self._rollout_batch_size % self._world:
             raise ValueError('rollout_batch_size must be a multiple of the world size')
         self._max_model_t = max_model_t
+        self._evaluation_environment = evaluation_environment
+        self._eval_n_episodes, self._eval_deterministic = eval_n_episodes, eval_deterministic
+        self._max_path_length = max_path_length
+        from .evaluation import ref_scores
+        self.min_ret, self.max_ret = ref_scores(model_name)                              # mopo.py:115-123
         self._model_train_metrics = None
 
     # -- mopo.py:675-687
@@ -166,13 +173,30 @@ class MOPO:
         t1 = time.perf_counter()
         logs = self._do_training_repeats(self._epoch_length * self._n_train_repeat)
         t2 = time.perf_counter()
+        evaluation = self._evaluate()
+        t3 = time.perf_counter()
         diag = OrderedDict()
+        diag.update(('evaluation/' + k, evaluation[k]) for k in sorted(evaluation))
         diag.update(('model/' + k, v) for k, v in metrics.items())
         diag.update(('training/' + k, v) for k, v in logs.items())
         diag.update({'Q_loss': (logs['Q/q1_loss'] + logs['sac_Q/q2_loss']) / 2, 'alpha': logs['sac_pi/alpha'],
                      'epoch': self._epoch, 'train-steps': self._num_train_steps,
-                     'times/epoch_rollout_model': t1 - t0, 'times/train': t2 - t1})
+                     'times/epoch_rollout_model': t1 - t0, 'times/train': t2 - t1,
+                     'times/evaluation_paths': t3 - t2})
+        if evaluation:
+            from .evaluation import perf_metrics
+            diag.update(perf_metrics(evaluation, self.min_ret, self.max_ret))
         return diag
+
+    # -- mopo.py:575-584: the current policy (deterministic: tanh(mu)) in the evaluation environment
+    def _evaluate(self):
+        from .evaluation import DevicePolicy, evaluate_rollouts, evaluation_paths
+        if self._evaluation_environment is None:
+            return {}
+        policy = DevicePolicy(self._sac.policy_params_ptr, self._obs_dim, self._act_dim, self._pi_hidden,
+                              deterministic=self._eval_deterministic)
+        paths = evaluation_paths(self._evaluation_environment, policy, self._eval_n_episodes, self._max_path_length)
+        return evaluate_rollouts(paths, self._evaluation_environment) if paths else {}
 
     def train(self, n_epochs=None):
         """Generator of per-epoch diagnostics (mopo.py:650-651)."""
