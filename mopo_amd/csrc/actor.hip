@@ -176,15 +176,22 @@ __device__ __forceinline__ void bias_relu(const float* b, const f32x4 (&acc)[1][
   }
 }
 
-__device__ __forceinline__ void actor_noise(uint64_t seed, uint32_t step, int64_t uid, int A, float* z) {
-  for (int blk = 0; blk * 4 < A; ++blk) {
-    u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32) ^ ((uint32_t)blk << 20), step, RNG_ACT};
-    u32x4 r = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    float zz[4];
-    box_muller(r.x, r.y, zz[0], zz[1]);
-    box_muller(r.z, r.w, zz[2], zz[3]);
-    for (int i = 0; i < 4 && blk * 4 + i < A; ++i) z[blk * 4 + i] = zz[i];
-  }
+// Four N(0, 1) policy-noise draws (actions 4 blk .. 4 blk + 3) of row ``uid``: one Philox block.
+__device__ __forceinline__ void actor_noise4(uint64_t seed, uint32_t step, int64_t uid, int blk, float (&zz)[4]) {
+  u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32) ^ ((uint32_t)blk << 20), step, RNG_ACT};
+  u32x4 r = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  box_muller(r.x, r.y, zz[0], zz[1]);
+  box_muller(r.z, r.w, zz[2], zz[3]);
+}
+
+// Four U[-1, 1) random actions (np.random.uniform(-1, 1, act.shape), mopo.py:738), 24-bit uniforms.
+__device__ __forceinline__ void actor_uniform4(uint64_t seed, uint32_t step, int64_t uid, int blk, float (&uu)[4]) {
+  u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32) ^ ((uint32_t)blk << 20), step, RNG_ACT_UNIFORM};
+  const u32x4 r = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  uu[0] = -1.0f + 2.0f * ((float)(r.x >> 8) * 5.9604645e-8f);
+  uu[1] = -1.0f + 2.0f * ((float)(r.y >> 8) * 5.9604645e-8f);
+  uu[2] = -1.0f + 2.0f * ((float)(r.z >> 8) * 5.9604645e-8f);
+  uu[3] = -1.0f + 2.0f * ((float)(r.w >> 8) * 5.9604645e-8f);
 }
 
 #ifndef ACT_WAVES_CFG
@@ -198,39 +205,41 @@ __device__ __forceinline__ void actor_finish(const ActorArgs& a, float (&head)[A
                                              int g, int64_t row, bool ok) {
   const int O = a.O, A = a.A;
   if (g == 0 && ok) {
-    float z[16];
     const int64_t uid = a.d_uid ? a.d_uid[row] : row + a.uid_offset;
-    if (a.eps) {
-      for (int j = 0; j < A; ++j) z[j] = a.eps[row * A + j];
-    } else {
-      actor_noise(a.seed, a.step, uid, A, z);
-    }
     int64_t pos = -1;
     if (a.pool_act) pos = a.stage_base >= 0 ? a.stage_base + row : (a.pool_state[0] + a.pool_off + row) % a.pool_max;
-    float uni[16];
-    if (a.rand_act) {  // np.random.uniform(low=-1, high=1, size=act.shape) (mopo.py:738)
-      if (a.act_uni) {
-        for (int j = 0; j < A; ++j) uni[j] = a.act_uni[row * A + j];
+    // four actions per Philox block; the per-block arrays are indexed by constants only (registers)
+    for (int blk = 0; blk * 4 < A; ++blk) {
+      float zz[4], uu[4];
+      if (a.eps) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) zz[i] = blk * 4 + i < A ? a.eps[row * A + blk * 4 + i] : 0.f;
       } else {
-        for (int blk = 0; blk * 4 < A; ++blk) {
-          u32x4 c{(uint32_t)uid, (uint32_t)((uint64_t)uid >> 32) ^ ((uint32_t)blk << 20), a.step, RNG_ACT_UNIFORM};
-          const u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
-          const uint32_t ws[4] = {r.x, r.y, r.z, r.w};
-          for (int i = 0; i < 4 && blk * 4 + i < A; ++i)
-            uni[blk * 4 + i] = -1.0f + 2.0f * ((float)(ws[i] >> 8) * 5.9604645e-8f);  // [-1, 1), 24-bit uniform
+        actor_noise4(a.seed, a.step, uid, blk, zz);
+      }
+      if (a.rand_act) {  // np.random.uniform(low=-1, high=1, size=act.shape) (mopo.py:738)
+        if (a.act_uni) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) uu[i] = blk * 4 + i < A ? a.act_uni[row * A + blk * 4 + i] : 0.f;
+        } else {
+          actor_uniform4(a.seed, a.step, uid, blk, uu);
         }
       }
-    }
-    for (int j = 0; j < A; ++j) {
-      const float mu = head[wv][m][j];
-      const float ls = fminf(fmaxf(head[wv][m][A + j], -20.f), 2.f);  // mopo.py:304
-      const float sd = expf(ls);                                      // mopo.py:305
-      const float u = mu + z[j] * sd;                                 // mopo.py:306
-      const float act = a.rand_act ? uni[j] : tanhf(u);               // mopo.py:295 / 738
-      head[wv][m][16 + j] = act;
-      if (a.act) a.act[row * A + j] = act;
-      if (a.mu) a.mu[row * A + j] = tanhf(mu);                        // mopo.py:294
-      if (pos >= 0) a.pool_act[pos * A + j] = act;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = blk * 4 + i;
+        if (j < A) {
+          const float mu = head[wv][m][j];
+          const float ls = fminf(fmaxf(head[wv][m][A + j], -20.f), 2.f);  // mopo.py:304
+          const float sd = expf(ls);                                      // mopo.py:305
+          const float u = mu + zz[i] * sd;                                // mopo.py:306
+          const float act = a.rand_act ? uu[i] : tanhf(u);                // mopo.py:295 / 738
+          head[wv][m][16 + j] = act;
+          if (a.act) a.act[row * A + j] = act;
+          if (a.mu) a.mu[row * A + j] = tanhf(mu);                        // mopo.py:294
+          if (pos >= 0) a.pool_act[pos * A + j] = act;
+        }
+      }
     }
     if (pos >= 0) {  // the observation half of the pool row (mopo.py:750), stored f32
       for (int k = 0; k < O; ++k)
@@ -285,7 +294,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? 4 : 2) void actor_kerne
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   if ((int64_t)blockIdx.x * ACT_WAVES * 16 >= count) return;  // whole workgroup past the live rows
   const int64_t row0 = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16;
-  const int O = a.O, A = a.A, Hp = a.Hp;
+  const int O = a.O, Hp = a.Hp;
   const float* w1f = a.Wpk;
   const float* w2f = w1f + KG0 * NBP * 256;
   const float* whf = w2f + NBP * NBP * 256;
