@@ -75,7 +75,7 @@ def parse():
                         'as 3 bf16 parts, f32-accurate (held to the fp32 parity tolerances)')
     p.add_argument('--no-alt-dtypes', action='store_true',
                    help='skip the extra headline-workload lines with the other ensemble dtypes')
-    p.add_argument('--prof-steps', type=int, default=5, help='untimed rollouts timed per kernel with HIP events')
+    p.add_argument('--prof-steps', type=int, default=20, help='untimed rollouts timed per kernel with HIP events')
     p.add_argument('--config', default='C2', choices=sorted(CONFIGS),
                    help='BASELINE.json workload of the main line (C2 = the headline); the per-rank batch is the '
                         "config's total rollout_batch / world for C4 / C5")

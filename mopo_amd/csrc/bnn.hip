@@ -437,6 +437,9 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
 // split_f16_scaled / row_scale), 3 products per k-group on v_mfma_f32_16x16x32_f16, f32 accumulate and
 // f32 epilogues.  Each layer's output is acc * (2^-k_w / s_row): the weight scale of the layer and
 // member, the row scale of the layer's input (both exact powers of two), folded into the bias add.
+#ifndef BNN_F16_XCD
+#define BNN_F16_XCD 1
+#endif
 #ifndef BNN_F16_MINB
 #define BNN_F16_MINB 2  // 4-wave workgroups per CU: 2 (170 VGPRs, no scratch) measured 0.5 % faster than 3 (28 B/lane spill)
 #endif
@@ -450,7 +453,17 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
+#if BNN_F16_XCD
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs; XCD x takes row groups
+  // [x C, (x + 1) C) of every member, member-major, so a row group's input is fetched from HBM once
+  // and re-read from that XCD's L2 by the other members (grid = 8 C E, see launch_f16s)
+  const int C = ceil_div(groups, 8);
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int e = j / C, grp = xcd * C + j % C;
+  if (grp >= groups) return;
+#else
   const int e = blockIdx.x / groups, grp = blockIdx.x % groups;
+#endif
   const int64_t row = (int64_t)(grp * WAVES + wv) * 16 + m;
   if ((int64_t)grp * WAVES * 16 >= count) return;
   const int IN = w.IN, O = w.O, E = w.E;
@@ -608,7 +621,11 @@ static int launch_f16s(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   constexpr int WV = BNN_SPLIT_WAVES, PS = BNN_SPLIT_PS == 0 ? 2 : BNN_SPLIT_PS;
   a.ntiles = (int)ceil_div((int)a.B, 16);
   if (a.ntiles == 0) return 0;
+#if BNN_F16_XCD
+  dim3 grid(8 * ceil_div(ceil_div(a.ntiles, WV), 8) * h->E), block(64 * WV);
+#else
   dim3 grid(ceil_div(a.ntiles, WV) * h->E), block(64 * WV);
+#endif
   if (mode == FWD_PREDICT)
     hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_PREDICT, WV, PS>), grid, block, 0, s, h->dev, a);
   else
