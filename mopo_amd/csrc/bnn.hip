@@ -322,7 +322,7 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
 #ifndef BNN_SPLIT_MINB
 #define BNN_SPLIT_MINB 3  // split kernels (P > 1): 4-wave workgroups per CU (3: 168 VGPRs; P = 3 spills 15, still 4 % faster than 2)
 #endif
-template <int NB2, int NBO, int MODE, int WAVES, int P = 1, int PS = 1>
+template <int NB2, int NBO, int MODE, int WAVES, int P = 1, int PS = 1, int NBU = NB2>
 __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB * 4 / WAVES) : 512 / (WAVES * 64)) void bnn_fwd_bf16_kernel(
     const BnnDev w, const FwdArgs a) {
   constexpr int KG = NB2 / 2;
@@ -384,13 +384,15 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
       const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), b1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
+        const bool pad = 2 * c + 1 >= NBU;  // padding block (odd hidden-block count): zero
+        (void)pad;
         if constexpr (P > 1) {
           if constexpr (HOLD) {
             hf[c][t] = swish_fast(acc[2 * c][t] + b0[t]);
-            hf[c][4 + t] = swish_fast(acc[2 * c + 1][t] + b1[t]);
+            hf[c][4 + t] = pad ? 0.f : swish_fast(acc[2 * c + 1][t] + b1[t]);
           } else {
             put(hin, c, t, swish_fast(acc[2 * c][t] + b0[t]));
-            put(hin, c, 4 + t, swish_fast(acc[2 * c + 1][t] + b1[t]));
+            put(hin, c, 4 + t, pad ? 0.f : swish_fast(acc[2 * c + 1][t] + b1[t]));
           }
           continue;
         }
@@ -399,7 +401,7 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
         hin[0][c][4 + t] = to_bf16(acc[2 * c + 1][t] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[2 * c + 1][t])));
 #elif !defined(BNN_KNOB_NOSWISH)
         hin[0][c][t] = to_bf16(swish_fast(acc[2 * c][t] + b0[t]));
-        hin[0][c][4 + t] = to_bf16(swish_fast(acc[2 * c + 1][t] + b1[t]));
+        hin[0][c][4 + t] = pad ? (short)0 : to_bf16(swish_fast(acc[2 * c + 1][t] + b1[t]));
 #else
         hin[0][c][t] = to_bf16(acc[2 * c][t] + b0[t]);
         hin[0][c][4 + t] = to_bf16(acc[2 * c + 1][t] + b1[t]);
@@ -408,16 +410,16 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
     }
   };
   if constexpr (P == 1) {
-    layer_lds_bf16<1, NB2, WAVES, SLOT>(w.w0b + (int64_t)e * NB2 * 256, x0[0], acc, lds, wv, lane);
+    layer_lds_bf16<1, NB2, WAVES, SLOT, NBU>(w.w0b + (int64_t)e * NB2 * 256, x0[0], acc, lds, wv, lane);
   } else {
-    layer_lds_split<1, NB2, WAVES, SLOT, P, PS>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane);
+    layer_lds_split<1, NB2, WAVES, SLOT, P, PS, false, NBU>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane);
   }
   to_input(w.b0 + e * bs);
   for (int l = 0; l < 3; ++l) {
     const float* wl = w.whb + ((int64_t)l * w.E + e) * KG * P * NB2 * 256;
-    if constexpr (P == 1) layer_lds_bf16<KG, NB2, WAVES, SLOT>(wl, hin[0], acc, lds, wv, lane);
-    else if constexpr (HOLD) layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS>(wl, hf, acc, lds, wv, lane);
-    else layer_lds_split<KG, NB2, WAVES, SLOT, P, PS>(wl, hin, acc, lds, wv, lane);
+    if constexpr (P == 1) layer_lds_bf16<KG, NB2, WAVES, SLOT, NBU>(wl, hin[0], acc, lds, wv, lane);
+    else if constexpr (HOLD) layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, false, NBU>(wl, hf, acc, lds, wv, lane);
+    else layer_lds_split<KG, NB2, WAVES, SLOT, P, PS, false, NBU>(wl, hin, acc, lds, wv, lane);
     to_input(w.bh + ((int64_t)l * w.E + e) * bs);
   }
   f32x4 hd[NBO];
@@ -443,7 +445,7 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
 #ifndef BNN_F16_MINB
 #define BNN_F16_MINB 2  // 4-wave workgroups per CU: 2 (170 VGPRs, no scratch) measured 0.5 % faster than 3 (28 B/lane spill)
 #endif
-template <int NB2, int NBO, int MODE, int WAVES, int PS = 1>
+template <int NB2, int NBO, int MODE, int WAVES, int PS = 1, int NBU = NB2>
 __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES) void bnn_fwd_f16s_kernel(
     const BnnDev w, const FwdArgs a) {
   constexpr int P = 2, KG = NB2 / 2;
@@ -528,16 +530,17 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         hf[c][t] = swish_fast(fmaf(acc[2 * c][t], f, b0[t]));
-        hf[c][4 + t] = swish_fast(fmaf(acc[2 * c + 1][t], f, b1[t]));
+        // an odd hidden-block count leaves the last block all padding: zero, not computed
+        hf[c][4 + t] = 2 * c + 1 < NBU ? swish_fast(fmaf(acc[2 * c + 1][t], f, b1[t])) : 0.f;
         mx = fmaxf(mx, fmaxf(fabsf(hf[c][t]), fabsf(hf[c][4 + t])));
       }
     }
     row_scale(row_max(mx), s_in, inv_row);
   };
-  layer_lds_split<1, NB2, WAVES, SLOT, P, PS, true>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane);
+  layer_lds_split<1, NB2, WAVES, SLOT, P, PS, true, NBU>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane);
   to_input(w.b0 + e * bs, inv_row * w.wscale[e]);
   for (int l = 0; l < 3; ++l) {
-    layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, true>(w.whb + ((int64_t)l * E + e) * KG * P * NB2 * 256, hf, acc,
+    layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, true, NBU>(w.whb + ((int64_t)l * E + e) * KG * P * NB2 * 256, hf, acc,
                                                            lds, wv, lane, s_in);
     to_input(w.bh + ((int64_t)l * E + e) * bs, inv_row * w.wscale[(1 + l) * E + e]);
   }
@@ -608,10 +611,16 @@ static int launch_bf16_p(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   a.ntiles = (int)ceil_div((int)a.B, 16);
   if (a.ntiles == 0) return 0;
   dim3 grid(ceil_div(a.ntiles, WV) * h->E), block(64 * WV);
-  if (mode == FWD_PREDICT)
+  if (h->dev.NBH == NB2 - 1) {  // odd hidden-block count: the last block is padding (e.g. H = 200)
+    if (mode == FWD_PREDICT)
+      hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_PREDICT, WV, P, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+    else
+      hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+  } else if (mode == FWD_PREDICT) {
     hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_PREDICT, WV, P, PS>), grid, block, 0, s, h->dev, a);
-  else
+  } else {
     hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, PS>), grid, block, 0, s, h->dev, a);
+  }
   MOPO_HIP(hipGetLastError());
   return 0;
 }
@@ -626,10 +635,18 @@ static int launch_f16s(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
 #else
   dim3 grid(ceil_div(a.ntiles, WV) * h->E), block(64 * WV);
 #endif
-  if (mode == FWD_PREDICT)
+  // NBU: hidden blocks in use (NB2 - 1 when the block count is odd, e.g. H = 200 -> 13 of 14).  Not at
+  // H = 400 (25 of 26): the register allocation it gets there (VGPR + AGPR split) measured 17 % slower.
+  if (NB2 <= 16 && h->dev.NBH == NB2 - 1) {
+    if (mode == FWD_PREDICT)
+      hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_PREDICT, WV, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+    else
+      hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_ROLLOUT, WV, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+  } else if (mode == FWD_PREDICT) {
     hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_PREDICT, WV, PS>), grid, block, 0, s, h->dev, a);
-  else
+  } else {
     hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_ROLLOUT, WV, PS>), grid, block, 0, s, h->dev, a);
+  }
   MOPO_HIP(hipGetLastError());
   return 0;
 }

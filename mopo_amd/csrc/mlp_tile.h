@@ -204,7 +204,7 @@ __host__ __device__ __forceinline__ int bf16_kperm(int g, int j) { return j < 4 
 
 __device__ __forceinline__ short to_bf16(float x) { return __builtin_bit_cast(short, (__bf16)x); }
 
-template <int KG, int NB, int WAVES, int SLOT>
+template <int KG, int NB, int WAVES, int SLOT, int NBU = NB>
 __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, const bf16x8 (&in)[KG], f32x4 (&acc)[NB],
                                                float* lds, int w, int lane) {
 #pragma unroll
@@ -225,7 +225,7 @@ __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, con
 #endif
     const float* b = lds + (kg & 1) * SLOT;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
+    for (int nb = 0; nb < NBU; ++nb) {  // blocks >= NBU: padding output block, skipped
       const bf16x8 fr = *reinterpret_cast<const bf16x8*>(b + (nb * 64 + lane) * 4);
 #ifndef BNN_KNOB_NOMFMA
       acc[nb] = mfma_bf16(fr, in[kg], acc[nb]);
@@ -258,7 +258,7 @@ __device__ __forceinline__ void split_bf16(float v, short (&out)[P]) {
 
 // PS: parts staged per slice (P: one slice of P * NB fragments per k-group; 1: P slices of NB).
 // F16: the parts are fp16 ("f16x3", split_f16_scaled) and the products run on the f16 MFMA.
-template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false>
+template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false, int NBU = NB>
 __device__ __forceinline__ void layer_lds_split(const float* __restrict__ wf, const bf16x8 (&in)[P][KG],
                                                 f32x4 (&acc)[NB], float* lds, int w, int lane) {
   static_assert(P % PS == 0, "parts per slice must divide the parts");
@@ -282,9 +282,11 @@ __device__ __forceinline__ void layer_lds_split(const float* __restrict__ wf, co
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
       const int pp = i / NB, nb = i % NB, p = (s % SPK) * PS + pp;
+      if (nb >= NBU) continue;  // padding output block (odd hidden-block count)
 #ifndef BNN_SPLIT_NOPF
       const bf16x8 fr = fr_next;
-      if (i + 1 < NF) fr_next = *reinterpret_cast<const bf16x8*>(b + ((i + 1) * 64 + lane) * 4);
+      const int nx = i + 1 + (((i + 1) % NB) >= NBU ? NB - NBU : 0);
+      if (nx < NF) fr_next = *reinterpret_cast<const bf16x8*>(b + (nx * 64 + lane) * 4);
 #else
       const bf16x8 fr = *reinterpret_cast<const bf16x8*>(b + (i * 64 + lane) * 4);
 #endif
@@ -343,7 +345,7 @@ __device__ __forceinline__ void row_scale(float mx, float& s, float& inv) {
 // layer_lds_split with f32 activations held (8 VGPRs per k-group instead of 4 * P): each k-group's P
 // bf16 parts are split when its first slice is consumed, so only one k-group's parts are live.
 // F16: the 2 fp16 parts of in * s (split_f16_scaled; s = the row scale) on the f16 MFMA.
-template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false>
+template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false, int NBU = NB>
 __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf, const float (&in)[KG][8],
                                                     f32x4 (&acc)[NB], float* lds, int w, int lane, float sc = 1.f) {
   static_assert(P % PS == 0, "parts per slice must divide the parts");
@@ -384,12 +386,16 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
     if (s + 1 < S) stage_slice<NF, WAVES>(wf + (s + 1) * NF * 256, lds + ((s + 1) & 1) * SLOT, w, lane);
     __builtin_amdgcn_sched_barrier(0);
     const float* b = lds + (s & 1) * SLOT;
+    // fragment i's successor is read before fragment i's MFMAs (one LDS read in flight); output
+    // blocks nb >= NBU (the padding block of an odd hidden-block count) are skipped
     bf16x8 fr_next = *reinterpret_cast<const bf16x8*>(b + lane * 4);
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
       const int pp = i / NB, nb = i % NB, p = (s % SPK) * PS + pp;
+      if (nb >= NBU) continue;
       const bf16x8 fr = fr_next;
-      if (i + 1 < NF) fr_next = *reinterpret_cast<const bf16x8*>(b + ((i + 1) * 64 + lane) * 4);
+      const int nx = i + 1 + (((i + 1) % NB) >= NBU ? NB - NBU : 0);
+      if (nx < NF) fr_next = *reinterpret_cast<const bf16x8*>(b + (nx * 64 + lane) * 4);
 #pragma unroll
       for (int q = P - 1 - p; q >= 0; --q) acc[nb] = mfma_16x16x32<F16>(fr, cur[q], acc[nb]);
     }
