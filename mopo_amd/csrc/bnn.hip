@@ -451,7 +451,9 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
   constexpr int P = 2, KG = NB2 / 2;
   constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
   constexpr int SLOT = Stage<PS * NBMAX, WAVES>::SLOTS * 256;
-  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
+  constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;  // the layer's bias (stage_bias pieces)
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + BIAS_LDS];  // one array (see layer_lds)
+  float* lds_bias = lds + 2 * SLOT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
@@ -526,7 +528,8 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
     float mx = 0.f;
 #pragma unroll
     for (int c = 0; c < KG; ++c) {
-      const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), b1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(b + (2 * c) * 16 + 4 * g);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(b + (2 * c + 1) * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         hf[c][t] = swish_fast(fmaf(acc[2 * c][t], f, b0[t]));
@@ -537,12 +540,15 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
     }
     row_scale(row_max(mx), s_in, inv_row);
   };
-  layer_lds_split<1, NB2, WAVES, SLOT, P, PS, true, NBU>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane);
-  to_input(w.b0 + e * bs, inv_row * w.wscale[e]);
+  // the bias of each hidden layer rides into LDS with the layer's first slice (lds_bias)
+  layer_lds_split<1, NB2, WAVES, SLOT, P, PS, true, NBU>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane,
+                                                         w.b0 + e * bs, lds_bias);
+  to_input(lds_bias, inv_row * w.wscale[e]);
   for (int l = 0; l < 3; ++l) {
     layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, true, NBU>(w.whb + ((int64_t)l * E + e) * KG * P * NB2 * 256, hf, acc,
-                                                           lds, wv, lane, s_in);
-    to_input(w.bh + ((int64_t)l * E + e) * bs, inv_row * w.wscale[(1 + l) * E + e]);
+                                                                lds, wv, lane, s_in, w.bh + ((int64_t)l * E + e) * bs,
+                                                                lds_bias);
+    to_input(lds_bias, inv_row * w.wscale[(1 + l) * E + e]);
   }
   f32x4 hd[NBO];
   layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, PS, true>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd, lds, wv,

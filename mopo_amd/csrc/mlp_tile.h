@@ -258,9 +258,12 @@ __device__ __forceinline__ void split_bf16(float v, short (&out)[P]) {
 
 // PS: parts staged per slice (P: one slice of P * NB fragments per k-group; 1: P slices of NB).
 // F16: the parts are fp16 ("f16x3", split_f16_scaled) and the products run on the f16 MFMA.
+// bias / lds_bias: the layer's NB * 16 bias values are copied to LDS with the first slice (published by
+// the first k-group's barrier), so the epilogue reads them from LDS instead of global memory.
 template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false, int NBU = NB>
 __device__ __forceinline__ void layer_lds_split(const float* __restrict__ wf, const bf16x8 (&in)[P][KG],
-                                                f32x4 (&acc)[NB], float* lds, int w, int lane) {
+                                                f32x4 (&acc)[NB], float* lds, int w, int lane,
+                                                const float* __restrict__ bias = nullptr, float* lds_bias = nullptr) {
   static_assert(P % PS == 0, "parts per slice must divide the parts");
   constexpr int SPK = P / PS, S = KG * SPK, NF = PS * NB;
   static_assert(Stage<NF, WAVES>::SLOTS * 256 <= SLOT, "slice larger than its buffer");
@@ -268,6 +271,7 @@ __device__ __forceinline__ void layer_lds_split(const float* __restrict__ wf, co
   for (int nb = 0; nb < NB; ++nb) acc[nb] = zero4();
   __syncthreads();
   stage_slice<NF, WAVES>(wf, lds, w, lane);
+  if (bias) stage_bias<NB * 4, WAVES>(bias, lds_bias, w, lane);
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     __syncthreads();
@@ -347,7 +351,9 @@ __device__ __forceinline__ void row_scale(float mx, float& s, float& inv) {
 // F16: the 2 fp16 parts of in * s (split_f16_scaled; s = the row scale) on the f16 MFMA.
 template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false, int NBU = NB>
 __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf, const float (&in)[KG][8],
-                                                    f32x4 (&acc)[NB], float* lds, int w, int lane, float sc = 1.f) {
+                                                    f32x4 (&acc)[NB], float* lds, int w, int lane, float sc = 1.f,
+                                                    const float* __restrict__ bias = nullptr,
+                                                    float* lds_bias = nullptr) {
   static_assert(P % PS == 0, "parts per slice must divide the parts");
   constexpr int SPK = P / PS, S = KG * SPK, NF = PS * NB;
   static_assert(Stage<NF, WAVES>::SLOTS * 256 <= SLOT, "slice larger than its buffer");
@@ -356,6 +362,7 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
   bf16x8 cur[P];
   __syncthreads();
   stage_slice<NF, WAVES>(wf, lds, w, lane);
+  if (bias) stage_bias<NB * 4, WAVES>(bias, lds_bias, w, lane);  // published by the first barrier below
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int kg = s / SPK;
