@@ -100,12 +100,13 @@ __global__ void pack_frags_f16s_kernel(const float* __restrict__ src, short* __r
 }
 
 // hidden biases in slot order (slot_feat)
+// mul: the f16x3 kernel keeps its hidden biases pre-multiplied by -log2(e) (see bnn_fwd_f16s_kernel)
 __global__ void pack_bias_kernel(const float* __restrict__ src, float* __restrict__ dst, int E, int N,
-                                 int NP) {
+                                 int NP, float mul) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= E * NP) return;
   int e = i / NP, n = slot_feat(i % NP, N);
-  dst[i] = n >= 0 ? src[e * N + n] : 0.f;
+  dst[i] = n >= 0 ? src[e * N + n] * mul : 0.f;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -523,7 +524,10 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
   // (layer_lds_split_f32): holding both parts would take 168 VGPRs and spill at H = 200
   float hf[KG][8];
   float s_in = 1.f;  // the held activations' row scale
-  // acc * f + bias, swish (fc.py:21), and the row scale of the result (the next layer's input)
+  // Epilogue in the log2 domain: u = -log2(e) t = acc * f + b' (f and the packed biases b' carry the
+  // factor), and the layer output is held as y' = u / (1 + 2^u) = -log2(e) swish(t) (fc.py:21); the next
+  // layer's scale takes the -ln 2 back (its f has no -log2(e) factor, the head's f gets -ln 2), which
+  // saves one multiply per value.  Then the row scale of y' (the next layer's input).
   auto to_input = [&](const float* b, float f) {
     float mx = 0.f;
 #pragma unroll
@@ -532,9 +536,9 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
       const f32x4 b1 = *reinterpret_cast<const f32x4*>(b + (2 * c + 1) * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        hf[c][t] = swish_fast(fmaf(acc[2 * c][t], f, b0[t]));
+        hf[c][t] = swish_log2(fmaf(acc[2 * c][t], f, b0[t]));
         // an odd hidden-block count leaves the last block all padding: zero, not computed
-        hf[c][4 + t] = 2 * c + 1 < NBU ? swish_fast(fmaf(acc[2 * c + 1][t], f, b1[t])) : 0.f;
+        hf[c][4 + t] = 2 * c + 1 < NBU ? swish_log2(fmaf(acc[2 * c + 1][t], f, b1[t])) : 0.f;
         mx = fmaxf(mx, fmaxf(fabsf(hf[c][t]), fabsf(hf[c][4 + t])));
       }
     }
@@ -543,7 +547,8 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
   // the bias of each hidden layer rides into LDS with the layer's first slice (lds_bias)
   layer_lds_split<1, NB2, WAVES, SLOT, P, PS, true, NBU>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane,
                                                          w.b0 + e * bs, lds_bias);
-  to_input(lds_bias, inv_row * w.wscale[e]);
+  constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.6931471805599453f;
+  to_input(lds_bias, inv_row * w.wscale[e] * kNegLog2e);  // layer 0's input is x itself
   for (int l = 0; l < 3; ++l) {
     layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, true, NBU>(w.whb + ((int64_t)l * E + e) * KG * P * NB2 * 256, hf, acc,
                                                                 lds, wv, lane, s_in, w.bh + ((int64_t)l * E + e) * bs,
@@ -553,7 +558,7 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
   f32x4 hd[NBO];
   layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, PS, true>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd, lds, wv,
                                                          lane, s_in);
-  const float f = inv_row * w.wscale[4 * E + e];
+  const float f = inv_row * w.wscale[4 * E + e] * kNegLn2;  // the head's input is y' = -log2(e) y
 #pragma unroll
   for (int nb = 0; nb < NBO; ++nb) hd[nb] *= f;
   head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
@@ -792,7 +797,8 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
   };
   auto packb = [&](const float* src, float* dst, int N, int NP) -> int {
     MOPO_HIP(hipMemcpy(stage, src, (size_t)E * N * sizeof(float), hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(pack_bias_kernel, dim3(ceil_div(E * NP, 256)), dim3(256), 0, 0, stage, dst, E, N, NP);
+    const float mul = h->dtype == DT_F16X3 ? -1.4426950408889634f : 1.f;
+    hipLaunchKernelGGL(pack_bias_kernel, dim3(ceil_div(E * NP, 256)), dim3(256), 0, 0, stage, dst, E, N, NP, mul);
     MOPO_HIP(hipGetLastError());
     MOPO_HIP(hipDeviceSynchronize());
     return 0;

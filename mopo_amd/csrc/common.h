@@ -57,6 +57,11 @@ __device__ __forceinline__ float swish_fast(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x * 1.4426950408889634f));
 }
 
+// swish in the log2 domain: for u = -log2(e) x returns -log2(e) swish(x) = u / (1 + 2^u)
+__device__ __forceinline__ float swish_log2(float u) {
+  return u * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
+}
+
 // tf.nn.softplus (Eigen): threshold = log(eps_f32) + 2
 __device__ __forceinline__ float softplusf(float x) {
   const float thr = -13.942385f;  // logf(1.1920929e-7f) + 2
