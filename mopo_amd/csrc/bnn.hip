@@ -327,6 +327,7 @@ template <int NB2, int NBO, int MODE, int WAVES, int P = 1, int PS = 1, int NBU 
 __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB * 4 / WAVES) : 512 / (WAVES * 64)) void bnn_fwd_bf16_kernel(
     const BnnDev w, const FwdArgs a) {
   constexpr int KG = NB2 / 2;
+  constexpr bool KH = NBU < NB2;  // the hidden layers' last k-group is half padding: 16-deep MFMAs there
   constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
   constexpr int SLOT = Stage<PS * NBMAX, WAVES>::SLOTS * 256;
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
@@ -418,19 +419,21 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
   to_input(w.b0 + e * bs);
   for (int l = 0; l < 3; ++l) {
     const float* wl = w.whb + ((int64_t)l * w.E + e) * KG * P * NB2 * 256;
-    if constexpr (P == 1) layer_lds_bf16<KG, NB2, WAVES, SLOT, NBU>(wl, hin[0], acc, lds, wv, lane);
-    else if constexpr (HOLD) layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, false, NBU>(wl, hf, acc, lds, wv, lane);
-    else layer_lds_split<KG, NB2, WAVES, SLOT, P, PS, false, NBU>(wl, hin, acc, lds, wv, lane);
+    if constexpr (P == 1) layer_lds_bf16<KG, NB2, WAVES, SLOT, NBU, KH>(wl, hin[0], acc, lds, wv, lane);
+    else if constexpr (HOLD) layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, false, NBU, KH>(wl, hf, acc, lds, wv, lane);
+    else layer_lds_split<KG, NB2, WAVES, SLOT, P, PS, false, NBU, KH>(wl, hin, acc, lds, wv, lane);
     to_input(w.bh + ((int64_t)l * w.E + e) * bs);
   }
   f32x4 hd[NBO];
   if constexpr (P == 1) {
-    layer_lds_bf16<KG, NBO, WAVES, SLOT>(w.whdb + (int64_t)e * KG * NBO * 256, hin[0], hd, lds, wv, lane);
+    layer_lds_bf16<KG, NBO, WAVES, SLOT, NBO, KH>(w.whdb + (int64_t)e * KG * NBO * 256, hin[0], hd, lds, wv, lane);
   } else {
     if constexpr (HOLD)
-      layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, PS>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd, lds, wv, lane);
+      layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, PS, false, NBO, KH>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd,
+                                                                        lds, wv, lane);
     else
-      layer_lds_split<KG, NBO, WAVES, SLOT, P, PS>(w.whdb + (int64_t)e * KG * P * NBO * 256, hin, hd, lds, wv, lane);
+      layer_lds_split<KG, NBO, WAVES, SLOT, P, PS, false, NBO, KH>(w.whdb + (int64_t)e * KG * P * NBO * 256, hin, hd,
+                                                                    lds, wv, lane);
   }
   head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
                            (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
@@ -450,6 +453,7 @@ template <int NB2, int NBO, int MODE, int WAVES, int PS = 1, int NBU = NB2>
 __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES) void bnn_fwd_f16s_kernel(
     const BnnDev w, const FwdArgs a) {
   constexpr int P = 2, KG = NB2 / 2;
+  constexpr bool KH = NBU < NB2;  // the hidden layers' last k-group is half padding: 16-deep MFMAs there
   constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
   constexpr int SLOT = Stage<PS * NBMAX, WAVES>::SLOTS * 256;
   constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;  // the layer's bias (stage_bias pieces)
@@ -550,14 +554,14 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
   constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.6931471805599453f;
   to_input(lds_bias, inv_row * w.wscale[e] * kNegLog2e);  // layer 0's input is x itself
   for (int l = 0; l < 3; ++l) {
-    layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, true, NBU>(w.whb + ((int64_t)l * E + e) * KG * P * NB2 * 256, hf, acc,
+    layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, true, NBU, KH>(w.whb + ((int64_t)l * E + e) * KG * P * NB2 * 256, hf, acc,
                                                                 lds, wv, lane, s_in, w.bh + ((int64_t)l * E + e) * bs,
                                                                 lds_bias);
     to_input(lds_bias, inv_row * w.wscale[(1 + l) * E + e]);
   }
   f32x4 hd[NBO];
-  layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, PS, true>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd, lds, wv,
-                                                         lane, s_in);
+  layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, PS, true, NBO, KH>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd, lds,
+                                                                  wv, lane, s_in);
   const float f = inv_row * w.wscale[4 * E + e] * kNegLn2;  // the head's input is y' = -log2(e) y
 #pragma unroll
   for (int nb = 0; nb < NBO; ++nb) hd[nb] *= f;

@@ -200,11 +200,24 @@ __device__ __forceinline__ f32x4 mfma_16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
   else return mfma_bf16(a, b, c);
 }
 
+// k-half MFMA (16x16x16) on the low 4 elements of 16x16x32 operands: by bf16_kperm those are k = 4 g + j,
+// j < 4, i.e. the first 16 of the k-group.  Used for a k-group whose upper 16 are all padding.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma_16x16x16_lo(bf16x8 a, bf16x8 b, f32x4 c) {
+  const s16x4 al = __builtin_shufflevector(a, a, 0, 1, 2, 3), bl = __builtin_shufflevector(b, b, 0, 1, 2, 3);
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(f16x4, al), __builtin_bit_cast(f16x4, bl), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bl, c, 0, 0, 0);
+}
+
 __host__ __device__ __forceinline__ int bf16_kperm(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
 
 __device__ __forceinline__ short to_bf16(float x) { return __builtin_bit_cast(short, (__bf16)x); }
 
-template <int KG, int NB, int WAVES, int SLOT, int NBU = NB>
+template <int KG, int NB, int WAVES, int SLOT, int NBU = NB, bool KH = false>
 __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, const bf16x8 (&in)[KG], f32x4 (&acc)[NB],
                                                float* lds, int w, int lane) {
 #pragma unroll
@@ -228,7 +241,9 @@ __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, con
     for (int nb = 0; nb < NBU; ++nb) {  // blocks >= NBU: padding output block, skipped
       const bf16x8 fr = *reinterpret_cast<const bf16x8*>(b + (nb * 64 + lane) * 4);
 #ifndef BNN_KNOB_NOMFMA
-      acc[nb] = mfma_bf16(fr, in[kg], acc[nb]);
+      // KH: the last k-group's upper 16 are padding (odd input-block count), so a 16-deep MFMA
+      if (KH && kg + 1 == KG) acc[nb] = mfma_16x16x16_lo<false>(fr, in[kg], acc[nb]);
+      else acc[nb] = mfma_bf16(fr, in[kg], acc[nb]);
 #else
       acc[nb][0] += (float)fr[0];
 #endif
@@ -260,7 +275,7 @@ __device__ __forceinline__ void split_bf16(float v, short (&out)[P]) {
 // F16: the parts are fp16 ("f16x3", split_f16_scaled) and the products run on the f16 MFMA.
 // bias / lds_bias: the layer's NB * 16 bias values are copied to LDS with the first slice (published by
 // the first k-group's barrier), so the epilogue reads them from LDS instead of global memory.
-template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false, int NBU = NB>
+template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false, int NBU = NB, bool KH = false>
 __device__ __forceinline__ void layer_lds_split(const float* __restrict__ wf, const bf16x8 (&in)[P][KG],
                                                 f32x4 (&acc)[NB], float* lds, int w, int lane,
                                                 const float* __restrict__ bias = nullptr, float* lds_bias = nullptr) {
@@ -295,7 +310,9 @@ __device__ __forceinline__ void layer_lds_split(const float* __restrict__ wf, co
       const bf16x8 fr = *reinterpret_cast<const bf16x8*>(b + (i * 64 + lane) * 4);
 #endif
 #pragma unroll
-      for (int q = P - 1 - p; q >= 0; --q) acc[nb] = mfma_16x16x32<F16>(fr, in[q][kg], acc[nb]);
+      for (int q = P - 1 - p; q >= 0; --q)
+        acc[nb] = (KH && kg + 1 == KG) ? mfma_16x16x16_lo<F16>(fr, in[q][kg], acc[nb])
+                                       : mfma_16x16x32<F16>(fr, in[q][kg], acc[nb]);
     }
   }
 }
@@ -349,7 +366,7 @@ __device__ __forceinline__ void row_scale(float mx, float& s, float& inv) {
 // layer_lds_split with f32 activations held (8 VGPRs per k-group instead of 4 * P): each k-group's P
 // bf16 parts are split when its first slice is consumed, so only one k-group's parts are live.
 // F16: the 2 fp16 parts of in * s (split_f16_scaled; s = the row scale) on the f16 MFMA.
-template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false, int NBU = NB>
+template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false, int NBU = NB, bool KH = false>
 __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf, const float (&in)[KG][8],
                                                     f32x4 (&acc)[NB], float* lds, int w, int lane, float sc = 1.f,
                                                     const float* __restrict__ bias = nullptr,
@@ -404,7 +421,9 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
       const int nx = i + 1 + (((i + 1) % NB) >= NBU ? NB - NBU : 0);
       if (nx < NF) fr_next = *reinterpret_cast<const bf16x8*>(b + (nx * 64 + lane) * 4);
 #pragma unroll
-      for (int q = P - 1 - p; q >= 0; --q) acc[nb] = mfma_16x16x32<F16>(fr, cur[q], acc[nb]);
+      for (int q = P - 1 - p; q >= 0; --q)
+        acc[nb] = (KH && kg + 1 == KG) ? mfma_16x16x16_lo<F16>(fr, cur[q], acc[nb])
+                                       : mfma_16x16x32<F16>(fr, cur[q], acc[nb]);
     }
   }
 }
