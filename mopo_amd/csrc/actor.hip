@@ -367,10 +367,13 @@ __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? 4 : 2) void actor_kerne
 
 // f16x3 policy forward (mlp_tile.h split_f16_pair / row_scale): observation row scaled per row, each
 // layer's output acc * (2^-k_W / s_row) + bias, relu; 16x16x32 f16 MFMAs, 3 products per k-group.
+#ifndef ACT_F16_PS
+#define ACT_F16_PS 1  // weight parts per staged slice (2: both parts of a k-group per barrier)
+#endif
 template <int NBP>
 __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16_kernel(const ActorArgs a) {
-  constexpr int P = 2, KG = NBP / 2;
-  constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
+  constexpr int P = 2, KG = NBP / 2, PS = ACT_F16_PS;
+  constexpr int SLOT = Stage<PS * NBP, ACT_WAVES>::SLOTS * 256;
   __shared__ float head[ACT_WAVES][16][25];
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
@@ -431,12 +434,12 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16_kernel(const Acto
     }
     row_scale(row_max(mx), s_in, inv_row);
   };
-  layer_lds_split<1, NBP, ACT_WAVES, SLOT, P, 1, true>(w1f, x0, acc, lds, wv, lane);
+  layer_lds_split<1, NBP, ACT_WAVES, SLOT, P, PS, true>(w1f, x0, acc, lds, wv, lane);
   to_input(b1, inv_row * inv_w[0]);
-  layer_lds_split_f32<KG, NBP, ACT_WAVES, SLOT, P, 1, true>(w2f, hf, acc, lds, wv, lane, s_in);
+  layer_lds_split_f32<KG, NBP, ACT_WAVES, SLOT, P, PS, true>(w2f, hf, acc, lds, wv, lane, s_in);
   to_input(b2, inv_row * inv_w[1]);
   f32x4 hd[1];
-  layer_lds_split_f32<KG, 1, ACT_WAVES, SLOT, P, 1, true>(whf, hf, hd, lds, wv, lane, s_in);
+  layer_lds_split_f32<KG, 1, ACT_WAVES, SLOT, P, PS, true>(whf, hf, hd, lds, wv, lane, s_in);
   const float f = inv_row * inv_w[2];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
