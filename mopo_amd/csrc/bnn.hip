@@ -327,7 +327,9 @@ template <int NB2, int NBO, int MODE, int WAVES, int P = 1, int PS = 1, int NBU 
 __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB * 4 / WAVES) : 512 / (WAVES * 64)) void bnn_fwd_bf16_kernel(
     const BnnDev w, const FwdArgs a) {
   constexpr int KG = NB2 / 2;
-  constexpr bool KH = NBU < NB2;  // the hidden layers' last k-group is half padding: 16-deep MFMAs there
+  // 16-deep MFMAs for a half-padded last k-group (as the f16x3 kernel does) measured slower here: the
+  // larger unrolled body stops the part loops from unrolling (C3 -4 %, bf16x6 70x via dynamic indexing)
+  constexpr bool KH = false;
   constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
   constexpr int SLOT = Stage<PS * NBMAX, WAVES>::SLOTS * 256;
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];

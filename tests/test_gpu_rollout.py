@@ -376,6 +376,31 @@ def test_bnn_predict_split_vs_oracle(E, H, B, dtype, tol):
         assert err(var, rv) <= max(2 * err(v32, rv), 2e-6), (err(var, rv), err(v32, rv))
 
 
+def test_ensemble_dtypes_no_pathological_slowdown():
+    """Guard against a code-generation cliff (a split kernel whose part loops stop unrolling turns
+    register arrays into select chains and ran 70x slower while still passing parity): every split
+    dtype's predict of 50k rows (device in / out) takes at most the fp32 kernel's time, 1.5x."""
+    import torch
+    E, H, B = 7, 200, 50000
+    rs = np.random.RandomState(11)
+    mats = obnn.to_mat_list(obnn.init_params(E, 17, 6, hidden=H, seed=3, inputs=rs.normal(size=(300, 23))))
+    x = torch.from_numpy(rs.normal(size=(B, 23)).astype(np.float32)).cuda()
+    ms = {}
+    for dt in ('fp32', 'bf16x6', 'f16x3', 'bf16x3', 'bf16'):
+        m = make_model(mats, E, H, dtype=dt)
+        for _ in range(3):
+            m.predict(x)
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(10):
+            m.predict(x)
+        t1.record()
+        torch.cuda.synchronize()
+        ms[dt] = t0.elapsed_time(t1) / 10
+    for dt, v in ms.items():
+        assert v <= 1.5 * ms['fp32'], ms
+
+
 @pytest.mark.parametrize('scale', [1e-6, 1.0, 1e3, 1e5])
 def test_f16x3_dynamic_range(scale):
     """f16x3 carries fp16 parts under power-of-two scales (per row for activations, per layer and member
