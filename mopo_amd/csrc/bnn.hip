@@ -100,7 +100,7 @@ __global__ void pack_frags_f16s_kernel(const float* __restrict__ src, short* __r
 }
 
 // hidden biases in slot order (slot_feat)
-// mul: the f16x3 kernel keeps its hidden biases pre-multiplied by -log2(e) (see bnn_fwd_f16s_kernel)
+// mul: the 16-bit kernels keep their hidden biases pre-multiplied by -log2(e) (see bnn_fwd_f16s_kernel)
 __global__ void pack_bias_kernel(const float* __restrict__ src, float* __restrict__ dst, int E, int N,
                                  int NP, float mul) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -332,7 +332,9 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
   constexpr bool KH = false;
   constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
   constexpr int SLOT = Stage<PS * NBMAX, WAVES>::SLOTS * 256;
-  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
+  constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;  // the layer's bias (stage_bias pieces)
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + BIAS_LDS];  // one array (see layer_lds)
+  float* lds_bias = lds + 2 * SLOT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
@@ -382,21 +384,25 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
   constexpr bool HOLD = BNN_SPLIT_HOLD_F32 && P >= 3;
   float hf[KG][8];
   (void)hf;
-  auto to_input = [&](const float* b) {  // bias + swish in f32, then the bf16 B operand parts
+  // Epilogue in the log2 domain, as in bnn_fwd_f16s_kernel: the packed biases carry -log2(e), a layer's
+  // input is y' = -log2(e) y, so u = -log2(e) t = acc + b' (layer 0, whose input is x: acc * -log2(e) + b')
+  // and the output y' = u / (1 + 2^u); the head's accumulators are taken back by -ln 2.
+  auto to_input = [&](const float* b, float f) {  // bias + swish in f32, then the bf16 B operand parts
 #pragma unroll
     for (int c = 0; c < KG; ++c) {
-      const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), b1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(b + (2 * c) * 16 + 4 * g);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(b + (2 * c + 1) * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const bool pad = 2 * c + 1 >= NBU;  // padding block (odd hidden-block count): zero
         (void)pad;
         if constexpr (P > 1) {
           if constexpr (HOLD) {
-            hf[c][t] = swish_fast(acc[2 * c][t] + b0[t]);
-            hf[c][4 + t] = pad ? 0.f : swish_fast(acc[2 * c + 1][t] + b1[t]);
+            hf[c][t] = swish_log2(fmaf(acc[2 * c][t], f, b0[t]));
+            hf[c][4 + t] = pad ? 0.f : swish_log2(fmaf(acc[2 * c + 1][t], f, b1[t]));
           } else {
-            put(hin, c, t, swish_fast(acc[2 * c][t] + b0[t]));
-            put(hin, c, 4 + t, pad ? 0.f : swish_fast(acc[2 * c + 1][t] + b1[t]));
+            put(hin, c, t, swish_log2(fmaf(acc[2 * c][t], f, b0[t])));
+            put(hin, c, 4 + t, pad ? 0.f : swish_log2(fmaf(acc[2 * c + 1][t], f, b1[t])));
           }
           continue;
         }
@@ -404,8 +410,8 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
         hin[0][c][t] = to_bf16(acc[2 * c][t] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[2 * c][t])));
         hin[0][c][4 + t] = to_bf16(acc[2 * c + 1][t] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[2 * c + 1][t])));
 #elif !defined(BNN_KNOB_NOSWISH)
-        hin[0][c][t] = to_bf16(swish_fast(acc[2 * c][t] + b0[t]));
-        hin[0][c][4 + t] = pad ? (short)0 : to_bf16(swish_fast(acc[2 * c + 1][t] + b1[t]));
+        hin[0][c][t] = to_bf16(swish_log2(fmaf(acc[2 * c][t], f, b0[t])));
+        hin[0][c][4 + t] = pad ? (short)0 : to_bf16(swish_log2(fmaf(acc[2 * c + 1][t], f, b1[t])));
 #else
         hin[0][c][t] = to_bf16(acc[2 * c][t] + b0[t]);
         hin[0][c][4 + t] = to_bf16(acc[2 * c + 1][t] + b1[t]);
@@ -413,18 +419,25 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
       }
     }
   };
+  constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.6931471805599453f;
+  const float* b0g = w.b0 + e * bs;
   if constexpr (P == 1) {
-    layer_lds_bf16<1, NB2, WAVES, SLOT, NBU>(w.w0b + (int64_t)e * NB2 * 256, x0[0], acc, lds, wv, lane);
+    layer_lds_bf16<1, NB2, WAVES, SLOT, NBU>(w.w0b + (int64_t)e * NB2 * 256, x0[0], acc, lds, wv, lane, b0g, lds_bias);
   } else {
-    layer_lds_split<1, NB2, WAVES, SLOT, P, PS, false, NBU>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane);
+    layer_lds_split<1, NB2, WAVES, SLOT, P, PS, false, NBU>(w.w0b + (int64_t)e * P * NB2 * 256, x0, acc, lds, wv, lane,
+                                                            b0g, lds_bias);
   }
-  to_input(w.b0 + e * bs);
+  to_input(lds_bias, kNegLog2e);
   for (int l = 0; l < 3; ++l) {
     const float* wl = w.whb + ((int64_t)l * w.E + e) * KG * P * NB2 * 256;
-    if constexpr (P == 1) layer_lds_bf16<KG, NB2, WAVES, SLOT, NBU, KH>(wl, hin[0], acc, lds, wv, lane);
-    else if constexpr (HOLD) layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, false, NBU, KH>(wl, hf, acc, lds, wv, lane);
-    else layer_lds_split<KG, NB2, WAVES, SLOT, P, PS, false, NBU, KH>(wl, hin, acc, lds, wv, lane);
-    to_input(w.bh + ((int64_t)l * w.E + e) * bs);
+    const float* bl = w.bh + ((int64_t)l * w.E + e) * bs;
+    if constexpr (P == 1)
+      layer_lds_bf16<KG, NB2, WAVES, SLOT, NBU, KH>(wl, hin[0], acc, lds, wv, lane, bl, lds_bias);
+    else if constexpr (HOLD)
+      layer_lds_split_f32<KG, NB2, WAVES, SLOT, P, PS, false, NBU, KH>(wl, hf, acc, lds, wv, lane, 1.f, bl, lds_bias);
+    else
+      layer_lds_split<KG, NB2, WAVES, SLOT, P, PS, false, NBU, KH>(wl, hin, acc, lds, wv, lane, bl, lds_bias);
+    to_input(lds_bias, 1.f);
   }
   f32x4 hd[NBO];
   if constexpr (P == 1) {
@@ -437,6 +450,8 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
       layer_lds_split<KG, NBO, WAVES, SLOT, P, PS, false, NBO, KH>(w.whdb + (int64_t)e * KG * P * NBO * 256, hin, hd,
                                                                     lds, wv, lane);
   }
+#pragma unroll
+  for (int nb = 0; nb < NBO; ++nb) hd[nb] *= kNegLn2;  // the head's input is y' = -log2(e) y
   head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
                            (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
 }
@@ -803,7 +818,7 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
   };
   auto packb = [&](const float* src, float* dst, int N, int NP) -> int {
     MOPO_HIP(hipMemcpy(stage, src, (size_t)E * N * sizeof(float), hipMemcpyHostToDevice));
-    const float mul = h->dtype == DT_F16X3 ? -1.4426950408889634f : 1.f;
+    const float mul = h->dtype != DT_FP32 ? -1.4426950408889634f : 1.f;  // 16-bit kernels: log2 domain
     hipLaunchKernelGGL(pack_bias_kernel, dim3(ceil_div(E * NP, 256)), dim3(256), 0, 0, stage, dst, E, N, NP, mul);
     MOPO_HIP(hipGetLastError());
     MOPO_HIP(hipDeviceSynchronize());

@@ -219,7 +219,8 @@ __device__ __forceinline__ short to_bf16(float x) { return __builtin_bit_cast(sh
 
 template <int KG, int NB, int WAVES, int SLOT, int NBU = NB, bool KH = false>
 __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, const bf16x8 (&in)[KG], f32x4 (&acc)[NB],
-                                               float* lds, int w, int lane) {
+                                               float* lds, int w, int lane, const float* __restrict__ bias = nullptr,
+                                               float* lds_bias = nullptr) {
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) acc[nb] = zero4();
 #ifndef BNN_KNOB_NOBARRIER
@@ -227,6 +228,7 @@ __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, con
 #endif
 #ifndef BNN_KNOB_NOSTAGE
   stage_slice<NB, WAVES>(wf, lds, w, lane);
+  if (bias) stage_bias<NB * 4, WAVES>(bias, lds_bias, w, lane);  // published by the first barrier below
 #endif
 #pragma unroll
   for (int kg = 0; kg < KG; ++kg) {
