@@ -138,12 +138,257 @@ struct LossTail {
   float* logs; float* beta_pow; int64_t* iter;
 };
 
+// buffer descriptor over n floats at p (wave-uniform inputs only)
+static __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)(n * 4), 0x00020000);
+}
+
+static __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t d, int idx) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(d, idx * 4, 0, 0));
+}
+
+// ---- SAC batch gather (_training_batch, mopo.py:801-821): rows [0, n_env) from the env pool, rest
+// from the model pool; each index uniform over the pool's live size (Philox) unless injected.  One
+// thread per (row, field column): every thread derives its row's source index itself (the Philox
+// draw is cheap), so the work is two dependent memory latencies (pool size + counter, then the field)
+// with no barrier.  Run by sac_gather_kernel (sac.hip) and by the gather blocks of a GemmGroup launch.
+struct Batch {
+  float *sa, *xpi, *xn, *rew, *term;  // [s, a], [s, pi(s)], [s', pi(s')], r, done
+  int64_t* idx;                       // [n] sampled rows
+};
+
+struct GatherArgs {
+  mopo_pool_desc env, mod;
+  int n, n_env, O, A;                // n: batch rows
+  const int64_t* idx_in;             // injected rows or NULL (Philox draw)
+  uint64_t seed;
+  const int64_t* iter;
+  Batch out;
+};
+
+// field c of batch row r (obs | act | next_obs | rew | term)
+static __device__ __forceinline__ void gather_elem(const GatherArgs& g, int r, int c) {
+  const int O = g.O, A = g.A, W = O + A;
+  const bool fe = r < g.n_env;
+  const mopo_pool_desc& p = fe ? g.env : g.mod;
+  int64_t src;
+  if (g.idx_in) {
+    src = g.idx_in[r];
+  } else {
+    const uint64_t size = (uint64_t)p.d_state[1];
+    const int64_t it = *g.iter;
+    u32x4 cc{(uint32_t)r, (uint32_t)it, (uint32_t)((uint64_t)it >> 32), RNG_SAC};
+    u32x4 q = philox(cc, (uint32_t)g.seed, (uint32_t)(g.seed >> 32));
+    src = (int64_t)(((uint64_t)q.x * size) >> 32);
+  }
+  const Batch& b = g.out;
+  if (c == 0) b.idx[r] = src;
+  if (c < O) {
+    const float v = p.d_obs[src * O + c];
+    b.sa[r * W + c] = v;
+    b.xpi[r * W + c] = v;
+  } else if (c < O + A) {
+    b.sa[r * W + c] = p.d_act[src * A + (c - O)];
+  } else if (c < 2 * O + A) {
+    b.xn[r * W + (c - O - A)] = p.d_next_obs[src * O + (c - O - A)];
+  } else if (c == 2 * O + A) {
+    b.rew[r] = p.d_rew[src];
+  } else {
+    b.term[r] = (float)p.d_term[src];
+  }
+}
+
+// ---- the policy's row-local backward chain (mopo.py:337-377 through the critics at (s, pi(s))),
+// run by extra blocks of the critic weight-gradient launch: block (rb, cq) owns batch rows
+// [16 rb, 16 rb + 16) and columns [64 cq, 64 cq + 64) of the policy's first hidden layer.
+//   dx_a   = dh1_Q1(s,pi) W1_Q1[O:]^T + dh1_Q2(s,pi) W1_Q2[O:]^T      (-d min Q / d action)
+//   dhead  = squashed-Gaussian head backward (mean, log_std; alpha / n on the log-prob)
+//   dh2p   = (dhead_mu Wm^T + dhead_ls Wl^T) * (h2p > 0)               (all H columns, in LDS)
+//   dh1p   = dh2p W2p^T * (h1p > 0)                                     (this block's 64 columns, MFMA)
+// Every quantity before dh1p is row-local, so each column block recomputes it (cheap: K = 2H for
+// A <= 8 outputs, K = 2A per dh2p value) and only cq == 0 stores dhead and dh2p, which the policy
+// weight gradients of the next launch read with dh1p.
+struct PolicyRows {
+  int nblk;                          // 0: none; ceil(n / 16) * ceil(H / 64)
+  int n, O, A, H;
+  const float* dh1[2];               // Q1 / Q2 at (s, pi(s)): [n][H]
+  const float* w1[2];                // their first-layer weights [O + A][H]
+  const float* head_s;               // [n][2A] mean | raw log_std
+  const float* eps_s;                // [n][A]
+  const float* log_alpha;
+  const float* Wm; const float* Wl;  // [H][A]
+  const float* h2p; const float* h1p;// [n][H]
+  const float* W2p;                  // [H][H]
+  float* dhead; float* dh2p; float* dh1p;
+};
+
+constexpr int PR_COLS = 64;          // dh1p columns per policy-row block (one 16-wide tile per wave)
+constexpr int PR_LDS = 2 * 256 * 16; // floats the grouped kernel's panel LDS offers it (H <= 508)
+
+// Latency layout: the chain's global operands come in three bursts of unconditional (range-checked)
+// loads, each issued before the compute that precedes its use -- (1) the dx operands (straight into
+// MFMA registers) and the head inputs; (2) once dx is formed, Wm / Wl / h2p at this thread's column and
+// the first half of the W2p operands of the dh1p tile; (3) once dh2p is formed, the second half and
+// the h1p mask.  No branch depends on a runtime width, so each phase's loads issue back to back.
+// S: >= 16 (H + 4) floats of LDS (PR_LDS); hs: >= 3 * 128 floats.
+// H % 16 == 0, H <= 256 (one dh2p column per thread), A <= 8.
+static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int H = c.H, A = c.A, O = c.O, HS = H + 4, n = c.n;
+  const int ncq = (H + PR_COLS - 1) / PR_COLS;
+  const int rb = x / ncq, cq = x % ncq, r0 = rb * 16;
+  // ---- burst 1: the dx operands straight into MFMA registers -- A(i, k) = [dh1_Q1 | dh1_Q2](r0 + i, k),
+  //      B(k, j) = [W1_Q1 ; W1_Q2](O + j, k) (j < A, else 0), K = 2H split over the 4 waves; lane
+  //      (li, lk) of wave w contracts k = w (2H / 4) + 32 lk + 4 t + u: 8 contiguous quads per operand
+  const int li = lane & 15, lk = lane >> 4;
+  const int KW = 2 * H / 4;           // k per wave (H % 16 == 0: whole quads, 32 lk + 4 t < KW)
+  f32x4 xa[8], xb[8];
+  {
+    const int qi = (w * KW) / H;      // waves 0-1: Q1, 2-3: Q2 (KW = H / 2)
+    const auto dd = rsrc(c.dh1[qi], (int64_t)n * H);
+    const auto dw = rsrc(c.w1[qi] + (int64_t)O * H, (int64_t)A * H);
+    const int kq = w * KW - qi * H + 32 * lk;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int k = kq + 4 * t;
+      const bool kin = 32 * lk + 4 * t < KW;
+      xa[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            dd, (kin ? (r0 + li) * H + k : -4) * 4, 0, 0));   // rows >= n: past the extent
+      xb[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            dw, (kin && li < A ? li * H + k : -4) * 4, 0, 0));
+    }
+  }
+  const int hr = tid >> 3, hj = tid & 7, hrow = r0 + hr;
+  const bool hon = tid < 128 && hj < A && hrow < n;
+  const auto dh = rsrc(c.head_s, (int64_t)n * 2 * A), de = rsrc(c.eps_s, (int64_t)n * A);
+  const float mu = bload(dh, hon ? hrow * 2 * A + hj : -1);
+  const float raw = bload(dh, hon ? hrow * 2 * A + A + hj : -1);
+  const float ep = bload(de, hon ? hrow * A + hj : -1);
+  const float la = *c.log_alpha;
+  {
+    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = mfma4(xa[t][u], xb[t][u], acc[u]);
+    float* pw = S + w * 256;          // the four waves' partial 16x16 tiles (D: col li, row 4 lk + r)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pw[(4 * lk + r) * 16 + li] = acc[0][r] + acc[1][r] + acc[2][r] + acc[3][r];
+  }
+  __syncthreads();
+  if (tid < 128) {                    // da (row hr, action hj) = sum of the four partials
+    const int o = hr * 16 + hj;
+    hs[hr * 8 + hj] = S[o] + S[256 + o] + S[512 + o] + S[768 + o];
+  }
+  // ---- burst 2: Wm / Wl / h2p at this thread's dh2p column, the first half of this wave's W2p
+  //      operands (B(k, j) = W2p[j][k]; lane (li, lk) contracts k = 64 lk + 4 t + u: contiguous quads)
+  const int hc = tid;
+  const auto dwm = rsrc(c.Wm, (int64_t)H * A), dwl = rsrc(c.Wl, (int64_t)H * A), dh2 = rsrc(c.h2p, (int64_t)n * H);
+  float wm[8], wl[8], h2v[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    wm[k] = bload(dwm, (k < A && hc < H) ? hc * A + k : -1);
+    wl[k] = bload(dwl, (k < A && hc < H) ? hc * A + k : -1);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) h2v[i] = bload(dh2, hc < H ? (r0 + i) * H + hc : -1);  // rows >= n: past the extent
+  const int j0 = cq * PR_COLS + w * 16, col = j0 + li;
+  const bool tile_on = j0 < H;
+  const auto dw2 = rsrc(c.W2p, (int64_t)H * H);
+  const int boff = (tile_on ? col : 0) * H;
+  auto bquad = [&](int t) {
+    const int k = 64 * lk + 4 * t;
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dw2, (k < H ? boff + k : -4) * 4, 0, 0));
+  };
+  f32x4 bq0[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) bq0[t] = bquad(t);
+  __syncthreads();
+  // ---- squashed-Gaussian head backward (mopo.py:282-308 differentiated; pi_loss mopo.py:371-377)
+  float* dmu_s = hs + 128;
+  float* dls_s = hs + 256;
+  if (tid < 128) {
+    float dmu = 0.f, dls = 0.f;
+    if (hon) {
+      const float g = expf(la) / (float)n;                         // d L_pi / d logp (stop_gradient(alpha))
+      const float ls = fminf(fmaxf(raw, -20.f), 2.f);
+      const float sd = expf(ls);
+      const float u = mu + ep * sd;
+      const float a = tanhf(u);
+      const float inv = 1.f / (sd + 1e-8f);
+      const float zz = (u - mu) * inv;
+      const float da = hs[hr * 8 + hj];                             // -dmin q / da through Q1/Q2
+      float du = da * (1.f - a * a);                                // tanh grad (y-based)
+      du += g * (-zz * inv);                                        // gaussian_likelihood wrt x
+      du += g * (2.f - 4.f / (1.f + expf(2.f * u)));                // squash correction: 2 - 4 sigmoid(-2u)
+      dmu = g * zz * inv + du;
+      const float dstd = g * zz * zz * inv + du * ep;
+      dls = -g + dstd * sd;
+      if (!(raw >= -20.f && raw <= 2.f)) dls = 0.f;                 // clip_by_value grad
+      if (cq == 0) {
+        c.dhead[(int64_t)hrow * 2 * A + hj] = dmu;
+        c.dhead[(int64_t)hrow * 2 * A + A + hj] = dls;
+      }
+    }
+    dmu_s[tid] = dmu;
+    dls_s[tid] = dls;
+  }
+  __syncthreads();
+  // ---- dh2p of the 16 rows at this thread's column -> LDS rows of stride HS (the wa rows are dead)
+  if (hc < H) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(dmu_s + i * 8), u1 = *reinterpret_cast<const f32x4*>(dmu_s + i * 8 + 4);
+      const f32x4 l0 = *reinterpret_cast<const f32x4*>(dls_s + i * 8), l1 = *reinterpret_cast<const f32x4*>(dls_s + i * 8 + 4);
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v += u0[k] * wm[k] + u1[k] * wm[4 + k] + l0[k] * wl[k] + l1[k] * wl[4 + k];
+      v = h2v[i] > 0.f ? v : 0.f;
+      S[i * HS + hc] = v;
+      if (cq == 0 && r0 + i < n) c.dh2p[(int64_t)(r0 + i) * H + hc] = v;
+    }
+  }
+  // ---- burst 3: the second half of the W2p operands and the h1p mask of this lane's four outputs
+  f32x4 bq1[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) bq1[t] = bquad(8 + t);
+  const auto dm1 = rsrc(c.h1p, (int64_t)n * H);
+  float m1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
+  __syncthreads();
+  // ---- dh1p tile = dh2p W2p^T * (h1p > 0): rows r0.., columns j0.. (wave w)
+  if (!tile_on) return;
+  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int k = 64 * lk + 4 * t;
+    const f32x4 a = k < H ? *reinterpret_cast<const f32x4*>(S + li * HS + k) : zero4();
+    const f32x4 b = t < 8 ? bq0[t] : bq1[t - 8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = mfma4(a[u], b[u], acc[u]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = r0 + 4 * lk + i;                                // D: col li, row 4 lk + i
+    if (row < n && col < H) {
+      const float v = acc[0][i] + acc[1][i] + acc[2][i] + acc[3][i];
+      c.dh1p[(int64_t)row * H + col] = m1[i] > 0.f ? v : 0.f;
+    }
+  }
+}
+
+// Blocks of a launch: [pr.nblk policy-row blocks] [the problems' tiles (prefix[n])] [LossTail block
+// if tail.part] [gather_blocks blocks of the next step's batch gather (ga)].
 struct GemmGroup {
   int n;
   int prefix[MAXP + 1];
   AdamCtx ad;
   HeadCtx hd;
   LossTail tail;                     // tail.part != NULL: block prefix[n] runs loss_tail_block
+  PolicyRows pr;
+  int gather_blocks;
+  GatherArgs ga;
   GemmProb p[MAXP];
 };
 
@@ -225,15 +470,6 @@ static __device__ __forceinline__ void panel_rk(int q, int tid, int& r, int& k) 
     if (rfast) { r = tid & 31; k = (tid >> 5) + 8 * q; }
     else { k = (tid & 63) + 64 * (q & 1); r = (tid >> 6) + 4 * (q >> 1); }
   }
-}
-
-// buffer descriptor over n floats at p (wave-uniform inputs only)
-static __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t n) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, (int)(n * 4), 0x00020000);
-}
-
-static __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t d, int idx) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(d, idx * 4, 0, 0));
 }
 
 template <int MODE, bool IS_A, int TW = 16>
@@ -415,20 +651,37 @@ static __device__ __forceinline__ void stage_dispatch(const GemmProb& p, int i0,
 // of LDS; partial tiles are summed through LDS and the epilogue fuses bias / activation / the
 // activation-derivative mask, and (for weight gradients) the optimizer.
 static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGroup g) {
-  __shared__ float As[GKC][16];
-  __shared__ float Bs[GKC][16];
+  __shared__ float ABs[2 * GKC * 16];  // the A and B panels (one array: the policy-row blocks use it whole)
+  float (*As)[16] = reinterpret_cast<float (*)[16]>(ABs);
+  float (*Bs)[16] = reinterpret_cast<float (*)[16]>(ABs + GKC * 16);
   __shared__ float part[4][256];
   __shared__ float csum[16][17];
   __shared__ float hv[16][17];
-  if (g.tail.part && (int)blockIdx.x >= g.prefix[g.n]) {
-    loss_tail_block(g.tail, g.ad, &part[0][0]);
+  // block order: [pr.nblk policy-row blocks (first: the longest chain starts at once)] [the problems'
+  // tiles (prefix[n])] [LossTail block if tail.part] [gather blocks]
+  if ((int)blockIdx.x < g.pr.nblk) {
+    policy_rows_block(g.pr, blockIdx.x, ABs, &part[0][0]);
+    return;
+  }
+  const int bid = (int)blockIdx.x - g.pr.nblk;
+  if (bid >= g.prefix[g.n]) {  // the extra blocks after the tiles
+    int x = bid - g.prefix[g.n];
+    if (g.tail.part) {
+      if (x == 0) {
+        loss_tail_block(g.tail, g.ad, &part[0][0]);
+        return;
+      }
+      --x;
+    }
+    const int C = 2 * g.ga.O + g.ga.A + 2, e = x * 256 + (int)threadIdx.x;
+    if (e < g.ga.n * C) gather_elem(g.ga, e / C, e % C);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int pi = 0;
-  while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
+  while (pi + 1 < g.n && bid >= g.prefix[pi + 1]) ++pi;
   const GemmProb& p = g.p[pi];
-  const int t = blockIdx.x - g.prefix[pi];
+  const int t = bid - g.prefix[pi];
   const int tn_cnt = ceil_div(p.N, 16);
   const int tm = t / tn_cnt, tn = t % tn_cnt;
   const int i0 = tm * 16, j0 = tn * 16;
@@ -543,7 +796,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
     if (tid == 0) {
       const float b = part[0][0] + part[0][1] + part[0][2] + part[0][3];
       const int64_t off = p.adam ? (int64_t)(p.C - ad.G) : -1;
-      float* np = ad.norm_part + 2 * (int64_t)(ad.slot0 + blockIdx.x);
+      float* np = ad.norm_part + 2 * (int64_t)(ad.slot0 + bid);
       np[0] = off >= 0 && off < ad.n_pi ? b : 0.f;
       np[1] = off >= ad.n_pi && off < ad.n_pi + ad.n_q ? b : 0.f;
     }
@@ -704,7 +957,8 @@ static inline int gemm_tile_override() {
 }
 
 static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const AdamCtx* ad = nullptr, int* slot = nullptr,
-                               const HeadCtx* hd = nullptr, const LossTail* tail = nullptr) {
+                               const HeadCtx* hd = nullptr, const LossTail* tail = nullptr,
+                               const PolicyRows* pr = nullptr, const GatherArgs* ga = nullptr) {
   GemmGroup g{};
   g.n = (int)ps.size();
   if (g.n > MAXP) return fail("gemm group too large");
@@ -738,8 +992,22 @@ static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const Ad
     if (TW != 16 || !ad || tail->nparts > 64) return fail("gemm group: bad loss tail");
     g.tail = *tail;
   }
+  int extra = tail ? 1 : 0;
+  if (pr) {
+    if (TW != 16 || pr->A > 8 || pr->H % 16 || pr->H > 256 || 16 * (pr->H + 4) > PR_LDS)
+      return fail("gemm group: bad policy rows (A <= 8, H <= 256, H % 16 == 0)");
+    g.pr = *pr;
+    g.pr.nblk = ceil_div(pr->n, 16) * ceil_div(pr->H, PR_COLS);
+    extra += g.pr.nblk;  // leading blocks (gemm_group_kernel)
+  }
+  if (ga) {
+    if (TW != 16) return fail("gemm group: gather blocks need the 16-wide kernel");
+    g.ga = *ga;
+    g.gather_blocks = ceil_div(ga->n * (2 * ga->O + ga->A + 2), 256);
+    extra += g.gather_blocks;
+  }
   if (TW == 32) hipLaunchKernelGGL(gemm32_group_kernel, dim3(tot), dim3(256), 0, s, g);
-  else hipLaunchKernelGGL(gemm_group_kernel, dim3(tot + (tail ? 1 : 0)), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL(gemm_group_kernel, dim3(tot + extra), dim3(256), 0, s, g);
   MOPO_HIP(hipGetLastError());
   return 0;
 }

@@ -5,13 +5,14 @@
 // Semantics: every forward and gradient uses the pre-step parameters; then pi, q1, q2
 // and alpha are updated by their own Adam (identical step counts -> one shared lr_t); then Polyak.
 //
-// Structure: 9 launches per step on one stream, captured into hipGraphs of 8 / 2 / 1 steps (no
+// Structure: 7 launches per step on one stream, captured into hipGraphs of 8 / 2 / 1 steps (no
 // host work per step): 2 grouped-GEMM forward launches for pi(s), pi(s'), Q1/Q2(s,a) (both hidden
 // layers in one: the first is recomputed per block from the <= 32 inputs; the policy output tile's
 // epilogue runs the squashed-Gaussian head), 1 for both hidden layers of Q1/Q2(s,pi) and the target
-// critics, sac_qloss_kernel (their 1-wide output layers, the losses and the alpha gradient), then 4
-// grouped-GEMM backward launches and the policy-head backward (which also gathers the next step's
-// batch).  The four TF1 Adams and Polyak run in the weight-gradient GEMM epilogues (gemm_group.h),
+// critics, sac_qloss_kernel (their 1-wide output layers, the losses and the alpha gradient), then 3
+// grouped-GEMM backward launches: the critics' dh1, the critics' weight gradients together with the
+// policy's row-local backward chain (dx over the actions -> head backward -> dh2p -> dh1p, extra
+// blocks of that launch), and the policy's weight gradients (+ the next step's batch gather).  The four TF1 Adams and Polyak run in the weight-gradient GEMM epilogues (gemm_group.h),
 // reading parameters Pb[p] and writing Pb[1 - p], so every gradient of the step sees pre-step
 // parameters.
 #include <vector>
@@ -48,11 +49,6 @@ static Offs make_offs(int O, int A, int H) {
 }
 
 
-struct Batch {
-  float *sa, *xpi, *xn, *rew, *term;  // [s, a], [s, pi(s)], [s', pi(s')], r, done
-  int64_t* idx;                       // [n] sampled rows
-};
-
 struct Sac {
   SacDims d{};
   Offs o{};
@@ -72,7 +68,7 @@ struct Sac {
   float *logp_s, *logp_n, *eps_s, *eps_n;
   float *dq[4];                   // dq for instances 2,3,4,5
   float *dh1[4];
-  float *dx1, *dx2, *dhead, *dh2p, *dh1p;
+  float *dhead, *dh2p, *dh1p;
   // graph
   bool use_graph = true;
   hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
@@ -83,53 +79,8 @@ struct Sac {
   uint64_t gseed = 0;
 };
 
-// ---- batch gather (_training_batch, mopo.py:801-821): rows [0, n_env) from the env pool, rest
-// from the model pool; each index uniform over the pool's live size (Philox) unless injected.
-// One thread per (row, field column): every thread derives its row's source index itself (the
-// Philox draw is cheap), so the kernel is two dependent memory latencies (pool size + counter,
-// then the field) with no barrier.
+// ---- batch gather (gemm_group.h gather_elem), as its own launch for a call's first step
 constexpr int GATHER_TPB = 256;
-struct GatherArgs {
-  mopo_pool_desc env, mod;
-  int n_env, O, A;
-  const int64_t* idx_in;             // injected rows or NULL (Philox draw)
-  uint64_t seed;
-  const int64_t* iter;
-  Batch out;
-};
-
-// field c of batch row r (obs | act | next_obs | rew | term)
-__device__ __forceinline__ void gather_elem(const GatherArgs& g, int r, int c) {
-  const int O = g.O, A = g.A, W = O + A;
-  const bool fe = r < g.n_env;
-  const mopo_pool_desc& p = fe ? g.env : g.mod;
-  int64_t src;
-  if (g.idx_in) {
-    src = g.idx_in[r];
-  } else {
-    const uint64_t size = (uint64_t)p.d_state[1];
-    const int64_t it = *g.iter;
-    u32x4 cc{(uint32_t)r, (uint32_t)it, (uint32_t)((uint64_t)it >> 32), RNG_SAC};
-    u32x4 q = philox(cc, (uint32_t)g.seed, (uint32_t)(g.seed >> 32));
-    src = (int64_t)(((uint64_t)q.x * size) >> 32);
-  }
-  const Batch& b = g.out;
-  if (c == 0) b.idx[r] = src;
-  if (c < O) {
-    const float v = p.d_obs[src * O + c];
-    b.sa[r * W + c] = v;
-    b.xpi[r * W + c] = v;
-  } else if (c < O + A) {
-    b.sa[r * W + c] = p.d_act[src * A + (c - O)];
-  } else if (c < 2 * O + A) {
-    b.xn[r * W + (c - O - A)] = p.d_next_obs[src * O + (c - O - A)];
-  } else if (c == 2 * O + A) {
-    b.rew[r] = p.d_rew[src];
-  } else {
-    b.term[r] = (float)p.d_term[src];
-  }
-}
-
 __global__ __launch_bounds__(GATHER_TPB) void sac_gather_kernel(const GatherArgs g, int n) {
   const int C = 2 * g.O + g.A + 2;
   const int e = blockIdx.x * GATHER_TPB + threadIdx.x;
@@ -271,58 +222,6 @@ __global__ __launch_bounds__(256) void sac_qloss_kernel(const QLossArgs a) {
   }
 }
 
-// ---- squashed Gaussian head backward + dh2 of the policy trunk (one block per batch row).
-// With `prefetch`, the block's second wave also gathers row r of the NEXT step's batch (the step
-// counter was advanced by this step's loss kernel), taking the gather off the step's critical path.
-__global__ __launch_bounds__(256) void pi_head_bwd_kernel(int n, int O, int A, int H, const float* head_s,
-                                                          const float* eps_s, const float* dx1, const float* dx2,
-                                                          const float* log_alpha, const float* Wm, const float* Wl,
-                                                          const float* h2p, float* dhead, float* dh2p,
-                                                          const GatherArgs next, int prefetch) {
-  __shared__ float dmu_s[8], dls_s[8];
-  const int r = blockIdx.x, tid = threadIdx.x;
-  if (prefetch && tid >= 64 && tid < 64 + 2 * O + A + 2) gather_elem(next, r, tid - 64);
-  if (tid < A) {
-    const int j = tid;
-    const float g = expf(*log_alpha) / (float)n;                    // d L_pi / d logp (stop_gradient(alpha))
-    const float mu = head_s[r * 2 * A + j], raw = head_s[r * 2 * A + A + j];
-    const float ls = fminf(fmaxf(raw, -20.f), 2.f);
-    const float sd = expf(ls);
-    const float e = eps_s[r * A + j];
-    const float u = mu + e * sd;
-    const float a = tanhf(u);
-    const float inv = 1.f / (sd + 1e-8f);
-    const float zz = (u - mu) * inv;
-    const float da = dx1[r * (O + A) + O + j] + dx2[r * (O + A) + O + j];  // -dmin q / da through Q1/Q2
-    float du = da * (1.f - a * a);                                  // tanh grad (y-based)
-    du += g * (-zz * inv);                                          // gaussian_likelihood wrt x
-    du += g * (2.f - 4.f / (1.f + expf(2.f * u)));                  // squash correction: 2 - 4 sigmoid(-2u)
-    const float dmu = g * zz * inv + du;
-    const float dstd = g * zz * zz * inv + du * e;
-    float dls = -g + dstd * sd;
-    if (!(raw >= -20.f && raw <= 2.f)) dls = 0.f;                   // clip_by_value grad
-    dhead[r * 2 * A + j] = dmu;
-    dhead[r * 2 * A + A + j] = dls;
-    dmu_s[j] = dmu;
-    dls_s[j] = dls;
-  }
-  __syncthreads();
-  for (int j = tid; j < H; j += blockDim.x) {
-    float wm[8], wl[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      wm[k] = k < A ? Wm[j * A + k] : 0.f;
-      wl[k] = k < A ? Wl[j * A + k] : 0.f;
-    }
-    const float hv = h2p[(int64_t)r * H + j];
-    float v = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k < A) v += dmu_s[k] * wm[k] + dls_s[k] * wl[k];
-    dh2p[(int64_t)r * H + j] = hv > 0.f ? v : 0.f;
-  }
-}
-
 // grad-norm logs of the last step (once per mopo_sac_step call): the per-block partials of the
 // fused optimizer epilogues, plus the alpha gradient (counted with neither network)
 __global__ __launch_bounds__(256) void sac_logs_kernel(const float* norm_part, int nslots, float* logs) {
@@ -343,7 +242,7 @@ __global__ __launch_bounds__(256) void sac_logs_kernel(const float* norm_part, i
 static GatherArgs gather_args(Sac* h, int par, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
                               const int64_t* idx_in) {
   GatherArgs g{};
-  g.env = *env; g.mod = *mod; g.n_env = h->d.n_env; g.O = h->d.O; g.A = h->d.A;
+  g.env = *env; g.mod = *mod; g.n = h->d.n; g.n_env = h->d.n_env; g.O = h->d.O; g.A = h->d.A;
   g.idx_in = idx_in; g.seed = seed; g.iter = h->iter; g.out = h->bt[par];
   return g;
 }
@@ -358,7 +257,7 @@ static int launch_gather(Sac* h, int par, const mopo_pool_desc* env, const mopo_
 }
 
 // One SAC step on batch bt[par], reading parameters Pb[par] and writing the updated ones to
-// Pb[1 - par].  With `prefetch`, the policy-head backward kernel also gathers the next step's batch
+// Pb[1 - par].  With `prefetch`, the policy weight-gradient launch also gathers the next step's batch
 // into bt[1 - par] (a separate gather launch, or a forked graph branch, costs more than it hides).
 static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
                          const float* eps_in_s, const float* eps_in_n, hipStream_t s, bool prefetch) {
@@ -456,7 +355,9 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     if (launch_group(g, s, &ad, &slot, nullptr, &lt)) return -1;
   }
   {
-    // dW2 / dW3 only need the rank-1 dh2 (not dh1), so they ride with the smaller second launch
+    // dW2 / dW3 only need the rank-1 dh2 (not dh1), so they ride with the smaller second launch; the
+    // extra policy-row blocks run the policy's row-local backward chain (dx over the actions through
+    // Q1/Q2(s, pi), the head backward, dh2p, dh1p: gemm_group.h policy_rows_block)
     std::vector<GemmProb> g;
     for (int qi = 0; qi < 2; ++qi) {  // dW2 = h1^T dh2 (+db2), dW3 = h2^T dq (+db3)
       auto w2 = mk(H, H, n, h->h1[2 + qi], H, 1, nullptr, H, 0, G + o.q[qi][2], H); w2.colsum = G + o.q[qi][3];
@@ -467,46 +368,42 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       w3.adam = 1;
       g.push_back(w3);
     }
-    g.push_back(mk(n, W, H, h->dh1[2], H, 0, Wq(0, 0), H, 1, h->dx1, W));   // d/dx of Q1(s, pi)
-    g.push_back(mk(n, W, H, h->dh1[3], H, 0, Wq(1, 0), H, 1, h->dx2, W));   // d/dx of Q2(s, pi)
     for (int qi = 0; qi < 2; ++qi) {  // dW1 = [s,a]^T dh1 (+db1)
       auto w1 = mk(W, H, n, bt.sa, W, 1, h->dh1[qi], H, 0, G + o.q[qi][0], H); w1.colsum = G + o.q[qi][1];
       w1.adam = 1;
       g.push_back(w1);
     }
-    if (launch_group(g, s, &ad, &slot)) return -1;
+    PolicyRows pr{};
+    pr.n = n; pr.O = O; pr.A = A; pr.H = H;
+    pr.dh1[0] = h->dh1[2]; pr.dh1[1] = h->dh1[3]; pr.w1[0] = Wq(0, 0); pr.w1[1] = Wq(1, 0);
+    pr.head_s = h->out[0]; pr.eps_s = h->eps_s; pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
+    pr.h2p = h->h2[0]; pr.h1p = h->h1[0]; pr.W2p = P + o.pW2;
+    pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p;
+    if (launch_group(g, s, &ad, &slot, nullptr, nullptr, &pr)) return -1;
   }
-  // ---- policy backward
-  hipLaunchKernelGGL(pi_head_bwd_kernel, dim3(n), dim3(256), 0, s, n, O, A, H, h->out[0], h->eps_s, h->dx1, h->dx2,
-                     P + o.total, P + o.pWm, P + o.pWl, h->h2[0], h->dhead, h->dh2p,
-                     gather_args(h, 1 - par, env, mod, seed, nullptr), prefetch ? 1 : 0);
-  MOPO_HIP(hipGetLastError());
   {
+    // the policy's weight gradients (+ Adam); with `prefetch`, extra blocks gather the next step's
+    // batch into the other buffer (the step counter was advanced by this step's loss tail)
     std::vector<GemmProb> g;
-    auto a = mk(n, H, H, h->dh2p, H, 0, P + o.pW2, H, 1, h->dh1p, H); a.mask = h->h1[0]; a.ldm = H; g.push_back(a);
     auto w2 = mk(H, H, n, h->h1[0], H, 1, h->dh2p, H, 0, G + o.pW2, H); w2.colsum = G + o.pb2; w2.adam = 1; g.push_back(w2);
     auto wm = mk(H, A, n, h->h2[0], H, 1, h->dhead, 2 * A, 0, G + o.pWm, A); wm.colsum = G + o.pbm; wm.adam = 1;
     g.push_back(wm);
     auto wl = mk(H, A, n, h->h2[0], H, 1, h->dhead + A, 2 * A, 0, G + o.pWl, A); wl.colsum = G + o.pbl; wl.adam = 1;
     g.push_back(wl);
-    if (launch_group(g, s, &ad, &slot)) return -1;
-  }
-  {
-    std::vector<GemmProb> g;
     auto w1 = mk(O, H, n, bt.sa, W, 1, h->dh1p, H, 0, G + o.pW1, H); w1.colsum = G + o.pb1; w1.adam = 1; g.push_back(w1);
-    if (launch_group(g, s, &ad, &slot)) return -1;
+    const GatherArgs ga = gather_args(h, 1 - par, env, mod, seed, nullptr);
+    if (launch_group(g, s, &ad, &slot, nullptr, nullptr, nullptr, prefetch ? &ga : nullptr)) return -1;
   }
   if (slot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
   h->nslots = slot;  // blocks of the four backward launches (tile choice: launch_group)
   return 0;
 }
 
-// upper bound of the blocks of the four backward launches (16x16 tiles; one grad-norm slot each)
+// the GEMM tiles of the three backward launches (16x16 tiles; one grad-norm slot each)
 static int count_slots(const SacDims& d) {
   auto t = [](int M, int N) { return ceil_div(M, 16) * ceil_div(N, 16); };
   const int n = d.n, H = d.H, O = d.O, A = d.A, W = O + A;
-  return 4 * t(n, H) + 2 * t(H, H) + 2 * t(H, 1) + 2 * t(n, W) + 2 * t(W, H) + t(n, H) + t(H, H) + 2 * t(H, A) +
-         t(O, H);
+  return 4 * t(n, H) + 2 * t(H, H) + 2 * t(H, 1) + 2 * t(W, H) + t(H, H) + 2 * t(H, A) + t(O, H);
 }
 
 }  // namespace mopo
@@ -519,7 +416,7 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   MOPO_REQUIRE(out && h_params, "mopo_sac_create: NULL argument");
   MOPO_REQUIRE(O >= 1 && A >= 1 && A <= 8 && H >= 1, "mopo_sac_create: bad dims (act_dim <= 8)");
   MOPO_REQUIRE(batch >= 1 && batch <= 1024, "mopo_sac_create: batch must be in [1, 1024]");
-  MOPO_REQUIRE(H % 16 == 0, "mopo_sac_create: hidden width must be a multiple of 16");
+  MOPO_REQUIRE(H % 16 == 0 && H <= 256, "mopo_sac_create: hidden width must be a multiple of 16, <= 256");
   MOPO_REQUIRE(n_env >= 0 && n_env <= batch, "mopo_sac_create: n_env must be in [0, batch]");
   Sac* h = new Sac();
   h->d = SacDims{O, A, H, batch, n_env, 0};
@@ -543,7 +440,7 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   for (int i = 0; i < 8; ++i) { f(&h->h1[i], n * H); f(&h->h2[i], n * H); f(&h->out[i], n * 2 * A); }
   f(&h->logp_s, n); f(&h->logp_n, n); f(&h->eps_s, n * A); f(&h->eps_n, n * A);
   for (int i = 0; i < 4; ++i) { f(&h->dq[i], n); f(&h->dh1[i], n * H); }
-  f(&h->dx1, n * W); f(&h->dx2, n * W); f(&h->dhead, n * 2 * A); f(&h->dh2p, n * H); f(&h->dh1p, n * H);
+  f(&h->dhead, n * 2 * A); f(&h->dh2p, n * H); f(&h->dh1p, n * H);
   size_t total = 0;
   for (auto& r : reg) total += (r.second + 255) & ~(size_t)255;
   if (hipMalloc(&h->mem, total) != hipSuccess) { delete h; return fail("mopo_sac_create: out of device memory"); }

@@ -4,7 +4,8 @@ Follows (reference xionghuichen/mopo):
   * ``MOPO._rollout_model``          mopo/algorithms/mopo.py:723-765
   * start states ``sampler.random_batch`` -> ``pool.random_batch``  softlearning/samplers/simple_sampler.py:103-108
   * ``get_action_meta`` (policy noise is TF's; injected here)       mopo/algorithms/mopo.py:468-485
-  * ``_reallocate_model_pool`` sizing                              mopo/algorithms/mopo.py:689-711
+  * ``_set_rollout_length`` schedule                               mopo/algorithms/mopo.py:675-684
+  * ``_reallocate_model_pool`` sizing + sample carry-over          mopo/algorithms/mopo.py:689-711
 
 RNG order per rollout (numpy legacy global state): randint(size, B) start rows; then per
 step normal(E, B_i, D) and choice(elites, B_i).  Policy noise eps_act[i] ([B_i, A]) is injected.
@@ -20,6 +21,33 @@ def model_pool_size(rollout_batch_size, epoch_length, model_train_freq, rollout_
     rollouts_per_epoch = rollout_batch_size * epoch_length / model_train_freq
     model_steps_per_epoch = int(rollout_length * rollouts_per_epoch)
     return retain_epochs * model_steps_per_epoch
+
+
+def rollout_length(epoch, schedule):
+    """mopo.py:675-684: linear ramp from min_length (epoch <= min_epoch) to max_length (epoch >= max_epoch),
+    truncated to int."""
+    min_epoch, max_epoch, min_length, max_length = schedule
+    if epoch <= min_epoch:
+        y = min_length
+    else:
+        y = min((epoch - min_epoch) / (max_epoch - min_epoch), 1) * (max_length - min_length) + min_length
+    return int(y)
+
+
+def reallocate(pool, obs_dim, act_dim, rollout_batch_size, epoch_length, model_train_freq, rollout_length,
+               retain_epochs):
+    """mopo.py:689-711 on an oracle ``Pool`` (None: first allocation).  Returns the pool to use: the
+    same object when the size is unchanged, else a new pool holding ``return_all_samples()``."""
+    from .replay_pool import Pool
+    size = model_pool_size(rollout_batch_size, epoch_length, model_train_freq, rollout_length, retain_epochs)
+    if pool is None:
+        return Pool(obs_dim, act_dim, size)
+    if pool._max_size == size:
+        return pool
+    new = Pool(obs_dim, act_dim, size)
+    new.add_samples(pool.return_all_samples())
+    assert new.size == pool.size
+    return new
 
 
 def rollout(env_pool, model_pool, bnn_params, elites, pi_params, B, horizon, termination_fn,

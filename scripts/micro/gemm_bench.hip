@@ -7,13 +7,32 @@ using namespace mopo;
 __global__ void empty_kernel(const GemmGroup g) {
   if (threadIdx.x == 0 && g.n < 0) g.p[0].C[0] = 1.f;
 }
+__global__ void empty_small(float* p, int n) {
+  if (threadIdx.x == 0 && n < 0) p[0] = 1.f;
+}
+// one dependent load + store per thread, big kernarg (the GemmGroup) read at a dynamic index
+__global__ void ldst_kernel(const GemmGroup g) {
+  int pi = 0;
+  while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
+  const GemmProb& p = g.p[pi];
+  p.C[blockIdx.x * 256 + threadIdx.x] = p.A[blockIdx.x * 256 + threadIdx.x] + 1.f;
+}
+__global__ void ldst_small(const float* a, float* c) {
+  c[blockIdx.x * 256 + threadIdx.x] = a[blockIdx.x * 256 + threadIdx.x] + 1.f;
+}
 
-static float time_graph(std::vector<GemmProb> ps, int reps, hipStream_t s, bool empty) {
+static float time_graph(std::vector<GemmProb> ps, int reps, hipStream_t s, int empty) {
   hipGraph_t gr; hipGraphExec_t ge;
   (void)hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
   for (int i = 0; i < 16; ++i) {
     if (!empty) launch_group(ps, s);
-    else { GemmGroup g{}; g.n = 1; g.p[0] = ps[0]; hipLaunchKernelGGL(empty_kernel, dim3(256), dim3(256), 0, s, g); }
+    else {
+      GemmGroup g{}; g.n = 1; g.p[0] = ps[0]; g.prefix[1] = 1 << 20;
+      if (empty == 1) hipLaunchKernelGGL(empty_kernel, dim3(256), dim3(256), 0, s, g);
+      if (empty == 2) hipLaunchKernelGGL(empty_small, dim3(256), dim3(256), 0, s, ps[0].C, 1);
+      if (empty == 3) hipLaunchKernelGGL(ldst_kernel, dim3(256), dim3(256), 0, s, g);
+      if (empty == 4) hipLaunchKernelGGL(ldst_small, dim3(256), dim3(256), 0, s, ps[0].A, ps[0].C);
+    }
   }
   (void)hipStreamEndCapture(s, &gr);
   (void)hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
@@ -34,16 +53,21 @@ int main() {
   (void)hipMalloc(&X, 8 * n * H * 4); (void)hipMalloc(&W, 8 * H * H * 4); (void)hipMalloc(&Y, 8 * n * H * 4);
   (void)hipMalloc(&M, n * H * 4);
   (void)hipMemset(X, 0, 8 * n * H * 4); (void)hipMemset(W, 0, 8 * H * H * 4); (void)hipMemset(M, 0, n * H * 4);
-  auto fwd = [&](int i) { auto p = mk(n, H, H, X + i * n * H, H, 0, W + i * H * H, H, 0, Y + i * n * H, H); p.relu = 1; p.bias = W; return p; };
+  auto fwd = [&](int i) { auto p = mk(n, H, H, X + i * n * H, H, 0, W + i * H * H, H, 0, Y + i * n * H, H); p.act = ACT_RELU; p.bias = W; return p; };
   auto bwd = [&](int i) { auto p = mk(n, H, H, X + i * n * H, H, 0, W + i * H * H, H, 1, Y + i * n * H, H); p.mask = M; p.ldm = H; return p; };
   auto wgt = [&](int i) { auto p = mk(H, H, n, X + i * n * H, H, 1, Y + i * n * H, H, 0, W + i * H * H, H); p.colsum = M; return p; };
-  printf("empty kernel (same kernarg):  %.2f us\n", time_graph({fwd(0)}, 200, s, true));
-  printf("1 tile 16x16x16:              %.2f us\n", time_graph({mk(16, 16, 16, X, 16, 0, W, 16, 0, Y, 16)}, 200, s, false));
-  printf("1 tile 16x16x256:             %.2f us\n", time_graph({mk(16, 16, 256, X, 256, 0, W, 16, 0, Y, 16)}, 200, s, false));
-  printf("fwd 1 x 256x256x256:          %.2f us\n", time_graph({fwd(0)}, 200, s, false));
-  printf("fwd 4 x 256x256x256:          %.2f us\n", time_graph({fwd(0), fwd(1), fwd(2), fwd(3)}, 200, s, false));
-  printf("bwd-data 4 x (W^T, mask):     %.2f us\n", time_graph({bwd(0), bwd(1), bwd(2), bwd(3)}, 200, s, false));
-  printf("wgrad 2 x (X^T dY, colsum):   %.2f us\n", time_graph({wgt(0), wgt(1)}, 200, s, false));
-  printf("fwd K=23 4 x 256x256:         %.2f us\n", time_graph({mk(n, H, 23, X, 23, 0, W, H, 0, Y, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + n * H, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + 2 * n * H, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + 3 * n * H, H)}, 200, s, false));
+  printf("empty kernel (GemmGroup kernarg): %.2f us\n", time_graph({fwd(0)}, 200, s, 1));
+  printf("empty kernel (16 B kernarg):      %.2f us\n", time_graph({fwd(0)}, 200, s, 2));
+  printf("load+store (GemmGroup kernarg):   %.2f us\n", time_graph({fwd(0)}, 200, s, 3));
+  printf("load+store (16 B kernarg):        %.2f us\n", time_graph({fwd(0)}, 200, s, 4));
+  auto w16 = [&](int i) { auto p = mk(16, 16, n, X + i * n * H, H, 1, Y + i * n * H, H, 0, W + i * H * H, H); return p; };
+  printf("1 tile wgrad 16x16 K=256 (T):  %.2f us\n", time_graph({w16(0)}, 200, s, 0));
+  printf("1 tile 16x16x16:              %.2f us\n", time_graph({mk(16, 16, 16, X, 16, 0, W, 16, 0, Y, 16)}, 200, s, 0));
+  printf("1 tile 16x16x256:             %.2f us\n", time_graph({mk(16, 16, 256, X, 256, 0, W, 16, 0, Y, 16)}, 200, s, 0));
+  printf("fwd 1 x 256x256x256:          %.2f us\n", time_graph({fwd(0)}, 200, s, 0));
+  printf("fwd 4 x 256x256x256:          %.2f us\n", time_graph({fwd(0), fwd(1), fwd(2), fwd(3)}, 200, s, 0));
+  printf("bwd-data 4 x (W^T, mask):     %.2f us\n", time_graph({bwd(0), bwd(1), bwd(2), bwd(3)}, 200, s, 0));
+  printf("wgrad 2 x (X^T dY, colsum):   %.2f us\n", time_graph({wgt(0), wgt(1)}, 200, s, 0));
+  printf("fwd K=23 4 x 256x256:         %.2f us\n", time_graph({mk(n, H, 23, X, 23, 0, W, H, 0, Y, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + n * H, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + 2 * n * H, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + 3 * n * H, H)}, 200, s, 0));
   return 0;
 }

@@ -36,3 +36,47 @@ def test_mopo_two_epochs_from_config(tmp_path):
     assert algo._model_pool._max_size == 5 * 5 * 2000
     assert algo._model_pool.size == 2 * 5 * 2000
     assert algo._num_train_steps == 200
+
+
+def test_reallocate_model_pool_vs_oracle():
+    """MOPO._reallocate_model_pool (mopo.py:689-711) over a rollout-length ramp: the device pool's
+    size after every epoch equals the oracle's, and the rows carried into a resized pool (also out of
+    a wrapped ring) are bit-identical to the oracle pool's; a shrink below the live row count trips
+    the reference's size assert (mopo.py:710) in both."""
+    from types import SimpleNamespace
+    from mopo_amd.mopo import MOPO
+    from oracle import rollout as orl
+    O, A = 5, 2
+    rs = np.random.RandomState(3)
+    stub = SimpleNamespace(_obs_dim=O, _act_dim=A, _rollout_batch_size=40, _epoch_length=10,
+                           _model_train_freq=5, _model_retain_epochs=2, _rollout_schedule=[1, 4, 1, 4])
+    opool = None
+    for epoch, n_add in zip(range(9), [50, 70, 200, 30, 300, 10, 400, 5, 90]):
+        stub._epoch = epoch
+        MOPO._set_rollout_length(stub)
+        if epoch == 6:  # grow out of a wrapped ring: the schedule's max length rises to 6
+            stub._rollout_schedule = [0, 1, 1, 6]
+            MOPO._set_rollout_length(stub)
+        MOPO._reallocate_model_pool(stub)
+        opool = orl.reallocate(opool, O, A, stub._rollout_batch_size, stub._epoch_length, stub._model_train_freq,
+                               stub._rollout_length, stub._model_retain_epochs)
+        assert stub._model_pool._max_size == opool._max_size, epoch
+        assert stub._model_pool.size == opool.size, epoch
+        got = stub._model_pool.return_all_samples(as_numpy=True)
+        ref = opool.return_all_samples()
+        for k in ref:
+            np.testing.assert_array_equal(got[k].reshape(ref[k].shape), ref[k], err_msg='%s epoch %d' % (k, epoch))
+        smp = {'observations': rs.normal(size=(n_add, O)).astype(np.float32),
+               'actions': rs.uniform(-1, 1, size=(n_add, A)).astype(np.float32),
+               'next_observations': rs.normal(size=(n_add, O)).astype(np.float32),
+               'rewards': rs.normal(size=(n_add, 1)).astype(np.float32),
+               'terminals': rs.uniform(size=(n_add, 1)) < 0.2}
+        stub._model_pool.add_samples(smp)
+        opool.add_samples(smp)
+    stub._rollout_schedule = [0, 1, 1, 1]
+    MOPO._set_rollout_length(stub)
+    with pytest.raises(AssertionError):
+        MOPO._reallocate_model_pool(stub)
+    with pytest.raises(AssertionError):
+        orl.reallocate(opool, O, A, stub._rollout_batch_size, stub._epoch_length, stub._model_train_freq,
+                       stub._rollout_length, stub._model_retain_epochs)

@@ -193,3 +193,34 @@ def test_perf_streams_shape_and_range():
     assert (rng.act_noise(uid, 7, 1, 6) != rng.act_noise(uid, 7, 2, 6)).all()   # step is in the counter
     sel = rng.model_choice(uid, 7, 1, [4, 1, 0, 6, 2])
     assert set(np.unique(sel)) == {0, 1, 2, 4, 6}
+
+
+# ---- rollout-length schedule and model-pool sizing (mopo.py:675-711) ----------------
+SCHEDULES = [[20, 100, 1, 1], [20, 100, 5, 5], [20, 100, 1, 5], [0, 10, 5, 1], [3, 7, 1, 15]]
+
+
+@pytest.mark.parametrize('schedule', SCHEDULES, ids=[str(s) for s in SCHEDULES])
+def test_set_rollout_length_vs_oracle(schedule):
+    """MOPO._set_rollout_length (the host mirror) against oracle.rollout.rollout_length for every
+    epoch of a 0..150 sweep, on a stub carrying only the fields the method reads."""
+    from types import SimpleNamespace
+    from mopo_amd.mopo import MOPO
+    from oracle import rollout as orl
+    for epoch in range(151):
+        stub = SimpleNamespace(_rollout_schedule=schedule, _epoch=epoch)
+        MOPO._set_rollout_length(stub)
+        assert stub._rollout_length == orl.rollout_length(epoch, schedule), epoch
+    # hand values of the ramp (mopo.py:680-684): int() truncates
+    assert orl.rollout_length(21, [20, 100, 1, 5]) == 1
+    assert orl.rollout_length(40, [20, 100, 1, 5]) == 2
+    assert orl.rollout_length(99, [20, 100, 1, 5]) == 4
+    assert orl.rollout_length(100, [20, 100, 1, 5]) == 5
+
+
+def test_model_pool_size_configs():
+    """mopo.py:693-695 at the D4RL configs' values (rollout_batch 50k, epoch_length 1000 = model_train_freq,
+    retain 5): h=5 -> 1.25e6 rows, h=1 -> 2.5e5."""
+    from oracle import rollout as orl
+    assert orl.model_pool_size(50000, 1000, 1000, 5, 5) == 1250000
+    assert orl.model_pool_size(50000, 1000, 1000, 1, 5) == 250000
+    assert orl.model_pool_size(100000, 1000, 250, 1, 20) == 8000000
