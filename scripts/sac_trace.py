@@ -1,5 +1,6 @@
 """SAC kernel durations from a rocprofv3 kernel trace: mean duration per kernel name (and calls per
-step), and the step period as the mean interval between consecutive (q)loss-kernel starts.
+step), the step period as the mean interval between consecutive starts of the step's anchor launch
+(the critic dh1 launch: the grouped-GEMM launch with the largest grid), and per-position durations.
 Usage: python scripts/sac_trace.py run_kernel_trace.csv"""
 import collections
 import csv
@@ -7,10 +8,13 @@ import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
 sac = [r for r in rows if any(k in r['Kernel_Name'] for k in ('gemm_group', 'sac_', 'pi_head'))]
-loss = [int(r['Start_Timestamp']) for r in sac if 'loss_kernel' in r['Kernel_Name']]
-skip = len(loss) // 4
-t0, t1 = loss[skip], loss[-1]
-steps = len(loss) - 1 - skip
+grid = lambda r: int(r.get('Grid_Size_X') or r.get('Grid_Size') or 0)
+# anchor: the largest-grid grouped-GEMM launch (critic dh1 + loss tail: 1025 blocks at batch 256)
+gmax = max(grid(r) for r in sac if 'gemm_group' in r['Kernel_Name'])
+anchor = [int(r['Start_Timestamp']) for r in sac if 'gemm_group' in r['Kernel_Name'] and grid(r) == gmax]
+skip = len(anchor) // 4
+t0, t1 = anchor[skip], anchor[-1]
+steps = len(anchor) - 1 - skip
 dur = collections.defaultdict(list)
 busy = 0
 for r in sac:
@@ -21,15 +25,15 @@ for r in sac:
         busy += d
 for n, v in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
     print('%-34s %5.1f calls/step  %6.2f us avg  %6.1f us/step' % (n, len(v) / steps, sum(v) / len(v), sum(v) / steps))
-print('step period %.1f us (loss-to-loss, %d steps); kernel-busy %.1f us/step'
+print('step period %.1f us (anchor-to-anchor, %d steps); kernel-busy %.1f us/step'
       % ((t1 - t0) / 1e3 / steps, steps, busy / steps))
 
-# per position within the period (dispatch order after a loss kernel)
+# per position within the period (dispatch order after an anchor launch)
 pos = collections.defaultdict(list)
 cur = -1
 for r in sac:
     st = int(r['Start_Timestamp'])
-    if 'loss_kernel' in r['Kernel_Name']:
+    if 'gemm_group' in r['Kernel_Name'] and grid(r) == gmax:
         cur = 0
     if cur < 0 or not (t0 <= st < t1):
         continue
