@@ -526,11 +526,12 @@ def main():
 
 
 # the ensemble-forward launch of each dtype at the C2 shapes (E=7, H=200, obs 17 + act 6), rollout mode
+# the rollout-mode kernel of each dtype at the C2 shapes (H = 200: 14 blocks of which 13 are used)
 ENSEMBLE_KERNEL = {'fp32': 'mopo::bnn_fwd_kernel<2, 13, 3, 1, 1, 4, 2, 2>',
-                   'f16x3': 'mopo::bnn_fwd_f16s_kernel<14, 3, 1, 4, 1>',
-                   'bf16x6': 'mopo::bnn_fwd_bf16_kernel<14, 3, 1, 4, 3, 1>',
-                   'bf16x3': 'mopo::bnn_fwd_bf16_kernel<14, 3, 1, 4, 2, 1>',
-                   'bf16': 'mopo::bnn_fwd_bf16_kernel<14, 3, 1, 4, 1, 1>'}
+                   'f16x3': 'mopo::bnn_fwd_f16s_kernel<14, 3, 1, 4, 1, 13>',
+                   'bf16x6': 'mopo::bnn_fwd_bf16_kernel<14, 3, 1, 4, 3, 1, 13>',
+                   'bf16x3': 'mopo::bnn_fwd_bf16_kernel<14, 3, 1, 4, 2, 1, 13>',
+                   'bf16': 'mopo::bnn_fwd_bf16_kernel<14, 3, 1, 4, 1, 1, 13>'}
 
 
 def workload_key(args):
