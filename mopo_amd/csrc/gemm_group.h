@@ -683,7 +683,22 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
   const GemmProb& p = g.p[pi];
   const int t = bid - g.prefix[pi];
   const int tn_cnt = ceil_div(p.N, 16);
-  const int tm = t / tn_cnt, tn = t % tn_cnt;
+#ifndef MOPO_GEMM_XCD
+#define MOPO_GEMM_XCD 1
+#endif
+  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (block b on XCD b mod 8),
+  // so when a problem's first block sits on XCD 0 and its column-tile count divides by 8, XCD x takes
+  // column tiles [x C/8, (x+1) C/8) of every row tile: each B panel (the weight columns of an MLP
+  // layer) is fetched into one XCD's L2 instead of all eight.
+  int tm, tn;
+  if (MOPO_GEMM_XCD && (tn_cnt & 7) == 0 && ((g.pr.nblk + g.prefix[pi]) & 7) == 0) {
+    const int per = tn_cnt >> 3, x = t & 7, j = t >> 3;
+    tn = x * per + j % per;
+    tm = j / per;
+  } else {
+    tm = t / tn_cnt;
+    tn = t % tn_cnt;
+  }
   const int i0 = tm * 16, j0 = tn * 16;
   const int li = lane & 15, lk = lane >> 4;
   const bool do_cs = p.colsum && tm == 0;
