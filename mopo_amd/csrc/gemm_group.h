@@ -222,6 +222,9 @@ struct PolicyRows {
   float* dhead; float* dh2p; float* dh1p;
 };
 
+#ifndef MOPO_PR_EARLY
+#define MOPO_PR_EARLY 0  // 1: the whole W2p operand tile and the h1p mask in burst 2 (no burst 3)
+#endif
 constexpr int PR_COLS = 64;          // dh1p columns per policy-row block (one 16-wide tile per wave)
 constexpr int PR_LDS = 2 * 256 * 16; // floats the grouped kernel's panel LDS offers it (H <= 508)
 
@@ -303,6 +306,15 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   f32x4 bq0[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) bq0[t] = bquad(t);
+#if MOPO_PR_EARLY
+  f32x4 bq1[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) bq1[t] = bquad(8 + t);
+  const auto dm1 = rsrc(c.h1p, (int64_t)n * H);
+  float m1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
+#endif
   __syncthreads();
   // ---- squashed-Gaussian head backward (mopo.py:282-308 differentiated; pi_loss mopo.py:371-377)
   float* dmu_s = hs + 128;
@@ -348,6 +360,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
       if (cq == 0 && r0 + i < n) c.dh2p[(int64_t)(r0 + i) * H + hc] = v;
     }
   }
+#if !MOPO_PR_EARLY
   // ---- burst 3: the second half of the W2p operands and the h1p mask of this lane's four outputs
   f32x4 bq1[8];
 #pragma unroll
@@ -356,6 +369,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   float m1[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
+#endif
   __syncthreads();
   // ---- dh1p tile = dh2p W2p^T * (h1p > 0): rows r0.., columns j0.. (wave w)
   if (!tile_on) return;
