@@ -174,3 +174,65 @@ def test_training_batch_mirror():
     assert set(got) == set(ref)
     for k in ref:
         np.testing.assert_array_equal(np.asarray(got[k], np.float64), ref[k], err_msg=k)
+
+
+@pytest.mark.parametrize('o,a,h,n', [(11, 3, 32, 100), (17, 6, 64, 250), (8, 8, 256, 40)])
+def test_sac_one_step_gradients_odd_shapes(o, a, h, n):
+    """One step's gradients at shapes the headline never uses: a batch that is not a multiple of 16
+    (the policy-row blocks' and tiles' out-of-range rows), H < 256 (the policy-row MFMA's partial
+    K split, column tiles not divisible by the 8 XCDs) and A = 8 (the widest head)."""
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.sac import SAC
+    import torch
+    rs = np.random.RandomState(7)
+    pl = []
+    for rows in (300, 900):
+        s = {'observations': rs.normal(size=(rows, o)).astype(np.float32),
+             'actions': rs.uniform(-1, 1, (rows, a)).astype(np.float32),
+             'next_observations': rs.normal(size=(rows, o)).astype(np.float32),
+             'rewards': rs.normal(size=(rows, 1)).astype(np.float32),
+             'terminals': rs.uniform(size=(rows, 1)) < 0.1}
+        p = SimpleReplayPool(obs_dim=o, act_dim=a, max_size=rows)
+        p.add_samples(s)
+        op = opool.Pool(o, a, rows)
+        op.add_samples(s)
+        pl.append((p, op))
+    torch.cuda.synchronize()
+    (env_p, env_op), (mod_p, mod_op) = pl
+    params = [p + rs.normal(size=p.shape) * 0.02 for p in osac.init_params(o, a, h, seed=9)]
+    sac = SAC(o, a, h, batch_size=n, real_ratio=0.05, target_entropy=-3, params=flat(params).astype(np.float32),
+              log_alpha=0.1)
+    ne = sac.n_env
+    idx = np.concatenate([rs.randint(0, 300, ne), rs.randint(0, 900, n - ne)])
+    e1 = rs.normal(size=(n, a)).astype(np.float32)
+    e2 = rs.normal(size=(n, a)).astype(np.float32)
+    st = osac.SACState([p.astype(np.float32).astype(np.float64) for p in params], log_alpha=np.float32(0.1))
+    batch = host_batch(env_op, mod_op, idx, n_env=ne)
+    # oracle_grads reads the module's O for the action slice: pass this case's split explicitly
+    s, act, s2 = batch['observations'], batch['actions'], batch['next_observations']
+    r, d = batch['rewards'][:, 0], batch['terminals'][:, 0]
+    P, Q1, Q2 = osac.split(st.params)
+    T = osac.split(st.target)
+    alpha = np.exp(st.log_alpha)
+    _, a_pi, logp_pi, _, cpi = osac.pi_forward(P, s, e1.astype(np.float64))
+    q1_pi, c1p = osac.q_forward(Q1, s, a_pi)
+    q2_pi, c2p = osac.q_forward(Q2, s, a_pi)
+    _, a_n, logp_n, _, _ = osac.pi_forward(P, s2, e2.astype(np.float64))
+    y = r + 0.99 * (1 - d) * (np.minimum(osac.q_forward(T[1], s2, a_n)[0], osac.q_forward(T[2], s2, a_n)[0])
+                              - alpha * logp_n)
+    g1, _ = osac.q_backward(Q1, osac.q_forward(Q1, s, act)[1], (osac.q_forward(Q1, s, act)[0] - y) / n)
+    g2, _ = osac.q_backward(Q2, osac.q_forward(Q2, s, act)[1], (osac.q_forward(Q2, s, act)[0] - y) / n)
+    sel = q1_pi <= q2_pi
+    _, dx1 = osac.q_backward(Q1, c1p, np.where(sel, -1.0 / n, 0.0), need_params=False)
+    _, dx2 = osac.q_backward(Q2, c2p, np.where(sel, 0.0, -1.0 / n), need_params=False)
+    gp = osac.pi_backward(P, cpi, np.full(n, alpha / n), dx1[:, o:] + dx2[:, o:])
+    gref = gp + g1 + g2
+    sac._do_training(0, env_p, mod_p, idx=idx, eps_s=e1, eps_n=e2)
+    g = sac.get_grads()[0].cpu().numpy()
+    off = 0
+    for i, gr in enumerate(gref):
+        m = gr.size
+        scale = np.abs(gr).max() + 1e-12
+        err = np.abs(g[off:off + m] - gr.ravel()).max()
+        assert err <= 1e-4 * scale + 1e-7, 'grad tensor %d: err %.3g scale %.3g' % (i, err, scale)
+        off += m
