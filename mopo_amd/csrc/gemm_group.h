@@ -965,6 +965,108 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
   }
 }
 
+// ---- both hidden layers of up to MAXP MLPs (operand mode ta == 2 only), one 16 x 64 output block per
+// 256-thread workgroup: the block recomputes its rows' 16 x K layer-1 slab ONCE for four 16-wide column
+// tiles (the 16x16-tile kernel recomputes it per tile, 16x per row block at H = 256: more MFMA work than
+// layer 2 itself), and each wave owns one column tile over the whole K (no cross-wave reduction), its
+// W2 panel staged wave-privately in LDS.  Epilogue: bias + relu (the mlp12 problems of the SAC forward).
+constexpr int WCOLS = 64;
+static __global__ __launch_bounds__(256, 1) void mlp12_wide_kernel(const GemmGroup g) {
+  __shared__ float As[GKC * 16];      // layer-1 slab, [k][r ^ psw(k)]
+  __shared__ float Bw[4][GKC * 16];   // wave w's 16-column W2 panel, [k][c]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int pi = 0;
+  while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
+  const GemmProb& p = g.p[pi];
+  const int t = blockIdx.x - g.prefix[pi];
+  const int tn_cnt = ceil_div(p.N, WCOLS);
+  const int tm = t / tn_cnt, tn = t % tn_cnt;
+  const int i0 = tm * 16, jw = tn * WCOLS + w * 16;
+  // 1. this wave's W2 panel (B(k, j) = B[k ldb + j], K <= 256 rows x 16 columns): lane l loads rows
+  //    l / 4 + 16 i, columns 4 (l % 4) .. + 3 -- issued first, consumed after the slab
+  const auto dbw = rsrc(p.B, (int64_t)(p.K - 1) * p.ldb + p.N);
+  f32x4 bp[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = (lane >> 2) + 16 * i, col = jw + 4 * (lane & 3);
+    bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          dbw, ((k < p.K && col < p.N) ? k * p.ldb + col : -4) * 4, 0, 0));
+  }
+  // 2. the layer-1 slab D(k, r) = relu(W1^T X^T + b1) (as stage_mlp1; the bias rides as input column K1)
+  {
+    const int r = lane & 15, q = lane >> 4;
+    const int k1 = p.a_ldm, ns = (k1 + 4) >> 2, sb = k1 >> 2;
+    const auto dx = rsrc(p.A, (int64_t)(p.M - 1) * p.lda + k1);
+    const auto dw = rsrc(p.a_u, (int64_t)k1 * p.K);
+    const auto db = rsrc(p.a_v, p.K);
+    float xb[8], wa[4][8], bv[4];
+    const int row = i0 + r;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int j = 4 * s + q;
+      const float v = bload(dx, row * p.lda + j);
+      xb[s] = (j < k1 && row < p.M) ? v : (j == k1 ? 1.f : 0.f);
+    }
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const int k = w * 64 + kt * 16 + r;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int j = 4 * s + q;
+        const float v = bload(dw, j * p.K + k);
+        wa[kt][s] = (j < k1 && k < p.K) ? v : 0.f;
+      }
+      bv[kt] = bload(db, k);
+    }
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        if (s == sb && q == (k1 & 3)) wa[kt][s] = bv[kt];
+    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s < ns)
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) acc[kt] = mfma4(wa[kt][s], xb[s], acc[kt]);
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int kl = w * 64 + kt * 16 + 4 * q + tt;
+        As[kl * 16 + (r ^ psw(kl))] = (row < p.M && kl < p.K) ? fmaxf(acc[kt][tt], 0.f) : 0.f;
+      }
+  }
+  // 3. the W2 panel into this wave's LDS (contiguous 1 KB per instruction: conflict-free)
+  float* B = Bw[w];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) *reinterpret_cast<f32x4*>(B + ((lane >> 2) + 16 * i) * 16 + 4 * (lane & 3)) = bp[i];
+  __syncthreads();
+  if (tn == 0 && p.a_m && tid < p.K) {  // first-layer slab for the backward pass (coalesced in k)
+    float* h1 = const_cast<float*>(p.a_m);
+#pragma unroll 4
+    for (int r = 0; r < 16; ++r)
+      if (i0 + r < p.M) h1[(int64_t)(i0 + r) * p.K + tid] = As[tid * 16 + (r ^ psw(tid))];
+  }
+  // 4. layer 2: the wave's 16 x 16 tile over the whole K (64 k-steps, four accumulators)
+  const int li = lane & 15, lk = lane >> 4;
+  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll 16
+  for (int s = 0; s < GKC / 4; ++s) {
+    const int k = 4 * s + lk;
+    acc[s & 3] = mfma4(As[k * 16 + (li ^ psw(k))], B[k * 16 + li], acc[s & 3]);
+  }
+  // 5. bias + relu, D: column li, rows 4 lk + r
+  const int col = jw + li;
+  const float bias = p.bias ? p.bias[min(col, p.N - 1)] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = i0 + 4 * lk + r;
+    if (row < p.M && col < p.N)
+      p.C[(int64_t)row * p.ldc + col] = fmaxf(acc[0][r] + acc[1][r] + acc[2][r] + acc[3][r] + bias, 0.f);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 static inline GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C,
                    int ldc) {
@@ -985,6 +1087,15 @@ static inline int gemm_tile_override() {
   return v;
 }
 
+// MOPO_MLP12_WIDE=0 runs the SAC forward's layer-1-recompute groups on the 16x16-tile kernel instead
+static inline bool wide_mlp12() {
+  static const bool v = [] {
+    const char* e = std::getenv("MOPO_MLP12_WIDE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+
 static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const AdamCtx* ad = nullptr, int* slot = nullptr,
                                const HeadCtx* hd = nullptr, const LossTail* tail = nullptr,
                                const PolicyRows* pr = nullptr, const GatherArgs* ga = nullptr) {
@@ -1001,6 +1112,25 @@ static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const Ad
     if (q.head && (!hd || q.N > 16 || q.N != 2 * hd->A)) return fail("bad head problem");
     big = big && q.M >= 32 && q.N >= 32 && c != 16;
     head = head || q.head;
+  }
+  // groups of layer-1-recompute problems only (the SAC forward) run on mlp12_wide_kernel
+  bool wide = !tail && !pr && !ga && !ad && !hd && wide_mlp12();
+  for (int i = 0; i < g.n && wide; ++i) {
+    const GemmProb& q = ps[i];
+    wide = operand_modes(q) == 16 && q.K <= GKC && q.act == ACT_RELU && !q.mask && !q.colsum && !q.adam && !q.head &&
+           !q.Z && q.mask_kind == MASK_RELU;
+  }
+  if (wide) {
+    int tot = 0;
+    for (int i = 0; i < g.n; ++i) {
+      g.p[i] = ps[i];
+      g.prefix[i] = tot;
+      tot += ceil_div(ps[i].M, 16) * ceil_div(ps[i].N, WCOLS);
+    }
+    g.prefix[g.n] = tot;
+    hipLaunchKernelGGL(mlp12_wide_kernel, dim3(tot), dim3(256), 0, s, g);
+    MOPO_HIP(hipGetLastError());
+    return 0;
   }
   const int ov = gemm_tile_override();
   const int TW = (ov == 32 && big && !head) ? 32 : 16;

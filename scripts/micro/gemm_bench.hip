@@ -68,6 +68,21 @@ int main() {
   printf("fwd 4 x 256x256x256:          %.2f us\n", time_graph({fwd(0), fwd(1), fwd(2), fwd(3)}, 200, s, 0));
   printf("bwd-data 4 x (W^T, mask):     %.2f us\n", time_graph({bwd(0), bwd(1), bwd(2), bwd(3)}, 200, s, 0));
   printf("wgrad 2 x (X^T dY, colsum):   %.2f us\n", time_graph({wgt(0), wgt(1)}, 200, s, 0));
+  {
+    // the SAC forward launch: both hidden layers of 4 MLPs (layer 1 recomputed per tile, ta == 2)
+    float *Xin, *W1, *B1, *H1;
+    (void)hipMalloc(&Xin, n * 23 * 4); (void)hipMalloc(&W1, 4 * 23 * H * 4); (void)hipMalloc(&B1, 4 * H * 4);
+    (void)hipMalloc(&H1, 4 * n * H * 4);
+    (void)hipMemset(Xin, 0, n * 23 * 4); (void)hipMemset(W1, 0, 4 * 23 * H * 4); (void)hipMemset(B1, 0, 4 * H * 4);
+    auto m12 = [&](int i, bool st) {
+      auto a = mk(n, H, H, Xin, 23, 2, W + i * H * H, H, 0, Y + i * n * H, H);
+      a.bias = W; a.act = ACT_RELU; a.a_u = W1 + i * 23 * H; a.a_v = B1 + i * H; a.a_ldm = 23; a.a_m = st ? H1 + i * n * H : nullptr;
+      return a;
+    };
+    printf("mlp12 4 x (23->256->256), h1 stored x3: %.2f us\n", time_graph({m12(0, true), m12(1, false), m12(2, true), m12(3, true)}, 200, s, 0));
+    printf("mlp12 4 x, no h1 store:        %.2f us\n", time_graph({m12(0, false), m12(1, false), m12(2, false), m12(3, false)}, 200, s, 0));
+    printf("mlp12 1 x:                     %.2f us\n", time_graph({m12(0, false)}, 200, s, 0));
+  }
   printf("fwd K=23 4 x 256x256:         %.2f us\n", time_graph({mk(n, H, 23, X, 23, 0, W, H, 0, Y, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + n * H, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + 2 * n * H, H), mk(n, H, 23, X, 23, 0, W, H, 0, Y + 3 * n * H, H)}, 200, s, 0));
   return 0;
 }

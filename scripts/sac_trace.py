@@ -7,7 +7,7 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
-sac = [r for r in rows if any(k in r['Kernel_Name'] for k in ('gemm_group', 'sac_', 'pi_head'))]
+sac = [r for r in rows if any(k in r['Kernel_Name'] for k in ('gemm_group', 'mlp12', 'sac_', 'pi_head'))]
 grid = lambda r: int(r.get('Grid_Size_X') or r.get('Grid_Size') or 0)
 # anchor: the largest-grid grouped-GEMM launch (critic dh1 + loss tail: 1025 blocks at batch 256)
 gmax = max(grid(r) for r in sac if 'gemm_group' in r['Kernel_Name'])
