@@ -1117,8 +1117,8 @@ static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const Ad
   bool wide = !tail && !pr && !ga && !ad && !hd && wide_mlp12();
   for (int i = 0; i < g.n && wide; ++i) {
     const GemmProb& q = ps[i];
-    wide = operand_modes(q) == 16 && q.K <= GKC && q.act == ACT_RELU && !q.mask && !q.colsum && !q.adam && !q.head &&
-           !q.Z && q.mask_kind == MASK_RELU;
+    wide = operand_modes(q) == 16 && q.K <= GKC && q.N % 4 == 0 && q.act == ACT_RELU && !q.mask && !q.colsum &&
+           !q.adam && !q.head && !q.Z && q.mask_kind == MASK_RELU;  // N % 4: whole-quad W2 panel loads
   }
   if (wide) {
     int tot = 0;
