@@ -48,6 +48,23 @@ struct Stage {
   static constexpr int SLOTS = PER * WAVES;
 };
 
+// One wave-wide 16-B-per-lane copy HBM -> LDS (lane l's quad lands at lds + 4 l): global_load_lds with a
+// 64-bit per-lane address (one v_lshl_add_u64 per copy).  MOPO_LDS_BUF = 1 issues it as buffer_load ...
+// lds with the wave-uniform part of the address in SGPRs (descriptor + soffset) and only lane * 16 in a
+// VGPR -- no VALU per copy, but measured 5 % slower on the headline rollout (same-box A/B: 122.7 vs
+// 129.2M transitions/s, ensemble 0.347 vs 0.333 ms), so it stays off.
+#ifndef MOPO_LDS_BUF
+#define MOPO_LDS_BUF 0
+#endif
+__device__ __forceinline__ void copy_lds16(const float* __restrict__ base, int lane_quad, int uni_quads, float* lds) {
+#if MOPO_LDS_BUF
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t)lds, 16, lane_quad * 16, uni_quads * 16, 0, 0);
+#else
+  __builtin_amdgcn_global_load_lds((const void*)(base + (uni_quads + lane_quad) * 4), (lds_void_t)lds, 16, 0, 0);
+#endif
+}
+
 template <int NB, int WAVES>
 __device__ __forceinline__ void stage_slice(const float* __restrict__ src, float* lds, int w, int lane) {
 #pragma unroll
@@ -56,7 +73,7 @@ __device__ __forceinline__ void stage_slice(const float* __restrict__ src, float
 // pad slots re-read a valid fragment (never consumed); measured: skipping them with a wave-uniform
     // branch is ~1.5 % slower for H = 200 (13 of 16 slots used)
     const int fs = f < NB ? f : NB - 1;
-    __builtin_amdgcn_global_load_lds((const void*)(src + (fs * 64 + lane) * 4), (lds_void_t)(lds + f * 256), 16, 0, 0);
+    copy_lds16(src, lane, fs * 64, lds + f * 256);
   }
 }
 
@@ -70,7 +87,7 @@ __device__ __forceinline__ void stage_bias(const float* __restrict__ bias, float
   static_assert(PIECES <= WAVES, "bias larger than one copy per wave");
   if (w < PIECES) {
     const int q = min(w * 64 + lane, BQ - 1);
-    __builtin_amdgcn_global_load_lds((const void*)(bias + q * 4), (lds_void_t)(lds_bias + w * 256), 16, 0, 0);
+    copy_lds16(bias, q, 0, lds_bias + w * 256);
   }
 }
 
@@ -86,8 +103,7 @@ __device__ __forceinline__ void stage_block(const float* __restrict__ src, float
     const int f = w + i * WAVES;
     int j = (f < NF ? f : NF - 1) / NB, nb = (f < NF ? f : NF - 1) % NB;
     if (j >= kg_valid) j = kg_valid - 1;
-    __builtin_amdgcn_global_load_lds((const void*)(src + ((j * NBS + nb) * 64 + lane) * 4), (lds_void_t)(lds + f * 256),
-                                     16, 0, 0);
+    copy_lds16(src, lane, (j * NBS + nb) * 64, lds + f * 256);
   }
 }
 
