@@ -531,7 +531,12 @@ static int copy_back(Sac* h, hipStream_t s) {
   return 0;
 }
 
-constexpr int GRAPH_STEPS = 8;  // steps per replay of the long graph (amortises the launch gap)
+#ifndef MOPO_SAC_GRAPH_STEPS
+#define MOPO_SAC_GRAPH_STEPS 8
+#endif
+// steps per replay of the long graph (amortises the launch gap); 32 measured the same as 8 (same-box
+// A/B 69.7 us/step both): the graph replay is not on the step's critical path
+constexpr int GRAPH_STEPS = MOPO_SAC_GRAPH_STEPS;
 
 // which = 0: GRAPH_STEPS steps, 1: two steps (parity 0, 1), 2: one step + copy back.  Every step
 // prefetches the other parity's batch, so a graph's last step prepares the next graph's first.
