@@ -46,8 +46,11 @@ typedef struct mopo_bnn_s* mopo_bnn_t;
  *        1 = bf16 weights/activations, f32 accumulate (~8 significand bits; the C3 config);
  *        2 = "bf16x3": every f32 operand split into 2 bf16 parts, 3 bf16 products per f32 product
  *            (~17 significand bits), f32 accumulate;
- *        3 = "bf16x6": 3 bf16 parts, 6 bf16 products per f32 product, f32 accumulate: f32-accurate
- *            (held to the fp32 parity tolerances; the headline configuration).
+ *        3 = "bf16x6": 3 bf16 parts, 6 bf16 products per f32 product, f32 accumulate (~22-bit
+ *            operands, held to the fp32 parity tolerances);
+ *        4 = "f16x3": every f32 operand as 2 fp16 parts under power-of-two scales (per weight block,
+ *            per activation row), 3 f16 products per f32 product, f32 accumulate (~22-bit operands,
+ *            held to the fp32 parity tolerances; MOPO's default and the bench headline).
  * Limits: obs_dim + act_dim <= 32 (one or two 16-wide input k-groups); hidden 32, 64, 200 or 400 (any
  * width with the same number of 16-wide blocks); the bf16 kinds need 2 (obs_dim + 1) <= 48 head
  * slots; E <= 256. */
@@ -61,6 +64,13 @@ int mopo_bnn_set_params(mopo_bnn_t h, const float* const* h_arrays, int n_arrays
  * -> d_mean, d_var [E, B, D] f32. */
 int mopo_bnn_predict(mopo_bnn_t h, const void* d_inputs, int inputs_f64, int64_t B,
                      float* d_mean, float* d_var, void* stream);
+/* The handle's packed device parameters (weights in the kernels' fragment layout, biases, scaler,
+ * log-var bounds, f16x3 scales) as one opaque byte image: packed_bytes() is its size (-1 before
+ * set_params); packed_copy(to_handle=0) writes it to d_buf, to_handle=1 loads it from d_buf into a
+ * handle of the same shapes and dtype that already had set_params called.  Multi-GPU: rank 0's image
+ * is broadcast device-to-device (no host round trip or repack) -- no reference counterpart. */
+int64_t mopo_bnn_packed_bytes(mopo_bnn_t h);
+int mopo_bnn_packed_copy(mopo_bnn_t h, int to_handle, void* d_buf, int64_t nbytes, void* stream);
 
 /* ---- FakeEnv.step ------------------------------------------------------------------- */
 enum { MOPO_TERM_NONE = 0, MOPO_TERM_HALFCHEETAH = 0, MOPO_TERM_WALKER2D = 1, MOPO_TERM_HOPPER = 2 };

@@ -11,12 +11,17 @@ ray resource flags (``--cpus``, ``--gpus``, ``--trial-*``, ``--resources*``, ``-
 are accepted and ignored: one process drives one GPU here (multi-GPU is torchrun, see bench.py).
 Offline additions: ``--data`` (local qlearning_dataset .npz: d4rl downloads are unavailable) --
 or ``$D4RL_DATASET_DIR/<task>.npz`` named after the config's ``pool_load_path`` -- ``--model-dir``
-(``<model_name>.mat``, bnn.py:276-281) and ``--epochs``.
+(``<model_name>.mat``, bnn.py:276-281), ``--epochs`` and ``--ensemble-dtype`` / ``--actor-dtype``
+(the forward arithmetic; default f16x3, held to the fp32 parity tolerances).  ``--config`` is any
+importable module holding a ``params`` dict (examples/development/__init__.py:19-22), or one of the
+restated D4RL config names when the reference's ``examples`` package is not installed.
 """
 import argparse
 import json
 import os
 import sys
+
+from .bnn import DEFAULT_ENSEMBLE_DTYPE, DTYPES
 
 EXAMPLES = ('examples.development',)
 COMMANDS = ('run_local', 'run_example_dry', 'run_example_debug')
@@ -33,6 +38,8 @@ def get_parser():
     p.add_argument('--data', default=None)
     p.add_argument('--model-dir', default=None)
     p.add_argument('--epochs', type=int, default=None)
+    p.add_argument('--ensemble-dtype', default=None, choices=DTYPES)
+    p.add_argument('--actor-dtype', default=None, choices=('fp32', 'f16x3'))
     for f in ('--cpus', '--gpus', '--trial-cpus', '--trial-extra-cpus', '--max-failures'):
         p.add_argument(f, type=int, default=None)
     for f in ('--trial-gpus', '--trial-extra-gpus'):
@@ -60,6 +67,11 @@ def variant_spec(args):
     """The resolved experiment (the part of examples/development/base.py:get_variant_spec this path uses)."""
     from .config import get_params
     params = get_params(args.config)
+    kw = params['kwargs']
+    for k in ('ensemble_dtype', 'actor_dtype'):
+        if getattr(args, k) is not None:
+            kw[k] = getattr(args, k)
+    kw.setdefault('ensemble_dtype', DEFAULT_ENSEMBLE_DTYPE)
     seeds = [args.seed + i for i in range(max(args.num_samples, 1))]
     return {'algorithm_params': params, 'run_params': {'seeds': seeds, 'checkpoint_frequency': args.checkpoint_frequency},
             'model_dir': args.model_dir, 'epochs': args.epochs}
@@ -89,6 +101,9 @@ def main(argv=None):
             rargv += ['--model-dir', args.model_dir]
         if args.epochs is not None:
             rargv += ['--epochs', str(args.epochs)]
+        for k in ('ensemble_dtype', 'actor_dtype'):
+            if getattr(args, k) is not None:
+                rargv += ['--' + k.replace('_', '-'), getattr(args, k)]
         run.main(rargv)
     return 0
 

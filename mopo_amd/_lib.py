@@ -47,6 +47,8 @@ SIGNATURES = {
     'mopo_bnn_destroy': (c_int, [c_void_p]),
     'mopo_bnn_set_params': (c_int, [c_void_p, C.POINTER(c_void_p), c_int]),
     'mopo_bnn_predict': (c_int, [c_void_p, c_void_p, c_int, c_i64, c_void_p, c_void_p, c_void_p]),
+    'mopo_bnn_packed_bytes': (c_i64, [c_void_p]),
+    'mopo_bnn_packed_copy': (c_int, [c_void_p, c_int, c_void_p, c_i64, c_void_p]),
     'mopo_fakeenv_step': (c_int, [c_void_p, C.POINTER(FakeEnvArgs), c_void_p]),
     'mopo_sac_param_count': (c_i64, [c_int, c_int, c_int]),
     'mopo_actor_forward': (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_i64, c_void_p,

@@ -772,6 +772,7 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
   const int64_t s_ws = (5LL * E + 63) / 64 * 64;  // f16x3 inverse weight scales [5][E]
   const int64_t total = s_w0 + s_wh + s_whd + s_b0 + s_bh + s_bhd + 2 * 64 + 2 * 64 + s_ws;
   if (!h->buf) MOPO_HIP(hipMalloc(&h->buf, total * sizeof(float)));
+  h->buf_bytes = total * (int64_t)sizeof(float);
   float* base = h->buf;
   float* w0 = base; float* wh = w0 + s_w0; float* whd = wh + s_wh;
   float* b0 = whd + s_whd; float* bh = b0 + s_b0; float* bhd = bh + s_bh;
@@ -853,6 +854,7 @@ extern "C" int mopo_bnn_set_params(mopo_bnn_t hh, const float* const* arrs, int 
     const int NB2 = d.NB2, KG = NB2 / 2, P = bf16_parts(h->dtype);
     const int64_t f0 = (int64_t)E * P * NB2, fh = 3LL * E * KG * P * NB2, fd = (int64_t)E * KG * P * NBO;
     if (!h->bbuf) MOPO_HIP(hipMalloc(&h->bbuf, (f0 + fh + fd) * 256 * sizeof(float)));
+    h->bbuf_bytes = (f0 + fh + fd) * 256 * (int64_t)sizeof(float);
     float* b0f = reinterpret_cast<float*>(h->bbuf);
     float* bhf = b0f + f0 * 256;
     float* bdf = bhf + fh * 256;
@@ -931,4 +933,28 @@ extern "C" int mopo_bnn_predict(mopo_bnn_t hh, const void* x, int x_f64, int64_t
   a.mean = mean;
   a.var = var;
   return launch_bnn_fwd(h, FWD_PREDICT, a, (hipStream_t)stream);
+}
+
+extern "C" int64_t mopo_bnn_packed_bytes(mopo_bnn_t hh) {
+  const Bnn* h = reinterpret_cast<const Bnn*>(hh);
+  if (!h || !h->has_params) return -1;
+  return h->buf_bytes + h->bbuf_bytes;
+}
+
+extern "C" int mopo_bnn_packed_copy(mopo_bnn_t hh, int to_handle, void* d_buf, int64_t nbytes, void* stream) {
+  Bnn* h = reinterpret_cast<Bnn*>(hh);
+  MOPO_REQUIRE(h != nullptr, "mopo_bnn_packed_copy: NULL handle");
+  MOPO_REQUIRE(h->has_params, "mopo_bnn_packed_copy: parameters not set (the packed layout comes from set_params)");
+  MOPO_REQUIRE(d_buf != nullptr && nbytes == h->buf_bytes + h->bbuf_bytes,
+               "mopo_bnn_packed_copy: buffer must hold exactly mopo_bnn_packed_bytes() bytes");
+  hipStream_t s = (hipStream_t)stream;
+  char* b = static_cast<char*>(d_buf);
+  if (to_handle) {
+    MOPO_HIP(hipMemcpyAsync(h->buf, b, h->buf_bytes, hipMemcpyDeviceToDevice, s));
+    if (h->bbuf_bytes) MOPO_HIP(hipMemcpyAsync(h->bbuf, b + h->buf_bytes, h->bbuf_bytes, hipMemcpyDeviceToDevice, s));
+  } else {
+    MOPO_HIP(hipMemcpyAsync(b, h->buf, h->buf_bytes, hipMemcpyDeviceToDevice, s));
+    if (h->bbuf_bytes) MOPO_HIP(hipMemcpyAsync(b + h->buf_bytes, h->bbuf, h->bbuf_bytes, hipMemcpyDeviceToDevice, s));
+  }
+  return 0;
 }

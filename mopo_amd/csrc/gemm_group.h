@@ -665,10 +665,10 @@ static __device__ __forceinline__ void stage_dispatch(const GemmProb& p, int i0,
 // of LDS; partial tiles are summed through LDS and the epilogue fuses bias / activation / the
 // activation-derivative mask, and (for weight gradients) the optimizer.
 static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGroup g) {
-  __shared__ float ABs[2 * GKC * 16];  // the A and B panels (one array: the policy-row blocks use it whole)
+  __shared__ __attribute__((aligned(16))) float ABs[2 * GKC * 16];  // the A and B panels (one array: the policy-row blocks use it whole)
   float (*As)[16] = reinterpret_cast<float (*)[16]>(ABs);
   float (*Bs)[16] = reinterpret_cast<float (*)[16]>(ABs + GKC * 16);
-  __shared__ float part[4][256];
+  __shared__ __attribute__((aligned(16))) float part[4][256];
   __shared__ float csum[16][17];
   __shared__ float hv[16][17];
   // block order: [pr.nblk policy-row blocks (first: the longest chain starts at once)] [the problems'
@@ -874,8 +874,8 @@ static __device__ __forceinline__ void epi_apply(const GemmProb& p, const AdamCt
 // the blocks.  Epilogue: the tile goes through LDS, 4 elements per thread (same fused operations).
 constexpr int GKC32 = 128;
 static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmGroup g) {
-  __shared__ float As[GKC32 * 32];
-  __shared__ float Bs[GKC32 * 32];
+  __shared__ __attribute__((aligned(16))) float As[GKC32 * 32];
+  __shared__ __attribute__((aligned(16))) float Bs[GKC32 * 32];
   __shared__ float tile[32][33];
   __shared__ float csum[8][33];
   __shared__ float red[4];
@@ -972,8 +972,8 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
 // W2 panel staged wave-privately in LDS.  Epilogue: bias + relu (the mlp12 problems of the SAC forward).
 constexpr int WCOLS = 64;
 static __global__ __launch_bounds__(256, 1) void mlp12_wide_kernel(const GemmGroup g) {
-  __shared__ float As[GKC * 16];      // layer-1 slab, [k][r ^ psw(k)]
-  __shared__ float Bw[4][GKC * 16];   // wave w's 16-column W2 panel, [k][c]
+  __shared__ __attribute__((aligned(16))) float As[GKC * 16];      // layer-1 slab, [k][r ^ psw(k)]
+  __shared__ __attribute__((aligned(16))) float Bw[4][GKC * 16];   // wave w's 16-column W2 panel, [k][c]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int pi = 0;
   while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;

@@ -44,6 +44,7 @@ struct Bnn {
   bool has_params = false;
   float* buf = nullptr;      // one device allocation for all packed params
   uint16_t* bbuf = nullptr;  // bf16 packed weights
+  int64_t buf_bytes = 0, bbuf_bytes = 0;  // sizes of buf / bbuf (mopo_bnn_packed_copy)
   BnnDev dev{};
 };
 

@@ -537,6 +537,8 @@ static int copy_back(Sac* h, hipStream_t s) {
 // steps per replay of the long graph (amortises the launch gap); 32 measured the same as 8 (same-box
 // A/B 69.7 us/step both): the graph replay is not on the step's critical path
 constexpr int GRAPH_STEPS = MOPO_SAC_GRAPH_STEPS;
+// every captured graph starts at parity 0 and must end having written Pb[0] and prefetched bt[0]
+static_assert(GRAPH_STEPS >= 2 && GRAPH_STEPS % 2 == 0, "MOPO_SAC_GRAPH_STEPS must be even and >= 2");
 
 // which = 0: GRAPH_STEPS steps, 1: two steps (parity 0, 1), 2: one step + copy back.  Every step
 // prefetches the other parity's batch, so a graph's last step prepares the next graph's first.

@@ -118,10 +118,11 @@ class DistributedRollout:
 
 # ---------------------------------------------------------------------------------------------------
 # State sync for the multi-GPU training loop (MOPO with torch.distributed initialised).  Rank 0 is
-# authoritative: before every rollout it broadcasts the ensemble (the .mat arrays + elites, ~3.7 MB at
-# E=7, H=200) and the whole SAC state (parameters, targets, Adam moments: ~3.5 MB at 256-256), so every
-# rank rolls out its shard with the same policy and model, and the replicated learners
-# stay identical even if some float reduction on the device were not bit-reproducible.
+# authoritative: it trains the ensemble and broadcasts its packed device image once (+ elites, ~4 MB at
+# E=7, H=200), and before every rollout it broadcasts the whole SAC state (parameters, targets, Adam
+# moments: ~3.5 MB at 256-256), so every rank rolls out its shard with the same policy and model
+# (SURVEY 8(e)), and the replicated learners stay identical even if some float reduction on the device
+# were not bit-reproducible.
 
 def world_info(group=None):
     import torch.distributed as dist
@@ -131,24 +132,50 @@ def world_info(group=None):
 
 
 def broadcast_model(model, src=0, group=None):
-    """BNN parameters and elites from ``src`` to every rank (repacked on each rank's device)."""
+    """The ensemble from ``src`` to every rank as its packed device image (weights in the kernels'
+    fragment layout, biases, scaler, log-var bounds, f16x3 scales: mopo_bnn_packed_copy) plus the
+    elite indices -- one device-to-device broadcast, no host copy and no repack.  Receiving ranks keep
+    no host .mat arrays afterwards (``BNN.get_params`` is rank ``src``'s)."""
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    dev = torch.device('cuda', torch.cuda.current_device())
+    buf = model.export_packed() if rank == src else torch.empty(model.packed_nbytes(), dtype=torch.uint8,
+                                                                  device=dev)
+    el = torch.tensor(list(model._model_inds), dtype=torch.int64, device=dev)
+    ne = torch.tensor([el.numel()], dtype=torch.int64, device=dev)
+    dist.broadcast(ne, src, group=group)
+    if rank != src:
+        el = torch.empty(int(ne.item()), dtype=torch.int64, device=dev)
+    dist.broadcast(buf, src, group=group)
+    dist.broadcast(el, src, group=group)
+    if rank != src:
+        model.import_packed(buf)
+        model.set_elites(el.cpu().tolist())
+    torch.cuda.current_stream().synchronize()
+
+
+def broadcast_numpy_rng(src=0, group=None):
+    """numpy's legacy global RandomState (MT19937 key, position, cached gaussian) from ``src``, so every
+    rank continues the single-process stream after a phase only ``src`` ran."""
     import numpy as np
     import torch.distributed as dist
-    mats = model.get_params()
-    shapes = [m.shape for m in mats]
-    dev = torch.device('cuda', torch.cuda.current_device())
-    flat = torch.from_numpy(np.concatenate([m.ravel() for m in mats]).astype(np.float32)).to(dev)
-    el = torch.tensor(list(model._model_inds), dtype=torch.int64, device=dev)
-    dist.broadcast(flat, src, group=group)
-    dist.broadcast(el, src, group=group)
-    h, off = flat.cpu().numpy(), 0
-    out = []
-    for shp in shapes:
-        n = int(np.prod(shp))
-        out.append(h[off:off + n].reshape(shp))
-        off += n
-    model.set_params(out)
-    model.set_elites(el.cpu().tolist())
+    _, key, pos, has_gauss, gauss = np.random.get_state()
+    t = torch.zeros(624 + 3, dtype=torch.float64)
+    t[:624] = torch.from_numpy(key.astype(np.float64))
+    t[624], t[625], t[626] = pos, has_gauss, gauss
+    if dist.get_backend(group) == 'nccl':
+        t = t.cuda()
+    dist.broadcast(t, src, group=group)
+    t = t.cpu().numpy()
+    np.random.set_state(('MT19937', t[:624].astype(np.uint32), int(t[624]), int(t[625]), float(t[626])))
+
+
+def broadcast_metrics(metrics, src=0, group=None):
+    """``src``'s model-training metrics dict (float values) to every rank."""
+    import torch.distributed as dist
+    obj = [metrics]
+    dist.broadcast_object_list(obj, src, group=group)
+    return dict(obj[0])
 
 
 def broadcast_sac(sac, src=0, group=None):

@@ -19,7 +19,7 @@ from collections import OrderedDict
 
 import numpy as np
 
-from .bnn import construct_model
+from .bnn import DEFAULT_ENSEMBLE_DTYPE, construct_model
 from .fake_env import FakeEnv
 from .replay_pool import SimpleReplayPool
 from .rollout import ModelRollout
@@ -34,7 +34,11 @@ class MOPO:
                  model_name=None, model_load_dir=None, deterministic=False, network_kwargs=None, epoch_length=1000,
                  n_epochs=1000, n_train_repeat=1, batch_size=256, seed=88, reparameterize=True, max_model_t=None,
                  rollout_random=False, evaluation_environment=None, eval_n_episodes=10, eval_deterministic=True,
-                 max_path_length=1000, **kwargs):
+                 max_path_length=1000, ensemble_dtype=None, actor_dtype=None, **kwargs):
+        """``ensemble_dtype``: the ensemble forward's arithmetic (``mopo_amd.bnn.DTYPES``), default
+        ``DEFAULT_ENSEMBLE_DTYPE`` ('f16x3': f32 operands as two fp16 parts, f32 accumulate, held to
+        the fp32 parity tolerances); 'fp32' runs exact-f32 MFMA.  ``actor_dtype``: the rollout
+        policy forward ('fp32' / 'f16x3'; default f16x3 with an f16x3 ensemble, else fp32)."""
         if target_update_interval != 1:
             raise NotImplementedError('target_update_interval != 1 (all D4RL configs use 1)')
         self._pool = pool                                   # device SimpleReplayPool of env data
@@ -44,7 +48,7 @@ class MOPO:
                                       num_networks=num_networks, num_elites=num_elites,
                                       separate_mean_var=separate_mean_var, name=model_name,
                                       load_dir=model_load_dir, deterministic=deterministic,
-                                      seed=seed)   # the run seed (simple_run/main.py:180 set_seed) fixes the init
+                                      dtype=ensemble_dtype or DEFAULT_ENSEMBLE_DTYPE, seed=seed)   # the run seed (simple_run/main.py:180 set_seed) fixes the init
         self.fake_env = FakeEnv(self._model, static_fns, penalty_coeff=penalty_coeff,
                                 penalty_learned_var=penalty_learned_var)
         self._rollout_schedule = [20, 100, rollout_length, rollout_length]                 # mopo.py:137
@@ -53,6 +57,7 @@ class MOPO:
         self._rollout_batch_size = int(rollout_batch_size)
         self._deterministic = deterministic
         self._rollout_random = rollout_random
+        self._actor_dtype = actor_dtype
         self._real_ratio = real_ratio
         self._epoch_length, self._n_epochs, self._n_train_repeat = epoch_length, n_epochs, n_train_repeat
         self._epoch = 0
@@ -134,7 +139,7 @@ class MOPO:
         steps = self._rollout.run(env_obs, self._sac.policy_params_ptr, self._model_pool, rollout_batch_size,
                                   self._rollout_length, self.fake_env.term_kind, self.fake_env.penalty_coeff,
                                   self._model._model_inds, seed=self._seed, epoch=self._epoch,
-                                  pi_hidden=self._pi_hidden, **modes)
+                                  pi_hidden=self._pi_hidden, actor_dtype=self._actor_dtype, **modes)
         added = int(steps.sum().item())
         return {'mean_rollout_length': added / rollout_batch_size}
 
@@ -142,8 +147,9 @@ class MOPO:
         """Rank r rolls out rows [r B/N, (r + 1) B/N) of the batch (Philox streams keyed by the global
         row id, so the N shards are exactly the single-GPU rollout's rows) after rank 0's model and SAC
         state are broadcast; every rank's model pool receives all transitions in the single-GPU order."""
-        from .distributed import DistributedRollout, broadcast_model, broadcast_sac
-        broadcast_model(self._model)
+        from .distributed import DistributedRollout, broadcast_sac
+        # the ensemble is fixed after _train_model (broadcast once, in train()); the replicated learners
+        # are re-synchronised from rank 0 before every rollout as a guard against any drift
         broadcast_sac(self._sac)
         b = rollout_batch_size // self._world
         h = max(self._rollout_length, 1)
@@ -151,7 +157,8 @@ class MOPO:
             self._rollout = DistributedRollout(self._model, b, h, self._obs_dim, self._act_dim)
         steps = self._rollout.run(env_obs, self._sac.policy_params_ptr, self._model_pool, self.fake_env.term_kind,
                                   self.fake_env.penalty_coeff, self._model._model_inds, seed=self._seed,
-                                  epoch=self._epoch, pi_hidden=self._pi_hidden, **modes)
+                                  epoch=self._epoch, pi_hidden=self._pi_hidden, actor_dtype=self._actor_dtype,
+                                  **modes)
         added = int(steps.sum().item())
         return {'mean_rollout_length': added / rollout_batch_size}
 
@@ -205,8 +212,14 @@ class MOPO:
         if self._model_train_metrics is None:                                            # mopo.py:526-531
             t0 = time.perf_counter()
             max_epochs = 1 if self._model.model_loaded else None
-            self._model_train_metrics = self._train_model(batch_size=256, max_epochs=max_epochs, holdout_ratio=0.2,
-                                                          max_t=self._max_model_t)
+            if self._rank == 0:   # multi-GPU: rank 0 trains, the others receive its packed weights below
+                self._model_train_metrics = self._train_model(batch_size=256, max_epochs=max_epochs,
+                                                              holdout_ratio=0.2, max_t=self._max_model_t)
+            if self._world > 1:
+                from .distributed import broadcast_model, broadcast_numpy_rng, broadcast_metrics
+                broadcast_model(self._model)
+                broadcast_numpy_rng()       # the training loop drew from numpy's global stream on rank 0 only
+                self._model_train_metrics = broadcast_metrics(self._model_train_metrics)
             self._model_train_metrics['train_time'] = time.perf_counter() - t0
         for self._epoch in range(self._epoch, n_epochs or self._n_epochs):
             d = self._train_epoch()

@@ -88,6 +88,7 @@ class SAC:
         self.n_env = int(self.batch_size * real_ratio)                       # mopo.py:803
         self._target_entropy = -float(act_dim) if target_entropy == 'auto' else float(target_entropy)
         self._discount, self._tau, self._reward_scale, self._lr = discount, tau, reward_scale, lr
+        self._seed = int(seed)
         flat = init_sac_params(obs_dim, act_dim, hidden, seed=seed) if params is None else \
             np.ascontiguousarray(params, np.float32)
         n = L.lib().mopo_sac_param_count(obs_dim, act_dim, hidden)
@@ -197,9 +198,13 @@ class SAC:
             p.add_samples({k: v[lo:hi] for k, v in batch.items() if k in p.fields})
             pools.append(p)
         idx = np.concatenate([np.arange(cut), np.arange(n - cut)]).astype(np.int64)
-        self._do_training(iteration, pools[0], pools[1], idx=idx, seed=iteration,
-                          eps_s=eps_s if eps_s is not None else np.random.normal(size=(n, self.act_dim)),
-                          eps_n=eps_n if eps_n is not None else np.random.normal(size=(n, self.act_dim)),
+        if eps_s is None or eps_n is None:
+            # the reference draws these in-graph (tf.random_normal, mopo.py:306); a private stream keyed by
+            # (seed, iteration) keeps numpy's global stream -- which drives BNN.train -- untouched
+            rs = np.random.RandomState([self._seed & 0xffffffff, int(iteration) & 0xffffffff])
+            eps_s = rs.normal(size=(n, self.act_dim)) if eps_s is None else eps_s
+            eps_n = rs.normal(size=(n, self.act_dim)) if eps_n is None else eps_n
+        self._do_training(iteration, pools[0], pools[1], idx=idx, seed=iteration, eps_s=eps_s, eps_n=eps_n,
                           stream=stream)
         return self.logs()
 

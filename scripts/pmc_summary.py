@@ -50,15 +50,18 @@ def summarize(agg):
 
 
 if __name__ == '__main__':
+    # usage: pmc_summary.py OUT.json PMC_DIR WORKLOAD -- merges this workload's kernels into OUT.json
+    # ({"workloads": {workload_key: {...}}}); bench.py reports a kernel's traffic only for the workload
+    # its passes ran (bench.py workload_key)
     dst = sys.argv[1]
     src = sys.argv[2] if len(sys.argv) > 2 else 'gpurun_out'
-    # the workload the passes ran (bench.py workload_key of that run): bench.py reports a kernel's
-    # traffic only for the same workload
-    workload = sys.argv[3] if len(sys.argv) > 3 else None
+    workload = sys.argv[3] if len(sys.argv) > 3 else 'unknown'
     s = summarize(load(src))
     s = {k: v for k, v in s.items() if 'mopo::' in k}
-    json.dump({'source': 'rocprofv3 --pmc passes of scripts/pmc.sh (bench.py --steps 3 --warmup 1 '
-                         '--sac-steps 50, default workload)', 'workload': workload, 'kernels': s}, open(dst, 'w'),
-              indent=1)
+    d = json.load(open(dst)) if os.path.exists(dst) else {}
+    d.setdefault('source', 'rocprofv3 --pmc passes of scripts/pmc.sh (bench.py --steps 3 --warmup 1 --sac-steps 50 '
+                           '--config/--ensemble-dtype of the workload), one counter group per pass')
+    d.setdefault('workloads', {})[workload] = {'kernels': s}
+    json.dump(d, open(dst, 'w'), indent=1)
     for k, v in s.items():
-        print(k, {a: round(b, 4) if isinstance(b, float) else b for a, b in v.items()})
+        print(workload, k, {a: round(b, 4) if isinstance(b, float) else b for a, b in v.items()})

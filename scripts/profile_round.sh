@@ -12,4 +12,4 @@ cd /tmp && MOPO_ROLLOUT_SPLIT=1 timeout -k 10 300 rocprofv3 --kernel-trace --sta
   python "$R/bench.py" --no-cpu-baseline --no-c3 --no-alt-dtypes --train-epochs 0 > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err" \
   || { tail -5 "$R/gpurun_out/prof.err"; exit 1; }
 echo "rocprof ok"
-cd "$R" && bash scripts/pmc.sh
+cd "$R" && bash scripts/pmc.sh gpurun_out/pmc_summary.json

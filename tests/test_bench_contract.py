@@ -1,14 +1,30 @@
-"""CPU: the bench line's roofline traffic comes from the committed PMC summary of the same workload and
-kernel (bench.py pmc_traffic); a kernel renamed by a template change must not silently null it."""
+"""CPU: the bench line's contract -- its headline dtype is the one the product runs, and its roofline
+traffic comes from the committed PMC summary of the same workload (bench.py pmc_traffic)."""
 import sys
 
 
-def test_committed_pmc_summary_prices_the_default_workload(monkeypatch):
+def test_headline_dtype_is_the_product_default(monkeypatch):
+    import inspect
+
     import bench
+    from mopo_amd.bnn import DEFAULT_ENSEMBLE_DTYPE
+    from mopo_amd.mopo import MOPO
     monkeypatch.setattr(sys, 'argv', ['bench.py'])
     args = bench.parse()
-    t = bench.pmc_traffic(args)
-    assert t is not None and t > 0, 'profiles PMC summary does not match %s / %s' % (
-        bench.workload_key(args), bench.ENSEMBLE_KERNEL[args.ensemble_dtype])
-    # HBM bytes per 50k-row ensemble launch: at least the algorithmic 19.6 MB, far below 1 GB
-    assert 19.6e6 <= t < 1e9
+    assert args.ensemble_dtype == DEFAULT_ENSEMBLE_DTYPE
+    # MOPO builds its ensemble with DEFAULT_ENSEMBLE_DTYPE unless ensemble_dtype is passed
+    assert inspect.signature(MOPO.__init__).parameters['ensemble_dtype'].default is None
+    assert 'DEFAULT_ENSEMBLE_DTYPE' in inspect.getsource(MOPO.__init__)
+
+
+def test_committed_pmc_summary_prices_the_measured_workloads(monkeypatch):
+    import bench
+    for argv, lo in ((['bench.py'], 19.6e6), (['bench.py', '--ensemble-dtype', 'fp32'], 19.6e6),
+                     (['bench.py', '--config', 'N2'], 39e6)):
+        monkeypatch.setattr(sys, 'argv', argv)
+        args = bench.parse()
+        t = bench.pmc_traffic(args)
+        assert t is not None and t > 0, 'profiles PMC summary has no pass for %s' % bench.workload_key(args)
+        # HBM bytes per ensemble launch: at least the algorithmic bytes, far below 1 GB
+        alg = bench.ensemble_bytes(args.batch, bench.CONFIGS[args.config], args.ensemble_dtype)
+        assert alg >= lo * 0.9 and alg * 0.9 <= t < 1e9, (bench.workload_key(args), alg, t)

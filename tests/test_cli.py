@@ -63,3 +63,67 @@ def test_console_command_entry_points():
                           '--config=examples.config.d4rl.walker2d_mixed'], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert '"domain": "walker2d"' in out.stdout
+
+
+USER_CFG = '''
+from copy import deepcopy
+params = {
+    'type': 'MOPO', 'universe': 'gym', 'domain': 'walker2d', 'task': 'medium-replay-v0',
+    'exp_name': 'walker2d_my_sweep',
+    'kwargs': {'epoch_length': 1000, 'model_train_freq': 1000, 'rollout_batch_size': 20e3,
+               'num_networks': 7, 'num_elites': 5, 'real_ratio': 0.05, 'target_entropy': -3,
+               'separate_mean_var': True, 'penalty_learned_var': True, 'lr': 1e-3,
+               'pool_load_path': 'd4rl/walker2d-medium-replay-v0', 'pool_load_max_size': 100930,
+               'rollout_length': 3, 'penalty_coeff': 2.5, 'hidden_dim': 64,
+               'network_kwargs': {'hidden_sizes': [128, 128]}},
+}
+'''
+
+
+def test_user_config_module_is_imported(tmp_path, monkeypatch, capsys):
+    """examples/development/__init__.py:19-22: --config names any importable module holding ``params``;
+    base.py:221-230 then deep-merges ALGORITHM_PARAMS_ADDITIONAL['MOPO'] over it (its lr / tau /
+    target_update_interval win), and utils.py:43-48 derives model_name from exp_name."""
+    pkg = tmp_path / 'mycfgs'
+    pkg.mkdir()
+    (pkg / '__init__.py').write_text('')
+    (pkg / 'walker_sweep.py').write_text(USER_CFG)
+    monkeypatch.syspath_prepend(str(tmp_path))
+    rc = main(['run_example_dry', 'examples.development', '--config=mycfgs.walker_sweep'])
+    assert rc == 0
+    out = capsys.readouterr().out
+    spec = json.loads(out[:out.rindex('}') + 1])
+    p = spec['algorithm_params']
+    kw = p['kwargs']
+    assert (p['domain'], kw['rollout_length'], kw['penalty_coeff'], kw['rollout_batch_size']) == \
+        ('walker2d', 3, 2.5, 20e3)
+    assert kw['lr'] == 3e-4 and kw['target_update_interval'] == 1          # ADDITIONAL wins (base.py:226-229)
+    assert kw['hidden_dim'] == 64 and kw['n_epochs'] == 1000                # module value / default underneath
+    assert kw['network_kwargs'] == {'hidden_sizes': [128, 128], 'activation': 'relu', 'output_activation': None}
+    assert kw['model_name'] == 'walker2d-my-sweep_smv_1_0'
+    assert kw['ensemble_dtype'] == 'f16x3'
+
+
+def test_user_config_errors(tmp_path, monkeypatch):
+    from mopo_amd.config import get_params
+    (tmp_path / 'broken_cfg.py').write_text('import not_a_module_anywhere\nparams = {}\n')
+    (tmp_path / 'no_params_cfg.py').write_text('x = 1\n')
+    monkeypatch.syspath_prepend(str(tmp_path))
+    with pytest.raises(ModuleNotFoundError, match='not_a_module_anywhere'):
+        get_params('broken_cfg')                       # an error inside the module is not swallowed
+    with pytest.raises(AttributeError, match='params'):
+        get_params('no_params_cfg')
+    with pytest.raises(KeyError, match='no importable module'):
+        get_params('examples.config.d4rl.nope')
+
+
+def test_dtype_flags_reach_the_spec(capsys):
+    rc = main(['run_example_dry', 'examples.development', '--config=examples.config.d4rl.halfcheetah_mixed',
+               '--ensemble-dtype=fp32', '--actor-dtype=fp32'])
+    assert rc == 0
+    out = capsys.readouterr().out
+    kw = json.loads(out[:out.rindex('}') + 1])['algorithm_params']['kwargs']
+    assert (kw['ensemble_dtype'], kw['actor_dtype']) == ('fp32', 'fp32')
+    from mopo_amd.run import main as run_main
+    with pytest.raises(SystemExit):
+        run_main(['--config', 'x', '--data', 'y', '--ensemble-dtype', 'fp8'])

@@ -94,7 +94,7 @@ def _state(algo):
     p, la = algo._sac.get_params()
     mp_ = algo._model_pool
     return dict(sac=p.cpu().numpy(), log_alpha=np.float32(la.item()), target=algo._sac.get_target().cpu().numpy(),
-                bnn=np.concatenate([m.ravel() for m in algo._model.get_params()]),
+                bnn=algo._model.export_packed().cpu().numpy(), elites=np.array(algo._model._model_inds),
                 **{'pool_' + k: v[:mp_.size].cpu().numpy() for k, v in mp_.fields.items()})
 
 
@@ -117,7 +117,8 @@ def _mopo_worker(rank, world, port, data_path, out, B):
 
 def test_mopo_train_sharded_matches_single_process(tmp_path):
     """Two ranks (gloo on the one GPU; RCCL on a real node) run MOPO.train(2) with the rollout rows
-    sharded: both ranks end with identical model pools, SAC states and ensembles, and those equal a
+    sharded: rank 0 alone trains the ensemble and broadcasts its packed device image; both ranks end
+    with identical model pools, SAC states and ensembles (packed images, elites), and those equal a
     single-process MOPO.train(2) of the same config bit for bit."""
     import torch
     import torch.multiprocessing as mp

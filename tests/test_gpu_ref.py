@@ -154,3 +154,39 @@ def test_softlearning_sac_api_vs_reference_graph():
         assert abs(lg[key] - ref) <= 2e-4 * abs(ref) + 1e-6, (key, lg[key], ref)
     with pytest.raises(NotImplementedError):
         SAC(env, env, policy, (policy,), None, reparameterize=False)
+
+
+QUANTILES = (0.5, 0.9, 0.99, 1.0)
+
+
+@pytest.mark.parametrize('path', FWD, ids=[os.path.basename(p)[12:-4] for p in FWD])
+def test_f16x3_error_distribution_is_fp32_class(path):
+    """The product default (f16x3, ~22-bit operands) against the reference's own graph executed in f64:
+    (1) an ABSOLUTE fp32 bound, |d| <= 2e-5 * (1 + |ref|) on mean and log-var, and (2) its error
+    DISTRIBUTION (quantiles 50 / 90 / 99 / 100 % of |d| / (1 + |ref|)) no wider than 2x the wider of
+    the exact-f32 MFMA kernel's and the reference's own f32 execution's (TF1's f32 rounding,
+    z['*_f32'] vs z['*_f64']), with a floor of 2 f32 ulps (2^-23) for quantiles where both are ~0."""
+    from oracle import bnn as obnn
+    from mopo_amd.bnn import BNN
+    z = dict(np.load(path))
+    E, H, smv = int(z['E']), int(z['H']), bool(z['smv'])
+    mats = obnn.to_mat_list(ref_bnn_params(z))
+
+    def run(dtype):
+        m = BNN({'name': 'ref', 'num_networks': E, 'num_elites': min(5, E), 'separate_mean_var': smv,
+                 'obs_dim': 17, 'act_dim': 6, 'hidden_dim': H, 'dtype': dtype}).set_params(mats)
+        mean, var = m.predict(z['x'], factored=True)
+        return mean, np.log(var)
+
+    def q(a, ref):
+        e = np.abs(np.asarray(a, np.float64) - ref) / (1 + np.abs(ref))
+        return np.quantile(e.ravel(), QUANTILES)
+
+    got, f32 = run('f16x3'), run('fp32')
+    tf32 = (z['mean_f32'], z['logvar_f32'])
+    for i, key in enumerate(('mean_f64', 'logvar_f64')):
+        ref = z[key]
+        e16, e32, etf = q(got[i], ref), q(f32[i], ref), q(tf32[i], ref)
+        assert e16[-1] <= 2e-5, (key, e16)
+        bound = np.maximum(2 * np.maximum(e32, etf), 2.0 ** -23)
+        assert np.all(e16 <= bound), (key, 'f16x3', e16, 'fp32 kernel', e32, 'TF f32', etf)

@@ -501,15 +501,26 @@ def test_empty_batches():
     assert steps.cpu().numpy().tolist() == [0, 0, 0] and pool.size == 0
 
 
-@pytest.mark.parametrize('domain,dtype,E,H,B,h', [
-    ('halfcheetah', 'fp32', 7, 200, 50000, 5), ('walker2d', 'fp32', 7, 200, 50000, 5),
-    ('halfcheetah', 'bf16x6', 7, 200, 50000, 5), ('walker2d', 'bf16x6', 7, 200, 50000, 5),
-    ('halfcheetah', 'f16x3', 7, 200, 50000, 5), ('walker2d', 'f16x3', 7, 200, 50000, 5),   # C2 (headline)
-    ('walker2d', 'bf16', 7, 200, 100000, 1),                                               # C3
-    ('halfcheetah', 'fp32', 32, 400, 125000, 5), ('halfcheetah', 'f16x3', 32, 400, 125000, 5)])  # C5 per GPU
-def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h):
+FULL_SIZE = [
+    ('halfcheetah', 'fp32', 7, 200, 50000, 5, 1.0, 40000), ('walker2d', 'fp32', 7, 200, 50000, 5, 1.0, 40000),
+    ('halfcheetah', 'bf16x6', 7, 200, 50000, 5, 1.0, 40000), ('walker2d', 'bf16x6', 7, 200, 50000, 5, 1.0, 40000),
+    ('halfcheetah', 'f16x3', 7, 200, 50000, 5, 1.0, 40000),                                 # C2 (headline)
+    ('walker2d', 'f16x3', 7, 200, 50000, 5, 1.0, 40000),
+    ('walker2d', 'bf16', 7, 200, 100000, 1, 1.0, 40000),                                     # C3
+    ('halfcheetah', 'f16x3', 7, 200, 50000, 5, 5.0, 1000000),     # C4 per GPU: medium-expert, 1e6-row env pool
+    ('halfcheetah', 'f16x3', 7, 200, 100000, 5, 1.0, 101000),     # N2: north_star's 100k rows, horizon 5
+    ('halfcheetah', 'fp32', 32, 400, 125000, 5, 1.0, 40000), ('halfcheetah', 'f16x3', 32, 400, 125000, 5, 1.0, 40000),
+    ('halfcheetah', 'bf16', 32, 400, 125000, 5, 1.0, 40000)]    # C5 per GPU
+
+
+@pytest.mark.parametrize('domain,dtype,E,H,B,h,coeff,env_n', FULL_SIZE,
+                         ids=['%s-%s-E%d-H%d-B%d-h%d-c%g-env%d' % c for c in FULL_SIZE])
+def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h, coeff, env_n):
     """BASELINE workloads at full size (C2: E=7, H=200, B=50,000, h=5; C3: walker2d, bf16, B=100,000, h=1;
-    C5: one GPU's share, E=32, H=400, B=125,000, h=5), learned-var penalty, perf-mode Philox streams
+    C4: one GPU's share of halfcheetah-medium-expert, penalty_coeff 5 (halfcheetah_medium_expert.py:12-13),
+    B=50,000 of 400k, h=5, from a 1e6-row env pool; N2: north_star's halfcheetah-mixed B=100,000, h=5;
+    C5: one GPU's share, E=32, H=400, B=125,000, h=5, in fp32, f16x3 and bf16), learned-var penalty,
+    perf-mode Philox streams
     (halfcheetah: split rollout, walker2d: order-preserving compaction between steps): 192 sampled rows
     are recomputed end to end by the oracle from the restated Philox streams (oracle/rng.py) and
     compared at their pool positions.  Start rows bit-exact, terminals bit-exact (bf16: except where the
@@ -517,6 +528,22 @@ def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h):
     (5e-5; bf16 3e-2).  Under compaction a row's position at step i+1 is its rank among step i's
     survivors (mopo.py:758), taken from the device's own terminal flags of the other rows (the sampled
     rows' flags are checked against the oracle)."""
+    _full_size_rows(domain, dtype, E, H, B, h, coeff, env_n)
+
+
+def test_full_size_f16x3_error_distribution_matches_fp32():
+    """The C2 headline at full size (B=50,000, h=5) in the product default f16x3 and in exact-f32 MFMA:
+    the scaled errors of the 192 sampled rows' next states (every step) against the f64 oracle have
+    quantiles (50 / 90 / 99 / 100 %) within 2x of the fp32 kernel's, floor 2^-23 (same seeds, same rows)."""
+    e16 = np.concatenate(_full_size_rows('halfcheetah', 'f16x3', 7, 200, 50000, 5, 1.0, 40000))
+    e32 = np.concatenate(_full_size_rows('halfcheetah', 'fp32', 7, 200, 50000, 5, 1.0, 40000))
+    q16, q32 = (np.quantile(e, (0.5, 0.9, 0.99, 1.0)) for e in (e16, e32))
+    assert np.all(q16 <= np.maximum(2 * q32, 2.0 ** -23)), (q16, q32)
+
+
+def _full_size_rows(domain, dtype, E, H, B, h, coeff, env_n):
+    """Runs one full-size perf-mode rollout and checks 192 sampled rows against the oracle (see the
+    test above); returns the per-step arrays of the rows' next-state scaled errors."""
     import torch
     from oracle import rng as orng
     from mopo_amd.replay_pool import SimpleReplayPool
@@ -526,7 +553,6 @@ def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h):
     tol = 3e-2 if dtype == 'bf16' else 5e-5
     seed, epoch = 0x1234567890ab, 3
     rs = np.random.RandomState(21)
-    env_n = 40000
     env_obs = rs.normal(size=(env_n, O)).astype(np.float32)
     if domain == 'walker2d':
         env_obs[:, 0] = rs.uniform(0.9, 1.9, env_n)
@@ -541,7 +567,7 @@ def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h):
     pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=B * h)
     ro = ModelRollout(model, B, h)
     steps = ro.run(torch.from_numpy(env_obs).cuda(), torch.from_numpy(flat).cuda(), pool, B, h,
-                   static_fns[domain].term_kind, 1.0, elites, seed=seed, epoch=epoch).cpu().numpy()
+                   static_fns[domain].term_kind, coeff, elites, seed=seed, epoch=epoch).cpu().numpy()
     assert steps[0] == B and pool.size == steps.sum()
     if domain == 'halfcheetah':
         assert steps.tolist() == [B] * h
@@ -549,7 +575,7 @@ def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h):
     rows = np.sort(rs.choice(B, 192, replace=False))   # uids (global row ids) of the sampled rows
     idx = rows.copy()                                   # their positions within the current step
     obs = env_obs[orng.start_rows(rows, seed, epoch * 4096, env_n)].astype(np.float64)
-    base, checked = 0, 0
+    base, checked, errs = 0, 0, []
     for i in range(h):
         if len(rows) == 0:
             break
@@ -559,7 +585,7 @@ def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h):
         act = act.astype(np.float32)
         sel = orng.model_choice(rows, seed, st, elites)
         noise = np.broadcast_to(orng.obs_noise(rows, seed, st, O + 1).astype(np.float64), (E, len(rows), O + 1))
-        nobs, rew, term, _ = ofe.step(p, elites, obs, act, ofe.TERMINATION[domain], penalty_coeff=1.0,
+        nobs, rew, term, _ = ofe.step(p, elites, obs, act, ofe.TERMINATION[domain], penalty_coeff=coeff,
                                       penalty_learned_var=True, noise=noise, model_inds=sel)
         pos = torch.from_numpy(base + idx).cuda()
         got = {k: v[pos].cpu().numpy() for k, v in pool.fields.items()}
@@ -568,6 +594,7 @@ def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h):
         close(got['observations'], obs, tol)
         close(got['actions'], act, 5e-5 if i == 0 else tol)
         close(got['next_observations'], nobs, tol)
+        errs.append((np.abs(got['next_observations'] - nobs) / (1 + np.abs(nobs))).ravel())
         close(got['rewards'], rew, tol)
         bad = got['terminals'][:, 0] != term[:, 0]
         if dtype == 'bf16' and bad.any():   # a bf16 next state may land on the other side of a bound
@@ -584,3 +611,4 @@ def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h):
         base += steps[i]
         rows, idx, obs = rows[live], rank[idx[live]], nobs[live]
     assert checked >= (192 * h if domain == 'halfcheetah' else min(192 * h, 192 + 64))   # walker: >= 1 compacted step
+    return errs
