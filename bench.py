@@ -84,11 +84,15 @@ def parse():
     p.add_argument('--config', default='C2', choices=sorted(CONFIGS),
                    help='BASELINE.json workload of the main line (C2 = the headline); the per-rank batch is the '
                         "config's total rollout_batch / world for C4 / C5")
+    p.add_argument('--shards', type=int, default=None,
+                   help='sharded configs (C4, C5): split the batch over this many GPUs (default: the world size); '
+                        '--shards 8 on one GPU runs one GPU\'s share of the 8-GPU config')
     a = p.parse_args()
     spec = CONFIGS[a.config]
     if a.config != 'C2':   # the config fixes the workload; --batch / --horizon apply to C2 only
         world = int(os.environ.get('WORLD_SIZE', '1'))
-        a.batch, a.horizon = spec['B_total'] // world if spec.get('sharded') else spec['B_total'], spec['h']
+        a.batch = spec['B_total'] // (a.shards or world) if spec.get('sharded') else spec['B_total']
+        a.horizon = spec['h']
         if a.ensemble_dtype == DEFAULT_ENSEMBLE_DTYPE and spec.get('dtype'):
             a.ensemble_dtype = spec['dtype']
     return a

@@ -92,6 +92,7 @@ SIGNATURES = {
                               c_void_p, c_void_p, c_void_p]),
     'mopo_sac_set_graph': (c_int, [c_void_p, c_int]),
     'mopo_sac_copy': (c_int, [c_void_p, c_int, c_int, c_void_p, c_i64, c_void_p]),
+    'mopo_sac_debug_stamps': (c_int, [c_void_p, c_void_p, c_i64]),
     'mopo_mt_create': (c_int, [C.POINTER(c_void_p), c_u32]),
     'mopo_mt_destroy': (c_int, [c_void_p]),
     'mopo_mt_seed': (c_int, [c_void_p, c_u32]),

@@ -202,17 +202,20 @@ static __device__ __forceinline__ void gather_elem(const GatherArgs& g, int r, i
 // run by extra blocks of the critic weight-gradient launch: block (rb, cq) owns batch rows
 // [16 rb, 16 rb + 16) and columns [64 cq, 64 cq + 64) of the policy's first hidden layer.
 //   dx_a   = dh1_Q1(s,pi) W1_Q1[O:]^T + dh1_Q2(s,pi) W1_Q2[O:]^T      (-d min Q / d action)
+//            -- the sum of the per-column-block partials the critic dh1 launch wrote (sac_rows.h)
 //   dhead  = squashed-Gaussian head backward (mean, log_std; alpha / n on the log-prob)
 //   dh2p   = (dhead_mu Wm^T + dhead_ls Wl^T) * (h2p > 0)               (all H columns, in LDS)
 //   dh1p   = dh2p W2p^T * (h1p > 0)                                     (this block's 64 columns, MFMA)
-// Every quantity before dh1p is row-local, so each column block recomputes it (cheap: K = 2H for
-// A <= 8 outputs, K = 2A per dh2p value) and only cq == 0 stores dhead and dh2p, which the policy
-// weight gradients of the next launch read with dh1p.
+// Every quantity before dh1p is row-local, so each column block recomputes it (cheap: ncq partials
+// per action, K = 2A per dh2p value) and only cq == 0 stores dhead and dh2p, which the policy weight
+// gradients of the next launch read with dh1p.
+constexpr int OPW = 16;              // floats per (column block, row) partial record (sac_rows.h)
+constexpr int MAX_NCQ = 4;           // column blocks of 64 (H <= 256)
+
 struct PolicyRows {
   int nblk;                          // 0: none; ceil(n / 16) * ceil(H / 64)
-  int n, O, A, H;
-  const float* dh1[2];               // Q1 / Q2 at (s, pi(s)): [n][H]
-  const float* w1[2];                // their first-layer weights [O + A][H]
+  int n, O, A, H, ncq;
+  const float* dapart[2];            // Q1 / Q2 at (s, pi(s)): [ncq][n][OPW] partials of dh1 W1[O:]^T
   const float* head_s;               // [n][2A] mean | raw log_std
   const float* eps_s;                // [n][A]
   const float* log_alpha;
@@ -222,69 +225,36 @@ struct PolicyRows {
   float* dhead; float* dh2p; float* dh1p;
 };
 
-#ifndef MOPO_PR_EARLY
-#define MOPO_PR_EARLY 0  // 1: the whole W2p operand tile and the h1p mask in burst 2 (no burst 3)
-#endif
 constexpr int PR_COLS = 64;          // dh1p columns per policy-row block (one 16-wide tile per wave)
 constexpr int PR_LDS = 2 * 256 * 16; // floats the grouped kernel's panel LDS offers it (H <= 508)
 
-// Latency layout: the chain's global operands come in three bursts of unconditional (range-checked)
-// loads, each issued before the compute that precedes its use -- (1) the dx operands (straight into
-// MFMA registers) and the head inputs; (2) once dx is formed, Wm / Wl / h2p at this thread's column and
-// the first half of the W2p operands of the dh1p tile; (3) once dh2p is formed, the second half and
-// the h1p mask.  No branch depends on a runtime width, so each phase's loads issue back to back.
+// Latency layout: every global operand of the chain is loaded in ONE burst of unconditional
+// (range-checked) loads at the start -- the action-gradient partials and head inputs, Wm / Wl / h2p at
+// this thread's dh2p column, this wave's W2p operands of the dh1p tile and the h1p mask -- so the
+// block pays one memory latency, then computes.
 // S: >= 16 (H + 4) floats of LDS (PR_LDS); hs: >= 3 * 128 floats.
 // H % 16 == 0, H <= 256 (one dh2p column per thread), A <= 8.
 static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int H = c.H, A = c.A, O = c.O, HS = H + 4, n = c.n;
+  const int H = c.H, A = c.A, HS = H + 4, n = c.n;
   const int ncq = (H + PR_COLS - 1) / PR_COLS;
   const int rb = x / ncq, cq = x % ncq, r0 = rb * 16;
-  // ---- burst 1: the dx operands straight into MFMA registers -- A(i, k) = [dh1_Q1 | dh1_Q2](r0 + i, k),
-  //      B(k, j) = [W1_Q1 ; W1_Q2](O + j, k) (j < A, else 0), K = 2H split over the 4 waves; lane
-  //      (li, lk) of wave w contracts k = w (2H / 4) + 32 lk + 4 t + u: 8 contiguous quads per operand
   const int li = lane & 15, lk = lane >> 4;
-  const int KW = 2 * H / 4;           // k per wave (H % 16 == 0: whole quads, 32 lk + 4 t < KW)
-  f32x4 xa[8], xb[8];
-  {
-    const int qi = (w * KW) / H;      // waves 0-1: Q1, 2-3: Q2 (KW = H / 2)
-    const auto dd = rsrc(c.dh1[qi], (int64_t)n * H);
-    const auto dw = rsrc(c.w1[qi] + (int64_t)O * H, (int64_t)A * H);
-    const int kq = w * KW - qi * H + 32 * lk;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int k = kq + 4 * t;
-      const bool kin = 32 * lk + 4 * t < KW;
-      xa[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            dd, (kin ? (r0 + li) * H + k : -4) * 4, 0, 0));   // rows >= n: past the extent
-      xb[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            dw, (kin && li < A ? li * H + k : -4) * 4, 0, 0));
-    }
-  }
+  // ---- the burst
   const int hr = tid >> 3, hj = tid & 7, hrow = r0 + hr;
   const bool hon = tid < 128 && hj < A && hrow < n;
+  float dap[2][MAX_NCQ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const auto dp = rsrc(c.dapart[i], (int64_t)c.ncq * n * OPW);
+#pragma unroll
+    for (int q = 0; q < MAX_NCQ; ++q) dap[i][q] = bload(dp, (hon && q < c.ncq) ? (q * n + hrow) * OPW + hj : -1);
+  }
   const auto dh = rsrc(c.head_s, (int64_t)n * 2 * A), de = rsrc(c.eps_s, (int64_t)n * A);
   const float mu = bload(dh, hon ? hrow * 2 * A + hj : -1);
   const float raw = bload(dh, hon ? hrow * 2 * A + A + hj : -1);
   const float ep = bload(de, hon ? hrow * A + hj : -1);
   const float la = *c.log_alpha;
-  {
-    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = mfma4(xa[t][u], xb[t][u], acc[u]);
-    float* pw = S + w * 256;          // the four waves' partial 16x16 tiles (D: col li, row 4 lk + r)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) pw[(4 * lk + r) * 16 + li] = acc[0][r] + acc[1][r] + acc[2][r] + acc[3][r];
-  }
-  __syncthreads();
-  if (tid < 128) {                    // da (row hr, action hj) = sum of the four partials
-    const int o = hr * 16 + hj;
-    hs[hr * 8 + hj] = S[o] + S[256 + o] + S[512 + o] + S[768 + o];
-  }
-  // ---- burst 2: Wm / Wl / h2p at this thread's dh2p column, the first half of this wave's W2p
-  //      operands (B(k, j) = W2p[j][k]; lane (li, lk) contracts k = 64 lk + 4 t + u: contiguous quads)
   const int hc = tid;
   const auto dwm = rsrc(c.Wm, (int64_t)H * A), dwl = rsrc(c.Wl, (int64_t)H * A), dh2 = rsrc(c.h2p, (int64_t)n * H);
   float wm[8], wl[8], h2v[16];
@@ -299,29 +269,27 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   const bool tile_on = j0 < H;
   const auto dw2 = rsrc(c.W2p, (int64_t)H * H);
   const int boff = (tile_on ? col : 0) * H;
-  auto bquad = [&](int t) {
+  f32x4 bq[16];                       // B(k, j) = W2p[j][k]: lane (li, lk) contracts k = 64 lk + 4 t + u
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
     const int k = 64 * lk + 4 * t;
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dw2, (k < H ? boff + k : -4) * 4, 0, 0));
-  };
-  f32x4 bq0[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) bq0[t] = bquad(t);
-#if MOPO_PR_EARLY
-  f32x4 bq1[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) bq1[t] = bquad(8 + t);
+    bq[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dw2, (k < H ? boff + k : -4) * 4, 0, 0));
+  }
   const auto dm1 = rsrc(c.h1p, (int64_t)n * H);
   float m1[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
-#endif
-  __syncthreads();
   // ---- squashed-Gaussian head backward (mopo.py:282-308 differentiated; pi_loss mopo.py:371-377)
   float* dmu_s = hs + 128;
   float* dls_s = hs + 256;
   if (tid < 128) {
     float dmu = 0.f, dls = 0.f;
     if (hon) {
+      float da = 0.f;                                               // -dmin q / da through Q1 / Q2:
+#pragma unroll
+      for (int i = 0; i < 2; ++i)                                   // partials in a fixed order
+#pragma unroll
+        for (int q = 0; q < MAX_NCQ; ++q) da += dap[i][q];
       const float g = expf(la) / (float)n;                         // d L_pi / d logp (stop_gradient(alpha))
       const float ls = fminf(fmaxf(raw, -20.f), 2.f);
       const float sd = expf(ls);
@@ -329,7 +297,6 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
       const float a = tanhf(u);
       const float inv = 1.f / (sd + 1e-8f);
       const float zz = (u - mu) * inv;
-      const float da = hs[hr * 8 + hj];                             // -dmin q / da through Q1/Q2
       float du = da * (1.f - a * a);                                // tanh grad (y-based)
       du += g * (-zz * inv);                                        // gaussian_likelihood wrt x
       du += g * (2.f - 4.f / (1.f + expf(2.f * u)));                // squash correction: 2 - 4 sigmoid(-2u)
@@ -346,7 +313,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
     dls_s[tid] = dls;
   }
   __syncthreads();
-  // ---- dh2p of the 16 rows at this thread's column -> LDS rows of stride HS (the wa rows are dead)
+  // ---- dh2p of the 16 rows at this thread's column -> LDS rows of stride HS
   if (hc < H) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -360,16 +327,6 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
       if (cq == 0 && r0 + i < n) c.dh2p[(int64_t)(r0 + i) * H + hc] = v;
     }
   }
-#if !MOPO_PR_EARLY
-  // ---- burst 3: the second half of the W2p operands and the h1p mask of this lane's four outputs
-  f32x4 bq1[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) bq1[t] = bquad(8 + t);
-  const auto dm1 = rsrc(c.h1p, (int64_t)n * H);
-  float m1[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
-#endif
   __syncthreads();
   // ---- dh1p tile = dh2p W2p^T * (h1p > 0): rows r0.., columns j0.. (wave w)
   if (!tile_on) return;
@@ -378,9 +335,8 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   for (int t = 0; t < 16; ++t) {
     const int k = 64 * lk + 4 * t;
     const f32x4 a = k < H ? *reinterpret_cast<const f32x4*>(S + li * HS + k) : zero4();
-    const f32x4 b = t < 8 ? bq0[t] : bq1[t - 8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = mfma4(a[u], b[u], acc[u]);
+    for (int u = 0; u < 4; ++u) acc[u] = mfma4(a[u], bq[t][u], acc[u]);
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {

@@ -5,20 +5,22 @@
 // Semantics: every forward and gradient uses the pre-step parameters; then pi, q1, q2
 // and alpha are updated by their own Adam (identical step counts -> one shared lr_t); then Polyak.
 //
-// Structure: 7 launches per step on one stream, captured into hipGraphs of 8 / 2 / 1 steps (no
-// host work per step): 2 grouped-GEMM forward launches for pi(s), pi(s'), Q1/Q2(s,a) (both hidden
-// layers in one: the first is recomputed per block from the <= 32 inputs; the policy output tile's
-// epilogue runs the squashed-Gaussian head), 1 for both hidden layers of Q1/Q2(s,pi) and the target
-// critics, sac_qloss_kernel (their 1-wide output layers, the losses and the alpha gradient), then 3
-// grouped-GEMM backward launches: the critics' dh1, the critics' weight gradients together with the
-// policy's row-local backward chain (dx over the actions -> head backward -> dh2p -> dh1p, extra
-// blocks of that launch), and the policy's weight gradients (+ the next step's batch gather).  The four TF1 Adams and Polyak run in the weight-gradient GEMM epilogues (gemm_group.h),
+// Structure: 5 launches per step on one stream, captured into hipGraphs of 8 / 2 / 1 steps (no host
+// work per step).  Everything up to the critics' first-layer gradients is row-local, so it runs in
+// three row-block launches (sac_rows.h) that hand each other per-column-block partial dot products
+// instead of full rows: F1 the hidden layers of pi(s), pi(s'), Q1/Q2(s,a) + partial output layers;
+// F2 the policy head (from F1's partials) feeding the hidden layers of Q1/Q2(s,pi) and the target
+// critics + partial output layers; B1 each row's TD target and dq (from the partials), the critics'
+// dh1, the action-gradient partials for the policy, and the batch loss tail.  Then 2 grouped-GEMM
+// launches (gemm_group.h): the critics' weight gradients together with the policy's row-local backward
+// chain (head backward -> dh2p -> dh1p, extra blocks), and the policy's weight gradients (+ the next
+// step's batch gather).  The four TF1 Adams and Polyak run in the weight-gradient GEMM epilogues,
 // reading parameters Pb[p] and writing Pb[1 - p], so every gradient of the step sees pre-step
 // parameters.
 #include <vector>
 #include <cstring>
 
-#include "gemm_group.h"
+#include "sac_rows.h"
 
 namespace mopo {
 
@@ -57,7 +59,6 @@ struct Sac {
   float *P, *G, *M, *V, *T;       // [total + 1]: last element = log_alpha
   float* Pb[2];                   // parameter ping-pong: Pb[0] == P is the canonical copy between calls
   float* norm_part = nullptr;     // [nslots][2]
-  float* loss_part = nullptr;     // [ceil(n / QL_ROWS)][8] sac_qloss_kernel block partials
   int nslots = 0, nslots_cap = 0;
   float* beta_pow;                // [3] f32 beta1_power, beta2_power (TF1 non-slot vars), this step's lr_t
   int64_t* iter;                  // device step counter (Philox)
@@ -68,6 +69,9 @@ struct Sac {
   float *logp_s, *logp_n, *eps_s, *eps_n;
   float *dq[4];                   // dq for instances 2,3,4,5
   float *dh1[4];
+  float *opart[8];                // [ncq][n][OPW] output-layer partials of the 8 instances (sac_rows.h)
+  float *dapart[2];               // [ncq][n][OPW] action-gradient partials of Q1 / Q2 at (s, pi(s))
+  uint64_t* stamps = nullptr;     // MOPO_SAC_STAMPS builds: [slot][block][8]
   float *dhead, *dh2p, *dh1p;
   // graph
   bool use_graph = true;
@@ -118,108 +122,6 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   float a[1] = {v};
   block_sums<1>(a, sh);
   return a[0];
-}
-
-// ---- critic output layers of Q1/Q2(s, pi(s)) and the targets Qt1/Qt2(s', pi(s')), fused with the
-// losses, output gradients, alpha gradient and logs (mopo.py:361-404).
-// Block = 16 batch rows; wave w computes instance 4 + w (q = h2 . w3 + b3, 4 lanes per row, K split
-// in 64-wide quarters); then one thread per row forms y, the row-local output gradients and its
-// share of the seven batch means.  The block partials are summed (in block order: deterministic) by
-// the LossTail block of the next launch, which also applies the alpha Adam, fixes this step's lr_t
-// for the fused optimizer epilogues and advances the TF1 beta powers and the step counter.
-constexpr int QL_ROWS = 16;
-struct QLossArgs {
-  int n, H, A;
-  float gamma, rscale;
-  const float* h2[4];               // instances Q1(s,pi) Q2(s,pi) Qt1(s',pi') Qt2(s',pi')
-  const float* w3[4];
-  const float* b3[4];
-  float* q[4];                      // outputs (out[4..7])
-  const float* q1; const float* q2; // Q1/Q2(s, a) from the forward output stage
-  const float* logp_s; const float* logp_n; const float* rew; const float* term; const float* head_s;
-  const float* log_alpha;
-  float* dq1; float* dq2; float* dq1p; float* dq2p;
-  float* part;                      // [blocks][8] -> LossTail (gemm_group.h)
-};
-
-__global__ __launch_bounds__(256) void sac_qloss_kernel(const QLossArgs a) {
-  __shared__ float qs[4][QL_ROWS];
-  __shared__ float ents[QL_ROWS];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r0 = blockIdx.x * QL_ROWS;
-  // the loss inputs of this block's rows (wave 0, one lane per row) and the alpha Adam state are
-  // fetched first, so their latency hides under the output-layer dot products
-  const int lr_row = min(r0 + lane, a.n - 1);
-  float in_q1 = 0.f, in_q2 = 0.f, in_rew = 0.f, in_term = 0.f, in_lps = 0.f, in_lpn = 0.f;
-  if (w == 0 && lane < QL_ROWS) {
-    in_q1 = a.q1[lr_row]; in_q2 = a.q2[lr_row]; in_rew = a.rew[lr_row]; in_term = a.term[lr_row];
-    in_lps = a.logp_s[lr_row]; in_lpn = a.logp_n[lr_row];
-  }
-  const float alpha = expf(*a.log_alpha);                           // mopo.py:361
-  {
-    const int rr = lane >> 2, part = lane & 3, r = r0 + rr;
-    const int rc = min(r, a.n - 1);
-    const int KQ = a.H / 4;         // H % 16 == 0 (checked at create)
-    const f32x4* hp = reinterpret_cast<const f32x4*>(a.h2[w] + (int64_t)rc * a.H + part * KQ);
-    const float* wp = a.w3[w] + part * KQ;  // Q2's W3 sits at an odd offset of the flat vector
-    float acc = 0.f;
-#pragma unroll 16
-    for (int k = 0; k < KQ / 4; ++k) {  // unrolled: the 16 row / weight loads of H = 256 issue together
-      const f32x4 x = hp[k];
-      acc += x[0] * wp[4 * k] + x[1] * wp[4 * k + 1] + x[2] * wp[4 * k + 2] + x[3] * wp[4 * k + 3];
-    }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    const float qv = acc + *a.b3[w];
-    if (part == 0) {
-      qs[w][rr] = qv;
-      if (r < a.n) a.q[w][r] = qv;
-    }
-    if (w == 1) {  // pi_entropy terms (mopo.py:341) of the 16 rows: 4 lanes per row, 2 actions each
-      float ent = 0.f;
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int j = part + 4 * jj;
-        if (j < a.A) {
-          const float ls = fminf(fmaxf(a.head_s[(int64_t)rc * 2 * a.A + a.A + j], -20.f), 2.f);
-          ent += logf(expf(ls) + 1e-8f) + 0.5f * logf(2.f * 3.14159265358979f * 2.718281828459045f);
-        }
-      }
-      ent += __shfl_xor(ent, 1);
-      ent += __shfl_xor(ent, 2);
-      if (part == 0) ents[rr] = ent;
-    }
-  }
-  __syncthreads();
-  if (w == 0) {
-    const int r = r0 + lane;
-    const bool ok = lane < QL_ROWS && r < a.n;
-    float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (ok) {
-      const float q1 = in_q1, q2 = in_q2, q1p = qs[0][lane], q2p = qs[1][lane];
-      const float qt = fminf(qs[2][lane], qs[3][lane]);            // mopo.py:368
-      const float y = a.rscale * in_rew + a.gamma * ((1.f - in_term) * (qt - alpha * in_lpn));  // :380-386
-      const float lps = in_lps;
-      const float inv_n = 1.f / (float)a.n;
-      a.dq1[r] = (q1 - y) * inv_n;                                  // d(0.5 mean (q-y)^2)
-      a.dq2[r] = (q2 - y) * inv_n;
-      const bool sel1 = q1p <= q2p;                                 // tf.minimum grad -> x where x <= y
-      a.dq1p[r] = sel1 ? -inv_n : 0.f;
-      a.dq2p[r] = sel1 ? 0.f : -inv_n;
-      const float ent = ents[lane];
-      red[0] = (q1 - y) * (q1 - y); red[1] = (q2 - y) * (q2 - y); red[2] = q1; red[3] = q2;
-      red[4] = lps; red[5] = ent; red[6] = alpha * lps - fminf(q1p, q2p);
-    }
-#pragma unroll
-    for (int i = 0; i < 7; ++i)
-#pragma unroll
-      for (int off = 8; off > 0; off >>= 1) red[i] += __shfl_xor(red[i], off);
-    if (lane == 0) {
-      float* pp = a.part + 8 * (int64_t)blockIdx.x;
-#pragma unroll
-      for (int i = 0; i < 7; ++i) pp[i] = red[i];
-    }
-  }
 }
 
 // grad-norm logs of the last step (once per mopo_sac_step call): the per-block partials of the
@@ -275,84 +177,76 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   const Batch& bt = h->bt[par];
   auto Wq = [&](int qi, int k) { return P + o.q[qi][k]; };
   auto Tq = [&](int qi, int k) { return T + o.q[qi][k]; };
-  // both hidden layers of an MLP instance in one problem: the first is recomputed per block from
-  // the K1 inputs (gemm_group.h, ta == 2) and stored once to h1 for the backward pass
-  auto mlp12 = [&](const float* x, int k1, const float* w1, const float* b1, const float* w2, const float* b2,
-                   float* h1, float* h2) {
-    auto a = mk(n, H, H, x, W, 2, w2, H, 0, h2, H);
-    a.bias = b2; a.act = ACT_RELU;
-    a.a_u = w1; a.a_v = b1; a.a_ldm = k1; a.a_m = h1;
-    return a;
-  };
-  // ---- forward stage 1-3: pi(s), pi(s'), Q1(s,a), Q2(s,a)
+  const int ncq = ceil_div(H, RB_COLS), nrb = ceil_div(n, 16);
+  // ---- F1: pi(s), pi(s'), Q1(s,a), Q2(s,a) hidden layers + partial output layers
   {
-    std::vector<GemmProb> g;
-    g.push_back(mlp12(bt.sa, O, P + o.pW1, P + o.pb1, P + o.pW2, P + o.pb2, h->h1[0], h->h2[0]));
-    g.push_back(mlp12(bt.xn, O, P + o.pW1, P + o.pb1, P + o.pW2, P + o.pb2, nullptr, h->h2[1]));  // no gradient
-    for (int qi = 0; qi < 2; ++qi)
-      g.push_back(mlp12(bt.sa, W, Wq(qi, 0), Wq(qi, 1), Wq(qi, 2), Wq(qi, 3), h->h1[2 + qi], h->h2[2 + qi]));
-    if (launch_group(g, s)) return -1;
-  }
-  {
-    // output layers: policy [mean | log_std] (one 2A-wide tile per 16 rows, whose epilogue runs the
-    // squashed-Gaussian head), Q1/Q2(s, a)
-    std::vector<GemmProb> g;
+    FwdArgsR f{};
+    f.ninst = 4; f.n = n; f.H = H; f.A = A; f.ncq = ncq; f.nrb = nrb;
     for (int i = 0; i < 2; ++i) {
-      auto m = mk(n, 2 * A, H, h->h2[i], H, 0, P + o.pWm, A, 0, h->out[i], 2 * A);
-      m.B2 = P + o.pWl; m.split = A; m.bias = P + o.pbm; m.bias2 = P + o.pbl; m.head = 1 + i;
-      g.push_back(m);
+      FwdInst& q = f.in[i];
+      q.x = i == 0 ? bt.sa : bt.xn; q.ldx = W; q.kx = O; q.k1 = O;
+      q.w1 = P + o.pW1; q.b1 = P + o.pb1; q.w2 = P + o.pW2; q.b2 = P + o.pb2;
+      q.h1 = i == 0 ? h->h1[0] : nullptr; q.h2 = i == 0 ? h->h2[0] : nullptr;   // pi(s') needs no gradient
+      q.wo = P + o.pWm; q.wo2 = P + o.pWl; q.nout = 2 * A; q.split = A; q.opart = h->opart[i];
     }
     for (int qi = 0; qi < 2; ++qi) {
-      auto q = mk(n, 1, H, h->h2[2 + qi], H, 0, Wq(qi, 4), 1, 0, h->out[2 + qi], 1); q.bias = Wq(qi, 5); g.push_back(q);
+      FwdInst& q = f.in[2 + qi];
+      q.x = bt.sa; q.ldx = W; q.kx = W; q.k1 = W;
+      q.w1 = Wq(qi, 0); q.b1 = Wq(qi, 1); q.w2 = Wq(qi, 2); q.b2 = Wq(qi, 3);
+      q.h1 = h->h1[2 + qi]; q.h2 = h->h2[2 + qi];
+      q.wo = Wq(qi, 4); q.wo2 = nullptr; q.nout = 1; q.split = 1; q.opart = h->opart[2 + qi];
     }
-    HeadCtx hc{};
-    hc.O = O; hc.A = A; hc.eps_in[0] = eps_in_s; hc.eps_in[1] = eps_in_n; hc.eps_out[0] = h->eps_s;
-    hc.eps_out[1] = h->eps_n; hc.x[0] = bt.xpi; hc.x[1] = bt.xn; hc.logp[0] = h->logp_s; hc.logp[1] = h->logp_n;
-    hc.seed = seed; hc.iter = h->iter;
-    if (launch_group(g, s, nullptr, nullptr, &hc)) return -1;
+    f.st = Stamps{h->stamps, 0};
+    hipLaunchKernelGGL(sac_fwd_kernel<false>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
+    MOPO_HIP(hipGetLastError());
   }
-  // ---- forward stage 4-6: Q1/Q2(s, pi(s)) with main params, Qt1/Qt2(s', pi(s')) with target params
+  // ---- F2: the policy head from F1's partials -> Q1/Q2(s, pi(s)) (main), Qt1/Qt2(s', pi(s')) (target)
   {
-    std::vector<GemmProb> g;
+    FwdArgsR f{};
+    f.ninst = 4; f.n = n; f.H = H; f.A = A; f.ncq = ncq; f.nrb = nrb;
     for (int i = 0; i < 4; ++i) {
       const int qi = i & 1;
       const bool tgt = i >= 2;
       auto L = [&](int k) { return tgt ? Tq(qi, k) : Wq(qi, k); };
-      g.push_back(mlp12(tgt ? bt.xn : bt.xpi, W, L(0), L(1), L(2), L(3), tgt ? nullptr : h->h1[4 + i], h->h2[4 + i]));
+      FwdInst& q = f.in[i];
+      q.x = tgt ? bt.xn : bt.sa; q.ldx = W; q.kx = O; q.k1 = W;
+      q.w1 = L(0); q.b1 = L(1); q.w2 = L(2); q.b2 = L(3);
+      q.h1 = tgt ? nullptr : h->h1[4 + i]; q.h2 = tgt ? nullptr : h->h2[4 + i];
+      q.wo = L(4); q.wo2 = nullptr; q.nout = 1; q.split = 1; q.opart = h->opart[4 + i];
+      q.head = tgt ? 1 : 0;
     }
-    if (launch_group(g, s)) return -1;
-  }
-  // ---- critic output layers (s, pi) / targets + losses (one launch)
-  {
-    QLossArgs q{};
-    q.n = n; q.H = H; q.A = A; q.gamma = h->gamma; q.rscale = h->rscale;
-    for (int i = 0; i < 4; ++i) {
-      const int qi = i & 1;
-      const bool tgt = i >= 2;
-      q.h2[i] = h->h2[4 + i];
-      q.w3[i] = tgt ? Tq(qi, 4) : Wq(qi, 4);
-      q.b3[i] = tgt ? Tq(qi, 5) : Wq(qi, 5);
-      q.q[i] = h->out[4 + i];
-    }
-    q.q1 = h->out[2]; q.q2 = h->out[3];
-    q.logp_s = h->logp_s; q.logp_n = h->logp_n; q.rew = bt.rew; q.term = bt.term; q.head_s = h->out[0];
-    q.log_alpha = P + o.total;
-    q.dq1 = h->dq[0]; q.dq2 = h->dq[1]; q.dq1p = h->dq[2]; q.dq2p = h->dq[3]; q.part = h->loss_part;
-    hipLaunchKernelGGL(sac_qloss_kernel, dim3(ceil_div(n, QL_ROWS)), dim3(256), 0, s, q);
+    FwdHead& hd = f.hd;
+    hd.opart[0] = h->opart[0]; hd.opart[1] = h->opart[1]; hd.bm = P + o.pbm; hd.bl = P + o.pbl;
+    hd.eps_in[0] = eps_in_s; hd.eps_in[1] = eps_in_n; hd.eps_out[0] = h->eps_s; hd.eps_out[1] = h->eps_n;
+    hd.head_out[0] = h->out[0]; hd.head_out[1] = h->out[1]; hd.logp[0] = h->logp_s; hd.logp[1] = h->logp_n;
+    hd.seed = seed; hd.iter = h->iter;
+    f.st = Stamps{h->stamps, 1};
+    hipLaunchKernelGGL(sac_fwd_kernel<true>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
     MOPO_HIP(hipGetLastError());
   }
-  // ---- critic backward.  The 1-wide output layer's backward dh2 = dq (x) W3 * (h2 > 0) is rank-1,
-  // so it is never materialised: the consumers below read it as a rank-1 masked operand.
+  // ---- B1: per-row TD targets and dq -> the critics' dh1 (Q1/Q2 at (s,a) and (s,pi)), the action-
+  //      gradient partials of the (s, pi) instances, and the batch loss tail (one extra block)
   {
-    std::vector<GemmProb> g;
-    for (int i = 0; i < 4; ++i) {  // dh1 = dh2 W2^T * (h1 > 0); instances Q1(sa) Q2(sa) Q1(pi) Q2(pi)
+    Dh1Args d{};
+    d.ninst = 4; d.n = n; d.H = H; d.A = A; d.ncq = ncq; d.nrb = nrb;
+    for (int i = 0; i < 4; ++i) {
       const int qi = i & 1;
-      auto a = mk(n, H, H, nullptr, H, 0, Wq(qi, 2), H, 1, h->dh1[i], H); a.mask = h->h1[2 + i]; a.ldm = H;
-      a.a_u = h->dq[i]; a.a_v = Wq(qi, 4); a.a_m = h->h2[2 + i]; a.a_ldm = H;
-      g.push_back(a);
+      Dh1Inst& q = d.in[i];
+      q.h1 = h->h1[2 + i]; q.h2 = h->h2[2 + i]; q.w2 = Wq(qi, 2); q.w3 = Wq(qi, 4); q.kind = i;
+      q.dh1 = i < 2 ? h->dh1[i] : nullptr; q.dq = i < 2 ? h->dq[i] : nullptr;
+      q.w1a = i < 2 ? nullptr : Wq(qi, 0) + (int64_t)O * H; q.dapart = i < 2 ? nullptr : h->dapart[qi];
     }
-    LossTail lt{h->loss_part, ceil_div(n, QL_ROWS), n, h->tent, h->lr, h->logs, h->beta_pow, h->iter};
-    if (launch_group(g, s, &ad, &slot, nullptr, &lt)) return -1;
+    LossRows& L = d.L;
+    for (int i = 0; i < 6; ++i) {
+      L.qpart[i] = h->opart[2 + i];
+      L.b3[i] = i < 4 ? Wq(i & 1, 5) : Tq(i & 1, 5);
+    }
+    L.logp_s = h->logp_s; L.logp_n = h->logp_n; L.head_s = h->out[0]; L.rew = bt.rew; L.term = bt.term;
+    L.log_alpha = P + o.total; L.gamma = h->gamma; L.rscale = h->rscale;
+    d.ad = ad; d.tent = h->tent; d.lr = h->lr; d.logs = h->logs; d.beta_pow = h->beta_pow; d.iter = h->iter;
+    d.st = Stamps{h->stamps, 2};
+    hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq, nrb, 5), dim3(256), 0, s, d);
+    MOPO_HIP(hipGetLastError());
   }
   {
     // dW2 / dW3 only need the rank-1 dh2 (not dh1), so they ride with the smaller second launch; the
@@ -374,8 +268,8 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       g.push_back(w1);
     }
     PolicyRows pr{};
-    pr.n = n; pr.O = O; pr.A = A; pr.H = H;
-    pr.dh1[0] = h->dh1[2]; pr.dh1[1] = h->dh1[3]; pr.w1[0] = Wq(0, 0); pr.w1[1] = Wq(1, 0);
+    pr.n = n; pr.O = O; pr.A = A; pr.H = H; pr.ncq = ncq;
+    pr.dapart[0] = h->dapart[0]; pr.dapart[1] = h->dapart[1];
     pr.head_s = h->out[0]; pr.eps_s = h->eps_s; pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
     pr.h2p = h->h2[0]; pr.h1p = h->h1[0]; pr.W2p = P + o.pW2;
     pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p;
@@ -416,6 +310,7 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   MOPO_REQUIRE(out && h_params, "mopo_sac_create: NULL argument");
   MOPO_REQUIRE(O >= 1 && A >= 1 && A <= 8 && H >= 1, "mopo_sac_create: bad dims (act_dim <= 8)");
   MOPO_REQUIRE(batch >= 1 && batch <= 1024, "mopo_sac_create: batch must be in [1, 1024]");
+  MOPO_REQUIRE(O + A <= 31, "mopo_sac_create: obs_dim + act_dim must be <= 31 (layer-1 inputs + the bias in one 32-wide group)");
   MOPO_REQUIRE(H % 16 == 0 && H <= 256, "mopo_sac_create: hidden width must be a multiple of 16, <= 256");
   MOPO_REQUIRE(n_env >= 0 && n_env <= batch, "mopo_sac_create: n_env must be in [0, batch]");
   Sac* h = new Sac();
@@ -428,7 +323,12 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   std::vector<std::pair<void**, size_t>> reg;
   auto f = [&](float** p, size_t cnt) { reg.push_back({(void**)p, cnt * 4}); };
   f(&h->Pb[1], tot); f(&h->norm_part, 2 * (size_t)h->nslots_cap);
-  f(&h->loss_part, 8 * (size_t)ceil_div(batch, QL_ROWS));
+  const size_t npart = (size_t)ceil_div(H, RB_COLS) * n * OPW;
+  for (int i = 0; i < 8; ++i) f(&h->opart[i], npart);
+  for (int i = 0; i < 2; ++i) f(&h->dapart[i], npart);
+#if MOPO_SAC_STAMPS
+  reg.push_back({(void**)&h->stamps, (size_t)3 * 1024 * 8 * 8});
+#endif
   f(&h->P, tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->T, tot);
   f(&h->beta_pow, 3); f(&h->logs, LOG_N);
   reg.push_back({(void**)&h->iter, 8});
@@ -606,5 +506,15 @@ extern "C" int mopo_sac_step(mopo_sac_t hh, const mopo_pool_desc* env, const mop
   if (launch_logs(h, gs)) return -1;
   MOPO_HIP(hipEventRecord(h->ev_out, gs));
   MOPO_HIP(hipStreamWaitEvent(s, h->ev_out, 0));
+  return 0;
+}
+
+extern "C" int mopo_sac_debug_stamps(mopo_sac_t hh, uint64_t* h_out, int64_t n) {
+  Sac* h = reinterpret_cast<Sac*>(hh);
+  MOPO_REQUIRE(h && h_out, "mopo_sac_debug_stamps: NULL argument");
+  if (!h->stamps) return fail("mopo_sac_debug_stamps: library built without MOPO_SAC_STAMPS");
+  MOPO_REQUIRE(n >= 0 && n <= 3 * 1024 * 8, "mopo_sac_debug_stamps: n exceeds the stamp buffer");
+  MOPO_HIP(hipDeviceSynchronize());
+  MOPO_HIP(hipMemcpy(h_out, h->stamps, n * 8, hipMemcpyDeviceToHost));
   return 0;
 }

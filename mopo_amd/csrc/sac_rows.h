@@ -1,0 +1,536 @@
+// Row-block kernels of the SAC step (sac.hip): the forward of all eight MLP instances and the critics'
+// first-layer backward, each as ONE launch whose workgroups own 16 batch rows x 64 columns of a
+// 256-wide layer, with every cross-column reduction the next stage needs (output layers, the policy
+// head, the critics' action gradient) carried as per-block PARTIAL dot products that the consumer
+// sums in a fixed order (bit-reproducible, no atomics, no in-launch hand-off).
+//
+//   F1  sac_fwd_kernel<false>: pi(s), pi(s'), Q1(s,a), Q2(s,a): layer 1 (recomputed per block from the
+//       <= 31 inputs) + layer 2 + the partial dots of the block's 64 outputs with the output layer
+//       ([W_mean | W_log_std] for the policy, W3 for a critic)                   (mopo.py:298-324)
+//   F2  sac_fwd_kernel<true>: Q1/Q2(s, pi(s)) with the main critics, Qt1/Qt2(s', pi(s')) with the
+//       targets; the prologue sums pi's partials of its 16 rows into the squashed-Gaussian head
+//       (action, log-prob, noise: mopo.py:282-308) -- the action is the critic's layer-1 input
+//   B1  sac_dh1_kernel: dh1 = (dq (x) W3 * (h2 > 0)) W2^T * (h1 > 0) for Q1/Q2(s,a) and Q1/Q2(s,pi), the
+//       prologue forming each row's dq from the critics' partials (the TD target y, mopo.py:380-404;
+//       the min-Q selection, :367-377); the (s, pi) instances emit partials of d(-min Q)/d action
+//       (dh1 W1[O:]^T) for the policy backward; one extra block reduces the batch losses (logs,
+//       alpha Adam, lr_t, beta powers, step counter: mopo.py:403-443)
+//
+// Replaces the previous 4-launch chain (forward hidden layers / output layers + head / (s, pi) hidden
+// layers / losses + critic output layers) + the critic dh1 launch: 5 -> 3 launches.
+#pragma once
+#include "gemm_group.h"
+
+namespace mopo {
+
+constexpr int RB_COLS = 64;  // second-layer columns per workgroup (4 waves x 16); OPW: gemm_group.h
+
+#ifndef MOPO_SAC_STAMPS
+#define MOPO_SAC_STAMPS 0    // 1: diagnostic build, per-workgroup phase timestamps (s_memrealtime)
+#endif
+
+// per-workgroup phase stamps of the diagnostic build: [launch slot][block][8] u64
+struct Stamps { uint64_t* p; int slot; };
+static __device__ __forceinline__ void stamp(const Stamps& s, int i) {
+#if MOPO_SAC_STAMPS
+  // wave 0 (a wave-uniform branch: a lane-divergent one here moved the workgroup ids into VGPRs and
+  // de-uniformised the whole kernel); its lanes all store the same value
+  if (s.p && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
+    uint64_t t = __builtin_amdgcn_s_memrealtime();
+    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    uint64_t* q = s.p + ((int64_t)s.slot * 1024 + b) * 8;
+    __hip_atomic_store(q + i, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#else
+  (void)s; (void)i;
+#endif
+}
+
+struct FwdInst {
+  const float* x; int ldx; int kx;   // layer-1 inputs from memory: columns [0, kx) of x[n][ldx]
+  int k1;                            // layer-1 input width (F2: kx + A, the action from the head)
+  const float* w1; const float* b1;  // [k1][H], [H]
+  const float* w2; const float* b2;  // [H][H], [H]
+  float* h1; float* h2;              // stored for the backward pass when non-NULL
+  const float* wo; const float* wo2; // output layer [H][nout]: columns [0, split) from wo (ld split),
+  int nout, split;                   //   [split, nout) from wo2 (ld nout - split)
+  float* opart;                      // [ncq][n][OPW] partial dots of the block's 64 outputs
+  int head;                          // F2: 0 = pi(s) head (s, pi(s)), 1 = pi(s') head
+};
+
+struct FwdHead {                     // F2: the squashed-Gaussian head of pi(s) / pi(s') (HeadCtx math)
+  const float* opart[2];             // pi(s), pi(s') partials: [ncq][n][OPW], mean j < A, log_std A + j
+  const float* bm; const float* bl;  // output biases
+  const float* eps_in[2];            // injected noise [n][A] or NULL (Philox)
+  float* eps_out[2]; float* head_out[2]; float* logp[2];   // written by the designated blocks
+  uint64_t seed; const int64_t* iter;
+};
+
+struct FwdArgsR {
+  int ninst, n, H, A, ncq, nrb;
+  FwdInst in[4];
+  FwdHead hd;
+  Stamps st;
+};
+
+// the head of row r, action j (8 lanes per row; every lane of the 8 calls it): pre-activation
+// mean / raw log_std from the partials, then head_fwd_elem's math; returns the action (tanh u)
+static __device__ __forceinline__ float rows_head(const FwdHead& h, int nxt, int n, int A, int ncq, int r, int j,
+                                                  bool ok, bool store) {
+  const bool on = ok && j < A;
+  float mu = 0.f, raw = 0.f, z = 0.f;
+  if (on) {
+    const auto dp = rsrc(h.opart[nxt], (int64_t)ncq * n * OPW);
+    float pm[MAX_NCQ], pl[MAX_NCQ];
+#pragma unroll
+    for (int c = 0; c < MAX_NCQ; ++c) {   // unconditional loads, then the sums in column-block order
+      pm[c] = bload(dp, c < ncq ? (c * n + r) * OPW + j : -1);
+      pl[c] = bload(dp, c < ncq ? (c * n + r) * OPW + A + j : -1);
+    }
+    mu = h.bm[j];
+    raw = h.bl[j];
+#pragma unroll
+    for (int c = 0; c < MAX_NCQ; ++c) {
+      mu += pm[c];
+      raw += pl[c];
+    }
+    const float* ein = h.eps_in[nxt];
+    if (ein) {
+      z = ein[r * A + j];
+    } else {
+      const int64_t it = *h.iter;
+      const int blk = j >> 2;
+      u32x4 c{(uint32_t)r | ((uint32_t)nxt << 31), (uint32_t)it ^ ((uint32_t)blk << 24), (uint32_t)((uint64_t)it >> 32),
+              RNG_SAC + 16};
+      u32x4 q = philox(c, (uint32_t)h.seed, (uint32_t)(h.seed >> 32));
+      float z0, z1;
+      if (j & 2) box_muller(q.z, q.w, z0, z1);
+      else box_muller(q.x, q.y, z0, z1);
+      z = (j & 1) ? z1 : z0;
+    }
+  }
+  float v = 0.f, act = 0.f;
+  if (on) {
+    const float ls = fminf(fmaxf(raw, -20.f), 2.f);               // mopo.py:304
+    const float sd = expf(ls);
+    const float u = mu + z * sd;                                    // mopo.py:306
+    const float zz = (u - mu) / (sd + 1e-8f);
+    v = -0.5f * (zz * zz + 2.f * ls + 1.8378770664093453f)          // gaussian_likelihood (:282-284)
+        - 2.f * (0.6931471805599453f - u - softplusf(-2.f * u));    // squash correction (:292)
+    act = tanhf(u);
+    if (store) {
+      h.eps_out[nxt][r * A + j] = z;
+      h.head_out[nxt][r * 2 * A + j] = mu;
+      h.head_out[nxt][r * 2 * A + A + j] = raw;
+    }
+  }
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  if (store && ok && j == 0) h.logp[nxt][r] = v;
+  return act;
+}
+
+// The instance of a workgroup, selected field by field from the kernel arguments with the uniform
+// blockIdx.z: a dynamically indexed argument array (a.in[blockIdx.z]) compiles to per-lane global loads
+// of the argument block and waterfall loops around every buffer descriptor built from it.
+template <typename T>
+static __device__ __forceinline__ T pick4(const T (&in)[4], int i) {
+  T p = in[0];
+  if (i == 1) p = in[1];
+  if (i == 2) p = in[2];
+  if (i == 3) p = in[3];
+  return p;
+}
+
+// LDS of the row-block kernels (floats)
+constexpr int RB_LDS_A = GKC * 16;        // the 16 x K A slab, [k][r ^ psw(k)]
+constexpr int RB_LDS_B = 4 * GKC * 16;    // four wave-private 16-column B panels, [k][c]
+constexpr int RB_LDS_T = 16 * RB_COLS;    // the block's 16 x 64 output tile
+constexpr int RB_LDS_W = RB_COLS * OPW;   // output-layer columns of the block's 64 rows, [c][j]
+
+// Grid (column block, row block, instance): linear block id cq + ncq (rb + nrb ii).  H <= GKC, H % 16 == 0.
+template <bool HEAD>
+static __global__ __launch_bounds__(256, 1) void sac_fwd_kernel(const FwdArgsR a) {
+  __shared__ __attribute__((aligned(16))) float As[RB_LDS_A];
+  __shared__ __attribute__((aligned(16))) float Bw[RB_LDS_B];
+  __shared__ __attribute__((aligned(16))) float Ts[RB_LDS_T];
+  __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_W];
+  __shared__ float act_s[16][8];
+  stamp(a.st, 0);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // grid (ncq, nrb, ninst): the indices are SGPRs, so the instance's fields come from the kernel
+  // arguments by scalar loads (a divided linear index made them VGPRs: every buffer descriptor built
+  // from them then needed a waterfall loop)
+  const int ii = blockIdx.z, rb = blockIdx.y, cq = blockIdx.x;
+  const FwdInst p = pick4(a.in, ii);
+  const int n = a.n, H = a.H, A = a.A;
+  const int i0 = rb * 16, c0 = cq * RB_COLS, jw = c0 + w * 16;
+  // ---- 1. every global operand, issued up front: this wave's W2 panel (rows k = lane / 4 + 16 i,
+  //         columns 4 (lane % 4) .. + 3), the output-layer columns of the block's 64 rows, layer 1
+  const auto dbw = rsrc(p.w2, (int64_t)(H - 1) * H + H);
+  f32x4 bp[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = (lane >> 2) + 16 * i, col = jw + 4 * (lane & 3);
+    bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          dbw, ((k < H && col < H) ? k * H + col : -4) * 4, 0, 0));
+  }
+  float wov[4];
+  {
+    const int ld2 = p.nout - p.split;
+    const auto d1 = rsrc(p.wo, (int64_t)H * p.split), d2 = rsrc(p.wo2, (int64_t)H * (ld2 > 0 ? ld2 : 1));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {           // element e = c * OPW + j of Wo: c = e / 16, j = e % 16
+      const int e = tid + 256 * q, c = c0 + (e >> 4), j = e & 15;
+      const bool in1 = j < p.split, on = c < H && j < p.nout;
+      const float v1 = bload(d1, on && in1 ? c * p.split + j : -1);
+      const float v2 = bload(d2, on && !in1 ? c * ld2 + (j - p.split) : -1);
+      wov[q] = in1 ? v1 : v2;
+    }
+  }
+  const int r = lane & 15, q4 = lane >> 4;
+  const int row = i0 + r;
+  const int k1 = p.k1, ns = (k1 + 4) >> 2, sb = k1 >> 2;
+  float xb[8], wa[4][8], bv[4];
+  {
+    const auto dx = rsrc(p.x, (int64_t)(n - 1) * p.ldx + p.kx);
+    const auto dw = rsrc(p.w1, (int64_t)k1 * H);
+    const auto db = rsrc(p.b1, H);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int j = 4 * s + q4;
+      const float v = bload(dx, (j < p.kx && row < n) ? row * p.ldx + j : -1);
+      xb[s] = j == k1 ? 1.f : v;
+    }
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const int k = w * 64 + kt * 16 + r;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int j = 4 * s + q4;
+        wa[kt][s] = bload(dw, (j < k1 && k < H) ? j * H + k : -1);
+      }
+      bv[kt] = bload(db, k < H ? k : -1);
+    }
+  }
+  float b2v = bload(rsrc(p.b2, H), jw + (lane & 15) < H ? jw + (lane & 15) : -1);
+  // ---- 2. F2: the policy head of the block's 16 rows (its action feeds layer 1)
+  if (HEAD) {
+    if (tid < 128) {
+      const int hr = tid >> 3, hj = tid & 7, hrow = i0 + hr;
+      const bool store = cq == 0 && (ii == 0 || ii == 2);  // Q1(s,pi) / Qt1(s',pi') blocks publish the head
+      act_s[hr][hj] = rows_head(a.hd, p.head, n, A, a.ncq, hrow, hj, hrow < n, store);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int j = 4 * s + q4;
+      if (j >= p.kx && j < k1) xb[s] = act_s[r][(j - p.kx) & 7];
+    }
+  }
+  stamp(a.st, 1);
+  // ---- 3. layer 1 on MFMA: D(k, r) = relu(W1^T X^T + b1) (the bias rides as input column k1)
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s == sb && q4 == (k1 & 3)) wa[kt][s] = bv[kt];
+  {
+    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s < ns)
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) acc[kt] = mfma4(wa[kt][s], xb[s], acc[kt]);
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int kl = w * 64 + kt * 16 + 4 * q4 + tt;
+        As[kl * 16 + (r ^ psw(kl))] = (row < n && kl < H) ? fmaxf(acc[kt][tt], 0.f) : 0.f;
+      }
+  }
+  float* B = Bw + w * GKC * 16;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) *reinterpret_cast<f32x4*>(B + ((lane >> 2) + 16 * i) * 16 + 4 * (lane & 3)) = bp[i];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Wo[tid + 256 * q] = wov[q];
+  __syncthreads();
+  stamp(a.st, 2);
+  if (cq == 0 && p.h1 && tid < H) {  // the first-layer slab for the backward pass (coalesced in k)
+#pragma unroll 4
+    for (int rr = 0; rr < 16; ++rr)
+      if (i0 + rr < n) p.h1[(int64_t)(i0 + rr) * H + tid] = As[tid * 16 + (rr ^ psw(tid))];
+  }
+  // ---- 4. layer 2: the wave's 16 x 16 tile over the whole K
+  const int li = lane & 15, lk = lane >> 4;
+  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+  if (jw < H) {
+#pragma unroll 16
+    for (int s = 0; s < GKC / 4; ++s) {
+      const int k = 4 * s + lk;
+      acc[s & 3] = mfma4(As[k * 16 + (li ^ psw(k))], B[k * 16 + li], acc[s & 3]);
+    }
+  }
+  stamp(a.st, 3);
+  // ---- 5. bias + relu (D: column li, rows 4 lk + rr); h2 store; the tile into LDS
+  const int col = jw + li;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int orow = i0 + 4 * lk + rr;
+    const float v = (col < H && orow < n) ? fmaxf(acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr] + b2v, 0.f) : 0.f;
+    if (p.h2 && orow < n && col < H) p.h2[(int64_t)orow * H + col] = v;
+    Ts[(4 * lk + rr) * RB_COLS + w * 16 + li] = v;
+  }
+  __syncthreads();
+  // ---- 6. partial output dots: thread (row tid / 16, output j = tid % 16) over the block's 64 columns
+  {
+    const int orr = tid >> 4, j = tid & 15, orow = i0 + orr;
+    if (j < p.nout && orow < n) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll 8
+      for (int c = 0; c < RB_COLS; c += 2) {
+        s0 += Ts[orr * RB_COLS + c] * Wo[c * OPW + j];
+        s1 += Ts[orr * RB_COLS + c + 1] * Wo[(c + 1) * OPW + j];
+      }
+      p.opart[((int64_t)cq * n + orow) * OPW + j] = s0 + s1;
+    }
+  }
+  stamp(a.st, 4);
+}
+
+// ---- B1 -----------------------------------------------------------------------------------------
+// The critics' per-row losses from the forward partials (mopo.py:361-404): q = sum of the column-block
+// partials + b3, in column-block order.  Instances of the partial arrays: 0 Q1(s,a) 1 Q2(s,a)
+// 2 Q1(s,pi) 3 Q2(s,pi) 4 Qt1(s',pi') 5 Qt2(s',pi').
+struct LossRows {
+  const float* qpart[6];             // [ncq][n][OPW] (element 0)
+  const float* b3[6];
+  const float* logp_s; const float* logp_n; const float* head_s; const float* rew; const float* term;
+  const float* log_alpha;
+  float gamma, rscale;
+};
+
+struct RowQ { float q[6]; float y, alpha; };
+
+static __device__ __forceinline__ RowQ row_losses(const LossRows& L, int n, int ncq, int r) {
+  RowQ o;
+  float pv[6][MAX_NCQ];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {           // unconditional loads, then the sums in column-block order
+    const auto dp = rsrc(L.qpart[i], (int64_t)ncq * n * OPW);
+#pragma unroll
+    for (int c = 0; c < MAX_NCQ; ++c) pv[i][c] = bload(dp, c < ncq ? (c * n + r) * OPW : -1);
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float s = *L.b3[i];
+#pragma unroll
+    for (int c = 0; c < MAX_NCQ; ++c) s += pv[i][c];
+    o.q[i] = s;
+  }
+  o.alpha = expf(*L.log_alpha);                                       // mopo.py:361
+  const float qt = fminf(o.q[4], o.q[5]);                             // mopo.py:368
+  o.y = L.rscale * L.rew[r] + L.gamma * ((1.f - L.term[r]) * (qt - o.alpha * L.logp_n[r]));  // :380-386
+  return o;
+}
+
+struct Dh1Inst {
+  const float* h1; const float* h2; const float* w2; const float* w3;
+  int kind;                          // dq of the row: 0 (q1 - y) / n, 1 (q2 - y) / n, 2 min-select Q1, 3 Q2
+  float* dh1;                        // stored when non-NULL
+  float* dq;                         // stored by the column-block-0 workgroups when non-NULL
+  const float* w1a;                  // (s, pi) instances: W1[O:] = the action rows [A][H]; NULL otherwise
+  float* dapart;                     // [ncq][n][OPW]: partial dh1 W1[O:]^T of the block's 64 columns
+};
+
+struct Dh1Args {
+  int ninst, n, H, A, ncq, nrb;
+  Dh1Inst in[4];
+  LossRows L;
+  // the loss tail (last block): batch means -> logs, the alpha gradient + Adam, lr_t, beta powers, step
+  AdamCtx ad;
+  float tent, lr;
+  float* logs; float* beta_pow; int64_t* iter;
+  Stamps st;
+};
+
+// the extra block: per-row loss terms of all n rows (thread t: rows t, t + 256, ...), block sums in a
+// fixed order (deterministic), then thread 0 applies the batch-level updates (loss_tail_block's tail)
+static __device__ __forceinline__ void loss_tail_rows(const Dh1Args& a, float* sh) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = a.n, A = a.A;
+  float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = tid; r < n; r += 256) {
+    const RowQ o = row_losses(a.L, n, a.ncq, r);
+    const float q1 = o.q[0], q2 = o.q[1], q1p = o.q[2], q2p = o.q[3];
+    const float lps = a.L.logp_s[r];
+    float ent = 0.f;                                                  // pi_entropy terms (mopo.py:341)
+    for (int j = 0; j < A; ++j) {
+      const float ls = fminf(fmaxf(a.L.head_s[(int64_t)r * 2 * A + A + j], -20.f), 2.f);
+      ent += logf(expf(ls) + 1e-8f) + 0.5f * logf(2.f * 3.14159265358979f * 2.718281828459045f);
+    }
+    red[0] += (q1 - o.y) * (q1 - o.y); red[1] += (q2 - o.y) * (q2 - o.y); red[2] += q1; red[3] += q2;
+    red[4] += lps; red[5] += ent; red[6] += o.alpha * lps - fminf(q1p, q2p);
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) red[i] += __shfl_xor(red[i], off);
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 7; ++i) sh[w * 8 + i] = red[i];
+  __syncthreads();
+  if (tid != 0) return;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) red[i] = sh[i] + sh[8 + i] + sh[16 + i] + sh[24 + i];
+  const AdamCtx& ad = a.ad;
+  const AdamIn al = adam_load(ad, ad.total);                          // log_alpha = the last parameter
+  const float fn = (float)n;
+  const float l1 = red[0] / fn * 0.5f, l2 = red[1] / fn * 0.5f;       // mopo.py:403-404
+  const float m1 = red[2] / fn, m2 = red[3] / fn, mlp = red[4] / fn, ment = red[5] / fn;
+  const float pil = red[6] / fn;                                      // mopo.py:371-377
+  const float ga = -(mlp + a.tent);                                   // d/dlog_alpha of -mean(la*(logp+H))
+  const_cast<float*>(ad.G)[ad.total] = ga;
+  float* logs = a.logs;
+  logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;
+  logs[LOG_ALPHA] = expf(al.p); logs[LOG_ENTROPY] = ment; logs[LOG_LOGP] = mlp; logs[LOG_PI_LOSS] = pil;
+  const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
+  const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);           // TF1 Adam step size
+  a.beta_pow[2] = lr_t;
+  a.beta_pow[0] = b1p * 0.9f;
+  a.beta_pow[1] = b2p * 0.999f;
+  *a.iter += 1;
+  adam_apply(ad, ad.total, ga, al, lr_t);
+}
+
+// Grid (column block, row block, instance + 1); instance ninst, block (0, 0): the loss tail.
+static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a) {
+  __shared__ __attribute__((aligned(16))) float As[RB_LDS_A];
+  __shared__ __attribute__((aligned(16))) float Bw[RB_LDS_B];
+  __shared__ __attribute__((aligned(16))) float Ts[RB_LDS_T];
+  __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_W];
+  __shared__ float dqs[16];
+  stamp(a.st, 0);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // grid (ncq, nrb, ninst + 1): SGPR indices (see sac_fwd_kernel); z = ninst is the loss tail (block 0)
+  const int ii = blockIdx.z, rb = blockIdx.y, cq = blockIdx.x;
+  if (ii >= a.ninst) {
+    if (rb == 0 && cq == 0) {
+      loss_tail_rows(a, Ts);
+      stamp(a.st, 4);
+    }
+    return;
+  }
+  const Dh1Inst p = pick4(a.in, ii);
+  const int n = a.n, H = a.H, A = a.A;
+  const int i0 = rb * 16, c0 = cq * RB_COLS, jw = c0 + w * 16;
+  const int li = lane & 15, lk = lane >> 4;
+  // ---- 1. operands up front: W2^T panel of this wave's 16 columns (B(m, c) = W2[c][m]: lane reads
+  //         W2 row c = jw + lane % 16 at m = 4 (lane / 16 + 4 i) .. + 3), the A slab's h2 rows and W3,
+  //         the h1 mask of this lane's outputs, W1[O:] columns of the block (the (s, pi) instances)
+  const auto dw2 = rsrc(p.w2, (int64_t)H * H);
+  f32x4 bp[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int m = 4 * (lk + 4 * i), c = jw + li;
+    bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          dw2, ((m < H && c < H) ? c * H + m : -4) * 4, 0, 0));
+  }
+  // A slab: thread (m-quad tid % 64, rows 4 (tid / 64) .. + 3)
+  const int am = 4 * (tid & 63), ar = 4 * w;
+  const auto dh2 = rsrc(p.h2, (int64_t)n * H);
+  f32x4 h2v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    h2v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           dh2, ((am < H && i0 + ar + q < n) ? (i0 + ar + q) * H + am : -4) * 4, 0, 0));
+  const f32x4 w3v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rsrc(p.w3, H), (am < H ? am : -4) * 4, 0, 0));
+  float m1[4];
+  {
+    const auto dm1 = rsrc(p.h1, (int64_t)n * H);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) m1[rr] = bload(dm1, (jw + li < H && i0 + 4 * lk + rr < n) ? (i0 + 4 * lk + rr) * H + jw + li : -1);
+  }
+  float wov[4] = {0.f, 0.f, 0.f, 0.f};
+  if (p.w1a) {
+    const auto d1 = rsrc(p.w1a, (int64_t)A * H);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {     // Wo[c][j] = W1[O + j][c0 + c]
+      const int e = tid + 256 * q, c = c0 + (e >> 4), j = e & 15;
+      wov[q] = bload(d1, (c < H && j < A) ? j * H + c : -1);
+    }
+  }
+  // ---- 2. dq of the block's 16 rows (one lane per row)
+  if (tid < 16) {
+    const int rr = i0 + tid;
+    float dq = 0.f;
+    if (rr < n) {
+      const RowQ o = row_losses(a.L, n, a.ncq, rr);
+      const float inv_n = 1.f / (float)n;
+      const bool sel1 = o.q[2] <= o.q[3];                             // tf.minimum grad -> x where x <= y
+      dq = p.kind == 0 ? (o.q[0] - o.y) * inv_n : p.kind == 1 ? (o.q[1] - o.y) * inv_n
+         : p.kind == 2 ? (sel1 ? -inv_n : 0.f) : (sel1 ? 0.f : -inv_n);
+      if (cq == 0 && p.dq) p.dq[rr] = dq;
+    }
+    dqs[tid] = dq;
+  }
+  __syncthreads();
+  stamp(a.st, 1);
+  // ---- 3. A slab dh2 = dq (x) W3 * (h2 > 0) and the W2^T panel into LDS
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float u = dqs[ar + q];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = am + e;
+      As[m * 16 + ((ar + q) ^ psw(m))] = (m < H && h2v[q][e] > 0.f) ? u * w3v[e] : 0.f;
+    }
+  }
+  float* B = Bw + w * GKC * 16;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) B[(4 * (lk + 4 * i) + e) * 16 + li] = bp[i][e];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Wo[tid + 256 * q] = wov[q];
+  __syncthreads();
+  stamp(a.st, 2);
+  // ---- 4. dh1 tile of the wave: 16 rows x 16 columns over the whole K
+  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+  if (jw < H) {
+#pragma unroll 16
+    for (int s = 0; s < GKC / 4; ++s) {
+      const int k = 4 * s + lk;
+      acc[s & 3] = mfma4(As[k * 16 + (li ^ psw(k))], B[k * 16 + li], acc[s & 3]);
+    }
+  }
+  stamp(a.st, 3);
+  // ---- 5. relu mask from h1; store; the (s, pi) instances' action-gradient partials
+  const int col = jw + li;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int orow = i0 + 4 * lk + rr;
+    const float v = (col < H && orow < n && m1[rr] > 0.f) ? acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr] : 0.f;
+    if (p.dh1 && orow < n && col < H) p.dh1[(int64_t)orow * H + col] = v;
+    Ts[(4 * lk + rr) * RB_COLS + w * 16 + li] = v;
+  }
+  if (p.w1a) {
+    __syncthreads();
+    const int orr = tid >> 4, j = tid & 15, orow = i0 + orr;
+    if (j < A && orow < n) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll 8
+      for (int c = 0; c < RB_COLS; c += 2) {
+        s0 += Ts[orr * RB_COLS + c] * Wo[c * OPW + j];
+        s1 += Ts[orr * RB_COLS + c + 1] * Wo[(c + 1) * OPW + j];
+      }
+      p.dapart[((int64_t)cq * n + orow) * OPW + j] = s0 + s1;
+    }
+  }
+  stamp(a.st, 4);
+}
+
+}  // namespace mopo
