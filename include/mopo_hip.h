@@ -281,7 +281,7 @@ int mopo_sac_set_graph(mopo_sac_t h, int enable);
  * 5 logs); to_handle=1 writes the handle's buffer from d_buf (e.g. loading a checkpoint). */
 int mopo_sac_copy(mopo_sac_t h, int which, int to_handle, void* d_buf, int64_t count, void* stream);
 /* Diagnostic builds only (MOPO_SAC_STAMPS=1; otherwise returns -1): per-workgroup phase timestamps
- * (s_memrealtime, 100 MHz) of the last step's three row-block launches, u64 [launch][block][8]. */
+ * (s_memrealtime, 100 MHz) of the last step's five launches, u64 [launch][block][8]. */
 int mopo_sac_debug_stamps(mopo_sac_t h, uint64_t* h_out, int64_t n);
 
 /* ---- numpy legacy RandomState replica (host) ------------------------------------------ */

@@ -1,5 +1,6 @@
 // Grouped small-GEMM kernel with fused epilogues (activation, activation-derivative masks,
-// bias-gradient column sums, TF1 Adam + Polyak, policy head), shared by the SAC step (sac.hip)
+// bias-gradient column sums, TF1 Adam + Polyak), shared by the SAC step's weight-gradient launches
+// (sac.hip; plus the policy's row-local backward chain and the next batch's gather as extra blocks)
 // and the ensemble training step (bnn_train.hip).
 //
 // One 16x16 output tile per 256-thread block; K is split over the four waves and reduced through
@@ -24,15 +25,34 @@ static __device__ __forceinline__ float dswish_fast(float z) {
 
 constexpr int MAXP = 16;
 
+#ifndef MOPO_SAC_STAMPS
+#define MOPO_SAC_STAMPS 0    // 1: diagnostic build, per-workgroup phase timestamps (s_memrealtime)
+#endif
+
+// per-workgroup phase stamps of the diagnostic build: [launch slot][block][8] u64
+struct Stamps { uint64_t* p; int slot; };
+static __device__ __forceinline__ void stamp(const Stamps& s, int i) {
+#if MOPO_SAC_STAMPS
+  // wave 0 (a wave-uniform branch: a lane-divergent one here moved the workgroup ids into VGPRs and
+  // de-uniformised the whole kernel); its lanes all store the same value
+  if (s.p && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
+    uint64_t t = __builtin_amdgcn_s_memrealtime();
+    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    uint64_t* q = s.p + ((int64_t)s.slot * 1024 + b) * 8;
+    __hip_atomic_store(q + i, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#else
+  (void)s; (void)i;
+#endif
+}
+
+
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2 };   // GemmProb::act
 enum { MASK_RELU = 0, MASK_DSWISH = 1 };             // GemmProb::mask_kind
 
 struct GemmProb {
   int M, N, K;
-  const float* A; int lda; int ta;   // ta=0: A(i,k)=A[i*lda+k]; ta=1: A(i,k)=A[k*lda+i]; ta=2: layer-1 recompute
-  // ta == 2: A(i,k) = relu(sum_j X(i,j) W1(j,k) + b1(k)) for j < K1 <= 31, X = A (row stride lda),
-  // W1 = a_u ([K1][K] row-major), b1 = a_v, K1 = a_ldm; tiles with tn == 0 store that 16 x K
-  // slab of the first hidden layer to a_m (row stride K) for the backward pass
+  const float* A; int lda; int ta;   // ta=0: A(i,k)=A[i*lda+k]; ta=1: A(i,k)=A[k*lda+i]
   const float* B; int ldb; int tb;   // tb=0: B(k,j)=B[k*ldb+j]; tb=1: B(k,j)=B[j*ldb+k]
   float* C; int ldc;
   const float* bias;                 // C += bias[j]
@@ -48,65 +68,9 @@ struct GemmProb {
   const float* b_u; const float* b_v; const float* b_m; int b_ldm;
   int adam;                          // C (and colsum) are gradient slices of AdamCtx::G: apply Adam
   // two-segment plain B (operand mode 3): columns [0, split) from B, [split, N) from B2 (same ldb),
-  // bias likewise from bias / bias2 -- the policy output layer [W_mean | W_log_std]
+  // bias likewise from bias / bias2
   const float* B2; int split; const float* bias2;
-  int head;                          // 1: pi(s), 2: pi(s'): squashed-Gaussian head epilogue (HeadCtx)
 };
-
-// ---- squashed Gaussian head, forward (mopo.py:282-308, 286-296) for one batch row of pi(s) or
-// pi(s'): action = tanh(mu + eps * exp(clip(log_std))) into the row's action slot, its log-prob
-// (with the tanh correction) and the noise used.  eps is Philox(seed, step counter, row) unless
-// injected (parity mode).
-struct HeadCtx {
-  int O, A;
-  const float* eps_in[2];            // injected noise or NULL
-  float* eps_out[2];
-  float* x[2];                       // [n][O + A] rows whose action part receives tanh(u)
-  float* logp[2];
-  uint64_t seed;
-  const int64_t* iter;
-};
-
-// One action j of row r (8 lanes per row, lanes j >= A idle): its normal (Philox block j / 4,
-// Box-Muller pair (j % 4) / 2 -- the numbers the per-row order draws), the tanh-squashed action,
-// and the row's log-prob as an 8-lane butterfly sum of (gaussian term - squash correction).
-// Called by all 8 lanes of the row's group (the shuffles need them); ok: the row exists.
-static __device__ __forceinline__ void head_fwd_elem(const HeadCtx& hc, int nxt, int r, int j, const float* hm,
-                                                     const float* hl, bool ok) {
-  const int A = hc.A;
-  const bool on = ok && j < A;
-  float v = 0.f;
-  if (on) {
-    float z;
-    const float* ein = hc.eps_in[nxt];
-    if (ein) {
-      z = ein[r * A + j];
-    } else {
-      const int64_t it = *hc.iter;
-      const int blk = j >> 2;
-      u32x4 c{(uint32_t)r | ((uint32_t)nxt << 31), (uint32_t)it ^ ((uint32_t)blk << 24), (uint32_t)((uint64_t)it >> 32),
-              RNG_SAC + 16};
-      u32x4 q = philox(c, (uint32_t)hc.seed, (uint32_t)(hc.seed >> 32));
-      float z0, z1;
-      if (j & 2) box_muller(q.z, q.w, z0, z1);
-      else box_muller(q.x, q.y, z0, z1);
-      z = (j & 1) ? z1 : z0;
-    }
-    const float mu = hm[j];
-    const float ls = fminf(fmaxf(hl[j], -20.f), 2.f);             // mopo.py:304
-    const float sd = expf(ls);
-    const float u = mu + z * sd;                                   // mopo.py:306
-    const float zz = (u - mu) / (sd + 1e-8f);
-    v = -0.5f * (zz * zz + 2.f * ls + 1.8378770664093453f)         // gaussian_likelihood (:282-284)
-        - 2.f * (0.6931471805599453f - u - softplusf(-2.f * u));   // squash correction (:292)
-    hc.x[nxt][r * (hc.O + A) + hc.O + j] = tanhf(u);
-    hc.eps_out[nxt][r * A + j] = z;
-  }
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  if (ok && j == 0) hc.logp[nxt][r] = v;
-}
 
 // Fused optimizer (the four TF1 Adams + Polyak, mopo.py:407-447): a weight-gradient tile is final
 // when its epilogue runs (K spans the whole batch), so the epilogue updates the parameters it
@@ -125,17 +89,6 @@ struct AdamCtx {
 enum {
   LOG_Q1_LOSS = 0, LOG_Q2_LOSS, LOG_Q1, LOG_Q2, LOG_ALPHA, LOG_ENTROPY, LOG_LOGP, LOG_PI_GNORM, LOG_Q_GNORM,
   LOG_PI_LOSS, LOG_PI_GSQ, LOG_Q_GSQ, LOG_N = 16
-};
-
-// Batch-level tail of the SAC losses (mopo.py:361-443): the per-block sums of sac_qloss_kernel
-// (written by the previous launch, so no in-launch hand-off) -> losses / logs, the alpha gradient
-// and its Adam, this step's lr_t, the TF1 beta powers and the step counter.  Run by ONE extra block
-// appended to the first critic-backward launch (none of whose GEMM blocks reads what it writes).
-struct LossTail {
-  const float* part;                 // [nparts][8]
-  int nparts, n;
-  float tent, lr;
-  float* logs; float* beta_pow; int64_t* iter;
 };
 
 // buffer descriptor over n floats at p (wave-uniform inputs only)
@@ -234,22 +187,20 @@ constexpr int PR_LDS = 2 * 256 * 16; // floats the grouped kernel's panel LDS of
 // block pays one memory latency, then computes.
 // S: >= 16 (H + 4) floats of LDS (PR_LDS); hs: >= 3 * 128 floats.
 // H % 16 == 0, H <= 256 (one dh2p column per thread), A <= 8.
-static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs) {
+// WAIT: called after every other operand of the chain is in flight, before the action-gradient
+// partials are loaded; SC1: load them with agent-scope (sc1) loads -- the partials were written by
+// other workgroups of the SAME launch (the in-launch hand-off of sac_dh1_kernel).
+template <bool SC1 = false, typename Wait>
+static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs, Wait wait) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int H = c.H, A = c.A, HS = H + 4, n = c.n;
   const int ncq = (H + PR_COLS - 1) / PR_COLS;
   const int rb = x / ncq, cq = x % ncq, r0 = rb * 16;
   const int li = lane & 15, lk = lane >> 4;
-  // ---- the burst
+  // ---- the burst: head inputs, Wm / Wl / h2p at this thread's dh2p column, this wave's W2p operands of
+  //      the dh1p tile and the h1p mask; then (after wait()) the action-gradient partials
   const int hr = tid >> 3, hj = tid & 7, hrow = r0 + hr;
   const bool hon = tid < 128 && hj < A && hrow < n;
-  float dap[2][MAX_NCQ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const auto dp = rsrc(c.dapart[i], (int64_t)c.ncq * n * OPW);
-#pragma unroll
-    for (int q = 0; q < MAX_NCQ; ++q) dap[i][q] = bload(dp, (hon && q < c.ncq) ? (q * n + hrow) * OPW + hj : -1);
-  }
   const auto dh = rsrc(c.head_s, (int64_t)n * 2 * A), de = rsrc(c.eps_s, (int64_t)n * A);
   const float mu = bload(dh, hon ? hrow * 2 * A + hj : -1);
   const float raw = bload(dh, hon ? hrow * 2 * A + A + hj : -1);
@@ -279,6 +230,22 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   float m1[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
+  wait();
+  float dap[2][MAX_NCQ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if constexpr (SC1) {
+#pragma unroll
+      for (int q = 0; q < MAX_NCQ; ++q)
+        dap[i][q] = (hon && q < c.ncq) ? __hip_atomic_load(c.dapart[i] + ((int64_t)q * n + hrow) * OPW + hj,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : 0.f;
+    } else {
+      const auto dp = rsrc(c.dapart[i], (int64_t)c.ncq * n * OPW);
+#pragma unroll
+      for (int q = 0; q < MAX_NCQ; ++q) dap[i][q] = bload(dp, (hon && q < c.ncq) ? (q * n + hrow) * OPW + hj : -1);
+    }
+  }
   // ---- squashed-Gaussian head backward (mopo.py:282-308 differentiated; pi_loss mopo.py:371-377)
   float* dmu_s = hs + 128;
   float* dls_s = hs + 256;
@@ -348,15 +315,15 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   }
 }
 
-// Blocks of a launch: [pr.nblk policy-row blocks] [the problems' tiles (prefix[n])] [LossTail block
-// if tail.part] [gather_blocks blocks of the next step's batch gather (ga)].
+// Blocks of a launch: [pr.nblk policy-row blocks] [the problems' tiles (prefix[n])] [gather_blocks
+// blocks of the next step's batch gather (ga)].
 struct GemmGroup {
   int n;
   int prefix[MAXP + 1];
   AdamCtx ad;
-  HeadCtx hd;
-  LossTail tail;                     // tail.part != NULL: block prefix[n] runs loss_tail_block
   PolicyRows pr;
+  int* zero; int nzero;              // block 0 zeroes zero[0, nzero) (SAC: the next step's hand-off counters)
+  Stamps st;                         // diagnostic builds (MOPO_SAC_STAMPS): per-block phase stamps
   int gather_blocks;
   GatherArgs ga;
   GemmProb p[MAXP];
@@ -379,36 +346,6 @@ static __device__ __forceinline__ void adam_apply(const AdamCtx& ad, int64_t i, 
   if (ad.T && i < ad.total) ad.T[i] = (1.f - ad.tau) * a.t + ad.tau * p;   // mopo.py:446-447 (after the updates)
 }
 
-
-// the extra block of a launch carrying a LossTail: sums the per-block partials in block order
-// (deterministic), then one thread applies the batch-level updates.  sh: >= 8 * 64 floats of LDS.
-static __device__ __forceinline__ void loss_tail_block(const LossTail& t, const AdamCtx& ad, float* sh) {
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 8 * t.nparts; i += blockDim.x) sh[i] = t.part[i];
-  __syncthreads();
-  if (tid != 0) return;
-  float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int b = 0; b < t.nparts; ++b)
-#pragma unroll
-    for (int i = 0; i < 7; ++i) red[i] += sh[8 * b + i];
-  const AdamIn al = adam_load(ad, ad.total);                       // log_alpha = the last parameter
-  const float fn = (float)t.n;
-  const float l1 = red[0] / fn * 0.5f, l2 = red[1] / fn * 0.5f;   // mopo.py:403-404
-  const float m1 = red[2] / fn, m2 = red[3] / fn, mlp = red[4] / fn, ment = red[5] / fn;
-  const float pil = red[6] / fn;                                  // mopo.py:371-377
-  const float ga = -(mlp + t.tent);                               // d/dlog_alpha of -mean(la*(logp+H))
-  const_cast<float*>(ad.G)[ad.total] = ga;                          // the alpha gradient (logs / tests)
-  float* logs = t.logs;
-  logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;
-  logs[LOG_ALPHA] = expf(al.p); logs[LOG_ENTROPY] = ment; logs[LOG_LOGP] = mlp; logs[LOG_PI_LOSS] = pil;
-  const float b1p = t.beta_pow[0], b2p = t.beta_pow[1];
-  const float lr_t = t.lr * sqrtf(1.f - b2p) / (1.f - b1p);       // TF1 Adam step size (identical step counts)
-  t.beta_pow[2] = lr_t;
-  t.beta_pow[0] = b1p * 0.9f;
-  t.beta_pow[1] = b2p * 0.999f;
-  *t.iter += 1;
-  adam_apply(ad, ad.total, ga, al, lr_t);
-}
 
 constexpr int GKC = 256;  // K chunk staged in LDS
 
@@ -529,7 +466,7 @@ static __device__ __forceinline__ void store_panel(const GemmProb& p, int r0, in
 
 // operand modes (A: 0 plain, 1 transposed, 2 rank-1; B: the same, 3 two-segment) as am * 4 + bm
 __host__ static __device__ __forceinline__ int operand_modes(const GemmProb& p) {
-  const int am = p.ta == 2 ? 4 : p.a_u ? 2 : p.ta, bm = p.b_u ? 2 : p.B2 ? 3 : p.tb;
+  const int am = p.a_u ? 2 : p.ta, bm = p.b_u ? 2 : p.B2 ? 3 : p.tb;
   return am * 4 + bm;
 }
 
@@ -545,62 +482,6 @@ static __device__ __forceinline__ void stage_ab(const GemmProb& p, int i0, int j
   store_panel<BM, false, TW>(p, j0, kn, tid, rb, Bs);
 }
 
-// A operand mode 4 (ta == 2): the block's 16 x GKC slab of an MLP's first hidden layer, recomputed
-// here from the K1 <= 32 inputs of its rows instead of being read back from a launch of its own:
-// D(k, r) = W1^T(k, :) X^T(:, r) on f32 MFMA, four 16-wide k tiles per wave (the 256 threads cover
-// one 256-deep chunk), then bias + relu straight into the swizzled A panel.
-template <int BM>
-static __device__ __forceinline__ void stage_mlp1(const GemmProb& p, int i0, int j0, int kc, int kn, int tid,
-                                                  float* As, float* Bs) {
-  PanelRegs rb;
-  load_panel<BM, false>(p, j0, kc, tid, rb);
-  const int lane = tid & 63, w = tid >> 6, r = lane & 15, q = lane >> 4;
-  // the bias rides in the contraction as input column K1 (X = 1, W1 row K1 = b1): K1 <= 31
-  const int k1 = p.a_ldm, ns = (k1 + 4) >> 2, sb = k1 >> 2;
-  const auto dx = rsrc(p.A, (int64_t)(p.M - 1) * p.lda + k1);
-  const auto dw = rsrc(p.a_u, (int64_t)k1 * p.K);
-  const auto db = rsrc(p.a_v, p.K);
-  float xb[8], wa[4][8], bv[4];
-  const int row = i0 + r;
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int j = 4 * s + q;
-    const float v = bload(dx, row * p.lda + j);
-    xb[s] = (j < k1 && row < p.M) ? v : (j == k1 ? 1.f : 0.f);
-  }
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt) {
-    const int k = kc + w * 64 + kt * 16 + r;  // A-operand row of this lane
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int j = 4 * s + q;
-      const float v = bload(dw, j * p.K + k);
-      wa[kt][s] = (j < k1 && k < p.K) ? v : 0.f;
-    }
-    bv[kt] = bload(db, k);
-  }
-  pin_panel<BM, false>(rb);
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-      if (s == sb && q == (k1 & 3)) wa[kt][s] = bv[kt];
-  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-    if (s < ns)
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) acc[kt] = mfma4(wa[kt][s], xb[s], acc[kt]);
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int kl = w * 64 + kt * 16 + 4 * q + t;  // D row = k within the chunk; D column = row r
-      As[kl * 16 + (r ^ psw(kl))] = (row < p.M && kl < kn) ? fmaxf(acc[kt][t], 0.f) : 0.f;
-    }
-  store_panel<BM, false>(p, j0, kn, tid, rb, Bs);
-}
-
 template <int TW>
 static __device__ __forceinline__ void stage_dispatch(const GemmProb& p, int i0, int j0, int kc, int kn, int t,
                                                       float* As, float* Bs) {
@@ -610,7 +491,6 @@ static __device__ __forceinline__ void stage_dispatch(const GemmProb& p, int i0,
     case 3: stage_ab<0, 3, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
     case 4: stage_ab<1, 0, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
     case 6: stage_ab<1, 2, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
-    case 16: if (TW == 16) stage_mlp1<0>(p, i0, j0, kc, kn, t, As, Bs); break;
     default: stage_ab<2, 1, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
   }
 }
@@ -626,25 +506,21 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
   float (*Bs)[16] = reinterpret_cast<float (*)[16]>(ABs + GKC * 16);
   __shared__ __attribute__((aligned(16))) float part[4][256];
   __shared__ float csum[16][17];
-  __shared__ float hv[16][17];
   // block order: [pr.nblk policy-row blocks (first: the longest chain starts at once)] [the problems'
-  // tiles (prefix[n])] [LossTail block if tail.part] [gather blocks]
+  // tiles (prefix[n])] [gather blocks]
+  stamp(g.st, 0);
+  if (blockIdx.x == 0 && (int)threadIdx.x < g.nzero) g.zero[threadIdx.x] = 0;
   if ((int)blockIdx.x < g.pr.nblk) {
-    policy_rows_block(g.pr, blockIdx.x, ABs, &part[0][0]);
+    policy_rows_block(g.pr, blockIdx.x, ABs, &part[0][0], [] {});
+    stamp(g.st, 4);
     return;
   }
   const int bid = (int)blockIdx.x - g.pr.nblk;
-  if (bid >= g.prefix[g.n]) {  // the extra blocks after the tiles
-    int x = bid - g.prefix[g.n];
-    if (g.tail.part) {
-      if (x == 0) {
-        loss_tail_block(g.tail, g.ad, &part[0][0]);
-        return;
-      }
-      --x;
-    }
+  if (bid >= g.prefix[g.n]) {  // the gather blocks after the tiles
+    const int x = bid - g.prefix[g.n];
     const int C = 2 * g.ga.O + g.ga.A + 2, e = x * 256 + (int)threadIdx.x;
     if (e < g.ga.n * C) gather_elem(g.ga, e / C, e % C);
+    stamp(g.st, 4);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -703,12 +579,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
     // per chunk instead of one per element.
     stage_dispatch<16>(p, i0, j0, kc, kn, t, &As[0][0], &Bs[0][0]);
     __syncthreads();
-    if (p.ta == 2 && tn == 0 && p.a_m && t < kn) {  // first-layer slab for the backward pass (coalesced in k)
-      float* h1 = const_cast<float*>(p.a_m);
-#pragma unroll 4
-      for (int r = 0; r < 16; ++r)
-        if (i0 + r < p.M) h1[(int64_t)(i0 + r) * p.K + kc + t] = As[t][r ^ psw(t)];
-    }
+    stamp(g.st, 1);
     // the staged panels are zero-padded to GKC rows, so every wave runs exactly 16 k-steps of its
     // quarter with no guards: all 32 LDS reads first, then 16 MFMAs on two accumulators
     float ra[16], rb[16];
@@ -728,6 +599,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
       for (int k = tid >> 4; k < kn; k += 16) cs += Bs[k][(tid & 15) ^ psw(k)];
     __syncthreads();
   }
+  stamp(g.st, 2);
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[w][(lk * 4 + r) * 16 + li] = acc0[r] + acc1[r];  // D: col li, row 4*lk+r
   if (do_cs) csum[tid >> 4][tid & 15] = cs;
@@ -747,7 +619,6 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
       else if (!(e_mask > 0.f)) v = 0.f;
       if (p.adam) v += p.wd * a_in.p;
       p.C[(int64_t)gi * p.ldc + gj] = v;
-      if (p.head) hv[ei][ej] = v;
       if (p.adam) {
         adam_apply(ad, a_idx, v, a_in, lr_t);
         gsq = v * v;
@@ -765,13 +636,6 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
       }
     }
   }
-  if (p.head) {  // the tile holds all 2A head outputs of its 16 rows: 8 lanes per row, one per action
-    __syncthreads();
-    if (tid < 128) {
-      const int hr = tid >> 3;
-      head_fwd_elem(g.hd, p.head - 1, i0 + hr, tid & 7, &hv[hr][0], &hv[hr][g.hd.A], i0 + hr < p.M);
-    }
-  }
   if (ad.norm_part) {  // per-block squared-gradient partial (grad-norm logs; summed by sac_logs_kernel)
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) gsq += __shfl_xor(gsq, off);
@@ -786,6 +650,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
       np[1] = off >= ad.n_pi && off < ad.n_pi + ad.n_q ? b : 0.f;
     }
   }
+  stamp(g.st, 4);
 }
 
 
@@ -921,108 +786,6 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
   }
 }
 
-// ---- both hidden layers of up to MAXP MLPs (operand mode ta == 2 only), one 16 x 64 output block per
-// 256-thread workgroup: the block recomputes its rows' 16 x K layer-1 slab ONCE for four 16-wide column
-// tiles (the 16x16-tile kernel recomputes it per tile, 16x per row block at H = 256: more MFMA work than
-// layer 2 itself), and each wave owns one column tile over the whole K (no cross-wave reduction), its
-// W2 panel staged wave-privately in LDS.  Epilogue: bias + relu (the mlp12 problems of the SAC forward).
-constexpr int WCOLS = 64;
-static __global__ __launch_bounds__(256, 1) void mlp12_wide_kernel(const GemmGroup g) {
-  __shared__ __attribute__((aligned(16))) float As[GKC * 16];      // layer-1 slab, [k][r ^ psw(k)]
-  __shared__ __attribute__((aligned(16))) float Bw[4][GKC * 16];   // wave w's 16-column W2 panel, [k][c]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int pi = 0;
-  while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
-  const GemmProb& p = g.p[pi];
-  const int t = blockIdx.x - g.prefix[pi];
-  const int tn_cnt = ceil_div(p.N, WCOLS);
-  const int tm = t / tn_cnt, tn = t % tn_cnt;
-  const int i0 = tm * 16, jw = tn * WCOLS + w * 16;
-  // 1. this wave's W2 panel (B(k, j) = B[k ldb + j], K <= 256 rows x 16 columns): lane l loads rows
-  //    l / 4 + 16 i, columns 4 (l % 4) .. + 3 -- issued first, consumed after the slab
-  const auto dbw = rsrc(p.B, (int64_t)(p.K - 1) * p.ldb + p.N);
-  f32x4 bp[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int k = (lane >> 2) + 16 * i, col = jw + 4 * (lane & 3);
-    bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                          dbw, ((k < p.K && col < p.N) ? k * p.ldb + col : -4) * 4, 0, 0));
-  }
-  // 2. the layer-1 slab D(k, r) = relu(W1^T X^T + b1) (as stage_mlp1; the bias rides as input column K1)
-  {
-    const int r = lane & 15, q = lane >> 4;
-    const int k1 = p.a_ldm, ns = (k1 + 4) >> 2, sb = k1 >> 2;
-    const auto dx = rsrc(p.A, (int64_t)(p.M - 1) * p.lda + k1);
-    const auto dw = rsrc(p.a_u, (int64_t)k1 * p.K);
-    const auto db = rsrc(p.a_v, p.K);
-    float xb[8], wa[4][8], bv[4];
-    const int row = i0 + r;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int j = 4 * s + q;
-      const float v = bload(dx, row * p.lda + j);
-      xb[s] = (j < k1 && row < p.M) ? v : (j == k1 ? 1.f : 0.f);
-    }
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      const int k = w * 64 + kt * 16 + r;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int j = 4 * s + q;
-        const float v = bload(dw, j * p.K + k);
-        wa[kt][s] = (j < k1 && k < p.K) ? v : 0.f;
-      }
-      bv[kt] = bload(db, k);
-    }
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int s = 0; s < 8; ++s)
-        if (s == sb && q == (k1 & 3)) wa[kt][s] = bv[kt];
-    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-      if (s < ns)
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) acc[kt] = mfma4(wa[kt][s], xb[s], acc[kt]);
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const int kl = w * 64 + kt * 16 + 4 * q + tt;
-        As[kl * 16 + (r ^ psw(kl))] = (row < p.M && kl < p.K) ? fmaxf(acc[kt][tt], 0.f) : 0.f;
-      }
-  }
-  // 3. the W2 panel into this wave's LDS (contiguous 1 KB per instruction: conflict-free)
-  float* B = Bw[w];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) *reinterpret_cast<f32x4*>(B + ((lane >> 2) + 16 * i) * 16 + 4 * (lane & 3)) = bp[i];
-  __syncthreads();
-  if (tn == 0 && p.a_m && tid < p.K) {  // first-layer slab for the backward pass (coalesced in k)
-    float* h1 = const_cast<float*>(p.a_m);
-#pragma unroll 4
-    for (int r = 0; r < 16; ++r)
-      if (i0 + r < p.M) h1[(int64_t)(i0 + r) * p.K + tid] = As[tid * 16 + (r ^ psw(tid))];
-  }
-  // 4. layer 2: the wave's 16 x 16 tile over the whole K (64 k-steps, four accumulators)
-  const int li = lane & 15, lk = lane >> 4;
-  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-#pragma unroll 16
-  for (int s = 0; s < GKC / 4; ++s) {
-    const int k = 4 * s + lk;
-    acc[s & 3] = mfma4(As[k * 16 + (li ^ psw(k))], B[k * 16 + li], acc[s & 3]);
-  }
-  // 5. bias + relu, D: column li, rows 4 lk + r
-  const int col = jw + li;
-  const float bias = p.bias ? p.bias[min(col, p.N - 1)] : 0.f;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = i0 + 4 * lk + r;
-    if (row < p.M && col < p.N)
-      p.C[(int64_t)row * p.ldc + col] = fmaxf(acc[0][r] + acc[1][r] + acc[2][r] + acc[3][r] + bias, 0.f);
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
 static inline GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C,
                    int ldc) {
@@ -1032,7 +795,7 @@ static inline GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, 
 }
 
 // Tile policy: 16x16 (gemm_group_kernel).  MOPO_GEMM_TILE=32 selects gemm32_group_kernel for launches
-// whose problems are all >= 32 x 32 (no head epilogue).  Measured on MI355X: 32x32 tiles are slower
+// whose problems are all >= 32 x 32.  Measured on MI355X: 32x32 tiles are slower
 // for both users (SAC step 115.7 vs 99.8 us, BNN.train 6.09k vs 6.51k steps/s): these launches are
 // latency-bound and the 16x16 tiles split K over four waves (16-deep MFMA chains instead of 64).
 static inline int gemm_tile_override() {
@@ -1043,53 +806,25 @@ static inline int gemm_tile_override() {
   return v;
 }
 
-// MOPO_MLP12_WIDE=0 runs the SAC forward's layer-1-recompute groups on the 16x16-tile kernel instead
-static inline bool wide_mlp12() {
-  static const bool v = [] {
-    const char* e = std::getenv("MOPO_MLP12_WIDE");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return v;
-}
-
 static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const AdamCtx* ad = nullptr, int* slot = nullptr,
-                               const HeadCtx* hd = nullptr, const LossTail* tail = nullptr,
-                               const PolicyRows* pr = nullptr, const GatherArgs* ga = nullptr) {
+                               const PolicyRows* pr = nullptr, const GatherArgs* ga = nullptr,
+                               const Stamps* st = nullptr, int* zero = nullptr, int nzero = 0) {
   GemmGroup g{};
+  if (st) g.st = *st;
+  if (nzero > 256) return fail("gemm group: at most 256 words to zero");
+  g.zero = zero; g.nzero = zero ? nzero : 0;
   g.n = (int)ps.size();
   if (g.n > MAXP) return fail("gemm group too large");
-  bool big = true, head = false;
+  bool big = true;
   for (int i = 0; i < g.n; ++i) {
     const GemmProb& q = ps[i];
     const int c = operand_modes(q);
-    if (!(c == 0 || c == 1 || c == 3 || c == 4 || c == 6 || c == 9 || c == 16)) return fail("unsupported gemm operand modes");
-    if (c == 16 && (q.a_ldm < 1 || q.a_ldm > 31 || !q.a_u || !q.a_v)) return fail("gemm layer-1 recompute: 1 <= K1 <= 31");
+    if (!(c == 0 || c == 1 || c == 3 || c == 4 || c == 6 || c == 9)) return fail("unsupported gemm operand modes");
     if ((int64_t)q.M * q.K >= (1ll << 29) || (int64_t)q.N * q.K >= (1ll << 29)) return fail("gemm operand too large");
-    if (q.head && (!hd || q.N > 16 || q.N != 2 * hd->A)) return fail("bad head problem");
-    big = big && q.M >= 32 && q.N >= 32 && c != 16;
-    head = head || q.head;
-  }
-  // groups of layer-1-recompute problems only (the SAC forward) run on mlp12_wide_kernel
-  bool wide = !tail && !pr && !ga && !ad && !hd && wide_mlp12();
-  for (int i = 0; i < g.n && wide; ++i) {
-    const GemmProb& q = ps[i];
-    wide = operand_modes(q) == 16 && q.K <= GKC && q.N % 4 == 0 && q.act == ACT_RELU && !q.mask && !q.colsum &&
-           !q.adam && !q.head && !q.Z && q.mask_kind == MASK_RELU;  // N % 4: whole-quad W2 panel loads
-  }
-  if (wide) {
-    int tot = 0;
-    for (int i = 0; i < g.n; ++i) {
-      g.p[i] = ps[i];
-      g.prefix[i] = tot;
-      tot += ceil_div(ps[i].M, 16) * ceil_div(ps[i].N, WCOLS);
-    }
-    g.prefix[g.n] = tot;
-    hipLaunchKernelGGL(mlp12_wide_kernel, dim3(tot), dim3(256), 0, s, g);
-    MOPO_HIP(hipGetLastError());
-    return 0;
+    big = big && q.M >= 32 && q.N >= 32;
   }
   const int ov = gemm_tile_override();
-  const int TW = (ov == 32 && big && !head) ? 32 : 16;
+  const int TW = (ov == 32 && big) ? 32 : 16;
   int tot = 0;
   for (int i = 0; i < g.n; ++i) {
     g.p[i] = ps[i];
@@ -1102,12 +837,7 @@ static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const Ad
     g.ad.slot0 = slot ? *slot : 0;
     if (slot) *slot += tot;
   }
-  if (hd) g.hd = *hd;
-  if (tail) {
-    if (TW != 16 || !ad || tail->nparts > 64) return fail("gemm group: bad loss tail");
-    g.tail = *tail;
-  }
-  int extra = tail ? 1 : 0;
+  int extra = 0;
   if (pr) {
     if (TW != 16 || pr->A > 8 || pr->H % 16 || pr->H > 256 || 16 * (pr->H + 4) > PR_LDS)
       return fail("gemm group: bad policy rows (A <= 8, H <= 256, H % 16 == 0)");

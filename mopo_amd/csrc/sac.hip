@@ -5,18 +5,18 @@
 // Semantics: every forward and gradient uses the pre-step parameters; then pi, q1, q2
 // and alpha are updated by their own Adam (identical step counts -> one shared lr_t); then Polyak.
 //
-// Structure: 5 launches per step on one stream, captured into hipGraphs of 8 / 2 / 1 steps (no host
-// work per step).  Everything up to the critics' first-layer gradients is row-local, so it runs in
-// three row-block launches (sac_rows.h) that hand each other per-column-block partial dot products
-// instead of full rows: F1 the hidden layers of pi(s), pi(s'), Q1/Q2(s,a) + partial output layers;
-// F2 the policy head (from F1's partials) feeding the hidden layers of Q1/Q2(s,pi) and the target
-// critics + partial output layers; B1 each row's TD target and dq (from the partials), the critics'
-// dh1, the action-gradient partials for the policy, and the batch loss tail.  Then 2 grouped-GEMM
-// launches (gemm_group.h): the critics' weight gradients together with the policy's row-local backward
-// chain (head backward -> dh2p -> dh1p, extra blocks), and the policy's weight gradients (+ the next
-// step's batch gather).  The four TF1 Adams and Polyak run in the weight-gradient GEMM epilogues,
-// reading parameters Pb[p] and writing Pb[1 - p], so every gradient of the step sees pre-step
-// parameters.
+// Structure: 4 launches per step on one stream, captured into hipGraphs of 8 / 2 / 1 steps (no host
+// work per step).  Everything up to the activation gradients is row-local, so it runs in three
+// row-block launches (sac_rows.h) that hand each other per-column-block partial dot products instead
+// of full rows: F1 the hidden layers of pi(s), pi(s'), Q1/Q2(s,a) + partial output layers; F2 the
+// policy head (from F1's partials) feeding the hidden layers of Q1/Q2(s,pi) and the target critics +
+// partial output layers; B1 each row's TD target and dq (from the partials), the critics' dh1, the
+// action-gradient partials of Q1/Q2(s,pi), the batch loss tail, and -- handed those partials inside
+// the launch through per-row-block counters -- the policy's row-local backward chain (head backward
+// -> dh2p -> dh1p).  Then ONE grouped-GEMM launch (gemm_group.h) computes every weight gradient with
+// its TF1 Adam (+ Polyak for the critics) fused into the epilogue, reading parameters Pb[p] and
+// writing Pb[1 - p] (every gradient of the step sees pre-step parameters), and gathers the next
+// step's batch.
 #include <vector>
 #include <cstring>
 
@@ -72,6 +72,7 @@ struct Sac {
   float *opart[8];                // [ncq][n][OPW] output-layer partials of the 8 instances (sac_rows.h)
   float *dapart[2];               // [ncq][n][OPW] action-gradient partials of Q1 / Q2 at (s, pi(s))
   uint64_t* stamps = nullptr;     // MOPO_SAC_STAMPS builds: [slot][block][8]
+  int* rb_ready = nullptr;        // [ceil(n / 16)] B1's in-launch hand-off counters (zeroed by B2)
   float *dhead, *dh2p, *dh1p;
   // graph
   bool use_graph = true;
@@ -244,16 +245,23 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     L.logp_s = h->logp_s; L.logp_n = h->logp_n; L.head_s = h->out[0]; L.rew = bt.rew; L.term = bt.term;
     L.log_alpha = P + o.total; L.gamma = h->gamma; L.rscale = h->rscale;
     d.ad = ad; d.tent = h->tent; d.lr = h->lr; d.logs = h->logs; d.beta_pow = h->beta_pow; d.iter = h->iter;
+    PolicyRows& pr = d.pr;
+    pr.n = n; pr.O = O; pr.A = A; pr.H = H; pr.ncq = ncq;
+    pr.dapart[0] = h->dapart[0]; pr.dapart[1] = h->dapart[1];
+    pr.head_s = h->out[0]; pr.eps_s = h->eps_s; pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
+    pr.h2p = h->h2[0]; pr.h1p = h->h1[0]; pr.W2p = P + o.pW2;
+    pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p;
+    d.rb_ready = h->rb_ready;
     d.st = Stamps{h->stamps, 2};
-    hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq, nrb, 5), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq, nrb, 6), dim3(256), 0, s, d);
     MOPO_HIP(hipGetLastError());
   }
+  // ---- B2: every weight gradient with its fused TF1 Adam (+ Polyak for the critics), the next step's
+  //      batch gather (with `prefetch`; the step counter was advanced by this step's loss tail), and
+  //      the zeroing of the next step's hand-off counters
   {
-    // dW2 / dW3 only need the rank-1 dh2 (not dh1), so they ride with the smaller second launch; the
-    // extra policy-row blocks run the policy's row-local backward chain (dx over the actions through
-    // Q1/Q2(s, pi), the head backward, dh2p, dh1p: gemm_group.h policy_rows_block)
     std::vector<GemmProb> g;
-    for (int qi = 0; qi < 2; ++qi) {  // dW2 = h1^T dh2 (+db2), dW3 = h2^T dq (+db3)
+    for (int qi = 0; qi < 2; ++qi) {  // critics: dW2 = h1^T dh2 (+db2), dW3 = h2^T dq (+db3)
       auto w2 = mk(H, H, n, h->h1[2 + qi], H, 1, nullptr, H, 0, G + o.q[qi][2], H); w2.colsum = G + o.q[qi][3];
       w2.adam = 1;
       w2.b_u = h->dq[qi]; w2.b_v = Wq(qi, 4); w2.b_m = h->h2[2 + qi]; w2.b_ldm = H;
@@ -262,23 +270,12 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       w3.adam = 1;
       g.push_back(w3);
     }
-    for (int qi = 0; qi < 2; ++qi) {  // dW1 = [s,a]^T dh1 (+db1)
+    for (int qi = 0; qi < 2; ++qi) {  // critics: dW1 = [s,a]^T dh1 (+db1)
       auto w1 = mk(W, H, n, bt.sa, W, 1, h->dh1[qi], H, 0, G + o.q[qi][0], H); w1.colsum = G + o.q[qi][1];
       w1.adam = 1;
       g.push_back(w1);
     }
-    PolicyRows pr{};
-    pr.n = n; pr.O = O; pr.A = A; pr.H = H; pr.ncq = ncq;
-    pr.dapart[0] = h->dapart[0]; pr.dapart[1] = h->dapart[1];
-    pr.head_s = h->out[0]; pr.eps_s = h->eps_s; pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
-    pr.h2p = h->h2[0]; pr.h1p = h->h1[0]; pr.W2p = P + o.pW2;
-    pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p;
-    if (launch_group(g, s, &ad, &slot, nullptr, nullptr, &pr)) return -1;
-  }
-  {
-    // the policy's weight gradients (+ Adam); with `prefetch`, extra blocks gather the next step's
-    // batch into the other buffer (the step counter was advanced by this step's loss tail)
-    std::vector<GemmProb> g;
+    // the policy (dh2p, dh1p, dhead from the policy-row blocks of B1)
     auto w2 = mk(H, H, n, h->h1[0], H, 1, h->dh2p, H, 0, G + o.pW2, H); w2.colsum = G + o.pb2; w2.adam = 1; g.push_back(w2);
     auto wm = mk(H, A, n, h->h2[0], H, 1, h->dhead, 2 * A, 0, G + o.pWm, A); wm.colsum = G + o.pbm; wm.adam = 1;
     g.push_back(wm);
@@ -286,18 +283,19 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     g.push_back(wl);
     auto w1 = mk(O, H, n, bt.sa, W, 1, h->dh1p, H, 0, G + o.pW1, H); w1.colsum = G + o.pb1; w1.adam = 1; g.push_back(w1);
     const GatherArgs ga = gather_args(h, 1 - par, env, mod, seed, nullptr);
-    if (launch_group(g, s, &ad, &slot, nullptr, nullptr, nullptr, prefetch ? &ga : nullptr)) return -1;
+    const Stamps st{h->stamps, 3};
+    if (launch_group(g, s, &ad, &slot, nullptr, prefetch ? &ga : nullptr, &st, h->rb_ready, nrb)) return -1;
   }
   if (slot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
-  h->nslots = slot;  // blocks of the four backward launches (tile choice: launch_group)
+  h->nslots = slot;  // tiles of the weight-gradient launch (tile choice: launch_group)
   return 0;
 }
 
-// the GEMM tiles of the three backward launches (16x16 tiles; one grad-norm slot each)
+// the GEMM tiles of the weight-gradient launch (16x16 tiles; one grad-norm slot each)
 static int count_slots(const SacDims& d) {
   auto t = [](int M, int N) { return ceil_div(M, 16) * ceil_div(N, 16); };
-  const int n = d.n, H = d.H, O = d.O, A = d.A, W = O + A;
-  return 4 * t(n, H) + 2 * t(H, H) + 2 * t(H, 1) + 2 * t(W, H) + t(H, H) + 2 * t(H, A) + t(O, H);
+  const int H = d.H, O = d.O, A = d.A, W = O + A;
+  return 2 * t(H, H) + 2 * t(H, 1) + 2 * t(W, H) + t(H, H) + 2 * t(H, A) + t(O, H);
 }
 
 }  // namespace mopo
@@ -326,8 +324,9 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   const size_t npart = (size_t)ceil_div(H, RB_COLS) * n * OPW;
   for (int i = 0; i < 8; ++i) f(&h->opart[i], npart);
   for (int i = 0; i < 2; ++i) f(&h->dapart[i], npart);
+  reg.push_back({(void**)&h->rb_ready, (size_t)ceil_div(batch, 16) * 4});
 #if MOPO_SAC_STAMPS
-  reg.push_back({(void**)&h->stamps, (size_t)3 * 1024 * 8 * 8});
+  reg.push_back({(void**)&h->stamps, (size_t)4 * 1024 * 8 * 8});
 #endif
   f(&h->P, tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->T, tot);
   f(&h->beta_pow, 3); f(&h->logs, LOG_N);
@@ -513,7 +512,7 @@ extern "C" int mopo_sac_debug_stamps(mopo_sac_t hh, uint64_t* h_out, int64_t n) 
   Sac* h = reinterpret_cast<Sac*>(hh);
   MOPO_REQUIRE(h && h_out, "mopo_sac_debug_stamps: NULL argument");
   if (!h->stamps) return fail("mopo_sac_debug_stamps: library built without MOPO_SAC_STAMPS");
-  MOPO_REQUIRE(n >= 0 && n <= 3 * 1024 * 8, "mopo_sac_debug_stamps: n exceeds the stamp buffer");
+  MOPO_REQUIRE(n >= 0 && n <= 4 * 1024 * 8, "mopo_sac_debug_stamps: n exceeds the stamp buffer");
   MOPO_HIP(hipDeviceSynchronize());
   MOPO_HIP(hipMemcpy(h_out, h->stamps, n * 8, hipMemcpyDeviceToHost));
   return 0;

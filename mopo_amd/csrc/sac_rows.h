@@ -14,7 +14,9 @@
 //       prologue forming each row's dq from the critics' partials (the TD target y, mopo.py:380-404;
 //       the min-Q selection, :367-377); the (s, pi) instances emit partials of d(-min Q)/d action
 //       (dh1 W1[O:]^T) for the policy backward; one extra block reduces the batch losses (logs,
-//       alpha Adam, lr_t, beta powers, step counter: mopo.py:403-443)
+//       alpha Adam, lr_t, beta powers, step counter: mopo.py:403-443); the policy's row-local
+//       backward chain runs in the same launch, each row block's 4 workgroups starting as soon as the
+//       8 workgroups that produce its action-gradient partials have published them
 //
 // Replaces the previous 4-launch chain (forward hidden layers / output layers + head / (s, pi) hidden
 // layers / losses + critic output layers) + the critic dh1 launch: 5 -> 3 launches.
@@ -24,27 +26,6 @@
 namespace mopo {
 
 constexpr int RB_COLS = 64;  // second-layer columns per workgroup (4 waves x 16); OPW: gemm_group.h
-
-#ifndef MOPO_SAC_STAMPS
-#define MOPO_SAC_STAMPS 0    // 1: diagnostic build, per-workgroup phase timestamps (s_memrealtime)
-#endif
-
-// per-workgroup phase stamps of the diagnostic build: [launch slot][block][8] u64
-struct Stamps { uint64_t* p; int slot; };
-static __device__ __forceinline__ void stamp(const Stamps& s, int i) {
-#if MOPO_SAC_STAMPS
-  // wave 0 (a wave-uniform branch: a lane-divergent one here moved the workgroup ids into VGPRs and
-  // de-uniformised the whole kernel); its lanes all store the same value
-  if (s.p && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
-    uint64_t t = __builtin_amdgcn_s_memrealtime();
-    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    uint64_t* q = s.p + ((int64_t)s.slot * 1024 + b) * 8;
-    __hip_atomic_store(q + i, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-#else
-  (void)s; (void)i;
-#endif
-}
 
 struct FwdInst {
   const float* x; int ldx; int kx;   // layer-1 inputs from memory: columns [0, kx) of x[n][ldx]
@@ -143,11 +124,51 @@ static __device__ __forceinline__ T pick4(const T (&in)[4], int i) {
   return p;
 }
 
-// LDS of the row-block kernels (floats)
-constexpr int RB_LDS_A = GKC * 16;        // the 16 x K A slab, [k][r ^ psw(k)]
-constexpr int RB_LDS_B = 4 * GKC * 16;    // four wave-private 16-column B panels, [k][c]
-constexpr int RB_LDS_T = 16 * RB_COLS;    // the block's 16 x 64 output tile
-constexpr int RB_LDS_W = RB_COLS * OPW;   // output-layer columns of the block's 64 rows, [c][j]
+// LDS of the row-block kernels (floats).  Operand panels are row-major with the contraction index
+// fastest and a 4-float pad per row: lane (li, lk) of the 16x16x4 MFMA contributes k = 64 lk + 4 s + u
+// at step (s, u) (any assignment of the K range to the four lane groups sums the same products), so
+// one ds_read_b128 feeds four MFMAs, and the 16 lanes of each b128 read group hit distinct bank quads
+// (row stride 260 = 65 quads: quad index li + s mod 16).
+constexpr int RB_LD = GKC + 4;            // the A slab [16 rows][K] and each B panel [16 cols][K]
+constexpr int RB_LDS_A = 16 * RB_LD;
+constexpr int RB_LDS_B = 4 * 16 * RB_LD;  // four wave-private 16-column B panels
+constexpr int RB_TLD = RB_COLS + 4;       // the block's 16 x 64 output tile [row][c], the output-layer
+constexpr int RB_LDS_T = 16 * RB_TLD;     //   columns [j][c] (j < 16) of the block's 64 rows
+
+// the wave's 16 x 16 tile over the whole K: D(r, c) = sum_k A[r][k] B[c][k] (A = As, B = the wave's panel)
+static __device__ __forceinline__ void rows_contract(const float* As, const float* B, int li, int lk, f32x4 (&acc)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = zero4();
+#pragma unroll
+  for (int s = 0; s < GKC / 16; ++s) {
+    const f32x4 a4 = ld4(As + li * RB_LD + 64 * lk + 4 * s), b4 = ld4(B + li * RB_LD + 64 * lk + 4 * s);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = mfma4(a4[u], b4[u], acc[u]);
+  }
+}
+
+// wave 0: partial output dots of the block's tile, Out[r][j] = sum_{c < 64} T[r][c] WT[j][c] (16 MFMAs);
+// rows r < n and j < nout are stored to part[row][OPW]
+template <bool SC1 = false>
+static __device__ __forceinline__ void rows_partial_out(const float* T, const float* WT, int li, int lk, int i0, int n,
+                                                        int nout, float* part) {
+  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+  for (int s = 0; s < RB_COLS / 16; ++s) {
+    const f32x4 a4 = ld4(T + li * RB_TLD + 16 * lk + 4 * s), b4 = ld4(WT + li * RB_TLD + 16 * lk + 4 * s);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = mfma4(a4[u], b4[u], acc[u]);
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {                          // D: column li = output j, row 4 lk + rr
+    const int orow = i0 + 4 * lk + rr;
+    if (li < nout && orow < n) {
+      const float v = acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr];
+      if constexpr (SC1) __hip_atomic_store(part + (int64_t)orow * OPW + li, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else part[(int64_t)orow * OPW + li] = v;
+    }
+  }
+}
 
 // Grid (column block, row block, instance): linear block id cq + ncq (rb + nrb ii).  H <= GKC, H % 16 == 0.
 template <bool HEAD>
@@ -155,7 +176,7 @@ static __global__ __launch_bounds__(256, 1) void sac_fwd_kernel(const FwdArgsR a
   __shared__ __attribute__((aligned(16))) float As[RB_LDS_A];
   __shared__ __attribute__((aligned(16))) float Bw[RB_LDS_B];
   __shared__ __attribute__((aligned(16))) float Ts[RB_LDS_T];
-  __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_W];
+  __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_T];
   __shared__ float act_s[16][8];
   stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -244,35 +265,37 @@ static __global__ __launch_bounds__(256, 1) void sac_fwd_kernel(const FwdArgsR a
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) acc[kt] = mfma4(wa[kt][s], xb[s], acc[kt]);
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int kt = 0; kt < 4; ++kt) {  // rows r, k = w 64 + kt 16 + 4 q4 .. + 3: one b128 store
+      const int kl = w * 64 + kt * 16 + 4 * q4;
+      f32x4 v;
 #pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const int kl = w * 64 + kt * 16 + 4 * q4 + tt;
-        As[kl * 16 + (r ^ psw(kl))] = (row < n && kl < H) ? fmaxf(acc[kt][tt], 0.f) : 0.f;
-      }
+      for (int tt = 0; tt < 4; ++tt) v[tt] = (row < n && kl + tt < H) ? fmaxf(acc[kt][tt], 0.f) : 0.f;
+      *reinterpret_cast<f32x4*>(As + r * RB_LD + kl) = v;
+    }
   }
-  float* B = Bw + w * GKC * 16;
+  float* B = Bw + w * 16 * RB_LD;   // B[c][k] = W2[k][jw + c]: the quad of 4 columns at row k, transposed
 #pragma unroll
-  for (int i = 0; i < 16; ++i) *reinterpret_cast<f32x4*>(B + ((lane >> 2) + 16 * i) * 16 + 4 * (lane & 3)) = bp[i];
+  for (int i = 0; i < 16; ++i) {
+    const int k = (lane >> 2) + 16 * i, c4 = 4 * (lane & 3);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) Wo[tid + 256 * q] = wov[q];
+    for (int e = 0; e < 4; ++e) B[(c4 + e) * RB_LD + k] = bp[i][e];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {     // Wo[j][c]: element e = c * 16 + j of the loads
+    const int e = tid + 256 * q;
+    Wo[(e & 15) * RB_TLD + (e >> 4)] = wov[q];
+  }
   __syncthreads();
   stamp(a.st, 2);
   if (cq == 0 && p.h1 && tid < H) {  // the first-layer slab for the backward pass (coalesced in k)
 #pragma unroll 4
     for (int rr = 0; rr < 16; ++rr)
-      if (i0 + rr < n) p.h1[(int64_t)(i0 + rr) * H + tid] = As[tid * 16 + (rr ^ psw(tid))];
+      if (i0 + rr < n) p.h1[(int64_t)(i0 + rr) * H + tid] = As[rr * RB_LD + tid];
   }
   // ---- 4. layer 2: the wave's 16 x 16 tile over the whole K
   const int li = lane & 15, lk = lane >> 4;
-  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-  if (jw < H) {
-#pragma unroll 16
-    for (int s = 0; s < GKC / 4; ++s) {
-      const int k = 4 * s + lk;
-      acc[s & 3] = mfma4(As[k * 16 + (li ^ psw(k))], B[k * 16 + li], acc[s & 3]);
-    }
-  }
+  f32x4 acc[4];
+  rows_contract(As, B, li, lk, acc);
   stamp(a.st, 3);
   // ---- 5. bias + relu (D: column li, rows 4 lk + rr); h2 store; the tile into LDS
   const int col = jw + li;
@@ -281,22 +304,11 @@ static __global__ __launch_bounds__(256, 1) void sac_fwd_kernel(const FwdArgsR a
     const int orow = i0 + 4 * lk + rr;
     const float v = (col < H && orow < n) ? fmaxf(acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr] + b2v, 0.f) : 0.f;
     if (p.h2 && orow < n && col < H) p.h2[(int64_t)orow * H + col] = v;
-    Ts[(4 * lk + rr) * RB_COLS + w * 16 + li] = v;
+    Ts[(4 * lk + rr) * RB_TLD + w * 16 + li] = v;
   }
   __syncthreads();
-  // ---- 6. partial output dots: thread (row tid / 16, output j = tid % 16) over the block's 64 columns
-  {
-    const int orr = tid >> 4, j = tid & 15, orow = i0 + orr;
-    if (j < p.nout && orow < n) {
-      float s0 = 0.f, s1 = 0.f;
-#pragma unroll 8
-      for (int c = 0; c < RB_COLS; c += 2) {
-        s0 += Ts[orr * RB_COLS + c] * Wo[c * OPW + j];
-        s1 += Ts[orr * RB_COLS + c + 1] * Wo[(c + 1) * OPW + j];
-      }
-      p.opart[((int64_t)cq * n + orow) * OPW + j] = s0 + s1;
-    }
-  }
+  // ---- 6. partial output dots of the block's 64 columns (wave 0, MFMA)
+  if (w == 0) rows_partial_out(Ts, Wo, li, lk, i0, n, p.nout, p.opart + (int64_t)cq * n * OPW);
   stamp(a.st, 4);
 }
 
@@ -353,8 +365,15 @@ struct Dh1Args {
   AdamCtx ad;
   float tent, lr;
   float* logs; float* beta_pow; int64_t* iter;
+  // the policy's row-local backward chain (gemm_group.h policy_rows_block) as blocks z = ninst + 1 of
+  // this launch: block (cq, rb) waits until the 2 ncq (s, pi) workgroups of row block rb published
+  // their action-gradient partials (agent-scope counter rb_ready[rb], zeroed by the step's last launch)
+  PolicyRows pr;
+  int* rb_ready;
   Stamps st;
 };
+
+constexpr int PR_SPIN_LIMIT = 1 << 22;   // ~ 0.2 s of polling: a hang guard, never reached in a sane launch
 
 // the extra block: per-row loss terms of all n rows (thread t: rows t, t + 256, ...), block sums in a
 // fixed order (deterministic), then thread 0 applies the batch-level updates (loss_tail_block's tail)
@@ -405,24 +424,46 @@ static __device__ __forceinline__ void loss_tail_rows(const Dh1Args& a, float* s
   adam_apply(ad, ad.total, ga, al, lr_t);
 }
 
-// Grid (column block, row block, instance + 1); instance ninst, block (0, 0): the loss tail.
+// Grid (column block, row block, 2 + ninst): z = 0, block (0, 0): the loss tail; z = 1 .. ninst: the
+// instances; z = ninst + 1: the policy-row blocks (they wait on the (s, pi) instances' partials).
 static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a) {
   __shared__ __attribute__((aligned(16))) float As[RB_LDS_A];
   __shared__ __attribute__((aligned(16))) float Bw[RB_LDS_B];
   __shared__ __attribute__((aligned(16))) float Ts[RB_LDS_T];
-  __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_W];
+  __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_T];
   __shared__ float dqs[16];
   stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // grid (ncq, nrb, ninst + 1): SGPR indices (see sac_fwd_kernel); z = ninst is the loss tail (block 0)
-  const int ii = blockIdx.z, rb = blockIdx.y, cq = blockIdx.x;
-  if (ii >= a.ninst) {
-    if (rb == 0 && cq == 0) {
+  // grid (ncq, nrb, ninst + 1): SGPR indices (see sac_fwd_kernel); z = 0 holds the loss tail (block
+  // (0, 0, 0), dispatched first: its ~6 us chain runs beside the tiles instead of after them -- as the
+  // last block it waited for a free CU and ended the launch ~5 us late), the instances are z = 1 ..
+  if (blockIdx.z == 0) {
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
       loss_tail_rows(a, Ts);
       stamp(a.st, 4);
     }
     return;
   }
+  if ((int)blockIdx.z > a.ninst) {    // the policy-row blocks (dispatched last)
+    const int rb = blockIdx.y, cq = blockIdx.x;
+    const int need = 2 * a.ncq;
+    bool late = false;
+    auto wait = [&] {
+      if (threadIdx.x == 0) {
+        int spins = 0;
+        while (__hip_atomic_load(a.rb_ready + rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > PR_SPIN_LIMIT) { late = true; break; }
+        }
+      }
+      __syncthreads();
+    };
+    policy_rows_block<true>(a.pr, rb * a.ncq + cq, Bw, Ts, wait);
+    if (late) a.logs[LOG_PI_LOSS] = __builtin_nanf("");   // hand-off timed out: poison the logs loudly
+    stamp(a.st, 4);
+    return;
+  }
+  const int ii = blockIdx.z - 1, rb = blockIdx.y, cq = blockIdx.x;
   const Dh1Inst p = pick4(a.in, ii);
   const int n = a.n, H = a.H, A = a.A;
   const int i0 = rb * 16, c0 = cq * RB_COLS, jw = c0 + w * 16;
@@ -479,34 +520,28 @@ static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a)
   }
   __syncthreads();
   stamp(a.st, 1);
-  // ---- 3. A slab dh2 = dq (x) W3 * (h2 > 0) and the W2^T panel into LDS
+  // ---- 3. A slab dh2 = dq (x) W3 * (h2 > 0) and the W2^T panel into LDS (both b128 stores)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const float u = dqs[ar + q];
+    f32x4 v;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = am + e;
-      As[m * 16 + ((ar + q) ^ psw(m))] = (m < H && h2v[q][e] > 0.f) ? u * w3v[e] : 0.f;
-    }
+    for (int e = 0; e < 4; ++e) v[e] = (am + e < H && h2v[q][e] > 0.f) ? u * w3v[e] : 0.f;
+    *reinterpret_cast<f32x4*>(As + (ar + q) * RB_LD + am) = v;
   }
-  float* B = Bw + w * GKC * 16;
+  float* B = Bw + w * 16 * RB_LD;   // B[c][m] = W2[jw + c][m]
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
+  for (int i = 0; i < 16; ++i) *reinterpret_cast<f32x4*>(B + li * RB_LD + 4 * (lk + 4 * i)) = bp[i];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) B[(4 * (lk + 4 * i) + e) * 16 + li] = bp[i][e];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) Wo[tid + 256 * q] = wov[q];
+  for (int q = 0; q < 4; ++q) {     // Wo[j][c]: element e = c * 16 + j of the loads
+    const int e = tid + 256 * q;
+    Wo[(e & 15) * RB_TLD + (e >> 4)] = wov[q];
+  }
   __syncthreads();
   stamp(a.st, 2);
   // ---- 4. dh1 tile of the wave: 16 rows x 16 columns over the whole K
-  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-  if (jw < H) {
-#pragma unroll 16
-    for (int s = 0; s < GKC / 4; ++s) {
-      const int k = 4 * s + lk;
-      acc[s & 3] = mfma4(As[k * 16 + (li ^ psw(k))], B[k * 16 + li], acc[s & 3]);
-    }
-  }
+  f32x4 acc[4];
+  rows_contract(As, B, li, lk, acc);
   stamp(a.st, 3);
   // ---- 5. relu mask from h1; store; the (s, pi) instances' action-gradient partials
   const int col = jw + li;
@@ -515,19 +550,16 @@ static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a)
     const int orow = i0 + 4 * lk + rr;
     const float v = (col < H && orow < n && m1[rr] > 0.f) ? acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr] : 0.f;
     if (p.dh1 && orow < n && col < H) p.dh1[(int64_t)orow * H + col] = v;
-    Ts[(4 * lk + rr) * RB_COLS + w * 16 + li] = v;
+    Ts[(4 * lk + rr) * RB_TLD + w * 16 + li] = v;
   }
   if (p.w1a) {
     __syncthreads();
-    const int orr = tid >> 4, j = tid & 15, orow = i0 + orr;
-    if (j < A && orow < n) {
-      float s0 = 0.f, s1 = 0.f;
-#pragma unroll 8
-      for (int c = 0; c < RB_COLS; c += 2) {
-        s0 += Ts[orr * RB_COLS + c] * Wo[c * OPW + j];
-        s1 += Ts[orr * RB_COLS + c + 1] * Wo[(c + 1) * OPW + j];
-      }
-      p.dapart[((int64_t)cq * n + orow) * OPW + j] = s0 + s1;
+    if (w == 0) {
+      // the policy-row blocks of this launch read these partials: agent-scope (sc1) stores, the wave's
+      // vmcnt(0), then one lane's agent-scope counter add (MI355X_MICROARCH.md hand-off, row 1)
+      rows_partial_out<true>(Ts, Wo, li, lk, i0, n, A, p.dapart + (int64_t)cq * n * OPW);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(a.rb_ready + rb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   stamp(a.st, 4);

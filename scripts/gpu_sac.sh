@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_sac.py tests/test_gpu_ref.py tests/test_gpu_mopo.py -q -x -p no:cacheprovider --timeout 200 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/sac_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_sac.py tests/test_gpu_ref.py tests/test_gpu_mopo.py tests/test_gpu_train.py -q -x -p no:cacheprovider --timeout 200 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/sac_tests.log 2>&1
 rc=$?
 tail -15 gpurun_out/sac_tests.log
 [ $rc -ne 0 ] && exit $rc

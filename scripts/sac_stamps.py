@@ -31,13 +31,30 @@ def main():
     for rep in range(3):
         sac._do_training(rep * steps, pools[0], pools[1], n_steps=steps, seed=5)
         torch.cuda.synchronize()
-    buf = np.zeros(3 * 1024 * 8, np.uint64)
+    buf = np.zeros(4 * 1024 * 8, np.uint64)
     L.check(L.lib().mopo_sac_debug_stamps(sac._h, buf.ctypes.data, buf.size))
-    st = buf.reshape(3, 1024, 8).astype(np.int64)
-    nblk = [256, 256, 256]   # B1's block 256 is the loss tail (stamps 0 and 4 only)
+    st = buf.reshape(4, 1024, 8).astype(np.int64)
+    nblk = [256, 256, 256]
     t_first = min(int(st[k, :nblk[k], 0].min()) for k in range(3))
+    for k in (3,):            # the grouped-GEMM launch: blocks with a stamp (gather blocks: 0 and 4 only)
+        nb = int((st[k, :, 0] > 0).sum())
+        s = st[k, :nb]
+        t0 = s[:, 0].min()
+        us = lambda x: x * 0.01
+        name = 'B2 every weight gradient + Adam + gather'
+        print('%s: %d blocks, launch span %.2f us (first start at +%.2f us); start spread p50 %.2f max %.2f' % (
+            name, nb, us(s[:, 4].max() - t0), us(t0 - t_first), us(np.median(s[:, 0] - t0)), us((s[:, 0] - t0).max())))
+        pr = s[:, 1] == 0
+        if pr.any():
+            d = us(s[pr, 4] - s[pr, 0])
+            print('   gather blocks (%d): p50 %.2f max %.2f us' % (pr.sum(), np.median(d), d.max()))
+        g = ~pr
+        for i, (a_, b_, ph) in enumerate(((0, 1, 'operands to LDS'), (1, 2, 'MFMA'), (2, 4, 'epilogue (+Adam)'))):
+            d = us(s[g, b_] - s[g, a_])
+            print('   %-18s p50 %5.2f  p90 %5.2f  max %5.2f us' % (ph, np.median(d), np.quantile(d, 0.9), d.max()))
     for k, name in enumerate(('F1 fwd (pi, Q(s,a))', 'F2 fwd (head + Q(s,pi), targets)', 'B1 dh1 + dq + loss tail')):
-        s = st[k, :nblk[k], :5]
+        off = 64 if k == 2 else 0   # B1: z = 0 (64 blocks) holds the loss tail (block 0: stamps 0 and 4)
+        s = st[k, off:off + nblk[k], :5]
         us = lambda x: x * 0.01   # 100 MHz ticks -> us
         t0 = s[:, 0].min()
         print('%s: launch span %.2f us (first start at +%.2f us); start spread p50 %.2f max %.2f' % (
@@ -46,7 +63,11 @@ def main():
             d = us(s[:, i + 1] - s[:, i])
             print('   %-18s p50 %5.2f  p90 %5.2f  max %5.2f us' % (ph, np.median(d), np.quantile(d, 0.9), d.max()))
         if k == 2:
-            print('   loss-tail block: %.2f us' % us(st[2, 256, 4] - st[2, 256, 0]))
+            print('   loss-tail block: start +%.2f us, %.2f us long' % (us(st[2, 0, 0] - t0), us(st[2, 0, 4] - st[2, 0, 0])))
+            prb = st[2, 320:384, :5]          # the policy-row blocks (z = 5): stamps 0 and 4
+            print('   policy-row blocks: start +%.2f..+%.2f us, end +%.2f..+%.2f us (launch end +%.2f)' % (
+                us(prb[:, 0].min() - t0), us(prb[:, 0].max() - t0), us(prb[:, 4].min() - t0), us(prb[:, 4].max() - t0),
+                us(max(prb[:, 4].max(), s[:, 4].max(), st[2, 0, 4]) - t0)))
 
 
 if __name__ == '__main__':

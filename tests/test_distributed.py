@@ -78,3 +78,42 @@ def test_allgather_global_order_world2():
     # both ranks hold identical pools
     for k in res[0][1]:
         np.testing.assert_array_equal(res[0][1][k], res[1][1][k])
+
+
+def _rng_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from mopo_amd.distributed import broadcast_metrics, broadcast_numpy_rng
+    np.random.seed(100 + rank)                  # the ranks' global streams differ ...
+    if rank == 0:                               # ... and only rank 0 runs the model-training phase
+        np.random.permutation(1000)
+        np.random.normal(size=3)                # leaves a cached gaussian (has_gauss = 1)
+    broadcast_numpy_rng()
+    m = broadcast_metrics({'val_loss': 0.25, 'epochs': 7.0} if rank == 0 else None)
+    q.put((rank, np.random.normal(size=5), np.random.randint(0, 1 << 30, 4), m))
+    dist.destroy_process_group()
+
+
+def test_numpy_stream_and_metrics_follow_rank0_world2():
+    """MOPO.train on several ranks trains the ensemble on rank 0 only (mopo_amd/mopo.py); rank 0's numpy
+    legacy stream (MT19937 key, position, cached gaussian) and training metrics are then broadcast, so
+    every rank continues exactly where a single process would."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rng_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in [q.get(timeout=60) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+    np.random.seed(100)
+    np.random.permutation(1000)
+    np.random.normal(size=3)
+    ref = (np.random.normal(size=5), np.random.randint(0, 1 << 30, 4))
+    for r in range(world):
+        np.testing.assert_array_equal(res[r][0], ref[0])
+        np.testing.assert_array_equal(res[r][1], ref[1])
+        assert res[r][2] == {'val_loss': 0.25, 'epochs': 7.0}
