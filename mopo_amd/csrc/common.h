@@ -36,6 +36,16 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
+// Workgroup barrier that orders LDS only: __syncthreads() is a workgroup-scope fence on every address
+// space, which makes each wave wait (s_waitcnt vmcnt(0)) for its own outstanding global loads and
+// STORES before the s_barrier -- a write-back's full latency on the critical path wherever a barrier
+// follows global stores.  Use this one where the barrier publishes LDS data only.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
 // ------------------------------------------------------------------ activations (TF1 f32 semantics)

@@ -178,23 +178,25 @@ struct PolicyRows {
   float* dhead; float* dh2p; float* dh1p;
 };
 
-constexpr int PR_COLS = 64;          // dh1p columns per policy-row block (one 16-wide tile per wave)
+constexpr int PR_COLS = 64;          // dh1p columns per 4-wave policy-row block (one 16-wide tile per wave)
 constexpr int PR_LDS = 2 * 256 * 16; // floats the grouped kernel's panel LDS offers it (H <= 508)
 
 // Latency layout: every global operand of the chain is loaded in ONE burst of unconditional
 // (range-checked) loads at the start -- the action-gradient partials and head inputs, Wm / Wl / h2p at
 // this thread's dh2p column, this wave's W2p operands of the dh1p tile and the h1p mask -- so the
 // block pays one memory latency, then computes.
-// S: >= 16 (H + 4) floats of LDS (PR_LDS); hs: >= 3 * 128 floats.
-// H % 16 == 0, H <= 256 (one dh2p column per thread), A <= 8.
+// S: >= 16 (H + 4) floats of LDS (PR_LDS); hs: >= 3 * 128 floats.  Blocks of 4 or 8 waves (64 or 128
+// dh1p columns).  H % 16 == 0, H <= 256 (one dh2p column per thread), A <= 8.
 // WAIT: called after every other operand of the chain is in flight, before the action-gradient
 // partials are loaded; SC1: load them with agent-scope (sc1) loads -- the partials were written by
 // other workgroups of the SAME launch (the in-launch hand-off of sac_dh1_kernel).
 template <bool SC1 = false, typename Wait>
-static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs, Wait wait) {
+static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs, Wait wait,
+                                                         const Stamps& st = Stamps{nullptr, 0}) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int H = c.H, A = c.A, HS = H + 4, n = c.n;
-  const int ncq = (H + PR_COLS - 1) / PR_COLS;
+  const int pcols = 16 * (int)(blockDim.x >> 6);   // dh1p columns of the block: one 16-wide tile per wave
+  const int ncq = (H + pcols - 1) / pcols;
   const int rb = x / ncq, cq = x % ncq, r0 = rb * 16;
   const int li = lane & 15, lk = lane >> 4;
   // ---- the burst: head inputs, Wm / Wl / h2p at this thread's dh2p column, this wave's W2p operands of
@@ -216,7 +218,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) h2v[i] = bload(dh2, hc < H ? (r0 + i) * H + hc : -1);  // rows >= n: past the extent
-  const int j0 = cq * PR_COLS + w * 16, col = j0 + li;
+  const int j0 = cq * pcols + w * 16, col = j0 + li;
   const bool tile_on = j0 < H;
   const auto dw2 = rsrc(c.W2p, (int64_t)H * H);
   const int boff = (tile_on ? col : 0) * H;
@@ -231,6 +233,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
 #pragma unroll
   for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
   wait();
+  stamp(st, 1);
   float dap[2][MAX_NCQ];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -279,7 +282,8 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
     dmu_s[tid] = dmu;
     dls_s[tid] = dls;
   }
-  __syncthreads();
+  lds_barrier();
+  stamp(st, 2);
   // ---- dh2p of the 16 rows at this thread's column -> LDS rows of stride HS
   if (hc < H) {
 #pragma unroll
@@ -294,7 +298,8 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
       if (cq == 0 && r0 + i < n) c.dh2p[(int64_t)(r0 + i) * H + hc] = v;
     }
   }
-  __syncthreads();
+  lds_barrier();
+  stamp(st, 3);
   // ---- dh1p tile = dh2p W2p^T * (h1p > 0): rows r0.., columns j0.. (wave w)
   if (!tile_on) return;
   f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
@@ -578,7 +583,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
     // branch) so that all 32+ loads are unconditional and issue back to back -- one memory latency
     // per chunk instead of one per element.
     stage_dispatch<16>(p, i0, j0, kc, kn, t, &As[0][0], &Bs[0][0]);
-    __syncthreads();
+    lds_barrier();
     stamp(g.st, 1);
     // the staged panels are zero-padded to GKC rows, so every wave runs exactly 16 k-steps of its
     // quarter with no guards: all 32 LDS reads first, then 16 MFMAs on two accumulators
@@ -597,13 +602,13 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
     }
     if (do_cs)
       for (int k = tid >> 4; k < kn; k += 16) cs += Bs[k][(tid & 15) ^ psw(k)];
-    __syncthreads();
+    lds_barrier();
   }
   stamp(g.st, 2);
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[w][(lk * 4 + r) * 16 + li] = acc0[r] + acc1[r];  // D: col li, row 4*lk+r
   if (do_cs) csum[tid >> 4][tid & 15] = cs;
-  __syncthreads();
+  lds_barrier();
   float gsq = 0.f;
   {
     float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
@@ -639,9 +644,9 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
   if (ad.norm_part) {  // per-block squared-gradient partial (grad-norm logs; summed by sac_logs_kernel)
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) gsq += __shfl_xor(gsq, off);
-    __syncthreads();
+    lds_barrier();
     if (lane == 0) part[0][w] = gsq;
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) {
       const float b = part[0][0] + part[0][1] + part[0][2] + part[0][3];
       const int64_t off = p.adam ? (int64_t)(p.C - ad.G) : -1;

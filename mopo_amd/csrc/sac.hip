@@ -229,7 +229,8 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   //      gradient partials of the (s, pi) instances, and the batch loss tail (one extra block)
   {
     Dh1Args d{};
-    d.ninst = 4; d.n = n; d.H = H; d.A = A; d.ncq = ncq; d.nrb = nrb;
+    const int ncq1 = ceil_div(H, B1_COLS);
+    d.ninst = 4; d.n = n; d.H = H; d.A = A; d.ncq = ncq; d.ncq1 = ncq1; d.nrb = nrb;
     for (int i = 0; i < 4; ++i) {
       const int qi = i & 1;
       Dh1Inst& q = d.in[i];
@@ -246,14 +247,14 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     L.log_alpha = P + o.total; L.gamma = h->gamma; L.rscale = h->rscale;
     d.ad = ad; d.tent = h->tent; d.lr = h->lr; d.logs = h->logs; d.beta_pow = h->beta_pow; d.iter = h->iter;
     PolicyRows& pr = d.pr;
-    pr.n = n; pr.O = O; pr.A = A; pr.H = H; pr.ncq = ncq;
+    pr.n = n; pr.O = O; pr.A = A; pr.H = H; pr.ncq = ncq1;
     pr.dapart[0] = h->dapart[0]; pr.dapart[1] = h->dapart[1];
     pr.head_s = h->out[0]; pr.eps_s = h->eps_s; pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
     pr.h2p = h->h2[0]; pr.h1p = h->h1[0]; pr.W2p = P + o.pW2;
     pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p;
     d.rb_ready = h->rb_ready;
     d.st = Stamps{h->stamps, 2};
-    hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq, nrb, 6), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq1, nrb, 6), dim3(B1_WAVES * 64), 0, s, d);
     MOPO_HIP(hipGetLastError());
   }
   // ---- B2: every weight gradient with its fused TF1 Adam (+ Polyak for the critics), the next step's

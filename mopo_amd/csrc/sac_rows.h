@@ -124,38 +124,42 @@ static __device__ __forceinline__ T pick4(const T (&in)[4], int i) {
   return p;
 }
 
-// LDS of the row-block kernels (floats).  Operand panels are row-major with the contraction index
-// fastest and a 4-float pad per row: lane (li, lk) of the 16x16x4 MFMA contributes k = 64 lk + 4 s + u
-// at step (s, u) (any assignment of the K range to the four lane groups sums the same products), so
-// one ds_read_b128 feeds four MFMAs, and the 16 lanes of each b128 read group hit distinct bank quads
-// (row stride 260 = 65 quads: quad index li + s mod 16).
-constexpr int RB_LD = GKC + 4;            // the A slab [16 rows][K] and each B panel [16 cols][K]
+// LDS of the row-block kernels (floats).  The A slab is row-major with the contraction index fastest
+// and a 4-float pad per row: lane (li, lk) of the 16x16x4 MFMA contributes k = 64 lk + 4 s + u at step
+// (s, u) (any assignment of the K range to the four lane groups sums the same products), so one
+// ds_read_b128 feeds four MFMAs, and the 16 lanes of each b128 read group hit distinct bank quads (row
+// stride 260 = 65 quads: quad index li + s mod 16).  The B operand (the wave's own 16 weight columns)
+// never touches LDS: each lane loads its 64 values for those k straight into registers, so the kernels
+// need 26 KB of LDS and run two workgroups per CU.
+constexpr int RB_LD = GKC + 4;            // the A slab [16 rows][K]
 constexpr int RB_LDS_A = 16 * RB_LD;
-constexpr int RB_LDS_B = 4 * 16 * RB_LD;  // four wave-private 16-column B panels
 constexpr int RB_TLD = RB_COLS + 4;       // the block's 16 x 64 output tile [row][c], the output-layer
 constexpr int RB_LDS_T = 16 * RB_TLD;     //   columns [j][c] (j < 16) of the block's 64 rows
 
-// the wave's 16 x 16 tile over the whole K: D(r, c) = sum_k A[r][k] B[c][k] (A = As, B = the wave's panel)
-static __device__ __forceinline__ void rows_contract(const float* As, const float* B, int li, int lk, f32x4 (&acc)[4]) {
+// the wave's 16 x 16 tile over the whole K: D(r, c) = sum_k A[r][k] B(k, c), with lane (li, lk) holding
+// B(64 lk + 4 s + u, c = li) in b[s][u]
+static __device__ __forceinline__ void rows_contract(const float* As, const f32x4 (&b)[16], int li, int lk,
+                                                     f32x4 (&acc)[4]) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) acc[u] = zero4();
 #pragma unroll
   for (int s = 0; s < GKC / 16; ++s) {
-    const f32x4 a4 = ld4(As + li * RB_LD + 64 * lk + 4 * s), b4 = ld4(B + li * RB_LD + 64 * lk + 4 * s);
+    const f32x4 a4 = ld4(As + li * RB_LD + 64 * lk + 4 * s);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = mfma4(a4[u], b4[u], acc[u]);
+    for (int u = 0; u < 4; ++u) acc[u] = mfma4(a4[u], b[s][u], acc[u]);
   }
 }
 
-// wave 0: partial output dots of the block's tile, Out[r][j] = sum_{c < 64} T[r][c] WT[j][c] (16 MFMAs);
-// rows r < n and j < nout are stored to part[row][OPW]
-template <bool SC1 = false>
+// wave 0: partial output dots of the block's tile, Out[r][j] = sum_{c < COLS} T[r][c] WT[j][c] (COLS / 4
+// MFMAs; row stride COLS + 4); rows r < n and j < nout are stored to part[row][OPW]
+template <int COLS, bool SC1 = false>
 static __device__ __forceinline__ void rows_partial_out(const float* T, const float* WT, int li, int lk, int i0, int n,
                                                         int nout, float* part) {
+  constexpr int LD = COLS + 4;
   f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
-  for (int s = 0; s < RB_COLS / 16; ++s) {
-    const f32x4 a4 = ld4(T + li * RB_TLD + 16 * lk + 4 * s), b4 = ld4(WT + li * RB_TLD + 16 * lk + 4 * s);
+  for (int s = 0; s < COLS / 16; ++s) {
+    const f32x4 a4 = ld4(T + li * LD + (COLS / 4) * lk + 4 * s), b4 = ld4(WT + li * LD + (COLS / 4) * lk + 4 * s);
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[u] = mfma4(a4[u], b4[u], acc[u]);
   }
@@ -172,9 +176,8 @@ static __device__ __forceinline__ void rows_partial_out(const float* T, const fl
 
 // Grid (column block, row block, instance): linear block id cq + ncq (rb + nrb ii).  H <= GKC, H % 16 == 0.
 template <bool HEAD>
-static __global__ __launch_bounds__(256, 1) void sac_fwd_kernel(const FwdArgsR a) {
+static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a) {
   __shared__ __attribute__((aligned(16))) float As[RB_LDS_A];
-  __shared__ __attribute__((aligned(16))) float Bw[RB_LDS_B];
   __shared__ __attribute__((aligned(16))) float Ts[RB_LDS_T];
   __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_T];
   __shared__ float act_s[16][8];
@@ -187,15 +190,21 @@ static __global__ __launch_bounds__(256, 1) void sac_fwd_kernel(const FwdArgsR a
   const FwdInst p = pick4(a.in, ii);
   const int n = a.n, H = a.H, A = a.A;
   const int i0 = rb * 16, c0 = cq * RB_COLS, jw = c0 + w * 16;
-  // ---- 1. every global operand, issued up front: this wave's W2 panel (rows k = lane / 4 + 16 i,
-  //         columns 4 (lane % 4) .. + 3), the output-layer columns of the block's 64 rows, layer 1
-  const auto dbw = rsrc(p.w2, (int64_t)(H - 1) * H + H);
+  // ---- 1. every global operand, issued up front: this wave's W2 operand straight into MFMA registers
+  //         (lane (li, lk): W2[64 lk + 4 s + u][jw + li]; 16 lanes read 64 contiguous bytes of a row),
+  //         the output-layer columns of the block's 64 rows, layer 1
+  const int li = lane & 15, lk = lane >> 4;
   f32x4 bp[16];
+  {
+    const auto dbw = rsrc(p.w2, (int64_t)H * H);
+    const bool con = jw + li < H;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int k = (lane >> 2) + 16 * i, col = jw + 4 * (lane & 3);
-    bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                          dbw, ((k < H && col < H) ? k * H + col : -4) * 4, 0, 0));
+    for (int s2 = 0; s2 < 16; ++s2)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = 64 * lk + 4 * s2 + u;
+        bp[s2][u] = bload(dbw, (con && k < H) ? k * H + jw + li : -1);
+      }
   }
   float wov[4];
   {
@@ -243,7 +252,7 @@ static __global__ __launch_bounds__(256, 1) void sac_fwd_kernel(const FwdArgsR a
       const bool store = cq == 0 && (ii == 0 || ii == 2);  // Q1(s,pi) / Qt1(s',pi') blocks publish the head
       act_s[hr][hj] = rows_head(a.hd, p.head, n, A, a.ncq, hrow, hj, hrow < n, store);
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int j = 4 * s + q4;
@@ -273,19 +282,12 @@ static __global__ __launch_bounds__(256, 1) void sac_fwd_kernel(const FwdArgsR a
       *reinterpret_cast<f32x4*>(As + r * RB_LD + kl) = v;
     }
   }
-  float* B = Bw + w * 16 * RB_LD;   // B[c][k] = W2[k][jw + c]: the quad of 4 columns at row k, transposed
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int k = (lane >> 2) + 16 * i, c4 = 4 * (lane & 3);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) B[(c4 + e) * RB_LD + k] = bp[i][e];
-  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {     // Wo[j][c]: element e = c * 16 + j of the loads
     const int e = tid + 256 * q;
     Wo[(e & 15) * RB_TLD + (e >> 4)] = wov[q];
   }
-  __syncthreads();
+  lds_barrier();
   stamp(a.st, 2);
   if (cq == 0 && p.h1 && tid < H) {  // the first-layer slab for the backward pass (coalesced in k)
 #pragma unroll 4
@@ -293,9 +295,8 @@ static __global__ __launch_bounds__(256, 1) void sac_fwd_kernel(const FwdArgsR a
       if (i0 + rr < n) p.h1[(int64_t)(i0 + rr) * H + tid] = As[rr * RB_LD + tid];
   }
   // ---- 4. layer 2: the wave's 16 x 16 tile over the whole K
-  const int li = lane & 15, lk = lane >> 4;
   f32x4 acc[4];
-  rows_contract(As, B, li, lk, acc);
+  rows_contract(As, bp, li, lk, acc);
   stamp(a.st, 3);
   // ---- 5. bias + relu (D: column li, rows 4 lk + rr); h2 store; the tile into LDS
   const int col = jw + li;
@@ -306,9 +307,9 @@ static __global__ __launch_bounds__(256, 1) void sac_fwd_kernel(const FwdArgsR a
     if (p.h2 && orow < n && col < H) p.h2[(int64_t)orow * H + col] = v;
     Ts[(4 * lk + rr) * RB_TLD + w * 16 + li] = v;
   }
-  __syncthreads();
+  lds_barrier();
   // ---- 6. partial output dots of the block's 64 columns (wave 0, MFMA)
-  if (w == 0) rows_partial_out(Ts, Wo, li, lk, i0, n, p.nout, p.opart + (int64_t)cq * n * OPW);
+  if (w == 0) rows_partial_out<RB_COLS>(Ts, Wo, li, lk, i0, n, p.nout, p.opart + (int64_t)cq * n * OPW);
   stamp(a.st, 4);
 }
 
@@ -354,11 +355,17 @@ struct Dh1Inst {
   float* dh1;                        // stored when non-NULL
   float* dq;                         // stored by the column-block-0 workgroups when non-NULL
   const float* w1a;                  // (s, pi) instances: W1[O:] = the action rows [A][H]; NULL otherwise
-  float* dapart;                     // [ncq][n][OPW]: partial dh1 W1[O:]^T of the block's 64 columns
+  float* dapart;                     // [ncq1][n][OPW]: partial dh1 W1[O:]^T of the block's 128 columns
 };
 
+constexpr int B1_WAVES = 8, B1_COLS = 16 * B1_WAVES;   // B1 workgroups: 16 rows x 128 columns
+constexpr int B1_TLD = B1_COLS + 4;
+
 struct Dh1Args {
-  int ninst, n, H, A, ncq, nrb;
+  int ninst, n, H, A;
+  int ncq;                           // column blocks of the forward partials (64 wide)
+  int ncq1;                          // B1's column blocks (128 wide): its action-gradient partials
+  int nrb;
   Dh1Inst in[4];
   LossRows L;
   // the loss tail (last block): batch means -> logs, the alpha gradient + Adam, lr_t, beta powers, step
@@ -366,7 +373,7 @@ struct Dh1Args {
   float tent, lr;
   float* logs; float* beta_pow; int64_t* iter;
   // the policy's row-local backward chain (gemm_group.h policy_rows_block) as blocks z = ninst + 1 of
-  // this launch: block (cq, rb) waits until the 2 ncq (s, pi) workgroups of row block rb published
+  // this launch: block (cq, rb) waits until the 2 ncq1 (s, pi) workgroups of row block rb published
   // their action-gradient partials (agent-scope counter rb_ready[rb], zeroed by the step's last launch)
   PolicyRows pr;
   int* rb_ready;
@@ -378,10 +385,18 @@ constexpr int PR_SPIN_LIMIT = 1 << 22;   // ~ 0.2 s of polling: a hang guard, ne
 // the extra block: per-row loss terms of all n rows (thread t: rows t, t + 256, ...), block sums in a
 // fixed order (deterministic), then thread 0 applies the batch-level updates (loss_tail_block's tail)
 static __device__ __forceinline__ void loss_tail_rows(const Dh1Args& a, float* sh) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   const int n = a.n, A = a.A;
+  // the alpha Adam state and the beta powers, fetched up front (thread 0; used after the reduction)
+  AdamIn al{0.f, 0.f, 0.f, 0.f};
+  float b1p = 0.f, b2p = 0.f;
+  if (tid == 0) {
+    al = adam_load(a.ad, a.ad.total);                                 // log_alpha = the last parameter
+    b1p = a.beta_pow[0];
+    b2p = a.beta_pow[1];
+  }
   float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int r = tid; r < n; r += 256) {
+  for (int r = tid; r < n; r += blockDim.x) {
     const RowQ o = row_losses(a.L, n, a.ncq, r);
     const float q1 = o.q[0], q2 = o.q[1], q1p = o.q[2], q2p = o.q[3];
     const float lps = a.L.logp_s[r];
@@ -400,12 +415,15 @@ static __device__ __forceinline__ void loss_tail_rows(const Dh1Args& a, float* s
   if (lane == 0)
 #pragma unroll
     for (int i = 0; i < 7; ++i) sh[w * 8 + i] = red[i];
-  __syncthreads();
+  lds_barrier();
   if (tid != 0) return;
 #pragma unroll
-  for (int i = 0; i < 7; ++i) red[i] = sh[i] + sh[8 + i] + sh[16 + i] + sh[24 + i];
+  for (int i = 0; i < 7; ++i) {                                       // wave partials in wave order
+    float t = 0.f;
+    for (int q = 0; q < nw; ++q) t += sh[8 * q + i];
+    red[i] = t;
+  }
   const AdamCtx& ad = a.ad;
-  const AdamIn al = adam_load(ad, ad.total);                          // log_alpha = the last parameter
   const float fn = (float)n;
   const float l1 = red[0] / fn * 0.5f, l2 = red[1] / fn * 0.5f;       // mopo.py:403-404
   const float m1 = red[2] / fn, m2 = red[3] / fn, mlp = red[4] / fn, ment = red[5] / fn;
@@ -415,7 +433,6 @@ static __device__ __forceinline__ void loss_tail_rows(const Dh1Args& a, float* s
   float* logs = a.logs;
   logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;
   logs[LOG_ALPHA] = expf(al.p); logs[LOG_ENTROPY] = ment; logs[LOG_LOGP] = mlp; logs[LOG_PI_LOSS] = pil;
-  const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
   const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);           // TF1 Adam step size
   a.beta_pow[2] = lr_t;
   a.beta_pow[0] = b1p * 0.9f;
@@ -426,17 +443,19 @@ static __device__ __forceinline__ void loss_tail_rows(const Dh1Args& a, float* s
 
 // Grid (column block, row block, 2 + ninst): z = 0, block (0, 0): the loss tail; z = 1 .. ninst: the
 // instances; z = ninst + 1: the policy-row blocks (they wait on the (s, pi) instances' partials).
-static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a) {
+// B1 runs 8-wave workgroups (16 rows x 128 columns), one per CU: the 1 + 4 x 32 + 32 busy workgroups
+// of a batch-256 step then all start at once on their own CUs -- the policy-row blocks prefetch their
+// operands beside the producers instead of queueing for a CU or sharing one with them.
+static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const Dh1Args a) {
   __shared__ __attribute__((aligned(16))) float As[RB_LDS_A];
-  __shared__ __attribute__((aligned(16))) float Bw[RB_LDS_B];
-  __shared__ __attribute__((aligned(16))) float Ts[RB_LDS_T];
-  __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_T];
+  __shared__ __attribute__((aligned(16))) float Ts[16 * B1_TLD];
+  __shared__ __attribute__((aligned(16))) float Wo[16 * B1_TLD];
   __shared__ float dqs[16];
   stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // grid (ncq, nrb, ninst + 1): SGPR indices (see sac_fwd_kernel); z = 0 holds the loss tail (block
-  // (0, 0, 0), dispatched first: its ~6 us chain runs beside the tiles instead of after them -- as the
-  // last block it waited for a free CU and ended the launch ~5 us late), the instances are z = 1 ..
+  // grid (ncq1, nrb, ninst + 2): SGPR indices (see sac_fwd_kernel); z = 0 holds the loss tail (block
+  // (0, 0, 0), dispatched first: its ~6 us chain runs beside the tiles instead of after them), the
+  // instances are z = 1 .. ninst, the policy-row blocks z = ninst + 1
   if (blockIdx.z == 0) {
     if (blockIdx.x == 0 && blockIdx.y == 0) {
       loss_tail_rows(a, Ts);
@@ -444,9 +463,9 @@ static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a)
     }
     return;
   }
-  if ((int)blockIdx.z > a.ninst) {    // the policy-row blocks (dispatched last)
+  if ((int)blockIdx.z > a.ninst) {    // the policy-row blocks
     const int rb = blockIdx.y, cq = blockIdx.x;
-    const int need = 2 * a.ncq;
+    const int need = 2 * a.ncq1;
     bool late = false;
     auto wait = [&] {
       if (threadIdx.x == 0) {
@@ -456,9 +475,9 @@ static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a)
           if (++spins > PR_SPIN_LIMIT) { late = true; break; }
         }
       }
-      __syncthreads();
+      __syncthreads();   // a full fence: the partials' agent-scope loads must not move above it
     };
-    policy_rows_block<true>(a.pr, rb * a.ncq + cq, Bw, Ts, wait);
+    policy_rows_block<true>(a.pr, rb * a.ncq1 + cq, As, Ts, wait, a.st);
     if (late) a.logs[LOG_PI_LOSS] = __builtin_nanf("");   // hand-off timed out: poison the logs loudly
     stamp(a.st, 4);
     return;
@@ -466,29 +485,30 @@ static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a)
   const int ii = blockIdx.z - 1, rb = blockIdx.y, cq = blockIdx.x;
   const Dh1Inst p = pick4(a.in, ii);
   const int n = a.n, H = a.H, A = a.A;
-  const int i0 = rb * 16, c0 = cq * RB_COLS, jw = c0 + w * 16;
+  const int i0 = rb * 16, c0 = cq * B1_COLS, jw = c0 + w * 16;
   const int li = lane & 15, lk = lane >> 4;
-  // ---- 1. operands up front: W2^T panel of this wave's 16 columns (B(m, c) = W2[c][m]: lane reads
-  //         W2 row c = jw + lane % 16 at m = 4 (lane / 16 + 4 i) .. + 3), the A slab's h2 rows and W3,
-  //         the h1 mask of this lane's outputs, W1[O:] columns of the block (the (s, pi) instances)
+  // ---- 1. operands up front: this wave's W2^T operand straight into MFMA registers (B(m, c) = W2[c][m]:
+  //         lane (li, lk) holds W2[jw + li][64 lk + 4 s .. + 3]), the A slab's h2 rows and W3 (waves
+  //         0-3), the h1 mask of this lane's outputs, W1[O:] columns of the block (the (s, pi) instances)
   const auto dw2 = rsrc(p.w2, (int64_t)H * H);
   f32x4 bp[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int m = 4 * (lk + 4 * i), c = jw + li;
+    const int m = 64 * lk + 4 * i, c = jw + li;
     bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                           dw2, ((m < H && c < H) ? c * H + m : -4) * 4, 0, 0));
   }
-  // A slab: thread (m-quad tid % 64, rows 4 (tid / 64) .. + 3)
-  const int am = 4 * (tid & 63), ar = 4 * w;
+  // A slab: thread (m-quad tid % 64, rows 4 (tid / 64) .. + 3), waves 0-3
+  const bool slab = w < 4;
+  const int am = 4 * (tid & 63), ar = 4 * (w & 3);
   const auto dh2 = rsrc(p.h2, (int64_t)n * H);
   f32x4 h2v[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     h2v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           dh2, ((am < H && i0 + ar + q < n) ? (i0 + ar + q) * H + am : -4) * 4, 0, 0));
+                                           dh2, ((slab && am < H && i0 + ar + q < n) ? (i0 + ar + q) * H + am : -4) * 4, 0, 0));
   const f32x4 w3v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  rsrc(p.w3, H), (am < H ? am : -4) * 4, 0, 0));
+                                                  rsrc(p.w3, H), ((slab && am < H) ? am : -4) * 4, 0, 0));
   float m1[4];
   {
     const auto dm1 = rsrc(p.h1, (int64_t)n * H);
@@ -499,8 +519,8 @@ static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a)
   if (p.w1a) {
     const auto d1 = rsrc(p.w1a, (int64_t)A * H);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {     // Wo[c][j] = W1[O + j][c0 + c]
-      const int e = tid + 256 * q, c = c0 + (e >> 4), j = e & 15;
+    for (int q = 0; q < 4; ++q) {     // Wo[c][j] = W1[O + j][c0 + c]: element e = c * 16 + j
+      const int e = tid + B1_WAVES * 64 * q, c = c0 + (e >> 4), j = e & 15;
       wov[q] = bload(d1, (c < H && j < A) ? j * H + c : -1);
     }
   }
@@ -518,30 +538,29 @@ static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a)
     }
     dqs[tid] = dq;
   }
-  __syncthreads();
+  lds_barrier();
   stamp(a.st, 1);
-  // ---- 3. A slab dh2 = dq (x) W3 * (h2 > 0) and the W2^T panel into LDS (both b128 stores)
+  // ---- 3. A slab dh2 = dq (x) W3 * (h2 > 0) into LDS (b128 stores; waves 0-3)
+  if (slab) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float u = dqs[ar + q];
-    f32x4 v;
+    for (int q = 0; q < 4; ++q) {
+      const float u = dqs[ar + q];
+      f32x4 v;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (am + e < H && h2v[q][e] > 0.f) ? u * w3v[e] : 0.f;
-    *reinterpret_cast<f32x4*>(As + (ar + q) * RB_LD + am) = v;
+      for (int e = 0; e < 4; ++e) v[e] = (am + e < H && h2v[q][e] > 0.f) ? u * w3v[e] : 0.f;
+      *reinterpret_cast<f32x4*>(As + (ar + q) * RB_LD + am) = v;
+    }
   }
-  float* B = Bw + w * 16 * RB_LD;   // B[c][m] = W2[jw + c][m]
 #pragma unroll
-  for (int i = 0; i < 16; ++i) *reinterpret_cast<f32x4*>(B + li * RB_LD + 4 * (lk + 4 * i)) = bp[i];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {     // Wo[j][c]: element e = c * 16 + j of the loads
-    const int e = tid + 256 * q;
-    Wo[(e & 15) * RB_TLD + (e >> 4)] = wov[q];
+  for (int q = 0; q < 4; ++q) {     // Wo[j][c]
+    const int e = tid + B1_WAVES * 64 * q;
+    Wo[(e & 15) * B1_TLD + (e >> 4)] = wov[q];
   }
-  __syncthreads();
+  lds_barrier();
   stamp(a.st, 2);
   // ---- 4. dh1 tile of the wave: 16 rows x 16 columns over the whole K
   f32x4 acc[4];
-  rows_contract(As, B, li, lk, acc);
+  rows_contract(As, bp, li, lk, acc);
   stamp(a.st, 3);
   // ---- 5. relu mask from h1; store; the (s, pi) instances' action-gradient partials
   const int col = jw + li;
@@ -550,14 +569,14 @@ static __global__ __launch_bounds__(256, 1) void sac_dh1_kernel(const Dh1Args a)
     const int orow = i0 + 4 * lk + rr;
     const float v = (col < H && orow < n && m1[rr] > 0.f) ? acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr] : 0.f;
     if (p.dh1 && orow < n && col < H) p.dh1[(int64_t)orow * H + col] = v;
-    Ts[(4 * lk + rr) * RB_TLD + w * 16 + li] = v;
+    Ts[(4 * lk + rr) * B1_TLD + w * 16 + li] = v;
   }
   if (p.w1a) {
-    __syncthreads();
+    lds_barrier();
     if (w == 0) {
       // the policy-row blocks of this launch read these partials: agent-scope (sc1) stores, the wave's
       // vmcnt(0), then one lane's agent-scope counter add (MI355X_MICROARCH.md hand-off, row 1)
-      rows_partial_out<true>(Ts, Wo, li, lk, i0, n, A, p.dapart + (int64_t)cq * n * OPW);
+      rows_partial_out<B1_COLS, true>(Ts, Wo, li, lk, i0, n, A, p.dapart + (int64_t)cq * n * OPW);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_fetch_add(a.rb_ready + rb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

@@ -34,7 +34,7 @@ def main():
     buf = np.zeros(4 * 1024 * 8, np.uint64)
     L.check(L.lib().mopo_sac_debug_stamps(sac._h, buf.ctypes.data, buf.size))
     st = buf.reshape(4, 1024, 8).astype(np.int64)
-    nblk = [256, 256, 256]
+    nblk = [256, 256, 128]
     t_first = min(int(st[k, :nblk[k], 0].min()) for k in range(3))
     for k in (3,):            # the grouped-GEMM launch: blocks with a stamp (gather blocks: 0 and 4 only)
         nb = int((st[k, :, 0] > 0).sum())
@@ -53,7 +53,7 @@ def main():
             d = us(s[g, b_] - s[g, a_])
             print('   %-18s p50 %5.2f  p90 %5.2f  max %5.2f us' % (ph, np.median(d), np.quantile(d, 0.9), d.max()))
     for k, name in enumerate(('F1 fwd (pi, Q(s,a))', 'F2 fwd (head + Q(s,pi), targets)', 'B1 dh1 + dq + loss tail')):
-        off = 64 if k == 2 else 0   # B1: z = 0 (64 blocks) holds the loss tail (block 0: stamps 0 and 4)
+        off = 32 if k == 2 else 0   # B1: z = 0 (32 blocks) holds the loss tail (block 0: stamps 0 and 4)
         s = st[k, off:off + nblk[k], :5]
         us = lambda x: x * 0.01   # 100 MHz ticks -> us
         t0 = s[:, 0].min()
@@ -64,10 +64,15 @@ def main():
             print('   %-18s p50 %5.2f  p90 %5.2f  max %5.2f us' % (ph, np.median(d), np.quantile(d, 0.9), d.max()))
         if k == 2:
             print('   loss-tail block: start +%.2f us, %.2f us long' % (us(st[2, 0, 0] - t0), us(st[2, 0, 4] - st[2, 0, 0])))
-            prb = st[2, 320:384, :5]          # the policy-row blocks (z = 5): stamps 0 and 4
+            prb = st[2, 160:192, :5]          # the policy-row blocks (z = 5)
             print('   policy-row blocks: start +%.2f..+%.2f us, end +%.2f..+%.2f us (launch end +%.2f)' % (
                 us(prb[:, 0].min() - t0), us(prb[:, 0].max() - t0), us(prb[:, 4].min() - t0), us(prb[:, 4].max() - t0),
                 us(max(prb[:, 4].max(), s[:, 4].max(), st[2, 0, 4]) - t0)))
+            for i, ph in enumerate(('flag seen at', 'head bwd done at', 'dh2p done at', 'end at')):
+                d = us(prb[:, i + 1] - t0)
+                print('      %-16s +%5.2f .. +%5.2f us (p50 +%5.2f)' % (ph, d.min(), d.max(), np.median(d)))
+            prod = st[2, 32 + 2 * 32:32 + 4 * 32, 4]   # the (s, pi) producer blocks (z = 3, 4): their end
+            print('   (s, pi) producers end +%.2f .. +%.2f us' % (us(prod.min() - t0), us(prod.max() - t0)))
 
 
 if __name__ == '__main__':
