@@ -586,6 +586,112 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
                            (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
 }
 
+// ---- f16x3 forward over R row blocks per wave (R = 2: 32 rows per wave, 128 per 4-wave workgroup, one
+// workgroup per CU with the accumulators in AGPRs): bnn_fwd_f16s_kernel's arithmetic, product for
+// product, with each LDS weight fragment feeding R row blocks (layer_f16_rows).
+#ifndef BNN_F16_R
+#define BNN_F16_R 1
+#endif
+#ifndef BNN_F16R_WAVES
+#define BNN_F16R_WAVES 4
+#endif
+template <int NB2, int NBO, int MODE, int WAVES, int R, int NBU = NB2>
+__global__ __launch_bounds__(WAVES * 64, 1) void bnn_fwd_f16r_kernel(const BnnDev w, const FwdArgs a) {
+  constexpr int KG = NB2 / 2;
+  constexpr bool KH = NBU < NB2;
+  constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
+  constexpr int SLOT = Stage<NBMAX, WAVES>::SLOTS * 256;
+  constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + BIAS_LDS];
+  float* lds_bias = lds + 2 * SLOT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
+  const int groups = ceil_div(a.ntiles, WAVES);  // ntiles: tiles of 16 R rows
+  const int C = ceil_div(groups, 8);             // XCD-aware order (bnn_fwd_f16s_kernel)
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int e = j / C, grp = xcd * C + j % C;
+  if (grp >= groups) return;
+  const int64_t row0 = (int64_t)(grp * WAVES + wv) * 16 * R + m;  // row block r: row0 + 16 r
+  if ((int64_t)grp * WAVES * 16 * R >= count) return;
+  const int IN = w.IN, E = w.E, O = w.O;
+  auto row_max = [&](float mx) {
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    return fmaxf(mx, __shfl_xor(mx, 32));
+  };
+  float xin[R][1][8], sc[R], inv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + 16 * r;
+    const bool ok = row < count;
+    if (a.xs) {
+      const f32x4 lo = ok ? ld4(a.xs + row * XS_STRIDE + 4 * g) : zero4();
+      const f32x4 hi = ok ? ld4(a.xs + row * XS_STRIDE + 16 + 4 * g) : zero4();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        xin[r][0][t] = lo[t];
+        xin[r][0][4 + t] = hi[t];
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int k = slot_feat(bf16_kperm(g, jj), IN);
+        float v = 0.f;
+        if (ok && k >= 0) {
+          float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
+                            : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
+          v = (raw - w.mu[k]) / w.sigma[k];
+        }
+        xin[r][0][jj] = v;
+      }
+    }
+    float mx = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) mx = fmaxf(mx, fabsf(xin[r][0][jj]));
+    row_scale(row_max(mx), sc[r], inv[r]);
+  }
+  const int64_t bs = w.BS;
+  f32x4 acc[R][NB2];
+  float hf[R][KG][8];
+  constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.6931471805599453f;
+  // bias + swish_log2 (bnn_fwd_f16s_kernel's to_input) of row block r, then its new row scale
+  auto to_input = [&](int r, const float* b, float f) {
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < KG; ++c) {
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(b + (2 * c) * 16 + 4 * g);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(b + (2 * c + 1) * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        hf[r][c][t] = swish_log2(fmaf(acc[r][2 * c][t], f, b0[t]));
+        hf[r][c][4 + t] = 2 * c + 1 < NBU ? swish_log2(fmaf(acc[r][2 * c + 1][t], f, b1[t])) : 0.f;
+        mx = fmaxf(mx, fmaxf(fabsf(hf[r][c][t]), fabsf(hf[r][c][4 + t])));
+      }
+    }
+    row_scale(row_max(mx), sc[r], inv[r]);
+  };
+  layer_f16_rows<1, NB2, R, WAVES, SLOT, NBU>(w.w0b + (int64_t)e * 2 * NB2 * 256, xin, acc, lds, wv, lane, sc,
+                                              w.b0 + e * bs, lds_bias);
+#pragma unroll
+  for (int r = 0; r < R; ++r) to_input(r, lds_bias, inv[r] * w.wscale[e] * kNegLog2e);
+  for (int l = 0; l < 3; ++l) {
+    layer_f16_rows<KG, NB2, R, WAVES, SLOT, NBU, KH>(w.whb + ((int64_t)l * E + e) * KG * 2 * NB2 * 256, hf, acc, lds, wv,
+                                                     lane, sc, w.bh + ((int64_t)l * E + e) * bs, lds_bias);
+#pragma unroll
+    for (int r = 0; r < R; ++r) to_input(r, lds_bias, inv[r] * w.wscale[(1 + l) * E + e]);
+  }
+  f32x4 hd[R][NBO];
+  layer_f16_rows<KG, NBO, R, WAVES, SLOT, NBO, KH>(w.whdb + (int64_t)e * KG * 2 * NBO * 256, hf, hd, lds, wv, lane, sc);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + 16 * r;
+    const float f = inv[r] * w.wscale[4 * E + e] * kNegLn2;
+#pragma unroll
+    for (int nb = 0; nb < NBO; ++nb) hd[r][nb] *= f;
+    head_epilogue<NBO, MODE>(w, a, hd[r], e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
+                             (MODE == FWD_ROLLOUT && a.sel && row < count) ? a.sel[row] : -1);
+  }
+}
+
 #ifndef BNN_R13
 #define BNN_R13 1  // row blocks per wave at H = 200
 #endif
@@ -657,8 +763,29 @@ static int launch_bf16_p(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   return 0;
 }
 
+template <int NB2, int NBO, int R>
+static int launch_f16r(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
+  constexpr int WV = BNN_F16R_WAVES;
+  a.ntiles = (int)ceil_div((int)a.B, 16 * R);
+  if (a.ntiles == 0) return 0;
+  dim3 grid(8 * ceil_div(ceil_div(a.ntiles, WV), 8) * h->E), block(64 * WV);
+  if (NB2 <= 16 && h->dev.NBH == NB2 - 1) {
+    if (mode == FWD_PREDICT)
+      hipLaunchKernelGGL((bnn_fwd_f16r_kernel<NB2, NBO, FWD_PREDICT, WV, R, NB2 - 1>), grid, block, 0, s, h->dev, a);
+    else
+      hipLaunchKernelGGL((bnn_fwd_f16r_kernel<NB2, NBO, FWD_ROLLOUT, WV, R, NB2 - 1>), grid, block, 0, s, h->dev, a);
+  } else if (mode == FWD_PREDICT) {
+    hipLaunchKernelGGL((bnn_fwd_f16r_kernel<NB2, NBO, FWD_PREDICT, WV, R>), grid, block, 0, s, h->dev, a);
+  } else {
+    hipLaunchKernelGGL((bnn_fwd_f16r_kernel<NB2, NBO, FWD_ROLLOUT, WV, R>), grid, block, 0, s, h->dev, a);
+  }
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
 template <int NB2, int NBO>
 static int launch_f16s(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
+  if constexpr (BNN_F16_R > 1 && NB2 <= 16) return launch_f16r<NB2, NBO, BNN_F16_R>(h, mode, a, s);
   constexpr int WV = BNN_SPLIT_WAVES, PS = BNN_SPLIT_PS == 0 ? 2 : BNN_SPLIT_PS;
   a.ntiles = (int)ceil_div((int)a.B, 16);
   if (a.ntiles == 0) return 0;

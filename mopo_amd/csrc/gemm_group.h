@@ -88,7 +88,9 @@ struct AdamCtx {
 // SAC log slots (sac.hip, mopo_sac_buffers)
 enum {
   LOG_Q1_LOSS = 0, LOG_Q2_LOSS, LOG_Q1, LOG_Q2, LOG_ALPHA, LOG_ENTROPY, LOG_LOGP, LOG_PI_GNORM, LOG_Q_GNORM,
-  LOG_PI_LOSS, LOG_PI_GSQ, LOG_Q_GSQ, LOG_N = 16
+  LOG_PI_LOSS, LOG_PI_GSQ, LOG_Q_GSQ,
+  LOG_HANDOFF,                       // sticky: 1 once an in-launch hand-off wait timed out (sac.py raises)
+  LOG_N = 16
 };
 
 // buffer descriptor over n floats at p (wave-uniform inputs only)
@@ -164,6 +166,7 @@ static __device__ __forceinline__ void gather_elem(const GatherArgs& g, int r, i
 // gradients of the next launch read with dh1p.
 constexpr int OPW = 16;              // floats per (column block, row) partial record (sac_rows.h)
 constexpr int MAX_NCQ = 4;           // column blocks of 64 (H <= 256)
+constexpr int DH2_TILES = 4;         // dh2p column tiles per wave (H <= 256 over >= 4 waves)
 
 struct PolicyRows {
   int nblk;                          // 0: none; ceil(n / 16) * ceil(H / 64)
@@ -208,16 +211,21 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   const float raw = bload(dh, hon ? hrow * 2 * A + A + hj : -1);
   const float ep = bload(de, hon ? hrow * A + hj : -1);
   const float la = *c.log_alpha;
-  const int hc = tid;
+  // dh2p tiles of this wave: 16 columns each, tiles w, w + nw, ... (at most DH2_TILES)
+  const int nw = (int)(blockDim.x >> 6), nt2 = (H + 15) >> 4;
   const auto dwm = rsrc(c.Wm, (int64_t)H * A), dwl = rsrc(c.Wl, (int64_t)H * A), dh2 = rsrc(c.h2p, (int64_t)n * H);
-  float wm[8], wl[8], h2v[16];
+  float wb[DH2_TILES][4], h2v[DH2_TILES][4];   // B(k, c) = k < 8 ? Wm[c][k] : Wl[c][k - 8]; lane k = 4 s + lk
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    wm[k] = bload(dwm, (k < A && hc < H) ? hc * A + k : -1);
-    wl[k] = bload(dwl, (k < A && hc < H) ? hc * A + k : -1);
+  for (int q = 0; q < DH2_TILES; ++q) {
+    const int c2 = (w + q * nw) * 16 + li;
+    const bool on = w + q * nw < nt2 && c2 < H;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int k = 4 * (s2 & 1) + lk;
+      wb[q][s2] = bload(s2 < 2 ? dwm : dwl, (on && k < A) ? c2 * A + k : -1);
+      h2v[q][s2] = bload(dh2, on ? (r0 + 4 * lk + s2) * H + c2 : -1);     // rows >= n: past the extent
+    }
   }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) h2v[i] = bload(dh2, hc < H ? (r0 + i) * H + hc : -1);  // rows >= n: past the extent
   const int j0 = cq * pcols + w * 16, col = j0 + li;
   const bool tile_on = j0 < H;
   const auto dw2 = rsrc(c.W2p, (int64_t)H * H);
@@ -284,18 +292,28 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   }
   lds_barrier();
   stamp(st, 2);
-  // ---- dh2p of the 16 rows at this thread's column -> LDS rows of stride HS
-  if (hc < H) {
+  // ---- dh2p = dhead [dWm; dWl]^T (K = 16: mu parts 0..7, log-std parts 8..15) masked by h2p > 0 ->
+  //      LDS rows of stride HS (and dh2p in HBM from the cq == 0 blocks)
+  {
+    float av[4];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const f32x4 u0 = *reinterpret_cast<const f32x4*>(dmu_s + i * 8), u1 = *reinterpret_cast<const f32x4*>(dmu_s + i * 8 + 4);
-      const f32x4 l0 = *reinterpret_cast<const f32x4*>(dls_s + i * 8), l1 = *reinterpret_cast<const f32x4*>(dls_s + i * 8 + 4);
-      float v = 0.f;
+    for (int s2 = 0; s2 < 4; ++s2) av[s2] = (s2 < 2 ? dmu_s : dls_s)[li * 8 + 4 * (s2 & 1) + lk];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v += u0[k] * wm[k] + u1[k] * wm[4 + k] + l0[k] * wl[k] + l1[k] * wl[4 + k];
-      v = h2v[i] > 0.f ? v : 0.f;
-      S[i * HS + hc] = v;
-      if (cq == 0 && r0 + i < n) c.dh2p[(int64_t)(r0 + i) * H + hc] = v;
+    for (int q = 0; q < DH2_TILES; ++q) {
+      if (w + q * nw >= nt2) break;
+      f32x4 d = zero4();
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) d = mfma4(av[s2], wb[q][s2], d);
+      const int c2 = (w + q * nw) * 16 + li;
+      if (c2 < H) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {                                // D: row 4 lk + i, col li
+          const int row = 4 * lk + i;
+          const float v = h2v[q][i] > 0.f ? d[i] : 0.f;
+          S[row * HS + c2] = v;
+          if (cq == 0 && r0 + row < n) c.dh2p[(int64_t)(r0 + row) * H + c2] = v;
+        }
+      }
     }
   }
   lds_barrier();

@@ -446,4 +446,58 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
   }
 }
 
+// layer_lds_split_f32's f16 form over R row blocks per wave: every weight fragment read from LDS feeds
+// the MFMAs of all R row blocks (R = 2 halves the LDS reads, the barriers and the staged bytes per row).
+// in[r]: row block r's f32 activations (scaled by sc[r] when split); parts made when a k-group is consumed.
+template <int KG, int NB, int R, int WAVES, int SLOT, int NBU = NB, bool KH = false>
+__device__ __forceinline__ void layer_f16_rows(const float* __restrict__ wf, const float (&in)[R][KG][8],
+                                               f32x4 (&acc)[R][NB], float* lds, int w, int lane, const float (&sc)[R],
+                                               const float* __restrict__ bias = nullptr, float* lds_bias = nullptr) {
+  constexpr int P = 2, S = KG * P;
+  static_assert(Stage<NB, WAVES>::SLOTS * 256 <= SLOT, "slice larger than its buffer");
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[r][nb] = zero4();
+  bf16x8 cur[R][P];
+  __syncthreads();
+  stage_slice<NB, WAVES>(wf, lds, w, lane);
+  if (bias) stage_bias<NB * 4, WAVES>(bias, lds_bias, w, lane);  // published by the first barrier below
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int kg = s / P, p = s % P;
+    if (p == 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        u32x4v h4, l4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const F16Pair pr = split_f16_pair(in[r][kg][2 * q], in[r][kg][2 * q + 1], sc[r]);
+          h4[q] = pr.hi;
+          l4[q] = pr.lo;
+        }
+        cur[r][0] = __builtin_bit_cast(bf16x8, h4);
+        cur[r][1] = __builtin_bit_cast(bf16x8, l4);
+      }
+    }
+    __syncthreads();
+    if (s + 1 < S) stage_slice<NB, WAVES>(wf + (s + 1) * NB * 256, lds + ((s + 1) & 1) * SLOT, w, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    const float* b = lds + (s & 1) * SLOT;
+    bf16x8 fr_next = *reinterpret_cast<const bf16x8*>(b + lane * 4);
+#pragma unroll
+    for (int nb = 0; nb < NBU; ++nb) {
+      const bf16x8 fr = fr_next;
+      if (nb + 1 < NBU) fr_next = *reinterpret_cast<const bf16x8*>(b + ((nb + 1) * 64 + lane) * 4);
+      // part 0 of W meets both activation parts, part 1 only the high part (the x1 w1 product is dropped)
+#pragma unroll
+      for (int q = P - 1 - p; q >= 0; --q)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          acc[r][nb] = (KH && kg + 1 == KG) ? mfma_16x16x16_lo<true>(fr, cur[r][q], acc[r][nb])
+                                            : mfma_16x16x32<true>(fr, cur[r][q], acc[r][nb]);
+    }
+  }
+}
+
 }  // namespace mopo

@@ -478,7 +478,7 @@ static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const 
       __syncthreads();   // a full fence: the partials' agent-scope loads must not move above it
     };
     policy_rows_block<true>(a.pr, rb * a.ncq1 + cq, As, Ts, wait, a.st);
-    if (late) a.logs[LOG_PI_LOSS] = __builtin_nanf("");   // hand-off timed out: poison the logs loudly
+    if (late) a.logs[LOG_HANDOFF] = 1.f;   // hand-off timed out: sac.py raises on the flag
     stamp(a.st, 4);
     return;
   }

@@ -17,7 +17,7 @@ cd /tmp
 i=0
 for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" "SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_$TAG/pmc$i" -o run -- python "$R/bench.py" $ARGS > "$R/gpurun_out/pmc_${TAG}_$i.log" 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_$TAG/pmc$i" -o run -- python "$R/bench.py" $ARGS > "$R/gpurun_out/pmc_${TAG}_$i.log" 2>&1
   rc=$?
   echo "$KEY pass $i ($C) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$R/gpurun_out/pmc_${TAG}_$i.log"; exit $rc; fi
