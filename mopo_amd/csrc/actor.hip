@@ -215,7 +215,11 @@ __device__ __forceinline__ void actor_finish(const ActorArgs& a, float (&head)[A
 #pragma unroll
         for (int i = 0; i < 4; ++i) zz[i] = blk * 4 + i < A ? a.eps[row * A + blk * 4 + i] : 0.f;
       } else {
+#ifndef ACT_KNOB_LITE_FINISH   // timing-only builds (scripts/build_variant_actor.sh): no noise draws
         actor_noise4(a.seed, a.step, uid, blk, zz);
+#else
+        zz[0] = zz[1] = zz[2] = zz[3] = 0.f;
+#endif
       }
       if (a.rand_act) {  // np.random.uniform(low=-1, high=1, size=act.shape) (mopo.py:738)
         if (a.act_uni) {
@@ -241,6 +245,9 @@ __device__ __forceinline__ void actor_finish(const ActorArgs& a, float (&head)[A
         }
       }
     }
+#ifdef ACT_KNOB_LITE_FINISH
+    pos = -1;
+#endif
     if (pos >= 0) {  // the observation half of the pool row (mopo.py:750), stored f32
       for (int k = 0; k < O; ++k)
         a.pool_obs[pos * O + k] = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
@@ -436,10 +443,17 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16_kernel(const Acto
   };
   layer_lds_split<1, NBP, ACT_WAVES, SLOT, P, PS, true>(w1f, x0, acc, lds, wv, lane);
   to_input(b1, inv_row * inv_w[0]);
+#ifndef ACT_KNOB_NOL2
   layer_lds_split_f32<KG, NBP, ACT_WAVES, SLOT, P, PS, true>(w2f, hf, acc, lds, wv, lane, s_in);
   to_input(b2, inv_row * inv_w[1]);
+#endif
   f32x4 hd[1];
+#ifndef ACT_KNOB_NOHEADL
   layer_lds_split_f32<KG, 1, ACT_WAVES, SLOT, P, PS, true>(whf, hf, hd, lds, wv, lane, s_in);
+#else
+  hd[0] = zero4();
+  for (int c = 0; c < KG; ++c) hd[0][0] += hf[c][0];
+#endif
   const float f = inv_row * inv_w[2];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -450,6 +464,95 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16_kernel(const Acto
   actor_finish(a, head, wv, m, g, row, ok);
 }
 
+// f16x3 policy forward over R row blocks per wave (layer_f16_rows): actor_f16_kernel's arithmetic,
+// product for product, with layer 2's first slice prefetched during layer 1's last one and the whole
+// head ([mu | log_std], 2 KG fragments) prefetched during layer 2's last slice, so no layer starts on
+// an exposed copy and the head runs behind ONE barrier instead of 2 KG.
+#ifndef ACT_F16_R
+#define ACT_F16_R 0  // 0: actor_f16_kernel; R >= 1: actor_f16r_kernel<R>
+#endif
+template <int NBP, int R>
+__global__ __launch_bounds__(ACT_WAVES * 64, R == 1 ? 2 : 1) void actor_f16r_kernel(const ActorArgs a) {
+  constexpr int KG = NBP / 2;
+  constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;   // also holds the head's 2 KG = NBP fragments
+  __shared__ float head[ACT_WAVES][16][25];
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
+  if ((int64_t)blockIdx.x * ACT_WAVES * 16 * R >= count) return;  // whole workgroup past the live rows
+  const int64_t row0 = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16 * R + m;   // row block r: row0 + 16 r
+  const int O = a.O;
+  const float* w1f = a.Wpk;
+  const float* w2f = w1f + 2 * NBP * 256;
+  const float* whf = w2f + KG * 2 * NBP * 256;
+  const float* b1 = whf + KG * 2 * 256;
+  const float* b2 = b1 + NBP * 16;
+  const float* bh = b2 + NBP * 16;
+  const float* inv_w = bh + 16;
+  auto row_max = [&](float mx) {
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    return fmaxf(mx, __shfl_xor(mx, 32));
+  };
+  float xin[R][1][8], sc[R], inv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + 16 * r;
+    const bool ok = row < count;
+    float mx = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = slot_feat(bf16_kperm(g, j), O);
+      float v = 0.f;
+      if (ok && k >= 0)
+        v = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
+                      : reinterpret_cast<const float*>(a.obs)[row * O + k];
+      xin[r][0][j] = v;
+      mx = fmaxf(mx, fabsf(v));
+    }
+    row_scale(row_max(mx), sc[r], inv[r]);
+  }
+  f32x4 acc[R][NBP];
+  float hf[R][KG][8];
+  auto to_input = [&](int r, const float* b, float f) {  // acc * f + bias, relu (mopo.py:277-278, 301), row scale
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < KG; ++c) {
+      const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), bb1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        hf[r][c][t] = fmaxf(fmaf(acc[r][2 * c][t], f, b0[t]), 0.f);
+        hf[r][c][4 + t] = fmaxf(fmaf(acc[r][2 * c + 1][t], f, bb1[t]), 0.f);
+        mx = fmaxf(mx, fmaxf(hf[r][c][t], hf[r][c][4 + t]));
+      }
+    }
+    row_scale(row_max(mx), sc[r], inv[r]);
+  };
+  // layer 1 (prefetching layer 2's first slice), layer 2 (prefetching the whole head); both have an
+  // even slice count, so each prefetch lands in buffer 0
+  layer_f16_rows<1, NBP, R, ACT_WAVES, SLOT, NBP, false, NBP>(w1f, xin, acc, lds, wv, lane, sc, nullptr, nullptr, w2f);
+#pragma unroll
+  for (int r = 0; r < R; ++r) to_input(r, b1, inv[r] * inv_w[0]);
+  layer_f16_rows<KG, NBP, R, ACT_WAVES, SLOT, NBP, false, 2 * KG, true>(w2f, hf, acc, lds, wv, lane, sc, nullptr, nullptr,
+                                                                      whf);
+#pragma unroll
+  for (int r = 0; r < R; ++r) to_input(r, b2, inv[r] * inv_w[1]);
+  f32x4 hd[R];
+  head_f16_rows<KG, R>(hf, hd, lds, lane, sc);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + 16 * r;
+    const float f = inv[r] * inv_w[2];
+    if (r > 0) __syncthreads();   // every wave is done with the previous row block's head rows
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int n = 4 * g + t;
+      head[wv][m][n] = fmaf(hd[r][t], f, bh[n]);   // mu | log_std (mopo.py:302-303)
+    }
+    __syncthreads();
+    actor_finish(a, head, wv, m, g, row, row < count);
+  }
+}
+
 int launch_actor(const ActorArgs& a, hipStream_t s) {
   if (a.B == 0) return 0;
   MOPO_REQUIRE(!a.xs || (a.xs_mu && a.xs_sigma && a.xs_in == a.O + a.A && a.xs_in <= XS_STRIDE),
@@ -458,6 +561,15 @@ int launch_actor(const ActorArgs& a, hipStream_t s) {
   MOPO_REQUIRE(a.O >= 1 && a.O <= 32, "actor: obs_dim must be in [1, 32]");
   MOPO_REQUIRE(a.Wpk, "actor: packed weights required");
   dim3 grid(ceil_div((int)a.B, 16 * ACT_WAVES)), block(64 * ACT_WAVES);
+  if (a.dtype == DT_F16X3 && ACT_F16_R > 0) {
+    constexpr int R = ACT_F16_R > 0 ? ACT_F16_R : 1;
+    const dim3 gr(ceil_div((int)a.B, 16 * ACT_WAVES * R));
+    if (a.Hp == 256) hipLaunchKernelGGL((actor_f16r_kernel<16, R>), gr, block, 0, s, a);
+    else if (a.Hp == 32) hipLaunchKernelGGL((actor_f16r_kernel<2, R>), gr, block, 0, s, a);
+    else return fail("actor f16x3: unsupported hidden size (256 or 32)");
+    MOPO_HIP(hipGetLastError());
+    return 0;
+  }
   if (a.dtype == DT_F16X3) {
     if (a.Hp == 256) hipLaunchKernelGGL(actor_f16_kernel<16>, grid, block, 0, s, a);
     else if (a.Hp == 32) hipLaunchKernelGGL(actor_f16_kernel<2>, grid, block, 0, s, a);

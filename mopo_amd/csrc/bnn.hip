@@ -590,13 +590,13 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
 // workgroup per CU with the accumulators in AGPRs): bnn_fwd_f16s_kernel's arithmetic, product for
 // product, with each LDS weight fragment feeding R row blocks (layer_f16_rows).
 #ifndef BNN_F16_R
-#define BNN_F16_R 1
+#define BNN_F16_R 0  // 0: bnn_fwd_f16s_kernel; R >= 1: bnn_fwd_f16r_kernel<R> (H <= 256)
 #endif
 #ifndef BNN_F16R_WAVES
 #define BNN_F16R_WAVES 4
 #endif
 template <int NB2, int NBO, int MODE, int WAVES, int R, int NBU = NB2>
-__global__ __launch_bounds__(WAVES * 64, 1) void bnn_fwd_f16r_kernel(const BnnDev w, const FwdArgs a) {
+__global__ __launch_bounds__(WAVES * 64, R == 1 ? 2 : 1) void bnn_fwd_f16r_kernel(const BnnDev w, const FwdArgs a) {
   constexpr int KG = NB2 / 2;
   constexpr bool KH = NBU < NB2;
   constexpr int NBMAX = NB2 > NBO ? NB2 : NBO;
@@ -669,18 +669,27 @@ __global__ __launch_bounds__(WAVES * 64, 1) void bnn_fwd_f16r_kernel(const BnnDe
     }
     row_scale(row_max(mx), sc[r], inv[r]);
   };
-  layer_f16_rows<1, NB2, R, WAVES, SLOT, NBU>(w.w0b + (int64_t)e * 2 * NB2 * 256, xin, acc, lds, wv, lane, sc,
-                                              w.b0 + e * bs, lds_bias);
+  // each layer's first slice is prefetched during the previous layer's last one (every layer has an
+  // even slice count: the prefetch lands in buffer 0, where the next layer starts)
+  auto whl = [&](int l) { return w.whb + ((int64_t)l * E + e) * KG * 2 * NB2 * 256; };
+  const float* whd = w.whdb + (int64_t)e * KG * 2 * NBO * 256;
+  layer_f16_rows<1, NB2, R, WAVES, SLOT, NBU, false, NB2>(w.w0b + (int64_t)e * 2 * NB2 * 256, xin, acc, lds, wv, lane, sc,
+                                                          w.b0 + e * bs, lds_bias, whl(0));
 #pragma unroll
   for (int r = 0; r < R; ++r) to_input(r, lds_bias, inv[r] * w.wscale[e] * kNegLog2e);
-  for (int l = 0; l < 3; ++l) {
-    layer_f16_rows<KG, NB2, R, WAVES, SLOT, NBU, KH>(w.whb + ((int64_t)l * E + e) * KG * 2 * NB2 * 256, hf, acc, lds, wv,
-                                                     lane, sc, w.bh + ((int64_t)l * E + e) * bs, lds_bias);
+#pragma unroll
+  for (int l = 0; l < 2; ++l) {
+    layer_f16_rows<KG, NB2, R, WAVES, SLOT, NBU, KH, NB2, true>(whl(l), hf, acc, lds, wv, lane, sc,
+                                                                w.bh + ((int64_t)l * E + e) * bs, lds_bias, whl(l + 1));
 #pragma unroll
     for (int r = 0; r < R; ++r) to_input(r, lds_bias, inv[r] * w.wscale[(1 + l) * E + e]);
   }
+  layer_f16_rows<KG, NB2, R, WAVES, SLOT, NBU, KH, NBO, true>(whl(2), hf, acc, lds, wv, lane, sc,
+                                                              w.bh + ((int64_t)2 * E + e) * bs, lds_bias, whd);
+#pragma unroll
+  for (int r = 0; r < R; ++r) to_input(r, lds_bias, inv[r] * w.wscale[3 * E + e]);
   f32x4 hd[R][NBO];
-  layer_f16_rows<KG, NBO, R, WAVES, SLOT, NBO, KH>(w.whdb + (int64_t)e * KG * 2 * NBO * 256, hf, hd, lds, wv, lane, sc);
+  layer_f16_rows<KG, NBO, R, WAVES, SLOT, NBO, KH, 0, true>(whd, hf, hd, lds, wv, lane, sc);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int64_t row = row0 + 16 * r;
@@ -785,7 +794,7 @@ static int launch_f16r(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
 
 template <int NB2, int NBO>
 static int launch_f16s(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
-  if constexpr (BNN_F16_R > 1 && NB2 <= 16) return launch_f16r<NB2, NBO, BNN_F16_R>(h, mode, a, s);
+  if constexpr (BNN_F16_R > 0 && NB2 <= 16) return launch_f16r<NB2, NBO, BNN_F16_R>(h, mode, a, s);
   constexpr int WV = BNN_SPLIT_WAVES, PS = BNN_SPLIT_PS == 0 ? 2 : BNN_SPLIT_PS;
   a.ntiles = (int)ceil_div((int)a.B, 16);
   if (a.ntiles == 0) return 0;

@@ -8,12 +8,14 @@
 // The loop control (holdout split, bootstrap indices, early stopping, elites) stays on the host
 // (mopo_amd/bnn.py), drawing from numpy's global stream in the reference's order.
 //
-// One minibatch step = 12 launches: gather (bootstrap rows, scaler), 5 grouped-GEMM forward
-// launches (E problems each: swish layers write the pre-activation for the backward), the
-// loss kernel (output gradients, max/min log-var gradients + their Adam, this step's lr_t), and
-// 5 grouped-GEMM backward launches, whose weight-gradient tiles apply weight decay and the TF1 Adam
-// in their epilogue (gemm_group.h; parameters ping-pong between two buffers).  Full-batch steps are
-// captured into hipGraphs (8 / 2 / 1+copy-back steps); the epoch's partial last batch runs eagerly.
+// One minibatch step = 3 launches (step_rows, train_rows.h): the row-block forward (gather + scaler,
+// 4 swish layers + heads, output gradient, loss partials), the row-block activation-gradient chain
+// (+ the batch-level tail: max/min log-var gradients and their Adam, this step's lr_t), and one
+// grouped-GEMM launch whose weight-gradient tiles apply weight decay and the TF1 Adam in their
+// epilogue (gemm_group.h; parameters ping-pong between two buffers).  The previous 12-launch form
+// (gather, 5 forward GEMM launches, loss kernel, 5 backward GEMM launches: step_impl) remains for
+// H > 256 and for the holdout evaluation's forward.  Full-batch steps are captured into hipGraphs
+// (8 / 2 / 1+copy-back steps); the epoch's partial last batch runs eagerly.
 //
 // Parameter layout (training master copy, f32): per member, the reference's optvars with the two
 // smv heads concatenated column-wise so one GEMM serves both:
@@ -25,7 +27,7 @@
 
 #include <hipcub/hipcub.hpp>
 
-#include "gemm_group.h"
+#include "train_rows.h"
 
 namespace mopo {
 
@@ -65,6 +67,7 @@ struct Train {
   int* bstep = nullptr;        // minibatch index within the epoch (device)
   unsigned* ticket = nullptr;
   float* part = nullptr;       // loss-kernel block partials
+  float* lpart = nullptr;      // row-block path: per (member, row block) loss partials (train_rows.h)
   float* logs = nullptr;       // [4]: last train loss (data term), ...
   float *mu = nullptr, *sigma = nullptr;
   float *X = nullptr, *T = nullptr, *Z[NHID] = {}, *Hh[NHID] = {}, *OUT = nullptr, *dOUT = nullptr, *dZ[NHID] = {};
@@ -386,6 +389,76 @@ int step_impl(Train* h, int par, int M, bool use_bstep, hipStream_t s) {
   return 0;
 }
 
+// The same step as three launches (train_rows.h): forward + output gradient, the activation-gradient
+// chain + the batch-level tail, and every weight gradient (+ decay, Adam) as one batched gemm launch.
+// Instantiated for the D4RL widths (inputs 14 / 23, hidden 32 / 200 / 256, 2D 24 / 36); H and 2D
+// multiples of 4 (b128 weight rows).  MOPO_TRAIN_ROWS=0 selects step_impl (twelve launches) instead.
+// the weight-gradient launch's tile width (MOPO_TRAIN_WGRAD_TILE: 16 or 32; default 32: 4,000 16x16
+// tiles of K = 256 re-read each operand panel 16x over, 32x32 tiles half as often)
+int train_wgrad_tile() {
+  static const int v = [] {
+    const char* e = std::getenv("MOPO_TRAIN_WGRAD_TILE");
+    return e ? std::atoi(e) : 32;
+  }();
+  return v == 16 ? 0 : 32;
+}
+
+bool use_rows(const Train* h) {
+  static const int env = [] {
+    const char* e = std::getenv("MOPO_TRAIN_ROWS");
+    return e ? std::atoi(e) : 1;
+  }();
+  const Layout& L = h->L;
+  const int g0 = ceil_div(L.IN, 16), gh = ceil_div(L.H, 16), gd = ceil_div(2 * L.D, 16);
+  const bool inst = (gh == 13 || gh == 16 || gh == 2) && ((g0 == 2 && gd == 3) || (g0 == 1 && gd == 2));  // step_rows
+  return env != 0 && inst && L.H % 4 == 0 && L.D % 2 == 0;
+}
+
+int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t* idx, int64_t stride, bool use_bstep,
+              int batch, int M, hipStream_t s) {
+  const Layout& L = h->L;
+  const int E = L.E, H = L.H, IN = L.IN, D = L.D, D2 = 2 * D;
+  const float* P = h->Pb[par];
+  AdamCtx ad{};
+  ad.G = h->G; ad.Pc = h->Pb[par]; ad.Pn = h->Pb[1 - par]; ad.M = h->M; ad.V = h->V; ad.T = nullptr;
+  ad.lr_t = h->beta_pow + 2; ad.tau = 0.f; ad.total = L.total; ad.n_pi = 0; ad.n_q = 0; ad.norm_part = nullptr;
+  TrainRows a{};
+  a.E = E; a.M = M; a.IN = IN; a.H = H; a.D = D; a.nrb = ceil_div(M, 16);
+  a.inputs = in; a.targets = tg; a.rows = idx; a.stride = stride; a.bstep = use_bstep ? h->bstep : nullptr;
+  a.batch = batch; a.mu = h->mu; a.sigma = h->sigma; a.P = P;
+  for (int l = 0; l <= NHID; ++l) { a.W[l] = L.W[l]; a.b[l] = L.b[l]; }
+  a.mx = L.mx; a.mn = L.mn;
+  a.X = h->X; a.T = h->T; a.OUT = h->OUT; a.dOUT = h->dOUT;
+  for (int l = 0; l < NHID; ++l) { a.Z[l] = h->Z[l]; a.Hh[l] = h->Hh[l]; a.dZ[l] = h->dZ[l]; }
+  a.lpart = h->lpart; a.logs = h->logs; a.beta_pow = h->beta_pow; a.bstep_inc = use_bstep ? h->bstep : nullptr;
+  a.lr = h->lr; a.G = h->G; a.ad = ad;
+  const int grid = 8 * a.nrb * ceil_div(E, 8);   // train_rows.h tr_block: a member's row blocks on one XCD
+  const int g0 = ceil_div(IN, 16), gh = ceil_div(H, 16), gd = ceil_div(D2, 16);
+#define MOPO_TRR(G0, GH, GD)                                                                                 \
+  if (g0 == G0 && gh == GH && gd == GD) {                                                                    \
+    hipLaunchKernelGGL((train_fwd_rows_kernel<G0, GH>), dim3(grid), dim3(256), 0, s, a);                     \
+    MOPO_HIP(hipGetLastError());                                                                             \
+    hipLaunchKernelGGL((train_bwd_rows_kernel<GD, GH>), dim3(grid + 1), dim3(256), 0, s, a);                 \
+    MOPO_HIP(hipGetLastError());                                                                             \
+  } else
+  MOPO_TRR(2, 13, 3) MOPO_TRR(1, 13, 2) MOPO_TRR(1, 2, 2) MOPO_TRR(2, 2, 3) MOPO_TRR(2, 16, 3) MOPO_TRR(1, 16, 2)
+  return fail("bnn train: no row-block instantiation for these widths (use_rows)");
+#undef MOPO_TRR
+  std::vector<GemmProb> g;
+  for (int l = NHID; l >= 0; --l) {   // dW_l = X_in^T dY (+ db = colsum dY), fused decay + Adam; batch = member
+    const int K = l == 0 ? IN : H, N = l == NHID ? D2 : H;
+    const float* dY = l == NHID ? h->dOUT : h->dZ[l];
+    const float* Xin = l == 0 ? h->X : h->Hh[l - 1];
+    auto w = mk(K, N, M, Xin, K, 1, dY, N, 0, h->G + L.W[l], N);
+    w.colsum = h->G + L.b[l];
+    w.adam = 1;
+    w.wd = WDECAY[l];
+    w.nb = E;
+    g.push_back(w);
+  }
+  return launch_group(g, s, &ad, nullptr, nullptr, nullptr, nullptr, nullptr, 0, train_wgrad_tile());
+}
+
 int copy_back(Train* h, hipStream_t s) {
   MOPO_HIP(hipMemcpyAsync(h->Pb[0], h->Pb[1], h->L.total * 4, hipMemcpyDeviceToDevice, s));
   return 0;
@@ -408,8 +481,12 @@ int capture(Train* h, int which, const float* in, const float* tg, const int32_t
   const int steps = which == 0 ? TRAIN_GRAPH_STEPS : which == 1 ? 2 : 1;
   int rc = 0;
   for (int i = 0; i < steps && !rc; ++i) {
-    rc = launch_gather(h, in, tg, idx, n_idx, true, batch, batch, gs);
-    if (!rc) rc = step_impl(h, i & 1, batch, true, gs);
+    if (use_rows(h)) {
+      rc = step_rows(h, i & 1, in, tg, idx, n_idx, true, batch, batch, gs);
+    } else {
+      rc = launch_gather(h, in, tg, idx, n_idx, true, batch, batch, gs);
+      if (!rc) rc = step_impl(h, i & 1, batch, true, gs);
+    }
   }
   if (!rc && which == 2) rc = copy_back(h, gs);
   hipGraph_t g = nullptr;
@@ -444,7 +521,8 @@ extern "C" int mopo_bnn_train_create(mopo_bnn_train_t* out, int E, int obs_dim, 
   std::vector<std::pair<void**, size_t>> reg;
   auto f = [&](float** p, int64_t cnt) { reg.push_back({(void**)p, (size_t)cnt * 4}); };
   f(&h->Pb[0], tot); f(&h->Pb[1], tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->S, tot);
-  f(&h->beta_pow, 3); f(&h->part, 4 * (int64_t)loss_blocks); f(&h->logs, 4); f(&h->mu, L.IN); f(&h->sigma, L.IN);
+  f(&h->beta_pow, 3); f(&h->part, 4 * (int64_t)loss_blocks);
+  f(&h->lpart, 4 * (int64_t)E * ceil_div(max_batch, 16) * L.D); f(&h->logs, 4); f(&h->mu, L.IN); f(&h->sigma, L.IN);
   reg.push_back({(void**)&h->bstep, 4});
   reg.push_back({(void**)&h->ticket, 4});
   f(&h->X, E * mM * L.IN); f(&h->T, E * mM * L.D); f(&h->OUT, E * mM * 2 * L.D); f(&h->dOUT, E * mM * 2 * L.D);
@@ -600,9 +678,12 @@ extern "C" int mopo_bnn_train_epoch(mopo_bnn_train_t hh, const float* d_in, cons
     if (i < nfull) MOPO_HIP(hipGraphLaunch(h->gexec[2], gs));
   }
   if (nfull < nb) {  // the epoch's partial last minibatch (bnn.py:426: idxs[:, b*bs:(b+1)*bs])
-    if (launch_gather(h, d_in, d_tg, d_idxs, n_idx, true, batch, last, gs) || step_impl(h, 0, last, true, gs) ||
-        copy_back(h, gs))
+    if (use_rows(h)) {
+      if (step_rows(h, 0, d_in, d_tg, d_idxs, n_idx, true, batch, last, gs) || copy_back(h, gs)) return -1;
+    } else if (launch_gather(h, d_in, d_tg, d_idxs, n_idx, true, batch, last, gs) || step_impl(h, 0, last, true, gs) ||
+               copy_back(h, gs)) {
       return -1;
+    }
   }
   MOPO_HIP(hipEventRecord(h->ev_out, gs));
   MOPO_HIP(hipStreamWaitEvent(s, h->ev_out, 0));

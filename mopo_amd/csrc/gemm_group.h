@@ -67,6 +67,9 @@ struct GemmProb {
   const float* a_u; const float* a_v; const float* a_m; int a_ldm;
   const float* b_u; const float* b_v; const float* b_m; int b_ldm;
   int adam;                          // C (and colsum) are gradient slices of AdamCtx::G: apply Adam
+  int nb;                            // > 1: nb independent problems of these dims with dense-packed operands
+                                     //   (batch b: A + b (ta ? K : M) lda, B + b (tb ? N : K) ldb, C + b M ldc,
+                                     //   colsum + b N); no bias / Z / mask / rank-1 / two-segment operands
   // two-segment plain B (operand mode 3): columns [0, split) from B, [split, N) from B2 (same ldb),
   // bias likewise from bias / bias2
   const float* B2; int split; const float* bias2;
@@ -403,7 +406,8 @@ static __device__ __forceinline__ void panel_rk(int q, int tid, int& r, int& k) 
 }
 
 template <int MODE, bool IS_A, int TW = 16>
-static __device__ __forceinline__ void load_panel(const GemmProb& p, int r0, int kc, int tid, PanelRegs& R) {
+static __device__ __forceinline__ void load_panel(const GemmProb& p, int r0, int kc, int tid, PanelRegs& R,
+                                                  int64_t off = 0) {
   constexpr int KPER = TW == 16 ? 4 : 2;  // k-fast panel: consecutive q share a row in runs of KPER
   const int Rn = IS_A ? p.M : p.N;  // panel axis extent
   if (MODE == 2) {
@@ -439,7 +443,7 @@ static __device__ __forceinline__ void load_panel(const GemmProb& p, int r0, int
       R.x[q] = src[(int64_t)gk * p.ldb];
     }
   } else {
-    const float* base = IS_A ? p.A : p.B;
+    const float* base = (IS_A ? p.A : p.B) + off;   // off: a batched problem's batch (plain modes only)
     const int ld = IS_A ? p.lda : p.ldb;
     // element (r, k) of the panel's operand lives at r*ld + k (row-major in r) or k*ld + r
     constexpr bool r_major = IS_A ? (MODE == 0) : (MODE == 1);
@@ -495,10 +499,10 @@ __host__ static __device__ __forceinline__ int operand_modes(const GemmProb& p) 
 
 template <int AM, int BM, int TW = 16>
 static __device__ __forceinline__ void stage_ab(const GemmProb& p, int i0, int j0, int kc, int kn, int tid, float* As,
-                                                float* Bs) {
+                                                float* Bs, int64_t oA = 0, int64_t oB = 0) {
   PanelRegs ra, rb;
-  load_panel<AM, true, TW>(p, i0, kc, tid, ra);
-  load_panel<BM, false, TW>(p, j0, kc, tid, rb);
+  load_panel<AM, true, TW>(p, i0, kc, tid, ra, oA);
+  load_panel<BM, false, TW>(p, j0, kc, tid, rb, oB);
   pin_panel<AM, true, TW>(ra);
   pin_panel<BM, false, TW>(rb);
   store_panel<AM, true, TW>(p, i0, kn, tid, ra, As);
@@ -507,12 +511,12 @@ static __device__ __forceinline__ void stage_ab(const GemmProb& p, int i0, int j
 
 template <int TW>
 static __device__ __forceinline__ void stage_dispatch(const GemmProb& p, int i0, int j0, int kc, int kn, int t,
-                                                      float* As, float* Bs) {
+                                                      float* As, float* Bs, int64_t oA = 0, int64_t oB = 0) {
   switch (operand_modes(p)) {  // the combinations the callers use (launch_group rejects others)
-    case 0: stage_ab<0, 0, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
-    case 1: stage_ab<0, 1, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
+    case 0: stage_ab<0, 0, TW>(p, i0, j0, kc, kn, t, As, Bs, oA, oB); break;
+    case 1: stage_ab<0, 1, TW>(p, i0, j0, kc, kn, t, As, Bs, oA, oB); break;
     case 3: stage_ab<0, 3, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
-    case 4: stage_ab<1, 0, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
+    case 4: stage_ab<1, 0, TW>(p, i0, j0, kc, kn, t, As, Bs, oA, oB); break;
     case 6: stage_ab<1, 2, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
     default: stage_ab<2, 1, TW>(p, i0, j0, kc, kn, t, As, Bs); break;
   }
@@ -550,8 +554,22 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
   int pi = 0;
   while (pi + 1 < g.n && bid >= g.prefix[pi + 1]) ++pi;
   const GemmProb& p = g.p[pi];
-  const int t = bid - g.prefix[pi];
+  int t = bid - g.prefix[pi];
   const int tn_cnt = ceil_div(p.N, 16);
+  int first = g.pr.nblk + g.prefix[pi];   // block id of this (batch's) tile 0
+  // batched problem: batch b's operands are dense-packed at these offsets (floats)
+  int64_t oA = 0, oB = 0, oC = 0, oCs = 0;
+  if (p.nb > 1) {
+    const int per = ceil_div(p.M, 16) * tn_cnt, b = t / per;
+    t -= b * per;
+    first += b * per;
+    oA = (int64_t)b * (p.ta ? p.K : p.M) * p.lda;
+    oB = (int64_t)b * (p.tb ? p.N : p.K) * p.ldb;
+    oC = (int64_t)b * p.M * p.ldc;
+    oCs = (int64_t)b * p.N;
+  }
+  float* const pC = p.C + oC;
+  float* const pcs = p.colsum ? p.colsum + oCs : nullptr;
 #ifndef MOPO_GEMM_XCD
 #define MOPO_GEMM_XCD 1
 #endif
@@ -560,7 +578,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
   // column tiles [x C/8, (x+1) C/8) of every row tile: each B panel (the weight columns of an MLP
   // layer) is fetched into one XCD's L2 instead of all eight.
   int tm, tn;
-  if (MOPO_GEMM_XCD && (tn_cnt & 7) == 0 && ((g.pr.nblk + g.prefix[pi]) & 7) == 0) {
+  if (MOPO_GEMM_XCD && (tn_cnt & 7) == 0 && (first & 7) == 0) {
     const int per = tn_cnt >> 3, x = t & 7, j = t >> 3;
     tn = x * per + j % per;
     tm = j / per;
@@ -579,8 +597,8 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
   float e_mask = p.mask ? p.mask[(int64_t)gic * p.ldm + gjc] : 1.f;
   asm volatile("" : "+v"(e_bias), "+v"(e_mask));
   const AdamCtx& ad = g.ad;
-  const int64_t a_idx = p.adam ? (int64_t)(p.C - ad.G) + (int64_t)gic * p.ldc + gjc : 0;
-  const int64_t c_idx = p.adam && p.colsum ? (int64_t)(p.colsum - ad.G) + min(j0 + (tid & 15), p.N - 1) : 0;
+  const int64_t a_idx = p.adam ? (int64_t)(pC - ad.G) + (int64_t)gic * p.ldc + gjc : 0;
+  const int64_t c_idx = p.adam && p.colsum ? (int64_t)(pcs - ad.G) + min(j0 + (tid & 15), p.N - 1) : 0;
   AdamIn a_in{0.f, 0.f, 0.f, 0.f}, c_in{0.f, 0.f, 0.f, 0.f};
   float lr_t = 0.f;
   if (p.adam) {
@@ -600,7 +618,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
     // 16 elements of each panel per thread; the per-operand mode is dispatched once (uniform
     // branch) so that all 32+ loads are unconditional and issue back to back -- one memory latency
     // per chunk instead of one per element.
-    stage_dispatch<16>(p, i0, j0, kc, kn, t, &As[0][0], &Bs[0][0]);
+    stage_dispatch<16>(p, i0, j0, kc, kn, t, &As[0][0], &Bs[0][0], oA, oB);
     lds_barrier();
     stamp(g.st, 1);
     // the staged panels are zero-padded to GKC rows, so every wave runs exactly 16 k-steps of its
@@ -641,7 +659,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
       if (p.mask_kind == MASK_DSWISH) v *= dswish_fast(e_mask);
       else if (!(e_mask > 0.f)) v = 0.f;
       if (p.adam) v += p.wd * a_in.p;
-      p.C[(int64_t)gi * p.ldc + gj] = v;
+      pC[(int64_t)gi * p.ldc + gj] = v;
       if (p.adam) {
         adam_apply(ad, a_idx, v, a_in, lr_t);
         gsq = v * v;
@@ -652,7 +670,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
     float c = 0.f;
     for (int q = 0; q < 16; ++q) c += csum[q][tid];
     if (j0 + tid < p.N) {
-      p.colsum[j0 + tid] = c;
+      pcs[j0 + tid] = c;
       if (p.adam) {
         adam_apply(ad, c_idx, c, c_in, lr_t);
         gsq += c * c;
@@ -667,7 +685,7 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
     lds_barrier();
     if (tid == 0) {
       const float b = part[0][0] + part[0][1] + part[0][2] + part[0][3];
-      const int64_t off = p.adam ? (int64_t)(p.C - ad.G) : -1;
+      const int64_t off = p.adam ? (int64_t)(pC - ad.G) : -1;
       float* np = ad.norm_part + 2 * (int64_t)(ad.slot0 + bid);
       np[0] = off >= 0 && off < ad.n_pi ? b : 0.f;
       np[1] = off >= ad.n_pi && off < ad.n_pi + ad.n_q ? b : 0.f;
@@ -680,19 +698,19 @@ static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGro
 // ---- epilogue helpers (gemm32_group_kernel) ---------------------------------------------------
 struct EpiPre { float bias, mask; AdamIn a; int64_t a_idx; };
 
-static __device__ __forceinline__ EpiPre epi_prefetch(const GemmProb& p, const AdamCtx& ad, int gi, int gj) {
+static __device__ __forceinline__ EpiPre epi_prefetch(const GemmProb& p, float* C, const AdamCtx& ad, int gi, int gj) {
   const int gic = min(gi, p.M - 1), gjc = min(gj, p.N - 1);
   EpiPre e;
   e.bias = p.bias ? (p.bias2 && gjc >= p.split ? p.bias2[gjc - p.split] : p.bias[gjc]) : 0.f;
   e.mask = p.mask ? p.mask[(int64_t)gic * p.ldm + gjc] : 1.f;
-  e.a_idx = p.adam ? (int64_t)(p.C - ad.G) + (int64_t)gic * p.ldc + gjc : 0;
+  e.a_idx = p.adam ? (int64_t)(C - ad.G) + (int64_t)gic * p.ldc + gjc : 0;
   e.a = AdamIn{0.f, 0.f, 0.f, 0.f};
   if (p.adam) e.a = adam_load(ad, e.a_idx);
   return e;
 }
 
 // bias, activation (+ pre-activation), activation-derivative mask, decay; store; fused Adam
-static __device__ __forceinline__ void epi_apply(const GemmProb& p, const AdamCtx& ad, int gi, int gj, float v,
+static __device__ __forceinline__ void epi_apply(const GemmProb& p, float* C, const AdamCtx& ad, int gi, int gj, float v,
                                                  const EpiPre& e, float lr_t, float& gsq) {
   v += e.bias;
   if (p.act == ACT_RELU) {
@@ -704,7 +722,7 @@ static __device__ __forceinline__ void epi_apply(const GemmProb& p, const AdamCt
   if (p.mask_kind == MASK_DSWISH) v *= dswish_fast(e.mask);
   else if (!(e.mask > 0.f)) v = 0.f;
   if (p.adam) v += p.wd * e.a.p;
-  p.C[(int64_t)gi * p.ldc + gj] = v;
+  C[(int64_t)gi * p.ldc + gj] = v;
   if (p.adam) {
     adam_apply(ad, e.a_idx, v, e.a, lr_t);
     gsq += v * v;
@@ -727,8 +745,19 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
   int pi = 0;
   while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
   const GemmProb& p = g.p[pi];
-  const int t0 = blockIdx.x - g.prefix[pi];
+  int t0 = blockIdx.x - g.prefix[pi];
   const int tn_cnt = ceil_div(p.N, 32);
+  int64_t oA = 0, oB = 0, oC = 0, oCs = 0;   // a batched problem's batch (gemm_group_kernel)
+  if (p.nb > 1) {
+    const int per = ceil_div(p.M, 32) * tn_cnt, b = t0 / per;
+    t0 -= b * per;
+    oA = (int64_t)b * (p.ta ? p.K : p.M) * p.lda;
+    oB = (int64_t)b * (p.tb ? p.N : p.K) * p.ldb;
+    oC = (int64_t)b * p.M * p.ldc;
+    oCs = (int64_t)b * p.N;
+  }
+  float* const pC = p.C + oC;
+  float* const pcs = p.colsum ? p.colsum + oCs : nullptr;
   const int tm = t0 / tn_cnt, tn = t0 % tn_cnt;
   const int i0 = tm * 32, j0 = tn * 32;
   const int wi = w >> 1, wj = w & 1, li = lane & 15, lk = lane >> 4;
@@ -736,8 +765,8 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
   const AdamCtx& ad = g.ad;
   EpiPre pre[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) pre[q] = epi_prefetch(p, ad, i0 + (tid >> 5) + 8 * q, j0 + (tid & 31));
-  const int64_t c_idx = p.adam && p.colsum ? (int64_t)(p.colsum - ad.G) + min(j0 + (tid & 31), p.N - 1) : 0;
+  for (int q = 0; q < 4; ++q) pre[q] = epi_prefetch(p, pC, ad, i0 + (tid >> 5) + 8 * q, j0 + (tid & 31));
+  const int64_t c_idx = p.adam && p.colsum ? (int64_t)(pcs - ad.G) + min(j0 + (tid & 31), p.N - 1) : 0;
   AdamIn c_in{0.f, 0.f, 0.f, 0.f};
   float lr_t = 0.f;
   if (p.adam) {
@@ -750,7 +779,7 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
     const int kn = min(GKC32, p.K - kc);
     int t = tid;
     asm volatile("" : "+v"(t));
-    stage_dispatch<32>(p, i0, j0, kc, kn, t, As, Bs);
+    stage_dispatch<32>(p, i0, j0, kc, kn, t, As, Bs, oA, oB);
     __syncthreads();
     const int ra_r = wi * 16 + (t & 15), rb_r = wj * 16 + (t & 15), tlk = (t >> 4) & 3;
 #pragma unroll
@@ -781,13 +810,13 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
   for (int q = 0; q < 4; ++q) {
     const int ei = (tid >> 5) + 8 * q, ej = tid & 31;
     const int gi = i0 + ei, gj = j0 + ej;
-    if (gi < p.M && gj < p.N) epi_apply(p, ad, gi, gj, tile[ei][ej], pre[q], lr_t, gsq);
+    if (gi < p.M && gj < p.N) epi_apply(p, pC, ad, gi, gj, tile[ei][ej], pre[q], lr_t, gsq);
   }
   if (do_cs && tid < 32) {
     float c = 0.f;
     for (int q = 0; q < 8; ++q) c += csum[q][tid];
     if (j0 + tid < p.N) {
-      p.colsum[j0 + tid] = c;
+      pcs[j0 + tid] = c;
       if (p.adam) {
         adam_apply(ad, c_idx, c, c_in, lr_t);
         gsq += c * c;
@@ -801,7 +830,7 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
     __syncthreads();
     if (tid == 0) {
       const float b = red[0] + red[1] + red[2] + red[3];
-      const int64_t off = p.adam ? (int64_t)(p.C - ad.G) : -1;
+      const int64_t off = p.adam ? (int64_t)(pC - ad.G) : -1;
       float* np = ad.norm_part + 2 * (int64_t)(ad.slot0 + blockIdx.x);
       np[0] = off >= 0 && off < ad.n_pi ? b : 0.f;
       np[1] = off >= ad.n_pi && off < ad.n_pi + ad.n_q ? b : 0.f;
@@ -829,9 +858,10 @@ static inline int gemm_tile_override() {
   return v;
 }
 
+// tile: 0 the policy above; 32 the 32x32 kernel whatever the problem sizes (partial tiles are range-checked)
 static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const AdamCtx* ad = nullptr, int* slot = nullptr,
                                const PolicyRows* pr = nullptr, const GatherArgs* ga = nullptr,
-                               const Stamps* st = nullptr, int* zero = nullptr, int nzero = 0) {
+                               const Stamps* st = nullptr, int* zero = nullptr, int nzero = 0, int tile = 0) {
   GemmGroup g{};
   if (st) g.st = *st;
   if (nzero > 256) return fail("gemm group: at most 256 words to zero");
@@ -840,19 +870,22 @@ static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const Ad
   if (g.n > MAXP) return fail("gemm group too large");
   bool big = true;
   for (int i = 0; i < g.n; ++i) {
-    const GemmProb& q = ps[i];
+    GemmProb& q = ps[i];
+    if (q.nb < 1) q.nb = 1;
+    if (q.nb > 1 && (q.bias || q.Z || q.mask || q.a_u || q.b_u || q.B2))
+      return fail("gemm group: a batched problem takes plain operands only");
     const int c = operand_modes(q);
     if (!(c == 0 || c == 1 || c == 3 || c == 4 || c == 6 || c == 9)) return fail("unsupported gemm operand modes");
     if ((int64_t)q.M * q.K >= (1ll << 29) || (int64_t)q.N * q.K >= (1ll << 29)) return fail("gemm operand too large");
     big = big && q.M >= 32 && q.N >= 32;
   }
   const int ov = gemm_tile_override();
-  const int TW = (ov == 32 && big) ? 32 : 16;
+  const int TW = (tile == 32 || (ov == 32 && big)) ? 32 : 16;
   int tot = 0;
   for (int i = 0; i < g.n; ++i) {
     g.p[i] = ps[i];
     g.prefix[i] = tot;
-    tot += ceil_div(ps[i].M, TW) * ceil_div(ps[i].N, TW);
+    tot += ps[i].nb * ceil_div(ps[i].M, TW) * ceil_div(ps[i].N, TW);
   }
   g.prefix[g.n] = tot;
   if (ad) {

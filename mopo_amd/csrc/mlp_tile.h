@@ -449,20 +449,28 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
 // layer_lds_split_f32's f16 form over R row blocks per wave: every weight fragment read from LDS feeds
 // the MFMAs of all R row blocks (R = 2 halves the LDS reads, the barriers and the staged bytes per row).
 // in[r]: row block r's f32 activations (scaled by sc[r] when split); parts made when a k-group is consumed.
-template <int KG, int NB, int R, int WAVES, int SLOT, int NBU = NB, bool KH = false>
+// NBN > 0: during the last slice, stage the NEXT layer's first slice (NBN fragments at wf_next) into the
+// other buffer; that layer is then called with PRE = true (no initial barrier + exposed copy; its bias
+// goes out with its second slice).  Every layer here has an even slice count, so slice s always uses
+// buffer s & 1.
+template <int KG, int NB, int R, int WAVES, int SLOT, int NBU = NB, bool KH = false, int NBN = 0, bool PRE = false>
 __device__ __forceinline__ void layer_f16_rows(const float* __restrict__ wf, const float (&in)[R][KG][8],
                                                f32x4 (&acc)[R][NB], float* lds, int w, int lane, const float (&sc)[R],
-                                               const float* __restrict__ bias = nullptr, float* lds_bias = nullptr) {
+                                               const float* __restrict__ bias = nullptr, float* lds_bias = nullptr,
+                                               const float* __restrict__ wf_next = nullptr) {
   constexpr int P = 2, S = KG * P;
   static_assert(Stage<NB, WAVES>::SLOTS * 256 <= SLOT, "slice larger than its buffer");
+  static_assert(Stage<NBN, WAVES>::SLOTS * 256 <= SLOT, "next slice larger than its buffer");
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[r][nb] = zero4();
   bf16x8 cur[R][P];
-  __syncthreads();
-  stage_slice<NB, WAVES>(wf, lds, w, lane);
-  if (bias) stage_bias<NB * 4, WAVES>(bias, lds_bias, w, lane);  // published by the first barrier below
+  if (!PRE) {
+    __syncthreads();
+    stage_slice<NB, WAVES>(wf, lds, w, lane);
+    if (bias) stage_bias<NB * 4, WAVES>(bias, lds_bias, w, lane);  // published by the first barrier below
+  }
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int kg = s / P, p = s % P;
@@ -482,6 +490,8 @@ __device__ __forceinline__ void layer_f16_rows(const float* __restrict__ wf, con
     }
     __syncthreads();
     if (s + 1 < S) stage_slice<NB, WAVES>(wf + (s + 1) * NB * 256, lds + ((s + 1) & 1) * SLOT, w, lane);
+    else if constexpr (NBN > 0) stage_slice<NBN, WAVES>(wf_next, lds + (S & 1) * SLOT, w, lane);
+    if (PRE && s == 0 && bias) stage_bias<NB * 4, WAVES>(bias, lds_bias, w, lane);  // published at s = 1
     __builtin_amdgcn_sched_barrier(0);
     const float* b = lds + (s & 1) * SLOT;
     bf16x8 fr_next = *reinterpret_cast<const bf16x8*>(b + lane * 4);
@@ -496,6 +506,36 @@ __device__ __forceinline__ void layer_f16_rows(const float* __restrict__ wf, con
         for (int r = 0; r < R; ++r)
           acc[r][nb] = (KH && kg + 1 == KG) ? mfma_16x16x16_lo<true>(fr, cur[r][q], acc[r][nb])
                                             : mfma_16x16x32<true>(fr, cur[r][q], acc[r][nb]);
+    }
+  }
+}
+
+// A narrow f16x3 layer (one 16-wide output block: the actor's [mu | log_std] head) whose 2 KG weight
+// fragments sit in ONE staged slice (buffer `buf`, copied beforehand, e.g. as layer_f16_rows' NBN
+// prefetch): one barrier for the whole layer instead of one per (k-group, part) slice.
+template <int KG, int R>
+__device__ __forceinline__ void head_f16_rows(const float (&in)[R][KG][8], f32x4 (&acc)[R], const float* lds_buf,
+                                              int lane, const float (&sc)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = zero4();
+  __syncthreads();   // vmcnt(0): the slice landed (every wave's copies), and is visible to all
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) {
+    const bf16x8 f0 = *reinterpret_cast<const bf16x8*>(lds_buf + ((2 * kg) * 64 + lane) * 4);
+    const bf16x8 f1 = *reinterpret_cast<const bf16x8*>(lds_buf + ((2 * kg + 1) * 64 + lane) * 4);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      u32x4v h4, l4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const F16Pair pr = split_f16_pair(in[r][kg][2 * q], in[r][kg][2 * q + 1], sc[r]);
+        h4[q] = pr.hi;
+        l4[q] = pr.lo;
+      }
+      const bf16x8 c0 = __builtin_bit_cast(bf16x8, h4), c1 = __builtin_bit_cast(bf16x8, l4);
+      acc[r] = mfma_16x16x32<true>(f0, c1, acc[r]);   // the product order of layer_f16_rows
+      acc[r] = mfma_16x16x32<true>(f0, c0, acc[r]);
+      acc[r] = mfma_16x16x32<true>(f1, c0, acc[r]);
     }
   }
 }

@@ -1,0 +1,306 @@
+// Row-block kernels of the ensemble training step (bnn_train.hip): one minibatch step in three launches
+// instead of twelve.
+//
+//   train_fwd_rows_kernel, grid (row blocks, members): the minibatch gather (bootstrap rows, scaler:
+//     utils.py:96), the four swish layers and the fused mean / log-var head of the member for its 16
+//     rows (fc.py:84-106; pre-activations Z and activations H stored for the backward), the output
+//     gradient of the Gaussian NLL through the soft log-var bounds (bnn.py:241-249, 669-701) and the
+//     block's partial sums of the max/min log-var gradients and of the loss
+//   train_bwd_rows_kernel, grid (row blocks, members + 1): row block (0, 0) reduces those partials in
+//     a fixed order and applies the batch-level updates (the 0.01 (sum maxlv - sum minlv) terms, their
+//     Adam, this step's lr_t, the TF1 beta powers, the minibatch counter); the others run the
+//     activation-gradient chain dZ_{l-1} = (dY_l W_l^T) * swish'(Z_{l-1}), l = 4 .. 1
+//   one gemm_group launch (bnn_train.hip): every weight gradient X_in^T dY (+ bias column sums, weight
+//     decay, TF1 Adam in the epilogue) as 5 batched problems, one per layer, the members as the batch
+//
+// Every row-local quantity stays in its workgroup: the layer's 16 x K input sits in LDS, each of the 4
+// waves contracts its 64 output columns (4 tiles of 16) over the whole K on v_mfma_f32_16x16x4_f32
+// (exact f32 products, f32 accumulation), its weight columns streamed from L2 straight into MFMA B
+// registers two k-groups ahead (b128 loads), and the layer's output goes back to LDS for the next layer.
+// A member's row blocks share one XCD (tr_block), so its weights are fetched into one L2.
+// Requires H, IN <= 256, 2D <= 256, H and 2D multiples of 4 (bnn_train.hip use_rows).
+#pragma once
+#include <type_traits>
+
+#include "gemm_group.h"
+
+namespace mopo {
+
+constexpr int TR_NHID = 4;
+constexpr int TR_LD = 260;   // LDS row stride (floats) of a 16-row activation block: K <= 256 (+4: b128 reads conflict-free)
+
+struct TrainRows {
+  int E, M, IN, H, D, nrb;
+  // gather: row = rows[e * stride + (*bstep) * batch + r] (rows == NULL: r)
+  const float* inputs; const float* targets; const int32_t* rows; int64_t stride; const int* bstep; int batch;
+  const float* mu; const float* sigma;
+  const float* P;                    // this step's parameters (training layout, bnn_train.hip)
+  int64_t W[TR_NHID + 1], b[TR_NHID + 1], mx, mn;
+  float* X; float* T; float* Z[TR_NHID]; float* Hh[TR_NHID]; float* OUT; float* dOUT; float* dZ[TR_NHID];
+  float* lpart;                      // [E][nrb][D][4]: d loss / d maxlv, d loss / d minlv, loss (per row block)
+  // the batch-level tail (train_bwd_rows_kernel's block (0, 0))
+  float* logs; float* beta_pow; int* bstep_inc; float lr; float* G; AdamCtx ad;
+};
+
+static __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t d, int idx) {   // idx < 0: zeros
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(d, idx * 4, 0, 0));
+}
+
+// acc[q] = A[16 x K] x B over the whole K for the wave's 64 output columns: tile q's column li is
+// column c0 + q, c0 = 64 w + 4 li, so a lane's four B values of one k are one b128 load (KT = false) and
+// its four output values of one row are one b128 store.  A in LDS (row stride TR_LD, zero past K up to
+// the next multiple of 16); B(k, c) = W[k * ldw + c] (KT = false) or W[c * ldw + k] (KT = true), zero
+// outside k < K, c < N (N and, for KT, K multiples of 4).  Lane (li, lk) contracts k = 16 grp + 4 lk + u
+// (one ds_read_b128 of A per k-group); B is loaded two k-groups ahead (4 b128 loads per k-group).
+// W, K, N, ldw are wave-uniform but computed from a runtime layer index: forced into SGPRs here, since a
+// buffer descriptor the compiler believes divergent is wrapped in a readfirstlane waterfall loop around
+// every load (measured: the step's forward kernel 2x slower)
+static __device__ __forceinline__ const float* uniform_ptr(const float* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const float*)(((uint64_t)hi << 32) | lo);
+}
+
+// G = ceil(K / 16) at compile time: straight-line code with the loads two k-groups ahead (a runtime
+// k-group loop made the compiler wait for all but 2 of the prefetched loads at its header, and guarded
+// unrolled groups for all but the last few at every join).
+template <bool KT, int G>
+static __device__ __forceinline__ void rows_gemm(const float* As, const float* Wv, int Kv, int Nv, int ldwv, int w,
+                                                 int lane, f32x4 (&acc)[4]) {
+  const float* W = uniform_ptr(Wv);
+  const int K = __builtin_amdgcn_readfirstlane(Kv), N = __builtin_amdgcn_readfirstlane(Nv);
+  const int ldw = __builtin_amdgcn_readfirstlane(ldwv);
+  const int li = lane & 15, lk = lane >> 4, c0 = 64 * w + 4 * li;
+  const auto d = rsrc(W, KT ? (int64_t)(N - 1) * ldw + K : (int64_t)(K - 1) * ldw + N);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = zero4();
+  if (64 * w >= N) return;                                 // no columns for this wave (wave-uniform)
+  auto ld = [&](int grp, f32x4 (&bv)[4]) {
+    const int k0 = 16 * grp + 4 * lk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = KT ? ((c0 + j < N) & (k0 < K)) : ((c0 < N) & (k0 + j < K));
+      const int idx = KT ? (c0 + j) * ldw + k0 : (k0 + j) * ldw + c0;
+      bv[j] = bload4(d, ok ? idx : -1);   // KT: column c0 + j, k0 .. + 3; else: row k0 + j, columns c0 .. + 3
+    }
+  };
+  auto mm = [&](int grp, const f32x4 (&bv)[4]) {
+    const f32x4 a4 = ld4(As + li * TR_LD + 16 * grp + 4 * lk);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = mfma4(a4[u], KT ? bv[q][u] : bv[u][q], acc[q]);
+  };
+  f32x4 bq[G + 2][4];
+  ld(0, bq[0]);
+  if constexpr (G > 1) ld(1, bq[1]);
+#pragma unroll
+  for (int grp = 0; grp < G; ++grp) {
+    if (grp + 2 < G) ld(grp + 2, bq[grp + 2]);            // two k-groups ahead
+    // keep them there: left alone the scheduler sinks each load to just before its first use, leaving
+    // one or two in flight
+    __builtin_amdgcn_sched_barrier(0);
+    mm(grp, bq[grp]);
+  }
+}
+
+// Workgroup b -> (member, row block): workgroups are dealt round-robin over the 8 XCDs (b mod 8), so
+// member e's row blocks all get b = e mod 8 (+ 8 per later row block): each member's weights are read
+// into ONE XCD's L2 (grid 8 nrb ceil(E / 8); ids past E exit).
+static __device__ __forceinline__ bool tr_block(int b, int nrb, int E, int& e, int& rb) {
+  const int j = b >> 3;
+  e = (b & 7) + 8 * (j / nrb);
+  rb = j % nrb;
+  return e < E;
+}
+
+// ---- forward + loss gradient ----------------------------------------------------------------------
+// G0 / GH: k-groups of the inputs / the hidden width (rows_gemm)
+template <int G0, int GH>
+static __global__ __launch_bounds__(256) void train_fwd_rows_kernel(const TrainRows a) {
+  __shared__ __attribute__((aligned(16))) float buf[2][16 * TR_LD];
+  __shared__ float red[3][64][17];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lk = lane >> 4;
+  int e, rb;
+  if (!tr_block(blockIdx.x, a.nrb, a.E, e, rb)) return;
+  const int M = a.M, IN = a.IN, H = a.H, D = a.D, i0 = rb * 16;
+  // ---- gather: X rows (scaled) into buf[0] (and HBM, for dW_0), targets into HBM; zero K padding
+  {
+    const int W = IN + D, KP = ((IN + 15) >> 4) << 4;
+    const int64_t base = a.bstep ? (int64_t)(*a.bstep) * a.batch : 0;
+    for (int i = tid; i < 16 * KP; i += 256) buf[0][(i / KP) * TR_LD + i % KP] = 0.f;
+    lds_barrier();
+    for (int i = tid; i < 16 * W; i += 256) {
+      const int r = i / W, c = i % W, row = i0 + r;
+      if (row >= M) continue;
+      const int64_t src = a.rows ? a.rows[e * a.stride + base + row] : row;
+      const int64_t er = (int64_t)e * M + row;
+      if (c < IN) {
+        const float x = (a.inputs[src * IN + c] - a.mu[c]) / a.sigma[c];   // utils.py:96
+        a.X[er * IN + c] = x;
+        buf[0][r * TR_LD + c] = x;
+      } else {
+        a.T[er * D + (c - IN)] = a.targets[src * D + (c - IN)];
+      }
+    }
+    lds_barrier();
+  }
+  // ---- 4 swish layers + the fused heads; lane (li, lk) holds rows 4 lk + i, columns c0 .. c0 + 3
+  const int c0 = 64 * w + 4 * li;
+  auto layer = [&](auto gtag, int l) {
+    constexpr int G = decltype(gtag)::value;
+    const int K = l == 0 ? IN : H, N = l == TR_NHID ? 2 * D : H;
+    const float* Wl = a.P + a.W[l] + (int64_t)e * K * N;
+    const f32x4 bias = c0 < N ? ld4(a.P + a.b[l] + (int64_t)e * N + c0) : zero4();
+    f32x4 acc[4];
+    rows_gemm<false, G>(buf[l & 1], Wl, K, N, N, w, lane, acc);
+    float* out = buf[(l + 1) & 1];
+    if (64 * w < N) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {                      // D: row 4 lk + i; tile q = column c0 + q
+        const int r = 4 * lk + i, row = i0 + r;
+        const bool ok = row < M && c0 < N;
+        f32x4 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = acc[q][i] + bias[q];
+        if (l < TR_NHID) {
+          const int64_t o = ((int64_t)e * M + row) * H + c0;
+          if (ok) *reinterpret_cast<f32x4*>(a.Z[l] + o) = v;   // pre-activation (swish' in the backward)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = swish_fast(v[q]);
+          if (ok) *reinterpret_cast<f32x4*>(a.Hh[l] + o) = v;
+        } else if (ok) {
+          *reinterpret_cast<f32x4*>(a.OUT + ((int64_t)e * M + row) * 2 * D + c0) = v;
+        }
+        *reinterpret_cast<f32x4*>(out + r * TR_LD + c0) = ok ? v : zero4();
+      }
+    }
+    lds_barrier();
+  };
+  layer(std::integral_constant<int, G0>{}, 0);
+  for (int l = 1; l <= TR_NHID; ++l) layer(std::integral_constant<int, GH>{}, l);   // 3 swish layers + the heads
+  // ---- output gradient (train_loss_kernel's math, per (row, d)) and the block's partial sums
+  const float* o = buf[(TR_NHID + 1) & 1];
+  const float s = 1.f / ((float)M * (float)D);
+  for (int i = tid; i < 16 * D; i += 256) {
+    const int r = i / D, d = i % D, row = i0 + r;
+    float c_mx = 0.f, c_mn = 0.f, c_loss = 0.f;
+    if (row < M) {
+      const int64_t er = (int64_t)e * M + row;
+      const float mx = a.P[a.mx + d], mn = a.P[a.mn + d];
+      const float mean = o[r * TR_LD + d], raw = o[r * TR_LD + D + d], y = a.T[er * D + d];
+      const float lv1 = mx - softplusf(mx - raw);
+      const float lv = mn + softplusf(lv1 - mn);
+      const float inv = expf(-lv);
+      const float err = mean - y;
+      const float dlv = (1.f - err * err * inv) * s;
+      const float sb = 1.f / (1.f + expf(-(lv1 - mn))), sa = 1.f / (1.f + expf(-(mx - raw)));
+      const float dlv1 = dlv * sb;
+      a.dOUT[er * 2 * D + d] = 2.f * err * inv * s;
+      a.dOUT[er * 2 * D + D + d] = dlv1 * sa;
+      c_mn = dlv * (1.f - sb);
+      c_mx = dlv1 * (1.f - sa);
+      c_loss = (err * err * inv + lv) * s;
+    }
+    red[0][d][r] = c_mx;
+    red[1][d][r] = c_mn;
+    red[2][d][r] = c_loss;
+  }
+  lds_barrier();
+  if (tid < D) {                                          // rows in order (deterministic)
+    float t3[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      for (int r = 0; r < 16; ++r) t3[k] += red[k][tid][r];
+    float* pp = a.lpart + (((int64_t)e * a.nrb + rb) * D + tid) * 4;
+    pp[0] = t3[0]; pp[1] = t3[1]; pp[2] = t3[2];
+  }
+}
+
+// ---- batch-level tail: partial sums in (member, row block) order, then train_loss_kernel's tail -----
+static __device__ __forceinline__ void train_loss_tail(const TrainRows& a, float* sh) {
+  const int D = a.D, n = a.E * a.nrb;
+  const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];  // every thread reads them before thread 0 advances them
+  const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  __syncthreads();
+  if ((int)threadIdx.x < D) {
+    const int dd = threadIdx.x;
+    float gmx = 0.f, gmn = 0.f, loss = 0.f;
+    for (int c = 0; c < n; ++c) {
+      const float* pp = a.lpart + ((int64_t)c * D + dd) * 4;
+      gmx += pp[0]; gmn += pp[1]; loss += pp[2];
+    }
+    gmx += 0.01f;                                                   // 0.01 * sum(max_logvar)
+    gmn -= 0.01f;                                                   // -0.01 * sum(min_logvar)
+    a.G[a.mx + dd] = gmx;
+    a.G[a.mn + dd] = gmn;
+    adam_apply(a.ad, a.mx + dd, gmx, adam_load(a.ad, a.mx + dd), lr_t);
+    adam_apply(a.ad, a.mn + dd, gmn, adam_load(a.ad, a.mn + dd), lr_t);
+    sh[dd] = loss;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float loss = 0.f;
+    for (int dd = 0; dd < D; ++dd) loss += sh[dd];
+    a.logs[0] = loss;                                               // data term of the train loss
+    a.beta_pow[2] = lr_t;
+    a.beta_pow[0] = b1p * 0.9f;
+    a.beta_pow[1] = b2p * 0.999f;
+    if (a.bstep_inc) *a.bstep_inc += 1;
+  }
+}
+
+// ---- activation-gradient chain ------------------------------------------------------------------
+// GD / GH: k-groups of the heads' width 2D / the hidden width
+template <int GD, int GH>
+static __global__ __launch_bounds__(256) void train_bwd_rows_kernel(const TrainRows a) {
+  __shared__ __attribute__((aligned(16))) float buf[2][16 * TR_LD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lk = lane >> 4;
+  if (blockIdx.x == gridDim.x - 1) {                      // the batch-level tail (last block)
+    train_loss_tail(a, buf[0]);
+    return;
+  }
+  int e, rb;
+  if (!tr_block(blockIdx.x, a.nrb, a.E, e, rb)) return;  // the forward's placement: weights L2-warm
+  const int M = a.M, H = a.H, D = a.D, i0 = rb * 16;
+  {  // dY of the heads into buf[0], zero-padded to a multiple of 16 columns
+    const int N = 2 * D, NP = ((N + 15) >> 4) << 4;
+    for (int i = tid; i < 16 * NP; i += 256) {
+      const int r = i / NP, c = i % NP, row = i0 + r;
+      buf[0][r * TR_LD + c] = (row < M && c < N) ? a.dOUT[((int64_t)e * M + row) * N + c] : 0.f;
+    }
+    lds_barrier();
+  }
+  const int c0 = 64 * w + 4 * li;
+  auto layer = [&](auto gtag, int l) {
+    constexpr int G = decltype(gtag)::value;
+    const int Kl = H, Nl = l == TR_NHID ? 2 * D : H;     // layer l: [Kl -> Nl]; dZ_{l-1} is 16 x Kl
+    const float* Wl = a.P + a.W[l] + (int64_t)e * Kl * Nl;
+    f32x4 zm[4];                                          // swish'(Z_{l-1}) operands, fetched up front
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = i0 + 4 * lk + i;
+      zm[i] = (c0 < Kl && row < M) ? ld4(a.Z[l - 1] + ((int64_t)e * M + row) * H + c0) : zero4();
+    }
+    f32x4 acc[4];
+    rows_gemm<true, G>(buf[(TR_NHID - l) & 1], Wl, Nl, Kl, Nl, w, lane, acc);
+    float* out = buf[(TR_NHID - l + 1) & 1];
+    if (64 * w < Kl) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * lk + i, row = i0 + r;
+        const bool ok = row < M && c0 < Kl;
+        f32x4 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ok ? acc[q][i] * dswish_fast(zm[i][q]) : 0.f;
+        if (ok) *reinterpret_cast<f32x4*>(a.dZ[l - 1] + ((int64_t)e * M + row) * H + c0) = v;
+        *reinterpret_cast<f32x4*>(out + r * TR_LD + c0) = v;
+      }
+    }
+    lds_barrier();
+  };
+  layer(std::integral_constant<int, GD>{}, TR_NHID);
+  for (int l = TR_NHID - 1; l >= 1; --l) layer(std::integral_constant<int, GH>{}, l);
+}
+
+}  // namespace mopo
