@@ -436,9 +436,9 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
   const int g0 = ceil_div(IN, 16), gh = ceil_div(H, 16), gd = ceil_div(D2, 16);
 #define MOPO_TRR(G0, GH, GD)                                                                                 \
   if (g0 == G0 && gh == GH && gd == GD) {                                                                    \
-    hipLaunchKernelGGL((train_fwd_rows_kernel<G0, GH>), dim3(grid), dim3(256), 0, s, a);                     \
+    hipLaunchKernelGGL((train_fwd_rows_kernel<G0, GH>), dim3(grid), dim3(TR_WAVES * 64), 0, s, a);                     \
     MOPO_HIP(hipGetLastError());                                                                             \
-    hipLaunchKernelGGL((train_bwd_rows_kernel<GD, GH>), dim3(grid + 1), dim3(256), 0, s, a);                 \
+    hipLaunchKernelGGL((train_bwd_rows_kernel<GD, GH>), dim3(grid + 1), dim3(TR_WAVES * 64), 0, s, a);                 \
     MOPO_HIP(hipGetLastError());                                                                             \
   } else
   MOPO_TRR(2, 13, 3) MOPO_TRR(1, 13, 2) MOPO_TRR(1, 2, 2) MOPO_TRR(2, 2, 3) MOPO_TRR(2, 16, 3) MOPO_TRR(1, 16, 2)

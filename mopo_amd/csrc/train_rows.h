@@ -13,10 +13,10 @@
 //   one gemm_group launch (bnn_train.hip): every weight gradient X_in^T dY (+ bias column sums, weight
 //     decay, TF1 Adam in the epilogue) as 5 batched problems, one per layer, the members as the batch
 //
-// Every row-local quantity stays in its workgroup: the layer's 16 x K input sits in LDS, each of the 4
-// waves contracts its 64 output columns (4 tiles of 16) over the whole K on v_mfma_f32_16x16x4_f32
+// Every row-local quantity stays in its workgroup: the layer's 16 x K input sits in LDS, each of the 8
+// waves contracts 2 output tiles of 16 columns over the whole K on v_mfma_f32_16x16x4_f32
 // (exact f32 products, f32 accumulation), its weight columns streamed from L2 straight into MFMA B
-// registers two k-groups ahead (b128 loads), and the layer's output goes back to LDS for the next layer.
+// registers two k-groups ahead (b64 / b128 loads), and the layer's output goes back to LDS for the next layer.
 // A member's row blocks share one XCD (tr_block), so its weights are fetched into one L2.
 // Requires H, IN <= 256, 2D <= 256, H and 2D multiples of 4 (bnn_train.hip use_rows).
 #pragma once
@@ -46,12 +46,12 @@ static __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t d, int idx
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(d, idx * 4, 0, 0));
 }
 
-// acc[q] = A[16 x K] x B over the whole K for the wave's 64 output columns: tile q's column li is
-// column c0 + q, c0 = 64 w + 4 li, so a lane's four B values of one k are one b128 load (KT = false) and
-// its four output values of one row are one b128 store.  A in LDS (row stride TR_LD, zero past K up to
-// the next multiple of 16); B(k, c) = W[k * ldw + c] (KT = false) or W[c * ldw + k] (KT = true), zero
-// outside k < K, c < N (N and, for KT, K multiples of 4).  Lane (li, lk) contracts k = 16 grp + 4 lk + u
-// (one ds_read_b128 of A per k-group); B is loaded two k-groups ahead (4 b128 loads per k-group).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+static __device__ __forceinline__ f32x2 bload2(__amdgpu_buffer_rsrc_t d, int idx) {   // idx < 0: zeros
+  return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(d, idx * 4, 0, 0));
+}
+
 // W, K, N, ldw are wave-uniform but computed from a runtime layer index: forced into SGPRs here, since a
 // buffer descriptor the compiler believes divergent is wrapped in a readfirstlane waterfall loop around
 // every load (measured: the step's forward kernel 2x slower)
@@ -61,37 +61,65 @@ static __device__ __forceinline__ const float* uniform_ptr(const float* p) {
   return (const float*)(((uint64_t)hi << 32) | lo);
 }
 
-// G = ceil(K / 16) at compile time: straight-line code with the loads two k-groups ahead (a runtime
-// k-group loop made the compiler wait for all but 2 of the prefetched loads at its header, and guarded
-// unrolled groups for all but the last few at every join).
-template <bool KT, int G>
-static __device__ __forceinline__ void rows_gemm(const float* As, const float* Wv, int Kv, int Nv, int ldwv, int w,
-                                                 int lane, f32x4 (&acc)[4]) {
+// Workgroups of TR_WAVES waves: wave w owns column block cb = w % 4 (64 columns) and TW = 16 / TR_WAVES
+// of its 4 tiles (two waves per SIMD at 8: one wave's memory waits overlap the other's MFMAs).
+#ifndef TR_WAVES_CFG
+#define TR_WAVES_CFG 8
+#endif
+constexpr int TR_WAVES = TR_WAVES_CFG, TR_TW = 16 / TR_WAVES;
+
+// acc[q] = A[16 x K] x B over the whole K for tiles q < TW of the wave: tile q's column li is column
+// c + q, c = 64 cb + 4 li + TW (w / 4), so a lane's B values of one k are one b64 / b128 load (KT = false)
+// and its outputs of one row one b64 / b128 store.  A in LDS (row stride TR_LD, zero past K up to the
+// next multiple of 16); B(k, c) = W[k * ldw + c] (KT = false) or W[c * ldw + k] (KT = true), zero outside
+// k < K, c < N (N and, for KT, K multiples of 4).  Lane (li, lk) contracts k = 16 grp + 4 lk + u (one
+// ds_read_b128 of A per k-group).  G = ceil(K / 16) at compile time: straight-line code with the loads
+// two k-groups ahead (a runtime k-group loop made the compiler wait for all but 2 of the prefetched
+// loads at its header).
+template <bool KT, int G, int TW>
+static __device__ __forceinline__ void rows_gemm(const float* As, const float* Wv, int Kv, int Nv, int ldwv, int c,
+                                                 int lane, f32x4 (&acc)[TW]) {
   const float* W = uniform_ptr(Wv);
   const int K = __builtin_amdgcn_readfirstlane(Kv), N = __builtin_amdgcn_readfirstlane(Nv);
   const int ldw = __builtin_amdgcn_readfirstlane(ldwv);
-  const int li = lane & 15, lk = lane >> 4, c0 = 64 * w + 4 * li;
+  const int li = lane & 15, lk = lane >> 4;
   const auto d = rsrc(W, KT ? (int64_t)(N - 1) * ldw + K : (int64_t)(K - 1) * ldw + N);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] = zero4();
-  if (64 * w >= N) return;                                 // no columns for this wave (wave-uniform)
-  auto ld = [&](int grp, f32x4 (&bv)[4]) {
+  for (int q = 0; q < TW; ++q) acc[q] = zero4();
+  if (__builtin_amdgcn_readfirstlane(c - 4 * li) >= N) return;   // no columns for this wave (wave-uniform)
+  auto ld = [&](int grp, float (&bv)[4][TW]) {
     const int k0 = 16 * grp + 4 * lk;
+    if constexpr (KT) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool ok = KT ? ((c0 + j < N) & (k0 < K)) : ((c0 < N) & (k0 + j < K));
-      const int idx = KT ? (c0 + j) * ldw + k0 : (k0 + j) * ldw + c0;
-      bv[j] = bload4(d, ok ? idx : -1);   // KT: column c0 + j, k0 .. + 3; else: row k0 + j, columns c0 .. + 3
+      for (int q = 0; q < TW; ++q) {                    // column c + q, k0 .. k0 + 3
+        const f32x4 v = bload4(d, ((c + q < N) & (k0 < K)) ? (c + q) * ldw + k0 : -1);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bv[u][q] = v[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {                     // row k0 + u, columns c .. c + TW - 1
+        const int idx = ((c < N) & (k0 + u < K)) ? (k0 + u) * ldw + c : -1;
+        if constexpr (TW == 4) {
+          const f32x4 v = bload4(d, idx);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bv[u][q] = v[q];
+        } else {
+          const f32x2 v = bload2(d, idx);
+          bv[u][0] = v[0];
+          bv[u][1] = v[1];
+        }
+      }
     }
   };
-  auto mm = [&](int grp, const f32x4 (&bv)[4]) {
+  auto mm = [&](int grp, const float (&bv)[4][TW]) {
     const f32x4 a4 = ld4(As + li * TR_LD + 16 * grp + 4 * lk);
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = mfma4(a4[u], KT ? bv[q][u] : bv[u][q], acc[q]);
+      for (int q = 0; q < TW; ++q) acc[q] = mfma4(a4[u], bv[u][q], acc[q]);
   };
-  f32x4 bq[G + 2][4];
+  float bq[G + 2][4][TW];
   ld(0, bq[0]);
   if constexpr (G > 1) ld(1, bq[1]);
 #pragma unroll
@@ -101,6 +129,23 @@ static __device__ __forceinline__ void rows_gemm(const float* As, const float* W
     // one or two in flight
     __builtin_amdgcn_sched_barrier(0);
     mm(grp, bq[grp]);
+  }
+}
+
+// a lane's TW consecutive floats at p (16-B / 8-B aligned)
+template <int TW>
+static __device__ __forceinline__ void st_tw(float* p, const float (&v)[TW]) {
+  if constexpr (TW == 4) *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+  else *reinterpret_cast<f32x2*>(p) = f32x2{v[0], v[1]};
+}
+template <int TW>
+static __device__ __forceinline__ void ld_tw(const float* p, float (&v)[TW]) {
+  if constexpr (TW == 4) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(p);
+    v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+  } else {
+    const f32x2 x = *reinterpret_cast<const f32x2*>(p);
+    v[0] = x[0]; v[1] = x[1];
   }
 }
 
@@ -117,7 +162,7 @@ static __device__ __forceinline__ bool tr_block(int b, int nrb, int E, int& e, i
 // ---- forward + loss gradient ----------------------------------------------------------------------
 // G0 / GH: k-groups of the inputs / the hidden width (rows_gemm)
 template <int G0, int GH>
-static __global__ __launch_bounds__(256) void train_fwd_rows_kernel(const TrainRows a) {
+static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_fwd_rows_kernel(const TrainRows a) {
   __shared__ __attribute__((aligned(16))) float buf[2][16 * TR_LD];
   __shared__ float red[3][64][17];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lk = lane >> 4;
@@ -128,9 +173,9 @@ static __global__ __launch_bounds__(256) void train_fwd_rows_kernel(const TrainR
   {
     const int W = IN + D, KP = ((IN + 15) >> 4) << 4;
     const int64_t base = a.bstep ? (int64_t)(*a.bstep) * a.batch : 0;
-    for (int i = tid; i < 16 * KP; i += 256) buf[0][(i / KP) * TR_LD + i % KP] = 0.f;
+    for (int i = tid; i < 16 * KP; i += TR_WAVES * 64) buf[0][(i / KP) * TR_LD + i % KP] = 0.f;
     lds_barrier();
-    for (int i = tid; i < 16 * W; i += 256) {
+    for (int i = tid; i < 16 * W; i += TR_WAVES * 64) {
       const int r = i / W, c = i % W, row = i0 + r;
       if (row >= M) continue;
       const int64_t src = a.rows ? a.rows[e * a.stride + base + row] : row;
@@ -146,33 +191,37 @@ static __global__ __launch_bounds__(256) void train_fwd_rows_kernel(const TrainR
     lds_barrier();
   }
   // ---- 4 swish layers + the fused heads; lane (li, lk) holds rows 4 lk + i, columns c0 .. c0 + 3
-  const int c0 = 64 * w + 4 * li;
+  const int c0 = 64 * (w & 3) + 4 * li + TR_TW * (w >> 2);   // this lane's first column
   auto layer = [&](auto gtag, int l) {
     constexpr int G = decltype(gtag)::value;
     const int K = l == 0 ? IN : H, N = l == TR_NHID ? 2 * D : H;
     const float* Wl = a.P + a.W[l] + (int64_t)e * K * N;
-    const f32x4 bias = c0 < N ? ld4(a.P + a.b[l] + (int64_t)e * N + c0) : zero4();
-    f32x4 acc[4];
-    rows_gemm<false, G>(buf[l & 1], Wl, K, N, N, w, lane, acc);
+    float bias[TR_TW] = {};
+    if (c0 < N) ld_tw<TR_TW>(a.P + a.b[l] + (int64_t)e * N + c0, bias);
+    f32x4 acc[TR_TW];
+    rows_gemm<false, G, TR_TW>(buf[l & 1], Wl, K, N, N, c0, lane, acc);
     float* out = buf[(l + 1) & 1];
-    if (64 * w < N) {
+    if (__builtin_amdgcn_readfirstlane(c0 - 4 * li) < N) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {                      // D: row 4 lk + i; tile q = column c0 + q
         const int r = 4 * lk + i, row = i0 + r;
         const bool ok = row < M && c0 < N;
-        f32x4 v;
+        float v[TR_TW];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = acc[q][i] + bias[q];
+        for (int q = 0; q < TR_TW; ++q) v[q] = acc[q][i] + bias[q];
         if (l < TR_NHID) {
           const int64_t o = ((int64_t)e * M + row) * H + c0;
-          if (ok) *reinterpret_cast<f32x4*>(a.Z[l] + o) = v;   // pre-activation (swish' in the backward)
+          if (ok) st_tw<TR_TW>(a.Z[l] + o, v);             // pre-activation (swish' in the backward)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = swish_fast(v[q]);
-          if (ok) *reinterpret_cast<f32x4*>(a.Hh[l] + o) = v;
+          for (int q = 0; q < TR_TW; ++q) v[q] = swish_fast(v[q]);
+          if (ok) st_tw<TR_TW>(a.Hh[l] + o, v);
         } else if (ok) {
-          *reinterpret_cast<f32x4*>(a.OUT + ((int64_t)e * M + row) * 2 * D + c0) = v;
+          st_tw<TR_TW>(a.OUT + ((int64_t)e * M + row) * 2 * D + c0, v);
         }
-        *reinterpret_cast<f32x4*>(out + r * TR_LD + c0) = ok ? v : zero4();
+        if (!ok)
+#pragma unroll
+          for (int q = 0; q < TR_TW; ++q) v[q] = 0.f;
+        st_tw<TR_TW>(out + r * TR_LD + c0, v);
       }
     }
     lds_barrier();
@@ -182,7 +231,7 @@ static __global__ __launch_bounds__(256) void train_fwd_rows_kernel(const TrainR
   // ---- output gradient (train_loss_kernel's math, per (row, d)) and the block's partial sums
   const float* o = buf[(TR_NHID + 1) & 1];
   const float s = 1.f / ((float)M * (float)D);
-  for (int i = tid; i < 16 * D; i += 256) {
+  for (int i = tid; i < 16 * D; i += TR_WAVES * 64) {
     const int r = i / D, d = i % D, row = i0 + r;
     float c_mx = 0.f, c_mn = 0.f, c_loss = 0.f;
     if (row < M) {
@@ -253,7 +302,7 @@ static __device__ __forceinline__ void train_loss_tail(const TrainRows& a, float
 // ---- activation-gradient chain ------------------------------------------------------------------
 // GD / GH: k-groups of the heads' width 2D / the hidden width
 template <int GD, int GH>
-static __global__ __launch_bounds__(256) void train_bwd_rows_kernel(const TrainRows a) {
+static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_bwd_rows_kernel(const TrainRows a) {
   __shared__ __attribute__((aligned(16))) float buf[2][16 * TR_LD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lk = lane >> 4;
   if (blockIdx.x == gridDim.x - 1) {                      // the batch-level tail (last block)
@@ -265,36 +314,38 @@ static __global__ __launch_bounds__(256) void train_bwd_rows_kernel(const TrainR
   const int M = a.M, H = a.H, D = a.D, i0 = rb * 16;
   {  // dY of the heads into buf[0], zero-padded to a multiple of 16 columns
     const int N = 2 * D, NP = ((N + 15) >> 4) << 4;
-    for (int i = tid; i < 16 * NP; i += 256) {
+    for (int i = tid; i < 16 * NP; i += TR_WAVES * 64) {
       const int r = i / NP, c = i % NP, row = i0 + r;
       buf[0][r * TR_LD + c] = (row < M && c < N) ? a.dOUT[((int64_t)e * M + row) * N + c] : 0.f;
     }
     lds_barrier();
   }
-  const int c0 = 64 * w + 4 * li;
+  const int c0 = 64 * (w & 3) + 4 * li + TR_TW * (w >> 2);   // this lane's first column
   auto layer = [&](auto gtag, int l) {
     constexpr int G = decltype(gtag)::value;
     const int Kl = H, Nl = l == TR_NHID ? 2 * D : H;     // layer l: [Kl -> Nl]; dZ_{l-1} is 16 x Kl
     const float* Wl = a.P + a.W[l] + (int64_t)e * Kl * Nl;
-    f32x4 zm[4];                                          // swish'(Z_{l-1}) operands, fetched up front
+    float zm[4][TR_TW];                                   // swish'(Z_{l-1}) operands, fetched up front
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = i0 + 4 * lk + i;
-      zm[i] = (c0 < Kl && row < M) ? ld4(a.Z[l - 1] + ((int64_t)e * M + row) * H + c0) : zero4();
+#pragma unroll
+      for (int q = 0; q < TR_TW; ++q) zm[i][q] = 0.f;
+      if (c0 < Kl && row < M) ld_tw<TR_TW>(a.Z[l - 1] + ((int64_t)e * M + row) * H + c0, zm[i]);
     }
-    f32x4 acc[4];
-    rows_gemm<true, G>(buf[(TR_NHID - l) & 1], Wl, Nl, Kl, Nl, w, lane, acc);
+    f32x4 acc[TR_TW];
+    rows_gemm<true, G, TR_TW>(buf[(TR_NHID - l) & 1], Wl, Nl, Kl, Nl, c0, lane, acc);
     float* out = buf[(TR_NHID - l + 1) & 1];
-    if (64 * w < Kl) {
+    if (__builtin_amdgcn_readfirstlane(c0 - 4 * li) < Kl) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 4 * lk + i, row = i0 + r;
         const bool ok = row < M && c0 < Kl;
-        f32x4 v;
+        float v[TR_TW];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = ok ? acc[q][i] * dswish_fast(zm[i][q]) : 0.f;
-        if (ok) *reinterpret_cast<f32x4*>(a.dZ[l - 1] + ((int64_t)e * M + row) * H + c0) = v;
-        *reinterpret_cast<f32x4*>(out + r * TR_LD + c0) = v;
+        for (int q = 0; q < TR_TW; ++q) v[q] = ok ? acc[q][i] * dswish_fast(zm[i][q]) : 0.f;
+        if (ok) st_tw<TR_TW>(a.dZ[l - 1] + ((int64_t)e * M + row) * H + c0, v);
+        st_tw<TR_TW>(out + r * TR_LD + c0, v);
       }
     }
     lds_barrier();
