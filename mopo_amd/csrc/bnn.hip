@@ -21,6 +21,7 @@
 
 #include <vector>
 #include <cstring>
+#include <type_traits>
 #include <cmath>
 
 namespace mopo {
@@ -701,6 +702,246 @@ __global__ __launch_bounds__(WAVES * 64, R == 1 ? 2 : 1) void bnn_fwd_f16r_kerne
   }
 }
 
+// ---- f16x3 forward over a 3-slot LDS ring (BNN_F16_RING): bnn_fwd_f16s_kernel's arithmetic, product for
+// product, with the weight slices of all five layers as ONE stream (layer 0: 2 slices, each hidden layer
+// and the head: 2 KG).  Slice j + 2 is copied while slice j is consumed, so two slices are in flight
+// across every barrier: the barrier is a raw s_barrier behind a counted `s_waitcnt vmcnt(N)` that retires
+// only slice j's copies (N = the next slice's copies per wave; __syncthreads() would drain vmcnt(0)), and
+// no layer starts on an exposed copy (the layer_lds_split_f32 path stages each layer's first slice behind a
+// barrier of its own).  A layer's bias goes out at the top of its first slice (after the barrier that
+// retires the previous layer's epilogue reads of lds_bias) and is retired by the next slice's wait.
+#ifndef BNN_F16_RING
+#define BNN_F16_RING 1
+#endif
+#ifndef BNN_F16Q_DEFER
+#define BNN_F16Q_DEFER 0  // 1: the swish of k-group c in the MFMA gaps of k-group c - 1 (see below)
+#endif
+
+template <int J, int JEND>
+struct RingRun {  // f(integral_constant<J>) for J in [J, JEND), unrolled at compile time
+  template <class F>
+  __device__ __forceinline__ static void run(F&& f) {
+    f(std::integral_constant<int, J>{});
+    RingRun<J + 1, JEND>::run(f);
+  }
+};
+template <int JEND>
+struct RingRun<JEND, JEND> {
+  template <class F>
+  __device__ __forceinline__ static void run(F&&) {}
+};
+
+// s_waitcnt vmcnt(N) expcnt(7) lgkmcnt(0) (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+  static_assert(N >= 0 && N < 64, "vmcnt out of range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
+}
+
+template <int NB2, int NBO, int MODE, int WAVES, int NBU = NB2>
+__global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES) void bnn_fwd_f16q_kernel(const BnnDev w,
+                                                                                            const FwdArgs a) {
+  constexpr int KG = NB2 / 2, NS = 2 + 8 * KG;
+  constexpr bool KH = NBU < NB2;
+  constexpr int SLOT = Stage<(NB2 > NBO ? NB2 : NBO), WAVES>::SLOTS * 256;
+  constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;
+  __shared__ __attribute__((aligned(16))) float lds[3 * SLOT + BIAS_LDS];  // one array (see layer_lds)
+  float* lds_bias = lds + 3 * SLOT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
+  const int groups = ceil_div(a.ntiles, WAVES);
+  const int C = ceil_div(groups, 8);  // XCD-aware order (bnn_fwd_f16s_kernel)
+  const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  // uniform (SGPR) member: its weight scales come in by scalar loads, which leave vmcnt alone
+  const int e = __builtin_amdgcn_readfirstlane(jb / C), grp = __builtin_amdgcn_readfirstlane(xcd * C + jb % C);
+  if (grp >= groups) return;
+  const int64_t row = (int64_t)(grp * WAVES + wv) * 16 + m;
+  if ((int64_t)grp * WAVES * 16 >= count) return;
+  const int IN = w.IN, O = w.O, E = w.E;
+  const bool ok = row < count;
+  auto row_max = [&](float mx) {
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    return fmaxf(mx, __shfl_xor(mx, 32));
+  };
+  // slice stream: layer L (0 input, 1..3 hidden, 4 head) owns slices [2 + 2 KG (L - 1), ...) (layer 0: [0, 2))
+  const float* src[5];
+  src[0] = w.w0b + (int64_t)e * 2 * NB2 * 256;
+#pragma unroll
+  for (int l = 0; l < 3; ++l) src[1 + l] = w.whb + ((int64_t)l * E + e) * KG * 2 * NB2 * 256;
+  src[4] = w.whdb + (int64_t)e * KG * 2 * NBO * 256;
+  auto issue = [&](auto jc) {  // every wave's copies of slice J (PER per wave, pads re-read a fragment)
+    constexpr int J = decltype(jc)::value;
+    if constexpr (J < NS) {
+      constexpr int L = J < 2 ? 0 : 1 + (J - 2) / (2 * KG);
+      constexpr int NF = L == 4 ? NBO : NB2;
+      constexpr int s = J - (L == 0 ? 0 : 2 + 2 * KG * (L - 1));
+      stage_slice<NF, WAVES>(src[L] + s * NF * 256, lds + (J % 3) * SLOT, wv, lane);
+    }
+  };
+
+  float xv[8];
+  if (a.xs) {  // rollout: the actor already wrote the scaled row in slot order (bf16_kperm)
+    const f32x4 lo = ok ? ld4(a.xs + row * XS_STRIDE + 4 * g) : zero4();
+    const f32x4 hi = ok ? ld4(a.xs + row * XS_STRIDE + 16 + 4 * g) : zero4();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      xv[t] = lo[t];
+      xv[4 + t] = hi[t];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = slot_feat(bf16_kperm(g, j), IN);
+      float v = 0.f;
+      if (ok && k >= 0) {
+        float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
+                          : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
+        v = (raw - w.mu[k]) / w.sigma[k];
+      }
+      xv[j] = v;
+    }
+  }
+  // the five layers' weight scales, loaded with the row and kept in SGPRs: a vector load of one later would
+  // be waited for with vmcnt(0), draining the two slices in flight
+  float wsc[5];
+#pragma unroll
+  for (int l = 0; l < 5; ++l) wsc[l] = w.wscale[l * E + e];
+#pragma unroll
+  for (int l = 0; l < 5; ++l) wsc[l] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wsc[l])));
+  float mx0 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mx0 = fmaxf(mx0, fabsf(xv[j]));
+  float s_in, inv_row;
+  row_scale(row_max(mx0), s_in, inv_row);
+  // the input row is in registers (its loads retired by the row scale) before the first copies go out
+  __builtin_amdgcn_sched_barrier(0);
+  issue(std::integral_constant<int, 0>{});
+  issue(std::integral_constant<int, 1>{});
+
+  const int64_t bs = w.BS;
+  constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.6931471805599453f;
+  f32x4 acc[NB2 > NBO ? NB2 : NBO];
+  float hf[KG][8];
+  bf16x8 cur[2];
+  // the bias is read with the fragments' type: read as f32x4, hipcc drained vmcnt(0) in front of it (the
+  // two slices in flight) as if it might alias the pending LDS-DMA writes
+  auto bias4 = [&](int off) { return __builtin_bit_cast(f32x4, *reinterpret_cast<const bf16x8*>(lds_bias + off)); };
+#if BNN_F16Q_DEFER
+  // Deferred swish: the epilogue right after a layer only forms u = -log2(e) t = acc f + b' and the row
+  // scale from max |u| (|y'| = |u| / (1 + 2^u) <= |u|, so y' s stays below 2^15), and the activation
+  // y' = u / (1 + 2^u) of k-group c is made during the MFMAs of k-group c - 1 of the next layer (its
+  // exp / rcp in the MFMA issue gaps) -- the transcendental half of the epilogue no longer runs between
+  // two layers' MFMA streams.
+  auto to_input = [&](float f) {
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < KG; ++c) {
+      const f32x4 b0 = bias4((2 * c) * 16 + 4 * g);
+      const f32x4 b1 = bias4((2 * c + 1) * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        hf[c][t] = fmaf(acc[2 * c][t], f, b0[t]);
+        hf[c][4 + t] = 2 * c + 1 < NBU ? fmaf(acc[2 * c + 1][t], f, b1[t]) : 0.f;
+        mx = fmaxf(mx, fmaxf(fabsf(hf[c][t]), fabsf(hf[c][4 + t])));
+      }
+    }
+    row_scale(row_max(mx), s_in, inv_row);
+  };
+  auto act = [&](int c, int j) {  // y' of value j of k-group c (the padding block of an odd count stays 0)
+    if (j < 4 || 2 * c + 1 < NBU) hf[c][j] = swish_log2(hf[c][j]);
+  };
+#else
+  auto to_input = [&](float f) {  // bnn_fwd_f16s_kernel's epilogue (log2 domain), then the new row scale
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < KG; ++c) {
+      const f32x4 b0 = bias4((2 * c) * 16 + 4 * g);
+      const f32x4 b1 = bias4((2 * c + 1) * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        hf[c][t] = swish_log2(fmaf(acc[2 * c][t], f, b0[t]));
+        hf[c][4 + t] = 2 * c + 1 < NBU ? swish_log2(fmaf(acc[2 * c + 1][t], f, b1[t])) : 0.f;
+        mx = fmaxf(mx, fmaxf(fabsf(hf[c][t]), fabsf(hf[c][4 + t])));
+      }
+    }
+    row_scale(row_max(mx), s_in, inv_row);
+  };
+  auto act = [&](int, int) {};
+#endif
+  // layer L: NBL output blocks (NBUL used), KGL k-groups of input `in`, slices [J0, J0 + 2 KGL)
+  auto layer = [&](auto Lc, auto& in) {
+    constexpr int L = decltype(Lc)::value;
+    constexpr int KGL = L == 0 ? 1 : KG, NBL = L == 4 ? NBO : NB2, NBUL = L == 4 ? NBO : NBU;
+    constexpr bool KHL = L > 0 && KH;
+    constexpr bool DEFER = BNN_F16Q_DEFER && L > 0;   // `in` holds u; y' made one k-group ahead
+    constexpr int J0 = L == 0 ? 0 : 2 + 2 * KG * (L - 1);
+#pragma unroll
+    for (int nb = 0; nb < NBL; ++nb) acc[nb] = zero4();
+    if constexpr (DEFER) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) act(0, j);
+    }
+    RingRun<J0, J0 + 2 * KGL>::run([&](auto jc) {
+      constexpr int J = decltype(jc)::value, s = J - J0, kg = s / 2, p = s % 2;
+      if constexpr (p == 0) {  // the k-group's two fp16 parts (split_f16_pair), made when first consumed
+        u32x4v h4, l4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const F16Pair pr = split_f16_pair(in[kg][2 * q], in[kg][2 * q + 1], s_in);
+          h4[q] = pr.hi;
+          l4[q] = pr.lo;
+        }
+        cur[0] = __builtin_bit_cast(bf16x8, h4);
+        cur[1] = __builtin_bit_cast(bf16x8, l4);
+      }
+      wait_vm_lgkm0<(J + 1 >= NS ? 0 : (((J + 1 >= 2 + 6 * KG) ? NBO : NB2) + WAVES - 1) / WAVES)>();  // slice J landed
+      __builtin_amdgcn_s_barrier();  // ... for every wave; every wave is done with slice J - 1's buffer
+      if constexpr (s == 0 && L < 4) stage_bias<NB2 * 4, WAVES>(L == 0 ? w.b0 + e * bs : w.bh + ((int64_t)(L - 1) * E + e) * bs,
+                                                              lds_bias, wv, lane);
+      issue(std::integral_constant<int, J + 2>{});
+      __builtin_amdgcn_sched_barrier(0);
+      const float* b = lds + (J % 3) * SLOT;
+      bf16x8 fr_next = *reinterpret_cast<const bf16x8*>(b + lane * 4);
+#pragma unroll
+      for (int nb = 0; nb < NBUL; ++nb) {
+        const bf16x8 fr = fr_next;
+        if (nb + 1 < NBUL) fr_next = *reinterpret_cast<const bf16x8*>(b + ((nb + 1) * 64 + lane) * 4);
+        // part 0 of W meets both activation parts (x1 first), part 1 only the high part: the product
+        // order of layer_lds_split_f32
+#pragma unroll
+        for (int q = 1 - p; q >= 0; --q)
+          acc[nb] = (KHL && kg + 1 == KGL) ? mfma_16x16x16_lo<true>(fr, cur[q], acc[nb])
+                                           : mfma_16x16x32<true>(fr, cur[q], acc[nb]);
+        // the next k-group's activations, spread over this k-group's two slices: values 4 p .. 4 p + 3
+        if constexpr (DEFER && kg + 1 < KGL) {
+          constexpr int step = NBUL / 4 > 0 ? NBUL / 4 : 1;
+          if (nb % step == step - 1 && nb / step < 4) act(kg + 1, 4 * p + nb / step);
+        }
+      }
+    });
+  };
+  {
+    float x1[1][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x1[0][j] = xv[j];
+    layer(std::integral_constant<int, 0>{}, x1);
+  }
+  to_input(inv_row * wsc[0] * kNegLog2e);  // layer 0's input is x itself
+  layer(std::integral_constant<int, 1>{}, hf);
+  to_input(inv_row * wsc[1]);
+  layer(std::integral_constant<int, 2>{}, hf);
+  to_input(inv_row * wsc[2]);
+  layer(std::integral_constant<int, 3>{}, hf);
+  to_input(inv_row * wsc[3]);
+  layer(std::integral_constant<int, 4>{}, hf);
+  f32x4 hd[NBO];
+  const float f = inv_row * wsc[4] * kNegLn2;  // the head's input is y' = -log2(e) y
+#pragma unroll
+  for (int nb = 0; nb < NBO; ++nb) hd[nb] = acc[nb] * f;
+  head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
+                           (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
+}
+
 #ifndef BNN_R13
 #define BNN_R13 1  // row blocks per wave at H = 200
 #endif
@@ -805,6 +1046,20 @@ static int launch_f16s(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
 #endif
   // NBU: hidden blocks in use (NB2 - 1 when the block count is odd, e.g. H = 200 -> 13 of 14).  Not at
   // H = 400 (25 of 26): the register allocation it gets there (VGPR + AGPR split) measured 17 % slower.
+  if constexpr (BNN_F16_RING && NB2 <= 16) {
+    if (h->dev.NBH == NB2 - 1) {
+      if (mode == FWD_PREDICT)
+        hipLaunchKernelGGL((bnn_fwd_f16q_kernel<NB2, NBO, FWD_PREDICT, WV, NB2 - 1>), grid, block, 0, s, h->dev, a);
+      else
+        hipLaunchKernelGGL((bnn_fwd_f16q_kernel<NB2, NBO, FWD_ROLLOUT, WV, NB2 - 1>), grid, block, 0, s, h->dev, a);
+    } else if (mode == FWD_PREDICT) {
+      hipLaunchKernelGGL((bnn_fwd_f16q_kernel<NB2, NBO, FWD_PREDICT, WV>), grid, block, 0, s, h->dev, a);
+    } else {
+      hipLaunchKernelGGL((bnn_fwd_f16q_kernel<NB2, NBO, FWD_ROLLOUT, WV>), grid, block, 0, s, h->dev, a);
+    }
+    MOPO_HIP(hipGetLastError());
+    return 0;
+  }
   if (NB2 <= 16 && h->dev.NBH == NB2 - 1) {
     if (mode == FWD_PREDICT)
       hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_PREDICT, WV, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);

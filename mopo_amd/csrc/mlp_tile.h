@@ -381,6 +381,9 @@ __device__ __forceinline__ void row_scale(float mx, float& s, float& inv) {
   inv = __uint_as_float((eb - 14u) << 23);
 }
 
+#ifndef MOPO_SPLIT_PF
+#define MOPO_SPLIT_PF 1  // LDS fragment reads in flight in layer_lds_split_f32
+#endif
 // layer_lds_split with f32 activations held (8 VGPRs per k-group instead of 4 * P): each k-group's P
 // bf16 parts are split when its first slice is consumed, so only one k-group's parts are live.
 // F16: the 2 fp16 parts of in * s (split_f16_scaled; s = the row scale) on the f16 MFMA.
@@ -428,6 +431,7 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
     if (s + 1 < S) stage_slice<NF, WAVES>(wf + (s + 1) * NF * 256, lds + ((s + 1) & 1) * SLOT, w, lane);
     __builtin_amdgcn_sched_barrier(0);
     const float* b = lds + (s & 1) * SLOT;
+#if MOPO_SPLIT_PF <= 1
     // fragment i's successor is read before fragment i's MFMAs (one LDS read in flight); output
     // blocks nb >= NBU (the padding block of an odd hidden-block count) are skipped
     bf16x8 fr_next = *reinterpret_cast<const bf16x8*>(b + lane * 4);
@@ -443,6 +447,27 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
         acc[nb] = (KH && kg + 1 == KG) ? mfma_16x16x16_lo<F16>(fr, cur[q], acc[nb])
                                        : mfma_16x16x32<F16>(fr, cur[q], acc[nb]);
     }
+#else
+    // MOPO_SPLIT_PF = D reads in flight: the used fragments of the slice (padding blocks skipped) are
+    // consumed in order u = 0, 1, ... and fragment u + D is read before fragment u's MFMAs
+    constexpr int D = MOPO_SPLIT_PF;
+    constexpr int NU = (NF / NB) * NBU;  // used fragments of the slice
+    auto frag_at = [&](int u) { return (u / NBU) * NB + u % NBU; };
+    bf16x8 ring[D];
+#pragma unroll
+    for (int u = 0; u < D && u < NU; ++u) ring[u] = *reinterpret_cast<const bf16x8*>(b + (frag_at(u) * 64 + lane) * 4);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = frag_at(u);
+      const int pp = i / NB, nb = i % NB, p = (s % SPK) * PS + pp;
+      const bf16x8 fr = ring[u % D];
+      if (u + D < NU) ring[u % D] = *reinterpret_cast<const bf16x8*>(b + (frag_at(u + D) * 64 + lane) * 4);
+#pragma unroll
+      for (int q = P - 1 - p; q >= 0; --q)
+        acc[nb] = (KH && kg + 1 == KG) ? mfma_16x16x16_lo<F16>(fr, cur[q], acc[nb])
+                                       : mfma_16x16x32<F16>(fr, cur[q], acc[nb]);
+    }
+#endif
   }
 }
 
