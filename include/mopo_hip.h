@@ -277,6 +277,12 @@ int mopo_sac_step(mopo_sac_t h, const mopo_pool_desc* env_pool, const mopo_pool_
                   int n_steps, uint64_t seed, const int64_t* d_idx, const float* d_eps_s,
                   const float* d_eps_n, void* stream);
 int mopo_sac_set_graph(mopo_sac_t h, int enable);
+/* Target-network schedule (mopo.py:834-845 `if iteration % target_update_interval == 0:
+ * _update_target()`, iteration = the epoch-local timestep of mopo.py:545-571, shared by the
+ * n_train_repeat steps of a timestep, :790-795): the step whose device step counter is c updates the
+ * targets iff ((c - base) / n_train_repeat) % interval == 0.  Enqueued on `stream` (it orders with
+ * mopo_sac_step); the default {0, 1, 1} updates on every step. */
+int mopo_sac_set_target_schedule(mopo_sac_t h, int64_t base, int64_t n_train_repeat, int64_t interval, void* stream);
 /* device<->device copy of a handle buffer (which: 0 params, 1 target, 2 adam_m, 3 adam_v, 4 grads,
  * 5 logs); to_handle=1 writes the handle's buffer from d_buf (e.g. loading a checkpoint). */
 int mopo_sac_copy(mopo_sac_t h, int which, int to_handle, void* d_buf, int64_t count, void* stream);

@@ -292,7 +292,10 @@ __device__ __forceinline__ void actor_finish(const ActorArgs& a, float (&head)[A
 
 // TQ0: k-steps in the last k-group of the observation (tail_steps(O); 4 = all)
 template <int KG0, int NBP, int TQ0 = 4>
-__global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? 4 : 2) void actor_kernel(const ActorArgs a) {
+#ifndef ACT_F32_OCC
+#define ACT_F32_OCC 4  // fp32 actor workgroups per CU at H = 256 (4: 128 VGPRs)
+#endif
+__global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? ACT_F32_OCC : 2) void actor_kernel(const ActorArgs a) {
   constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
   __shared__ float head[ACT_WAVES][16][25];  // head outputs [0, 16), then the actions [16, 16 + A)
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + (NBP * 4 + 63) / 64 * 256];  // one array (bnn.hip)
@@ -553,6 +556,165 @@ __global__ __launch_bounds__(ACT_WAVES * 64, R == 1 ? 2 : 1) void actor_f16r_ker
   }
 }
 
+// f16x3 policy forward over a 3-slot LDS ring (ACT_F16_RING; bnn.hip bnn_fwd_f16q_kernel's pipeline):
+// actor_f16_kernel's arithmetic, product for product, with the weight slices as ONE stream -- layer 1
+// (2 slices: the fp16 parts), layer 2 (2 KG slices) and the whole head (its 2 KG fragments as one
+// slice) -- slice j + 2 copied while slice j is consumed, behind counted vmcnt + raw barriers.  The
+// hidden biases ride into LDS once, ahead of the first slices; the head's output rows reuse a ring slot.
+#ifndef ACT_F16_RING
+#define ACT_F16_RING 0  // same-box A/B: actor 0.062 -> 0.054 ms alone, but the rollout 1.6 % slower (203 VGPRs
+                        // beside the concurrent ensemble launch of the other row part), so it stays off
+#endif
+template <int NBP>
+__global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16q_kernel(const ActorArgs a) {
+  static_assert(NBP == 16, "ring actor: hidden 256");
+  constexpr int KG = NBP / 2, NS = 2 + 2 * KG + 1;  // layer 1, layer 2, head
+  constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256, PER = Stage<NBP, ACT_WAVES>::PER;
+  static_assert(2 * KG <= NBP, "the head's fragments fit one slice");
+  static_assert(ACT_WAVES * 16 * 25 <= SLOT, "the head rows fit one ring slot");
+  constexpr int BQ = (2 * NBP * 16 + 16) / 4;   // b1 | b2 | bh quads (contiguous in the packing)
+  __shared__ __attribute__((aligned(16))) float lds[3 * SLOT + (BQ + 63) / 64 * 256];  // one array (see layer_lds)
+  float* lds_bias = lds + 3 * SLOT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
+  if ((int64_t)blockIdx.x * ACT_WAVES * 16 >= count) return;  // whole workgroup past the live rows
+  const int64_t row = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16 + m;
+  const bool ok = row < count;
+  const int O = a.O;
+  const float* w1f = a.Wpk;
+  const float* w2f = w1f + 2 * NBP * 256;
+  const float* whf = w2f + KG * 2 * NBP * 256;
+  const float* b1 = whf + KG * 2 * 256;
+  const float* b2 = b1 + NBP * 16;
+  const float* bh = b2 + NBP * 16;
+  const float* inv_w = bh + 16;
+  auto row_max = [&](float mx) {
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    return fmaxf(mx, __shfl_xor(mx, 32));
+  };
+  float xv[8], mx = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = slot_feat(bf16_kperm(g, j), O);
+    float v = 0.f;
+    if (ok && k >= 0)
+      v = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
+                    : reinterpret_cast<const float*>(a.obs)[row * O + k];
+    xv[j] = v;
+    mx = fmaxf(mx, fabsf(v));
+  }
+  // per-matrix weight scales in SGPRs (a vector load of one later would be waited for with vmcnt(0),
+  // draining the slices in flight)
+  float sw[3];
+#pragma unroll
+  for (int l = 0; l < 3; ++l) sw[l] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(inv_w[l])));
+  (void)bh;
+  float s_in, inv_row;
+  row_scale(row_max(mx), s_in, inv_row);
+  // slice J: 0, 1 layer 1's parts, 2 .. 2 KG + 1 layer 2 (k-group (J - 2) / 2, part (J - 2) % 2), 2 KG + 2 the head
+  auto issue = [&](auto jc) {
+    constexpr int J = decltype(jc)::value;
+    if constexpr (J < NS) {
+      const float* src = J < 2 ? w1f + J * NBP * 256 : (J < NS - 1 ? w2f + (J - 2) * NBP * 256 : whf);
+      stage_slice<NBP, ACT_WAVES>(src, lds + (J % 3) * SLOT, wv, lane);
+    }
+  };
+  __builtin_amdgcn_sched_barrier(0);
+  stage_bias<BQ, ACT_WAVES>(b1, lds_bias, wv, lane);
+  issue(std::integral_constant<int, 0>{});
+  issue(std::integral_constant<int, 1>{});
+  auto bias4 = [&](int off) { return __builtin_bit_cast(f32x4, *reinterpret_cast<const bf16x8*>(lds_bias + off)); };
+  f32x4 acc[NBP];
+  float hf[KG][8];
+  bf16x8 cur[2];
+  auto to_input = [&](int boff, float f) {  // acc * f + bias, relu (mopo.py:277-278, 301), row scale
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < KG; ++c) {
+      const f32x4 b0 = bias4(boff + (2 * c) * 16 + 4 * g), bb1 = bias4(boff + (2 * c + 1) * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        hf[c][t] = fmaxf(fmaf(acc[2 * c][t], f, b0[t]), 0.f);
+        hf[c][4 + t] = fmaxf(fmaf(acc[2 * c + 1][t], f, bb1[t]), 0.f);
+        mx = fmaxf(mx, fmaxf(hf[c][t], hf[c][4 + t]));
+      }
+    }
+    row_scale(row_max(mx), s_in, inv_row);
+  };
+  auto split = [&](const float (&v)[8]) {
+    u32x4v h4, l4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const F16Pair pr = split_f16_pair(v[2 * q], v[2 * q + 1], s_in);
+      h4[q] = pr.hi;
+      l4[q] = pr.lo;
+    }
+    cur[0] = __builtin_bit_cast(bf16x8, h4);
+    cur[1] = __builtin_bit_cast(bf16x8, l4);
+  };
+  auto top = [&](auto jc) {  // slice J landed for every wave; slice J + 2 goes out
+    constexpr int J = decltype(jc)::value;
+    wait_vm_lgkm0<(J + 1 < NS ? PER : 0)>();
+    __builtin_amdgcn_s_barrier();
+    issue(std::integral_constant<int, J + 2>{});
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // layer 1 and layer 2: slice J (k-group kg, weight part p) feeds NBP blocks
+  auto slices = [&](auto j0c, auto kgc, auto& in) {
+    constexpr int J0 = decltype(j0c)::value, KGL = decltype(kgc)::value;
+#pragma unroll
+    for (int nb = 0; nb < NBP; ++nb) acc[nb] = zero4();
+    RingRun<J0, J0 + 2 * KGL>::run([&](auto jc) {
+      constexpr int J = decltype(jc)::value, s = J - J0, kg = s / 2, p = s % 2;
+      if constexpr (p == 0) split(in[kg]);
+      top(jc);
+      const float* b = lds + (J % 3) * SLOT;
+      bf16x8 fr_next = *reinterpret_cast<const bf16x8*>(b + lane * 4);
+#pragma unroll
+      for (int nb = 0; nb < NBP; ++nb) {
+        const bf16x8 fr = fr_next;
+        if (nb + 1 < NBP) fr_next = *reinterpret_cast<const bf16x8*>(b + ((nb + 1) * 64 + lane) * 4);
+#pragma unroll
+        for (int q = 1 - p; q >= 0; --q) acc[nb] = mfma_16x16x32<true>(fr, cur[q], acc[nb]);
+      }
+    });
+  };
+  {
+    float x1[1][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x1[0][j] = xv[j];
+    slices(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, x1);
+  }
+  to_input(0, inv_row * sw[0]);
+  slices(std::integral_constant<int, 2>{}, std::integral_constant<int, KG>{}, hf);
+  to_input(NBP * 16, inv_row * sw[1]);
+  // the head: its 2 KG fragments (k-group kg: part 0 at 2 kg, part 1 at 2 kg + 1) in slice NS - 1
+  split(hf[0]);
+  top(std::integral_constant<int, NS - 1>{});
+  f32x4 hd = zero4();
+  {
+    const float* b = lds + ((NS - 1) % 3) * SLOT;
+#pragma unroll
+    for (int kg = 0; kg < KG; ++kg) {
+      if (kg > 0) split(hf[kg]);
+      const bf16x8 f0 = *reinterpret_cast<const bf16x8*>(b + ((2 * kg) * 64 + lane) * 4);
+      const bf16x8 f1 = *reinterpret_cast<const bf16x8*>(b + ((2 * kg + 1) * 64 + lane) * 4);
+      hd = mfma_16x16x32<true>(f0, cur[1], hd);   // the product order of layer_lds_split_f32
+      hd = mfma_16x16x32<true>(f0, cur[0], hd);
+      hd = mfma_16x16x32<true>(f1, cur[0], hd);
+    }
+  }
+  // mu | log_std (mopo.py:302-303) into a free ring slot (slot (NS - 1) % 3 holds the head's weights,
+  // the slots of slices NS and NS + 1 were never filled)
+  float (&head)[ACT_WAVES][16][25] = *reinterpret_cast<float (*)[ACT_WAVES][16][25]>(lds + (NS % 3) * SLOT);
+  const float f = inv_row * sw[2];
+  const f32x4 bn = bias4(2 * NBP * 16 + 4 * g);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) head[wv][m][4 * g + t] = fmaf(hd[t], f, bn[t]);
+  __syncthreads();
+  actor_finish(a, head, wv, m, g, row, ok);
+}
+
 int launch_actor(const ActorArgs& a, hipStream_t s) {
   if (a.B == 0) return 0;
   MOPO_REQUIRE(!a.xs || (a.xs_mu && a.xs_sigma && a.xs_in == a.O + a.A && a.xs_in <= XS_STRIDE),
@@ -571,7 +733,8 @@ int launch_actor(const ActorArgs& a, hipStream_t s) {
     return 0;
   }
   if (a.dtype == DT_F16X3) {
-    if (a.Hp == 256) hipLaunchKernelGGL(actor_f16_kernel<16>, grid, block, 0, s, a);
+    if (a.Hp == 256 && ACT_F16_RING) hipLaunchKernelGGL(actor_f16q_kernel<16>, grid, block, 0, s, a);
+    else if (a.Hp == 256) hipLaunchKernelGGL(actor_f16_kernel<16>, grid, block, 0, s, a);
     else if (a.Hp == 32) hipLaunchKernelGGL(actor_f16_kernel<2>, grid, block, 0, s, a);
     else return fail("actor f16x3: unsupported hidden size (256 or 32)");
     MOPO_HIP(hipGetLastError());

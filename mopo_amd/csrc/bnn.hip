@@ -702,51 +702,47 @@ __global__ __launch_bounds__(WAVES * 64, R == 1 ? 2 : 1) void bnn_fwd_f16r_kerne
   }
 }
 
-// ---- f16x3 forward over a 3-slot LDS ring (BNN_F16_RING): bnn_fwd_f16s_kernel's arithmetic, product for
-// product, with the weight slices of all five layers as ONE stream (layer 0: 2 slices, each hidden layer
-// and the head: 2 KG).  Slice j + 2 is copied while slice j is consumed, so two slices are in flight
-// across every barrier: the barrier is a raw s_barrier behind a counted `s_waitcnt vmcnt(N)` that retires
-// only slice j's copies (N = the next slice's copies per wave; __syncthreads() would drain vmcnt(0)), and
-// no layer starts on an exposed copy (the layer_lds_split_f32 path stages each layer's first slice behind a
-// barrier of its own).  A layer's bias goes out at the top of its first slice (after the barrier that
-// retires the previous layer's epilogue reads of lds_bias) and is retired by the next slice's wait.
+// ---- ensemble forward over an LDS ring (bnn_fwd_ring_kernel): P = 2 is bnn_fwd_f16s_kernel's f16x3
+// arithmetic (BNN_F16_RING), P = 1 bnn_fwd_bf16_kernel's single-bf16 arithmetic (BNN_BF16_RING), product
+// for product, with the weight slices of all five layers as ONE stream (layer 0: P slices, each hidden
+// layer and the head: P KG; a slice is one weight part of one 32-deep k-group).  Slice j + DEPTH - 1 is
+// copied while slice j is consumed, so DEPTH - 1 slices are in flight across every barrier: the barrier is
+// a raw s_barrier behind a counted `s_waitcnt vmcnt(N)` that retires only slice j's copies (N = the later
+// slices' copies per wave; __syncthreads() would drain vmcnt(0)), and no layer starts on an exposed copy
+// (the layer_lds_split_f32 path stages each layer's first slice behind a barrier of its own).  Layer 0's
+// bias goes out ahead of the first slices, layer L's (L = 1..3) at the top of layer L - 1's first slice,
+// into one of two bias slots (a layer of slice waits and barriers behind it at any depth).
 #ifndef BNN_F16_RING
 #define BNN_F16_RING 1
+#endif
+#ifndef BNN_BF16_RING
+#define BNN_BF16_RING 0
+#endif
+#ifndef BNN_RING_DEPTH_F16
+#define BNN_RING_DEPTH_F16 3  // 3 x 16 KB slots: 3 workgroups per CU
+#endif
+#ifndef BNN_RING_DEPTH_BF16
+#define BNN_RING_DEPTH_BF16 3
 #endif
 #ifndef BNN_F16Q_DEFER
 #define BNN_F16Q_DEFER 0  // 1: the swish of k-group c in the MFMA gaps of k-group c - 1 (see below)
 #endif
 
-template <int J, int JEND>
-struct RingRun {  // f(integral_constant<J>) for J in [J, JEND), unrolled at compile time
-  template <class F>
-  __device__ __forceinline__ static void run(F&& f) {
-    f(std::integral_constant<int, J>{});
-    RingRun<J + 1, JEND>::run(f);
-  }
-};
-template <int JEND>
-struct RingRun<JEND, JEND> {
-  template <class F>
-  __device__ __forceinline__ static void run(F&&) {}
-};
-
-// s_waitcnt vmcnt(N) expcnt(7) lgkmcnt(0) (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
-template <int N>
-__device__ __forceinline__ void wait_vm_lgkm0() {
-  static_assert(N >= 0 && N < 64, "vmcnt out of range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
-}
-
-template <int NB2, int NBO, int MODE, int WAVES, int NBU = NB2>
-__global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES) void bnn_fwd_f16q_kernel(const BnnDev w,
+template <int NB2, int NBO, int MODE, int WAVES, int P, int DEPTH, int NBU = NB2>
+__global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES) void bnn_fwd_ring_kernel(const BnnDev w,
                                                                                             const FwdArgs a) {
-  constexpr int KG = NB2 / 2, NS = 2 + 8 * KG;
+  static_assert(P == 1 || P == 2, "1: bf16, 2: f16x3");
+  static_assert(DEPTH >= 3, "ring of at least 3 slots");
+  constexpr bool F16 = P == 2;
+  constexpr int KG = NB2 / 2, NS = P + 4 * KG * P;
+  constexpr int JHEAD = P + 3 * KG * P;  // the head's first slice
   constexpr bool KH = NBU < NB2;
   constexpr int SLOT = Stage<(NB2 > NBO ? NB2 : NBO), WAVES>::SLOTS * 256;
   constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;
-  __shared__ __attribute__((aligned(16))) float lds[3 * SLOT + BIAS_LDS];  // one array (see layer_lds)
-  float* lds_bias = lds + 3 * SLOT;
+  // two bias slots: layer L's bias (slot L & 1) goes out at the top of layer L - 1's first slice, so it
+  // has a whole layer of slice waits behind it whatever the depth
+  __shared__ __attribute__((aligned(16))) float lds[DEPTH * SLOT + 2 * BIAS_LDS];  // one array (see layer_lds)
+  float* lds_bias0 = lds + DEPTH * SLOT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
@@ -763,21 +759,22 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES) void bnn_fwd_
     mx = fmaxf(mx, __shfl_xor(mx, 16));
     return fmaxf(mx, __shfl_xor(mx, 32));
   };
-  // slice stream: layer L (0 input, 1..3 hidden, 4 head) owns slices [2 + 2 KG (L - 1), ...) (layer 0: [0, 2))
+  // slice stream: layer L (0 input, 1..3 hidden, 4 head) owns slices [P + P KG (L - 1), ...) (layer 0: [0, P))
   const float* src[5];
-  src[0] = w.w0b + (int64_t)e * 2 * NB2 * 256;
+  src[0] = w.w0b + (int64_t)e * P * NB2 * 256;
 #pragma unroll
-  for (int l = 0; l < 3; ++l) src[1 + l] = w.whb + ((int64_t)l * E + e) * KG * 2 * NB2 * 256;
-  src[4] = w.whdb + (int64_t)e * KG * 2 * NBO * 256;
+  for (int l = 0; l < 3; ++l) src[1 + l] = w.whb + ((int64_t)l * E + e) * KG * P * NB2 * 256;
+  src[4] = w.whdb + (int64_t)e * KG * P * NBO * 256;
   auto issue = [&](auto jc) {  // every wave's copies of slice J (PER per wave, pads re-read a fragment)
     constexpr int J = decltype(jc)::value;
     if constexpr (J < NS) {
-      constexpr int L = J < 2 ? 0 : 1 + (J - 2) / (2 * KG);
+      constexpr int L = J < P ? 0 : 1 + (J - P) / (P * KG);
       constexpr int NF = L == 4 ? NBO : NB2;
-      constexpr int s = J - (L == 0 ? 0 : 2 + 2 * KG * (L - 1));
-      stage_slice<NF, WAVES>(src[L] + s * NF * 256, lds + (J % 3) * SLOT, wv, lane);
+      constexpr int s = J - (L == 0 ? 0 : P + P * KG * (L - 1));
+      stage_slice<NF, WAVES>(src[L] + s * NF * 256, lds + (J % DEPTH) * SLOT, wv, lane);
     }
   };
+  const int64_t bs = w.BS;
 
   float xv[8];
   if (a.xs) {  // rollout: the actor already wrote the scaled row in slot order (bf16_kperm)
@@ -801,37 +798,40 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES) void bnn_fwd_
       xv[j] = v;
     }
   }
-  // the five layers' weight scales, loaded with the row and kept in SGPRs: a vector load of one later would
-  // be waited for with vmcnt(0), draining the two slices in flight
-  float wsc[5];
+  // f16x3: the five layers' weight scales, loaded with the row and kept in SGPRs (a vector load of one
+  // later would be waited for with vmcnt(0), draining the slices in flight); the input row's scale
+  float wsc[5] = {1.f, 1.f, 1.f, 1.f, 1.f};
+  float s_in = 1.f, inv_row = 1.f;
+  if constexpr (F16) {
 #pragma unroll
-  for (int l = 0; l < 5; ++l) wsc[l] = w.wscale[l * E + e];
+    for (int l = 0; l < 5; ++l) wsc[l] = w.wscale[l * E + e];
 #pragma unroll
-  for (int l = 0; l < 5; ++l) wsc[l] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wsc[l])));
-  float mx0 = 0.f;
+    for (int l = 0; l < 5; ++l) wsc[l] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wsc[l])));
+    float mx0 = 0.f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) mx0 = fmaxf(mx0, fabsf(xv[j]));
-  float s_in, inv_row;
-  row_scale(row_max(mx0), s_in, inv_row);
-  // the input row is in registers (its loads retired by the row scale) before the first copies go out
+    for (int j = 0; j < 8; ++j) mx0 = fmaxf(mx0, fabsf(xv[j]));
+    row_scale(row_max(mx0), s_in, inv_row);
+  }
+  // the row is in registers before the first copies go out (a later first use of its loads would wait
+  // for the copies too: vmcnt is in order)
+  wait_vm_lgkm0<0>();
   __builtin_amdgcn_sched_barrier(0);
-  issue(std::integral_constant<int, 0>{});
-  issue(std::integral_constant<int, 1>{});
+  stage_bias<NB2 * 4, WAVES>(w.b0 + e * bs, lds_bias0, wv, lane);   // layer 0's bias (slot 0), ahead of every slice
+  RingRun<0, DEPTH - 1>::run([&](auto jc) { issue(jc); });
 
-  const int64_t bs = w.BS;
   constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.6931471805599453f;
   f32x4 acc[NB2 > NBO ? NB2 : NBO];
   float hf[KG][8];
-  bf16x8 cur[2];
+  bf16x8 cur[P];
   // the bias is read with the fragments' type: read as f32x4, hipcc drained vmcnt(0) in front of it (the
-  // two slices in flight) as if it might alias the pending LDS-DMA writes
+  // slices in flight) as if it might alias the pending LDS-DMA writes
+  const float* lds_bias = lds_bias0;   // the slot of the layer whose epilogue runs next
   auto bias4 = [&](int off) { return __builtin_bit_cast(f32x4, *reinterpret_cast<const bf16x8*>(lds_bias + off)); };
-#if BNN_F16Q_DEFER
-  // Deferred swish: the epilogue right after a layer only forms u = -log2(e) t = acc f + b' and the row
-  // scale from max |u| (|y'| = |u| / (1 + 2^u) <= |u|, so y' s stays below 2^15), and the activation
-  // y' = u / (1 + 2^u) of k-group c is made during the MFMAs of k-group c - 1 of the next layer (its
-  // exp / rcp in the MFMA issue gaps) -- the transcendental half of the epilogue no longer runs between
-  // two layers' MFMA streams.
+  // Deferred swish (BNN_F16Q_DEFER): the epilogue right after a layer only forms u = -log2(e) t = acc f + b'
+  // (f16x3: and the row scale from max |u|; |y'| = |u| / (1 + 2^u) <= |u|, so y' s stays below 2^15), and
+  // the activation y' = u / (1 + 2^u) of k-group c is made during the MFMAs of k-group c - 1 of the next
+  // layer (its exp / rcp in the MFMA issue gaps).
+  constexpr bool DEF = BNN_F16Q_DEFER;
   auto to_input = [&](float f) {
     float mx = 0.f;
 #pragma unroll
@@ -840,82 +840,86 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES) void bnn_fwd_
       const f32x4 b1 = bias4((2 * c + 1) * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        hf[c][t] = fmaf(acc[2 * c][t], f, b0[t]);
-        hf[c][4 + t] = 2 * c + 1 < NBU ? fmaf(acc[2 * c + 1][t], f, b1[t]) : 0.f;
-        mx = fmaxf(mx, fmaxf(fabsf(hf[c][t]), fabsf(hf[c][4 + t])));
+        const float u0 = fmaf(acc[2 * c][t], f, b0[t]);
+        const float u1 = 2 * c + 1 < NBU ? fmaf(acc[2 * c + 1][t], f, b1[t]) : 0.f;
+        hf[c][t] = DEF ? u0 : swish_log2(u0);
+        // an odd hidden-block count leaves the last block all padding: zero, not computed
+        hf[c][4 + t] = DEF || 2 * c + 1 >= NBU ? u1 : swish_log2(u1);
+        if constexpr (F16) mx = fmaxf(mx, fmaxf(fabsf(hf[c][t]), fabsf(hf[c][4 + t])));
       }
     }
-    row_scale(row_max(mx), s_in, inv_row);
+    if constexpr (F16) row_scale(row_max(mx), s_in, inv_row);
   };
   auto act = [&](int c, int j) {  // y' of value j of k-group c (the padding block of an odd count stays 0)
     if (j < 4 || 2 * c + 1 < NBU) hf[c][j] = swish_log2(hf[c][j]);
   };
-#else
-  auto to_input = [&](float f) {  // bnn_fwd_f16s_kernel's epilogue (log2 domain), then the new row scale
-    float mx = 0.f;
+  // the operand parts of k-group kg of `in`: f16x3 the two scaled fp16 parts, bf16 the RN bf16 values
+  auto parts = [&](const float (&v)[8]) {
+    if constexpr (F16) {
+      u32x4v h4, l4;
 #pragma unroll
-    for (int c = 0; c < KG; ++c) {
-      const f32x4 b0 = bias4((2 * c) * 16 + 4 * g);
-      const f32x4 b1 = bias4((2 * c + 1) * 16 + 4 * g);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        hf[c][t] = swish_log2(fmaf(acc[2 * c][t], f, b0[t]));
-        hf[c][4 + t] = 2 * c + 1 < NBU ? swish_log2(fmaf(acc[2 * c + 1][t], f, b1[t])) : 0.f;
-        mx = fmaxf(mx, fmaxf(fabsf(hf[c][t]), fabsf(hf[c][4 + t])));
+      for (int q = 0; q < 4; ++q) {
+        const F16Pair pr = split_f16_pair(v[2 * q], v[2 * q + 1], s_in);
+        h4[q] = pr.hi;
+        l4[q] = pr.lo;
       }
+      cur[0] = __builtin_bit_cast(bf16x8, h4);
+      cur[P - 1] = __builtin_bit_cast(bf16x8, l4);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cur[0][j] = to_bf16(v[j]);
     }
-    row_scale(row_max(mx), s_in, inv_row);
   };
-  auto act = [&](int, int) {};
-#endif
-  // layer L: NBL output blocks (NBUL used), KGL k-groups of input `in`, slices [J0, J0 + 2 KGL)
+  // layer L: NBL output blocks (NBUL used), KGL k-groups of input `in`, slices [J0, J0 + P KGL)
   auto layer = [&](auto Lc, auto& in) {
     constexpr int L = decltype(Lc)::value;
     constexpr int KGL = L == 0 ? 1 : KG, NBL = L == 4 ? NBO : NB2, NBUL = L == 4 ? NBO : NBU;
     constexpr bool KHL = L > 0 && KH;
-    constexpr bool DEFER = BNN_F16Q_DEFER && L > 0;   // `in` holds u; y' made one k-group ahead
-    constexpr int J0 = L == 0 ? 0 : 2 + 2 * KG * (L - 1);
+    constexpr bool DEFER = DEF && L > 0;   // `in` holds u; y' made one k-group ahead
+    constexpr int J0 = L == 0 ? 0 : P + P * KG * (L - 1);
 #pragma unroll
     for (int nb = 0; nb < NBL; ++nb) acc[nb] = zero4();
     if constexpr (DEFER) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) act(0, j);
     }
-    RingRun<J0, J0 + 2 * KGL>::run([&](auto jc) {
-      constexpr int J = decltype(jc)::value, s = J - J0, kg = s / 2, p = s % 2;
-      if constexpr (p == 0) {  // the k-group's two fp16 parts (split_f16_pair), made when first consumed
-        u32x4v h4, l4;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const F16Pair pr = split_f16_pair(in[kg][2 * q], in[kg][2 * q + 1], s_in);
-          h4[q] = pr.hi;
-          l4[q] = pr.lo;
-        }
-        cur[0] = __builtin_bit_cast(bf16x8, h4);
-        cur[1] = __builtin_bit_cast(bf16x8, l4);
-      }
-      wait_vm_lgkm0<(J + 1 >= NS ? 0 : (((J + 1 >= 2 + 6 * KG) ? NBO : NB2) + WAVES - 1) / WAVES)>();  // slice J landed
-      __builtin_amdgcn_s_barrier();  // ... for every wave; every wave is done with slice J - 1's buffer
-      if constexpr (s == 0 && L < 4) stage_bias<NB2 * 4, WAVES>(L == 0 ? w.b0 + e * bs : w.bh + ((int64_t)(L - 1) * E + e) * bs,
-                                                              lds_bias, wv, lane);
-      issue(std::integral_constant<int, J + 2>{});
+    RingRun<J0, J0 + P * KGL>::run([&](auto jc) {
+      constexpr int J = decltype(jc)::value, s = J - J0, kg = s / P, p = s % P;
+      if constexpr (p == 0) parts(in[kg]);   // made when the k-group is first consumed
+      // slice J landed (every later slice still in flight may stay so) ... for every wave, and every wave
+      // is done with the buffer slice J + DEPTH - 1 goes into (slice J - 1's)
+      constexpr int N = [] {
+        int n = 0;
+        for (int i = 1; i <= DEPTH - 2; ++i) n += (J + i >= NS ? 0 : (((J + i >= JHEAD) ? NBO : NB2) + WAVES - 1) / WAVES);
+        return n;
+      }();
+      wait_vm_lgkm0<N>();
+      __builtin_amdgcn_s_barrier();
+      // the next layer's bias into slot (L + 1) & 1: every wave is past layer L - 1's epilogue, the last
+      // reader of that slot
+      if constexpr (s == 0 && L < 3)
+        stage_bias<NB2 * 4, WAVES>(w.bh + ((int64_t)L * E + e) * bs, lds_bias0 + ((L + 1) & 1) * BIAS_LDS, wv, lane);
+      issue(std::integral_constant<int, J + DEPTH - 1>{});
       __builtin_amdgcn_sched_barrier(0);
-      const float* b = lds + (J % 3) * SLOT;
+      const float* b = lds + (J % DEPTH) * SLOT;
       bf16x8 fr_next = *reinterpret_cast<const bf16x8*>(b + lane * 4);
 #pragma unroll
       for (int nb = 0; nb < NBUL; ++nb) {
         const bf16x8 fr = fr_next;
         if (nb + 1 < NBUL) fr_next = *reinterpret_cast<const bf16x8*>(b + ((nb + 1) * 64 + lane) * 4);
-        // part 0 of W meets both activation parts (x1 first), part 1 only the high part: the product
-        // order of layer_lds_split_f32
+        // f16x3: part 0 of W meets both activation parts (x1 first), part 1 only the high part (the
+        // product order of layer_lds_split_f32)
 #pragma unroll
-        for (int q = 1 - p; q >= 0; --q)
-          acc[nb] = (KHL && kg + 1 == KGL) ? mfma_16x16x16_lo<true>(fr, cur[q], acc[nb])
-                                           : mfma_16x16x32<true>(fr, cur[q], acc[nb]);
-        // the next k-group's activations, spread over this k-group's two slices: values 4 p .. 4 p + 3
+        for (int q = P - 1 - p; q >= 0; --q)
+          acc[nb] = (KHL && kg + 1 == KGL) ? mfma_16x16x16_lo<F16>(fr, cur[q], acc[nb])
+                                           : mfma_16x16x32<F16>(fr, cur[q], acc[nb]);
+        // the next k-group's activations, spread over this k-group's P slices: values 8 p / P ..,
+        // value v after fragment max((v + 1) NBUL / V - 1, 0) (V = 8 / P per slice)
         if constexpr (DEFER && kg + 1 < KGL) {
-          constexpr int step = NBUL / 4 > 0 ? NBUL / 4 : 1;
-          if (nb % step == step - 1 && nb / step < 4) act(kg + 1, 4 * p + nb / step);
+          constexpr int V = 8 / P;
+#pragma unroll
+          for (int v = 0; v < V; ++v)
+            if (nb == ((v + 1) * NBUL / V - 1 > 0 ? (v + 1) * NBUL / V - 1 : 0)) act(kg + 1, V * p + v);
         }
       }
     });
@@ -928,10 +932,13 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES) void bnn_fwd_
   }
   to_input(inv_row * wsc[0] * kNegLog2e);  // layer 0's input is x itself
   layer(std::integral_constant<int, 1>{}, hf);
+  lds_bias = lds_bias0 + BIAS_LDS;
   to_input(inv_row * wsc[1]);
   layer(std::integral_constant<int, 2>{}, hf);
+  lds_bias = lds_bias0;
   to_input(inv_row * wsc[2]);
   layer(std::integral_constant<int, 3>{}, hf);
+  lds_bias = lds_bias0 + BIAS_LDS;
   to_input(inv_row * wsc[3]);
   layer(std::integral_constant<int, 4>{}, hf);
   f32x4 hd[NBO];
@@ -941,6 +948,34 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES) void bnn_fwd_
   head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
                            (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
 }
+
+template <int NB2, int NBO, int P, int DEPTH>
+static int launch_ring(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
+  constexpr int WV = 4;
+  a.ntiles = (int)ceil_div((int)a.B, 16);
+  if (a.ntiles == 0) return 0;
+  dim3 grid(8 * ceil_div(ceil_div(a.ntiles, WV), 8) * h->E), block(64 * WV);
+  if constexpr (NB2 == 14) {  // H = 200: an odd hidden-block count, the last block is padding (NBU = 13)
+    if (h->dev.NBH == NB2 - 1) {
+      if (mode == FWD_PREDICT)
+        hipLaunchKernelGGL((bnn_fwd_ring_kernel<NB2, NBO, FWD_PREDICT, WV, P, DEPTH, NB2 - 1>), grid, block, 0, s, h->dev, a);
+      else
+        hipLaunchKernelGGL((bnn_fwd_ring_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, DEPTH, NB2 - 1>), grid, block, 0, s, h->dev, a);
+      MOPO_HIP(hipGetLastError());
+      return 0;
+    }
+  }
+  if (mode == FWD_PREDICT) {
+    hipLaunchKernelGGL((bnn_fwd_ring_kernel<NB2, NBO, FWD_PREDICT, WV, P, DEPTH>), grid, block, 0, s, h->dev, a);
+  } else {
+    hipLaunchKernelGGL((bnn_fwd_ring_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, DEPTH>), grid, block, 0, s, h->dev, a);
+  }
+  MOPO_HIP(hipGetLastError());
+  return 0;
+}
+// the ring kernel's shapes: H = 200 (NB2 14, 13 used), or a whole even block count (NBH = NB2)
+template <int NB2>
+static bool ring_shape(const Bnn* h) { return NB2 <= 16 && (h->dev.NBH == NB2 || (NB2 == 14 && h->dev.NBH == 13)); }
 
 #ifndef BNN_R13
 #define BNN_R13 1  // row blocks per wave at H = 200
@@ -994,6 +1029,8 @@ static int launch_fwd_h(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s)
 
 template <int NB2, int NBO, int P>
 static int launch_bf16_p(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
+  if constexpr (P == 1 && BNN_BF16_RING && NB2 <= 16)
+    if (ring_shape<NB2>(h)) return launch_ring<NB2, NBO, 1, BNN_RING_DEPTH_BF16>(h, mode, a, s);
   constexpr int WV = P == 1 ? FWD_WAVES : BNN_SPLIT_WAVES;
   constexpr int PS = P == 1 ? 1 : (BNN_SPLIT_PS == 0 ? P : BNN_SPLIT_PS);
   a.ntiles = (int)ceil_div((int)a.B, 16);
@@ -1046,20 +1083,8 @@ static int launch_f16s(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
 #endif
   // NBU: hidden blocks in use (NB2 - 1 when the block count is odd, e.g. H = 200 -> 13 of 14).  Not at
   // H = 400 (25 of 26): the register allocation it gets there (VGPR + AGPR split) measured 17 % slower.
-  if constexpr (BNN_F16_RING && NB2 <= 16) {
-    if (h->dev.NBH == NB2 - 1) {
-      if (mode == FWD_PREDICT)
-        hipLaunchKernelGGL((bnn_fwd_f16q_kernel<NB2, NBO, FWD_PREDICT, WV, NB2 - 1>), grid, block, 0, s, h->dev, a);
-      else
-        hipLaunchKernelGGL((bnn_fwd_f16q_kernel<NB2, NBO, FWD_ROLLOUT, WV, NB2 - 1>), grid, block, 0, s, h->dev, a);
-    } else if (mode == FWD_PREDICT) {
-      hipLaunchKernelGGL((bnn_fwd_f16q_kernel<NB2, NBO, FWD_PREDICT, WV>), grid, block, 0, s, h->dev, a);
-    } else {
-      hipLaunchKernelGGL((bnn_fwd_f16q_kernel<NB2, NBO, FWD_ROLLOUT, WV>), grid, block, 0, s, h->dev, a);
-    }
-    MOPO_HIP(hipGetLastError());
-    return 0;
-  }
+  if constexpr (BNN_F16_RING && NB2 <= 16)
+    if (ring_shape<NB2>(h)) return launch_ring<NB2, NBO, 2, BNN_RING_DEPTH_F16>(h, mode, a, s);
   if (NB2 <= 16 && h->dev.NBH == NB2 - 1) {
     if (mode == FWD_PREDICT)
       hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_PREDICT, WV, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);

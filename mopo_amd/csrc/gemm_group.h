@@ -10,6 +10,7 @@
 // staged through an XOR-swizzled LDS layout.  Everything here has internal linkage: each
 // translation unit that includes it gets its own copy of the kernel.
 #pragma once
+#include <type_traits>
 #include <cstdlib>
 #include <vector>
 
@@ -86,6 +87,7 @@ struct AdamCtx {
   float tau; int64_t total, n_pi, n_q; // grad-norm logs: [0, n_pi) policy, [n_pi, n_pi + n_q) Q1
   float* norm_part;                  // [slot][2] squared-gradient partials (pi, q) per block
   int slot0;                         // this launch's first slot
+  const float* tgt_on;               // SAC: this step's target-update flag (mopo.py:843-845; NULL: every step)
 };
 
 // SAC log slots (sac.hip, mopo_sac_buffers)
@@ -369,7 +371,8 @@ static __device__ __forceinline__ void adam_apply(const AdamCtx& ad, int64_t i, 
   ad.M[i] = m;
   ad.V[i] = v;
   ad.Pn[i] = p;
-  if (ad.T && i < ad.total) ad.T[i] = (1.f - ad.tau) * a.t + ad.tau * p;   // mopo.py:446-447 (after the updates)
+  // mopo.py:446-447 (after the updates), on the steps whose timestep % target_update_interval == 0 (:843-845)
+  if (ad.T && i < ad.total && (!ad.tgt_on || *ad.tgt_on != 0.f)) ad.T[i] = (1.f - ad.tau) * a.t + ad.tau * p;
 }
 
 
@@ -775,12 +778,10 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
   }
   f32x4 acc0 = zero4(), acc1 = zero4();
   float cs = 0.f;
-  for (int kc = 0; kc < p.K; kc += GKC32) {
-    const int kn = min(GKC32, p.K - kc);
-    int t = tid;
-    asm volatile("" : "+v"(t));
-    stage_dispatch<32>(p, i0, j0, kc, kn, t, As, Bs, oA, oB);
-    __syncthreads();
+  // one 128-deep chunk of the tile out of the staged panels (measured: loading chunk c + 1 during chunk
+  // c's MFMAs from a second LDS buffer pair took 238 VGPRs and 68 KB, 2 workgroups per CU instead of 4,
+  // and BNN.train fell 10.24k -> 9.47k grad-steps/s, same-box A/B)
+  auto compute = [&](const float* A_s, const float* B_s, int kn, int t) {
     const int ra_r = wi * 16 + (t & 15), rb_r = wj * 16 + (t & 15), tlk = (t >> 4) & 3;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -788,8 +789,8 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const int k = 4 * (half * 16 + s) + tlk;
-        ra[s] = As[k * 32 + (ra_r ^ pswz<32>(k))];
-        rb[s] = Bs[k * 32 + (rb_r ^ pswz<32>(k))];
+        ra[s] = A_s[k * 32 + (ra_r ^ pswz<32>(k))];
+        rb[s] = B_s[k * 32 + (rb_r ^ pswz<32>(k))];
       }
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
@@ -798,7 +799,15 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
       }
     }
     if (do_cs)
-      for (int k = tid >> 5; k < kn; k += 8) cs += Bs[k * 32 + ((tid & 31) ^ pswz<32>(k))];
+      for (int k = tid >> 5; k < kn; k += 8) cs += B_s[k * 32 + ((tid & 31) ^ pswz<32>(k))];
+  };
+  for (int kc = 0; kc < p.K; kc += GKC32) {
+    const int kn = min(GKC32, p.K - kc);
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    stage_dispatch<32>(p, i0, j0, kc, kn, t, As, Bs, oA, oB);
+    __syncthreads();
+    compute(As, Bs, kn, t);
     __syncthreads();
   }
 #pragma unroll

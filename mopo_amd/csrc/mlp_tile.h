@@ -1,5 +1,7 @@
 // Register-resident MLP tiles on f32 MFMA with LDS-staged weight slices (shared by bnn.hip, actor.hip).
 #pragma once
+#include <type_traits>
+
 #include "internal.h"
 
 namespace mopo {
@@ -563,6 +565,28 @@ __device__ __forceinline__ void head_f16_rows(const float (&in)[R][KG][8], f32x4
       acc[r] = mfma_16x16x32<true>(f1, c0, acc[r]);
     }
   }
+}
+
+// ---- LDS-ring pipelines (bnn.hip bnn_fwd_f16q_kernel, actor.hip actor_f16q_kernel) --------------
+template <int J, int JEND>
+struct RingRun {  // f(integral_constant<J>) for J in [J, JEND), unrolled at compile time
+  template <class F>
+  __device__ __forceinline__ static void run(F&& f) {
+    f(std::integral_constant<int, J>{});
+    RingRun<J + 1, JEND>::run(f);
+  }
+};
+template <int JEND>
+struct RingRun<JEND, JEND> {
+  template <class F>
+  __device__ __forceinline__ static void run(F&&) {}
+};
+
+// s_waitcnt vmcnt(N) expcnt(7) lgkmcnt(0) (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+  static_assert(N >= 0 && N < 64, "vmcnt out of range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
 }
 
 }  // namespace mopo

@@ -60,8 +60,10 @@ struct Sac {
   float* Pb[2];                   // parameter ping-pong: Pb[0] == P is the canonical copy between calls
   float* norm_part = nullptr;     // [nslots][2]
   int nslots = 0, nslots_cap = 0;
-  float* beta_pow;                // [3] f32 beta1_power, beta2_power (TF1 non-slot vars), this step's lr_t
+  float* beta_pow;                // [4] f32 beta1_power, beta2_power (TF1 non-slot vars), this step's lr_t,
+                                  //     this step's target-update flag
   int64_t* iter;                  // device step counter (Philox)
+  int64_t* tctl;                  // [3] target schedule: base step, n_train_repeat, target_update_interval
   float* logs;                    // [LOG_N]
   // activations
   Batch bt[2];                    // double-buffered batch (step parity)
@@ -172,6 +174,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   ad.G = h->G; ad.Pc = h->Pb[par]; ad.Pn = h->Pb[1 - par]; ad.M = h->M; ad.V = h->V; ad.T = h->T;
   ad.lr_t = h->beta_pow + 2; ad.tau = h->tau; ad.total = o.total; ad.n_pi = o.n_pi; ad.n_q = o.n_q;
   ad.norm_part = h->norm_part;
+  ad.tgt_on = h->beta_pow + 3;
   int slot = 0;
   const float* T = h->T;
   float* G = h->G;
@@ -245,7 +248,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     }
     L.logp_s = h->logp_s; L.logp_n = h->logp_n; L.head_s = h->out[0]; L.rew = bt.rew; L.term = bt.term;
     L.log_alpha = P + o.total; L.gamma = h->gamma; L.rscale = h->rscale;
-    d.ad = ad; d.tent = h->tent; d.lr = h->lr; d.logs = h->logs; d.beta_pow = h->beta_pow; d.iter = h->iter;
+    d.ad = ad; d.tent = h->tent; d.lr = h->lr; d.logs = h->logs; d.beta_pow = h->beta_pow; d.iter = h->iter; d.tctl = h->tctl;
     PolicyRows& pr = d.pr;
     pr.n = n; pr.O = O; pr.A = A; pr.H = H; pr.ncq = ncq1;
     pr.dapart[0] = h->dapart[0]; pr.dapart[1] = h->dapart[1];
@@ -330,8 +333,9 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   reg.push_back({(void**)&h->stamps, (size_t)4 * 1024 * 8 * 8});
 #endif
   f(&h->P, tot); f(&h->G, tot); f(&h->M, tot); f(&h->V, tot); f(&h->T, tot);
-  f(&h->beta_pow, 3); f(&h->logs, LOG_N);
+  f(&h->beta_pow, 4); f(&h->logs, LOG_N);
   reg.push_back({(void**)&h->iter, 8});
+  reg.push_back({(void**)&h->tctl, 3 * 8});
   for (int b = 0; b < 2; ++b) {
     Batch& t = h->bt[b];
     f(&t.sa, n * W); f(&t.xpi, n * W); f(&t.xn, n * W); f(&t.rew, n); f(&t.term, n);
@@ -356,6 +360,8 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   MOPO_HIP(hipMemcpy(h->T, pv.data(), tot * 4, hipMemcpyHostToDevice));
   float bp[2] = {0.9f, 0.999f};
   MOPO_HIP(hipMemcpy(h->beta_pow, bp, 8, hipMemcpyHostToDevice));
+  const int64_t tc[3] = {0, 1, 1};   // target_update_interval = 1: every step
+  MOPO_HIP(hipMemcpy(h->tctl, tc, sizeof(tc), hipMemcpyHostToDevice));
   *out = reinterpret_cast<mopo_sac_t>(h);
   return 0;
 }
@@ -506,6 +512,24 @@ extern "C" int mopo_sac_step(mopo_sac_t hh, const mopo_pool_desc* env, const mop
   if (launch_logs(h, gs)) return -1;
   MOPO_HIP(hipEventRecord(h->ev_out, gs));
   MOPO_HIP(hipStreamWaitEvent(s, h->ev_out, 0));
+  return 0;
+}
+
+namespace mopo {
+__global__ void sac_set_tctl_kernel(int64_t* tctl, int64_t base, int64_t repeat, int64_t interval) {
+  tctl[0] = base; tctl[1] = repeat; tctl[2] = interval;
+}
+}  // namespace mopo
+
+extern "C" int mopo_sac_set_target_schedule(mopo_sac_t hh, int64_t base, int64_t n_train_repeat, int64_t interval,
+                                            void* stream) {
+  Sac* h = reinterpret_cast<Sac*>(hh);
+  MOPO_REQUIRE(h, "mopo_sac_set_target_schedule: NULL handle");
+  MOPO_REQUIRE(n_train_repeat >= 1 && interval >= 1, "mopo_sac_set_target_schedule: repeat and interval must be >= 1");
+  // a launch (not a copy from host memory) so it orders with the caller's stream and with graph replays
+  hipLaunchKernelGGL(sac_set_tctl_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, h->tctl, base, n_train_repeat,
+                     interval);
+  MOPO_HIP(hipGetLastError());
   return 0;
 }
 

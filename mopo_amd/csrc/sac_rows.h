@@ -372,6 +372,7 @@ struct Dh1Args {
   AdamCtx ad;
   float tent, lr;
   float* logs; float* beta_pow; int64_t* iter;
+  const int64_t* tctl;               // target schedule {base, n_train_repeat, interval} (sac.hip mopo_sac_set_target_schedule)
   // the policy's row-local backward chain (gemm_group.h policy_rows_block) as blocks z = ninst + 1 of
   // this launch: block (cq, rb) waits until the 2 ncq1 (s, pi) workgroups of row block rb published
   // their action-gradient partials (agent-scope counter rb_ready[rb], zeroed by the step's last launch)
@@ -437,6 +438,11 @@ static __device__ __forceinline__ void loss_tail_rows(const Dh1Args& a, float* s
   a.beta_pow[2] = lr_t;
   a.beta_pow[0] = b1p * 0.9f;
   a.beta_pow[1] = b2p * 0.999f;
+  {  // the step's timestep (mopo.py:780-799: n_train_repeat steps share one) and its target-update flag
+    const int64_t rep = a.tctl[1] > 0 ? a.tctl[1] : 1, every = a.tctl[2] > 0 ? a.tctl[2] : 1;
+    const int64_t ts = (*a.iter - a.tctl[0]) / rep;
+    a.beta_pow[3] = ((ts % every) + every) % every == 0 ? 1.f : 0.f;
+  }
   *a.iter += 1;
   adam_apply(ad, ad.total, ga, al, lr_t);
 }

@@ -62,7 +62,8 @@ static __device__ __forceinline__ const float* uniform_ptr(const float* p) {
 }
 
 // Workgroups of TR_WAVES waves: wave w owns column block cb = w % 4 (64 columns) and TW = 16 / TR_WAVES
-// of its 4 tiles (two waves per SIMD at 8: one wave's memory waits overlap the other's MFMAs).
+// of its 4 tiles (two waves per SIMD at 8: one wave's memory waits overlap the other's MFMAs; 16: one
+// tile per wave, four waves per SIMD).
 #ifndef TR_WAVES_CFG
 #define TR_WAVES_CFG 8
 #endif
@@ -104,10 +105,12 @@ static __device__ __forceinline__ void rows_gemm(const float* As, const float* W
           const f32x4 v = bload4(d, idx);
 #pragma unroll
           for (int q = 0; q < 4; ++q) bv[u][q] = v[q];
-        } else {
+        } else if constexpr (TW == 2) {
           const f32x2 v = bload2(d, idx);
           bv[u][0] = v[0];
           bv[u][1] = v[1];
+        } else {
+          bv[u][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(d, idx * 4, 0, 0));
         }
       }
     }
@@ -136,13 +139,16 @@ static __device__ __forceinline__ void rows_gemm(const float* As, const float* W
 template <int TW>
 static __device__ __forceinline__ void st_tw(float* p, const float (&v)[TW]) {
   if constexpr (TW == 4) *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
-  else *reinterpret_cast<f32x2*>(p) = f32x2{v[0], v[1]};
+  else if constexpr (TW == 2) *reinterpret_cast<f32x2*>(p) = f32x2{v[0], v[1]};
+  else *p = v[0];
 }
 template <int TW>
 static __device__ __forceinline__ void ld_tw(const float* p, float (&v)[TW]) {
   if constexpr (TW == 4) {
     const f32x4 x = *reinterpret_cast<const f32x4*>(p);
     v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+  } else if constexpr (TW == 1) {
+    v[0] = *p;
   } else {
     const f32x2 x = *reinterpret_cast<const f32x2*>(p);
     v[0] = x[0]; v[1] = x[1];

@@ -39,8 +39,6 @@ class MOPO:
         ``DEFAULT_ENSEMBLE_DTYPE`` ('f16x3': f32 operands as two fp16 parts, f32 accumulate, held to
         the fp32 parity tolerances); 'fp32' runs exact-f32 MFMA.  ``actor_dtype``: the rollout
         policy forward ('fp32' / 'f16x3'; default f16x3 with an f16x3 ensemble, else fp32)."""
-        if target_update_interval != 1:
-            raise NotImplementedError('target_update_interval != 1 (all D4RL configs use 1)')
         self._pool = pool                                   # device SimpleReplayPool of env data
         self._static_fns = static_fns
         self._obs_dim, self._act_dim = obs_dim, act_dim
@@ -68,7 +66,7 @@ class MOPO:
             raise NotImplementedError('policy/Q hidden_sizes must be [H, H] (reference: [256, 256])')
         self._sac = SAC(obs_dim, act_dim, hidden=hs[0], batch_size=batch_size, real_ratio=real_ratio, lr=lr,
                         discount=discount, tau=tau, reward_scale=reward_scale, target_entropy=target_entropy,
-                        seed=seed, reparameterize=reparameterize)
+                        seed=seed, reparameterize=reparameterize, target_update_interval=target_update_interval)
         self._pi_hidden = hs[0]
         self._rollout = None
         self._rollout_length = rollout_length
@@ -126,24 +124,25 @@ class MOPO:
         return self._model.train(x, y, permuted=True, **kwargs)
 
     # -- mopo.py:723-765 (device-resident, perf-mode RNG); ``deterministic`` as mopo.py:558-559 passes it
-    def _rollout_model(self, rollout_batch_size, deterministic=None, **kwargs):
+    def _rollout_model(self, rollout_batch_size, deterministic=None, rollout_key=None, **kwargs):
+        key = self._epoch if rollout_key is None else rollout_key
         modes = dict(penalty_learned_var=self.fake_env.penalty_learned_var,
                      deterministic=self._deterministic if deterministic is None else deterministic,
                      rollout_random=self._rollout_random)
         env_obs = self._pool.fields['observations'][:self._pool.size]
         if self._world > 1:
-            return self._rollout_model_sharded(rollout_batch_size, env_obs, modes)
+            return self._rollout_model_sharded(rollout_batch_size, env_obs, modes, key)
         if self._rollout is None or self._rollout.max_batch < rollout_batch_size or \
                 self._rollout.max_horizon < self._rollout_length:
             self._rollout = ModelRollout(self._model, rollout_batch_size, max(self._rollout_length, 1))
         steps = self._rollout.run(env_obs, self._sac.policy_params_ptr, self._model_pool, rollout_batch_size,
                                   self._rollout_length, self.fake_env.term_kind, self.fake_env.penalty_coeff,
-                                  self._model._model_inds, seed=self._seed, epoch=self._epoch,
+                                  self._model._model_inds, seed=self._seed, epoch=key,
                                   pi_hidden=self._pi_hidden, actor_dtype=self._actor_dtype, **modes)
         added = int(steps.sum().item())
         return {'mean_rollout_length': added / rollout_batch_size}
 
-    def _rollout_model_sharded(self, rollout_batch_size, env_obs, modes):
+    def _rollout_model_sharded(self, rollout_batch_size, env_obs, modes, key):
         """Rank r rolls out rows [r B/N, (r + 1) B/N) of the batch (Philox streams keyed by the global
         row id, so the N shards are exactly the single-GPU rollout's rows) after rank 0's model and SAC
         state are broadcast; every rank's model pool receives all transitions in the single-GPU order."""
@@ -157,28 +156,38 @@ class MOPO:
             self._rollout = DistributedRollout(self._model, b, h, self._obs_dim, self._act_dim)
         steps = self._rollout.run(env_obs, self._sac.policy_params_ptr, self._model_pool, self.fake_env.term_kind,
                                   self.fake_env.penalty_coeff, self._model._model_inds, seed=self._seed,
-                                  epoch=self._epoch, pi_hidden=self._pi_hidden, actor_dtype=self._actor_dtype,
+                                  epoch=key, pi_hidden=self._pi_hidden, actor_dtype=self._actor_dtype,
                                   **modes)
         added = int(steps.sum().item())
         return {'mean_rollout_length': added / rollout_batch_size}
 
-    # -- mopo.py:780-799 + 834-853: n steps of (_training_batch, _do_training, _update_target)
-    def _do_training_repeats(self, n_steps):
-        self._sac._do_training(self._num_train_steps, self._pool, self._model_pool, n_steps=n_steps,
-                               seed=self._seed + 7919 * self._epoch)
+    # -- mopo.py:780-799 + 834-853: n steps of (_training_batch, _do_training, _update_target); the first
+    #    is timestep `first_timestep` of the epoch, each timestep n_train_repeat steps
+    def _do_training_repeats(self, n_steps, first_timestep=0):
+        self._sac._do_training(first_timestep, self._pool, self._model_pool, n_steps=n_steps,
+                               seed=self._seed + 7919 * self._epoch, n_train_repeat=self._n_train_repeat)
         self._num_train_steps += n_steps
         return self._sac.logs()
 
     def _train_epoch(self):
-        """One epoch of mopo.py:536-573 with model_train_freq == epoch_length (all D4RL configs)."""
-        t0 = time.perf_counter()
-        self._set_rollout_length()
-        self._reallocate_model_pool()
-        metrics = self._rollout_model(self._rollout_batch_size)
+        """One epoch of mopo.py:536-573: a model rollout at every ``model_train_freq``-th timestep
+        (mopo.py:554-563; all D4RL configs: one, at timestep 0), and between rollouts the SAC steps of
+        those timesteps (``n_train_repeat`` per timestep, mopo.py:780-799).  The k-th rollout of epoch e
+        draws its Philox streams under the key e * rollouts_per_epoch + k (= e for one rollout per epoch)."""
         import torch
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        logs = self._do_training_repeats(self._epoch_length * self._n_train_repeat)
+        f = self._model_train_freq
+        per_epoch = -(-self._epoch_length // f)
+        metrics, logs = {}, {}
+        t_roll = t_train = 0.0
+        for k, ts in enumerate(range(0, self._epoch_length, f)):
+            t0 = time.perf_counter()
+            self._set_rollout_length()
+            self._reallocate_model_pool()
+            metrics.update(self._rollout_model(self._rollout_batch_size, rollout_key=self._epoch * per_epoch + k))
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            logs = self._do_training_repeats(min(f, self._epoch_length - ts) * self._n_train_repeat, first_timestep=ts)
+            t_roll, t_train = t_roll + t1 - t0, t_train + time.perf_counter() - t1
         t2 = time.perf_counter()
         evaluation = self._evaluate()
         t3 = time.perf_counter()
@@ -188,7 +197,7 @@ class MOPO:
         diag.update(('training/' + k, v) for k, v in logs.items())
         diag.update({'Q_loss': (logs['Q/q1_loss'] + logs['sac_Q/q2_loss']) / 2, 'alpha': logs['sac_pi/alpha'],
                      'epoch': self._epoch, 'train-steps': self._num_train_steps,
-                     'times/epoch_rollout_model': t1 - t0, 'times/train': t2 - t1,
+                     'times/epoch_rollout_model': t_roll, 'times/train': t_train,
                      'times/evaluation_paths': t3 - t2})
         if evaluation:
             from .evaluation import perf_metrics
@@ -207,8 +216,6 @@ class MOPO:
 
     def train(self, n_epochs=None):
         """Generator of per-epoch diagnostics (mopo.py:650-651)."""
-        if self._model_train_freq != self._epoch_length:
-            raise NotImplementedError('model_train_freq must equal epoch_length (all D4RL configs: 1000)')
         if self._model_train_metrics is None:                                            # mopo.py:526-531
             t0 = time.perf_counter()
             max_epochs = 1 if self._model.model_loaded else None

@@ -55,8 +55,6 @@ class SAC:
                            batch_size=256, real_ratio=1.0, **kwargs):
         if action_prior != 'uniform':
             raise NotImplementedError("action_prior must be 'uniform' (sac.py:255-262 normal prior not on this path)")
-        if target_update_interval != 1:
-            raise NotImplementedError('target_update_interval != 1')
         if store_extra_policy_info:
             raise NotImplementedError('store_extra_policy_info')
         env = training_environment
@@ -74,11 +72,11 @@ class SAC:
         self._policy, self._Qs, self._pool, self._plotter = policy, Qs, pool, plotter
         self._init(obs_dim, act_dim, hidden=hs[0], batch_size=batch_size, real_ratio=real_ratio, lr=lr,
                    discount=discount, tau=tau, reward_scale=reward_scale, target_entropy=target_entropy,
-                   reparameterize=reparameterize, **kwargs)
+                   reparameterize=reparameterize, target_update_interval=target_update_interval, **kwargs)
 
     def _init(self, obs_dim, act_dim, hidden=256, batch_size=256, real_ratio=0.05, lr=3e-4, discount=0.99,
               tau=5e-3, reward_scale=1.0, target_entropy='auto', params=None, log_alpha=0.0, seed=2,
-              reparameterize=True, use_graph=True):
+              reparameterize=True, use_graph=True, target_update_interval=1):
         if not reparameterize:
             raise NotImplementedError('only the reparameterized policy loss is implemented (mopo.py:370-374; '
                                       'every config sets reparameterize=True, examples/config/d4rl/base.py)')
@@ -90,6 +88,10 @@ class SAC:
         self._target_entropy = -float(act_dim) if target_entropy == 'auto' else float(target_entropy)
         self._discount, self._tau, self._reward_scale, self._lr = discount, tau, reward_scale, lr
         self._seed = int(seed)
+        if int(target_update_interval) < 1:
+            raise ValueError('target_update_interval must be >= 1')
+        self._target_update_interval = int(target_update_interval)
+        self._schedule = (0, 1, 1)       # the device's target schedule (mopo_sac_set_target_schedule)
         flat = init_sac_params(obs_dim, act_dim, hidden, seed=seed) if params is None else \
             np.ascontiguousarray(params, np.float32)
         n = L.lib().mopo_sac_param_count(obs_dim, act_dim, hidden)
@@ -158,9 +160,12 @@ class SAC:
         return d
 
     def _do_training(self, iteration, env_pool=None, model_pool=None, n_steps=1, seed=0, idx=None, eps_s=None,
-                     eps_n=None, stream=None):
+                     eps_n=None, stream=None, n_train_repeat=1):
         """``n_steps`` x (_training_batch + _do_training + _update_target) on the device.  With
         injected ``idx`` ([batch] rows: first n_env index the env pool) and policy noise, one step.
+        ``iteration`` is the timestep of the first step (each timestep runs ``n_train_repeat`` steps,
+        mopo.py:780-799); the targets move on the steps whose timestep % target_update_interval == 0
+        (mopo.py:843-845).
         ``_do_training(iteration, batch)`` with a batch dict (sac.py:340-349 / mopo.py:834-850): one step
         on exactly those rows (host or device arrays, ``batch_size`` rows)."""
         import torch
@@ -179,6 +184,13 @@ class SAC:
             keep.append(t)
             return L.ptr(t)
 
+        sched = (self._num_train_steps - int(iteration) * int(n_train_repeat), int(n_train_repeat),
+                 self._target_update_interval)
+        if self._target_update_interval == 1:
+            sched = (0, 1, 1)            # every step; the schedule's base is irrelevant
+        if sched != self._schedule:
+            L.check(L.lib().mopo_sac_set_target_schedule(self._h, *sched, L.stream_ptr(stream)))
+            self._schedule = sched
         L.check(L.lib().mopo_sac_step(self._h, env_pool.desc(), model_pool.desc(), int(n_steps),
                                       int(seed) & (2 ** 64 - 1), dp(idx, torch.int64), dp(eps_s, torch.float32),
                                       dp(eps_n, torch.float32), L.stream_ptr(stream)))
@@ -238,7 +250,7 @@ class SAC:
         return {k: cat((env_batch[k], model_batch[k]), 0) for k in keys}
 
     def _update_target(self):
-        """Folded into every device step (target_update_interval=1, mopo.py:843-845)."""
+        """Folded into the device step: Polyak on the steps of the target schedule (mopo.py:843-845)."""
 
     def get_diagnostics(self, *args, **kwargs):
         """mopo.py:900-905 keys (the arguments of sac.py's get_diagnostics are accepted and unused)."""

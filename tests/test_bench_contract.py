@@ -20,7 +20,7 @@ def test_headline_dtype_is_the_product_default(monkeypatch):
 def test_committed_pmc_summary_prices_the_measured_workloads(monkeypatch):
     import bench
     for argv, lo in ((['bench.py'], 19.6e6), (['bench.py', '--ensemble-dtype', 'fp32'], 19.6e6),
-                     (['bench.py', '--config', 'N2'], 39e6)):
+                     (['bench.py', '--config', 'N2'], 31.7e6)):
         monkeypatch.setattr(sys, 'argv', argv)
         args = bench.parse()
         t = bench.pmc_traffic(args)

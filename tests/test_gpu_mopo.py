@@ -108,3 +108,38 @@ def test_reallocate_model_pool_vs_oracle():
     with pytest.raises(AssertionError):
         orl.reallocate(opool, O, A, stub._rollout_batch_size, stub._epoch_length, stub._model_train_freq,
                        stub._rollout_length, stub._model_retain_epochs)
+
+
+def test_mopo_rollouts_every_model_train_freq_steps():
+    """model_train_freq < epoch_length (mopo.py:554-563): a rollout at timesteps 0, 40, 80 of a 100-step
+    epoch, the SAC steps of the timesteps in between (n_train_repeat 2), each rollout under its own
+    Philox key; target_update_interval 2 runs through the same loop."""
+    import torch
+    from mopo_amd.mopo import MOPO
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.static import static_fns
+    rs = np.random.RandomState(2)
+    n = 3000
+    obs = rs.normal(size=(n, 17)).astype(np.float32)
+    pool = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=n)
+    pool.add_samples({'observations': obs, 'actions': rs.uniform(-1, 1, (n, 6)), 'rewards': rs.normal(size=(n, 1)),
+                      'terminals': np.zeros((n, 1), bool), 'next_observations': obs + 0.1})
+    algo = MOPO(pool, static_fns['halfcheetah'], 17, 6, rollout_batch_size=500, rollout_length=1, epoch_length=100,
+                model_train_freq=40, n_train_repeat=2, target_update_interval=2, separate_mean_var=True,
+                penalty_coeff=1.0, penalty_learned_var=True, real_ratio=0.05, target_entropy=-3, max_model_t=3)
+    seen = []
+    orig = algo._rollout_model
+
+    def spy(*a, **k):
+        seen.append((algo._epoch, k.get('rollout_key')))
+        return orig(*a, **k)
+    algo._rollout_model = spy
+    d = list(algo.train(2))
+    assert seen == [(0, 0), (0, 1), (0, 2), (1, 3), (1, 4), (1, 5)]
+    # mopo.py:689-711: rollouts per epoch = 500 * 100 / 40, retained 20 epochs, rollout length 1
+    assert algo._model_pool._max_size == 20 * int(1 * 500 * 100 / 40)
+    assert algo._model_pool.size == 6 * 500
+    assert algo._num_train_steps == 2 * 100 * 2 and d[-1]['train-steps'] == 400
+    assert all(np.isfinite(v) for v in d[-1].values())
+    rows = algo._model_pool.fields['observations'][:algo._model_pool.size].reshape(6, 500, 17)
+    assert not torch.equal(rows[0], rows[1])          # distinct start-row draws per rollout

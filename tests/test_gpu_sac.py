@@ -139,6 +139,52 @@ def test_sac_twenty_steps_track_oracle():
             np.testing.assert_allclose(lg[k], ref[k], rtol=1e-3, atol=1e-5, err_msg='%s @ step %d' % (k, it))
 
 
+def test_sac_target_update_interval_vs_oracle():
+    """target_update_interval = 2 (mopo.py:843-845): the Polyak update runs after the steps whose
+    iteration is even; the others leave the targets as they were (oracle: tau = 0 on those steps)."""
+    from mopo_amd.sac import SAC
+    rs = np.random.RandomState(3)
+    (env_p, env_op), (mod_p, mod_op) = pools(rs)
+    params = osac.init_params(O, A, H, seed=7)
+    sac = SAC(O, A, H, batch_size=256, real_ratio=0.05, target_entropy=-3, params=flat(params).astype(np.float32),
+              target_update_interval=2)
+    st = osac.SACState([p.astype(np.float64) for p in params])
+    lr_t = 3e-4 * np.sqrt(1 - 0.999) / (1 - 0.9)
+    for it in range(4):
+        idx, e1, e2 = draw(rs, env_p.size, mod_p.size)
+        before = sac.get_target().cpu().numpy()
+        osac.sac_step(st, host_batch(env_op, mod_op, idx), e1.astype(np.float64), e2.astype(np.float64),
+                      tau=5e-3 if it % 2 == 0 else 0.0)
+        sac._do_training(it, env_p, mod_p, idx=idx, eps_s=e1, eps_n=e2)
+        tgt = sac.get_target().cpu().numpy()
+        if it % 2:
+            np.testing.assert_array_equal(tgt, before)
+        else:
+            assert not np.array_equal(tgt, before)
+        np.testing.assert_allclose(tgt, flat(st.target), atol=2e-6 + 5e-3 * 2 * lr_t * (it + 1), err_msg='step %d' % it)
+
+
+@pytest.mark.parametrize('interval,repeat', [(3, 1), (2, 2)])
+def test_sac_target_schedule_graph_matches_eager(interval, repeat):
+    """The target schedule inside replayed graphs (8-step, 2-step, 1-step) equals eager steps, over two
+    calls whose first timesteps are 0 and 5 (the base moves with the call), and differs from interval 1."""
+    import torch
+    from mopo_amd.rollout import init_sac_params
+    from mopo_amd.sac import SAC
+    rs = np.random.RandomState(4)
+    (env_p, _), (mod_p, _) = pools(rs)
+    init = init_sac_params(O, A, H, seed=10)
+    runs = []
+    for graph, every in ((True, interval), (False, interval), (True, 1)):
+        s = SAC(O, A, H, params=init, use_graph=graph, target_entropy=-3, target_update_interval=every)
+        s._do_training(0, env_p, mod_p, n_steps=5 * repeat, seed=77, n_train_repeat=repeat)
+        s._do_training(5, env_p, mod_p, n_steps=13 * repeat, seed=77, n_train_repeat=repeat)
+        torch.cuda.synchronize()
+        runs.append((s.get_params()[0], s.get_target()))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
+    assert not torch.equal(runs[0][1], runs[2][1])
+
+
 def test_sac_graph_replay_matches_eager():
     import torch
     from mopo_amd.sac import SAC
