@@ -728,8 +728,11 @@ __global__ __launch_bounds__(WAVES * 64, R == 1 ? 2 : 1) void bnn_fwd_f16r_kerne
 #define BNN_F16Q_DEFER 0  // 1: the swish of k-group c in the MFMA gaps of k-group c - 1 (see below)
 #endif
 
+#ifndef BNN_RING_WAVES
+#define BNN_RING_WAVES 4  // waves per workgroup (16 rows each) sharing one ring
+#endif
 template <int NB2, int NBO, int MODE, int WAVES, int P, int DEPTH, int NBU = NB2>
-__global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES) void bnn_fwd_ring_kernel(const BnnDev w,
+__global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES > 0 ? BNN_F16_MINB * 4 / WAVES : 1) void bnn_fwd_ring_kernel(const BnnDev w,
                                                                                             const FwdArgs a) {
   static_assert(P == 1 || P == 2, "1: bf16, 2: f16x3");
   static_assert(DEPTH >= 3, "ring of at least 3 slots");
@@ -951,7 +954,7 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES) void bnn_fwd_
 
 template <int NB2, int NBO, int P, int DEPTH>
 static int launch_ring(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
-  constexpr int WV = 4;
+  constexpr int WV = BNN_RING_WAVES;
   a.ntiles = (int)ceil_div((int)a.B, 16);
   if (a.ntiles == 0) return 0;
   dim3 grid(8 * ceil_div(ceil_div(a.ntiles, WV), 8) * h->E), block(64 * WV);

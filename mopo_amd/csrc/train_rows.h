@@ -63,7 +63,7 @@ static __device__ __forceinline__ const float* uniform_ptr(const float* p) {
 
 // Workgroups of TR_WAVES waves: wave w owns column block cb = w % 4 (64 columns) and TW = 16 / TR_WAVES
 // of its 4 tiles (two waves per SIMD at 8: one wave's memory waits overlap the other's MFMAs; 16: one
-// tile per wave, four waves per SIMD).
+// tile per wave, four waves per SIMD -- measured 10.07k -> 8.5k grad-steps/s, same-box A/B).
 #ifndef TR_WAVES_CFG
 #define TR_WAVES_CFG 8
 #endif
