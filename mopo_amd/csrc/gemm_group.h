@@ -177,6 +177,10 @@ struct PolicyRows {
   int nblk;                          // 0: none; ceil(n / 16) * ceil(H / 64)
   int n, O, A, H, ncq;
   const float* dapart[2];            // Q1 / Q2 at (s, pi(s)): [ncq][n][OPW] partials of dh1 W1[O:]^T
+  // non-NULL: the partials are unselected (dq = 1, sac_fwd_kernel<true> step 7) and the consumer applies
+  // the min-Q selection (mopo.py:367-377; tf.minimum's gradient to x where x <= y) and -1/n itself, from
+  // Q1 / Q2(s, pi) = b3 + the critics' forward partials [qncq][n][OPW] (element 0)
+  const float* qpart[2]; const float* b3[2]; int qncq;
   const float* head_s;               // [n][2A] mean | raw log_std
   const float* eps_s;                // [n][A]
   const float* log_alpha;
@@ -198,7 +202,8 @@ constexpr int PR_LDS = 2 * 256 * 16; // floats the grouped kernel's panel LDS of
 // WAIT: called after every other operand of the chain is in flight, before the action-gradient
 // partials are loaded; SC1: load them with agent-scope (sc1) loads -- the partials were written by
 // other workgroups of the SAME launch (the in-launch hand-off of sac_dh1_kernel).
-template <bool SC1 = false, typename Wait>
+// UNSEL: the partials are the unselected ones of sac_fwd_kernel<true> (PolicyRows::qpart)
+template <bool SC1 = false, bool UNSEL = false, typename Wait>
 static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs, Wait wait,
                                                          const Stamps& st = Stamps{nullptr, 0}) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -245,6 +250,15 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   float m1[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
+  float qv[2][MAX_NCQ] = {};           // Q1 / Q2(s, pi) partials of this thread's row (UNSEL)
+  if constexpr (UNSEL) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const auto dq = rsrc(c.qpart[i], (int64_t)c.qncq * n * OPW);
+#pragma unroll
+      for (int q = 0; q < MAX_NCQ; ++q) qv[i][q] = bload(dq, (hon && q < c.qncq) ? (q * n + hrow) * OPW : -1);
+    }
+  }
   wait();
   stamp(st, 1);
   float dap[2][MAX_NCQ];
@@ -269,10 +283,25 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
     float dmu = 0.f, dls = 0.f;
     if (hon) {
       float da = 0.f;                                               // -dmin q / da through Q1 / Q2:
+      if constexpr (UNSEL) {                                        // the selected critic's partials, x -1/n
+        float q12[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)                                   // partials in a fixed order
+        for (int i = 0; i < 2; ++i) {
+          float qs = *c.b3[i];
 #pragma unroll
-        for (int q = 0; q < MAX_NCQ; ++q) da += dap[i][q];
+          for (int q = 0; q < MAX_NCQ; ++q) qs += qv[i][q];
+          q12[i] = qs;
+        }
+        const int sel = q12[0] <= q12[1] ? 0 : 1;
+#pragma unroll
+        for (int q = 0; q < MAX_NCQ; ++q) da += sel == 0 ? dap[0][q] : dap[1][q];
+        da *= -1.f / (float)n;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)                                 // partials in a fixed order
+#pragma unroll
+          for (int q = 0; q < MAX_NCQ; ++q) da += dap[i][q];
+      }
       const float g = expf(la) / (float)n;                         // d L_pi / d logp (stop_gradient(alpha))
       const float ls = fminf(fmaxf(raw, -20.f), 2.f);
       const float sd = expf(ls);

@@ -161,6 +161,10 @@ static int launch_gather(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   return 0;
 }
 
+#ifndef MOPO_SAC_F2_DA
+#define MOPO_SAC_F2_DA 1  // the (s, pi) critics' action gradient in F2 (sac_rows.h step 7), not B1
+#endif
+
 // One SAC step on batch bt[par], reading parameters Pb[par] and writing the updated ones to
 // Pb[1 - par].  With `prefetch`, the policy weight-gradient launch also gathers the next step's batch
 // into bt[1 - par] (a separate gather launch, or a forked graph branch, costs more than it hides).
@@ -218,6 +222,9 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       q.h1 = tgt ? nullptr : h->h1[4 + i]; q.h2 = tgt ? nullptr : h->h2[4 + i];
       q.wo = L(4); q.wo2 = nullptr; q.nout = 1; q.split = 1; q.opart = h->opart[4 + i];
       q.head = tgt ? 1 : 0;
+      // Q1 / Q2(s, pi): the blocks' (unselected) action-gradient partials for the policy backward
+      q.w1a = (MOPO_SAC_F2_DA && !tgt) ? Wq(qi, 0) + (int64_t)O * H : nullptr;
+      q.dapart = (MOPO_SAC_F2_DA && !tgt) ? h->dapart[qi] : nullptr;
     }
     FwdHead& hd = f.hd;
     hd.opart[0] = h->opart[0]; hd.opart[1] = h->opart[1]; hd.bm = P + o.pbm; hd.bl = P + o.pbl;
@@ -233,7 +240,9 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   {
     Dh1Args d{};
     const int ncq1 = ceil_div(H, B1_COLS);
-    d.ninst = 4; d.n = n; d.H = H; d.A = A; d.ncq = ncq; d.ncq1 = ncq1; d.nrb = nrb;
+    // MOPO_SAC_F2_DA: the (s, pi) critics' backward ran in F2 (their action-gradient partials), so only
+    // Q1 / Q2(s, a) get a dh1 here and the policy-row blocks start at once (no in-launch hand-off)
+    d.ninst = MOPO_SAC_F2_DA ? 2 : 4; d.n = n; d.H = H; d.A = A; d.ncq = ncq; d.ncq1 = ncq1; d.nrb = nrb;
     for (int i = 0; i < 4; ++i) {
       const int qi = i & 1;
       Dh1Inst& q = d.in[i];
@@ -250,14 +259,18 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     L.log_alpha = P + o.total; L.gamma = h->gamma; L.rscale = h->rscale;
     d.ad = ad; d.tent = h->tent; d.lr = h->lr; d.logs = h->logs; d.beta_pow = h->beta_pow; d.iter = h->iter; d.tctl = h->tctl;
     PolicyRows& pr = d.pr;
-    pr.n = n; pr.O = O; pr.A = A; pr.H = H; pr.ncq = ncq1;
+    pr.n = n; pr.O = O; pr.A = A; pr.H = H; pr.ncq = MOPO_SAC_F2_DA ? ncq : ncq1;
     pr.dapart[0] = h->dapart[0]; pr.dapart[1] = h->dapart[1];
+    if (MOPO_SAC_F2_DA) {
+      pr.qpart[0] = h->opart[4]; pr.qpart[1] = h->opart[5]; pr.qncq = ncq;
+      pr.b3[0] = Wq(0, 5); pr.b3[1] = Wq(1, 5);
+    }
     pr.head_s = h->out[0]; pr.eps_s = h->eps_s; pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
     pr.h2p = h->h2[0]; pr.h1p = h->h1[0]; pr.W2p = P + o.pW2;
     pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p;
     d.rb_ready = h->rb_ready;
     d.st = Stamps{h->stamps, 2};
-    hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq1, nrb, 6), dim3(B1_WAVES * 64), 0, s, d);
+    hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq1, nrb, d.ninst + 2), dim3(B1_WAVES * 64), 0, s, d);
     MOPO_HIP(hipGetLastError());
   }
   // ---- B2: every weight gradient with its fused TF1 Adam (+ Polyak for the critics), the next step's

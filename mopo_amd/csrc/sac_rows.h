@@ -37,6 +37,10 @@ struct FwdInst {
   int nout, split;                   //   [split, nout) from wo2 (ld nout - split)
   float* opart;                      // [ncq][n][OPW] partial dots of the block's 64 outputs
   int head;                          // F2: 0 = pi(s) head (s, pi(s)), 1 = pi(s') head
+  // F2 (s, pi) critics: the block's partial of d Q / d action = (W3 * (h2 > 0)) W2^T * (h1 > 0) W1[O:]^T
+  // over its 64 columns (dq = 1; the policy-row consumer applies the min-Q selection and -1/n)
+  const float* w1a;                  // W1[O:] = the action rows [A][H], or NULL
+  float* dapart;                     // [ncq][n][OPW]
 };
 
 struct FwdHead {                     // F2: the squashed-Gaussian head of pi(s) / pi(s') (HeadCtx math)
@@ -181,6 +185,7 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
   __shared__ __attribute__((aligned(16))) float Ts[RB_LDS_T];
   __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_T];
   __shared__ float act_s[16][8];
+  __shared__ float da_s[HEAD ? 4 : 1][16][9];
   stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // grid (ncq, nrb, ninst): the indices are SGPRs, so the instance's fields come from the kernel
@@ -310,6 +315,68 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
   lds_barrier();
   // ---- 6. partial output dots of the block's 64 columns (wave 0, MFMA)
   if (w == 0) rows_partial_out<RB_COLS>(Ts, Wo, li, lk, i0, n, p.nout, p.opart + (int64_t)cq * n * OPW);
+  // ---- 7. F2, Q1 / Q2 at (s, pi(s)): this block's share of the critic's action gradient (dq = 1), so the
+  //         policy's backward needs no critic backward at (s, pi) in the next launch.  Wave w: dh1 rows
+  //         k in [64 w, 64 w + 64) of D(k, r) = sum_c W2[k][c0 + c] G(r, c), G = W3[c0 + c] (h2 > 0) (K =
+  //         the block's 64 columns), masked by h1 > 0, then its partial of sum_k dh1(r, k) W1[O + a][k]
+  if constexpr (HEAD) {
+    if (p.dapart) {
+      const int kw = 64 * w;
+      // A(m = k, K = c): lane (li, lk) holds W2[kw + 16 t + li][c0 + 16 s + 4 lk + u] (one b128 per (t, s))
+      const auto dw2 = rsrc(p.w2, (int64_t)H * H);
+      f32x4 wa2[4][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int k = kw + 16 * t + li, c = c0 + 16 * s2 + 4 * lk;
+          wa2[t][s2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     dw2, ((k < H && c < H) ? k * H + c : -4) * 4, 0, 0));
+        }
+      // B(K = k, n = a) of the action contraction: W1[O + a = li][kw + 16 t + 4 lk .. + 3]
+      const auto dwa = rsrc(p.w1a, (int64_t)A * H);
+      f32x4 wb1[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int k = kw + 16 * t + 4 * lk;
+        wb1[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               dwa, ((li < A && k < H) ? li * H + k : -4) * 4, 0, 0));
+      }
+      // G(r = li, c = 16 s + 4 lk + u) from the block's h2 tile and W3 (Wo row 0)
+      float gb[4][4];
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int c = 16 * s2 + 4 * lk + u;
+          gb[s2][u] = Ts[li * RB_TLD + c] > 0.f ? Wo[c] : 0.f;
+        }
+      f32x4 da = zero4();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        f32x4 d = zero4();                                   // D: k = kw + 16 t + 4 lk + i, r = li
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) d = mfma4(wa2[t][s2][u], gb[s2][u], d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {                        // * (h1 > 0); A(m = r = li, K = k)
+          const int k = kw + 16 * t + 4 * lk + i;
+          const float v = (k < H && As[li * RB_LD + k] > 0.f) ? d[i] : 0.f;
+          da = mfma4(v, wb1[t][i], da);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)                            // D: r = 4 lk + i, a = li
+        if (li < 8) da_s[w][4 * lk + i][li] = da[i];
+      lds_barrier();
+      if (tid < 128) {                                       // waves' partials in wave order
+        const int rr = tid >> 3, aa = tid & 7, orow = i0 + rr;
+        const float v = da_s[0][rr][aa] + da_s[1][rr][aa] + da_s[2][rr][aa] + da_s[3][rr][aa];
+        if (aa < A && orow < n) p.dapart[((int64_t)cq * n + orow) * OPW + aa] = v;
+      }
+    }
+  }
   stamp(a.st, 4);
 }
 
@@ -471,6 +538,11 @@ static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const 
   }
   if ((int)blockIdx.z > a.ninst) {    // the policy-row blocks
     const int rb = blockIdx.y, cq = blockIdx.x;
+    if (a.pr.qpart[0]) {                // the action-gradient partials come from F2 (the previous launch)
+      policy_rows_block<false, true>(a.pr, rb * a.ncq1 + cq, As, Ts, [] {}, a.st);
+      stamp(a.st, 4);
+      return;
+    }
     const int need = 2 * a.ncq1;
     bool late = false;
     auto wait = [&] {
