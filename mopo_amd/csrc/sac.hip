@@ -73,6 +73,7 @@ struct Sac {
   float *dh1[4];
   float *opart[8];                // [ncq][n][OPW] output-layer partials of the 8 instances (sac_rows.h)
   float *dapart[2];               // [ncq][n][OPW] action-gradient partials of Q1 / Q2 at (s, pi(s))
+  float *upart[2];                // [ncq][n][H] F1's dh1 / dq partials of Q1 / Q2(s, a) (sac_rows.h step 7)
   uint64_t* stamps = nullptr;     // MOPO_SAC_STAMPS builds: [slot][block][8]
   int* rb_ready = nullptr;        // [ceil(n / 16)] B1's in-launch hand-off counters (zeroed by B2)
   float *dhead, *dh2p, *dh1p;
@@ -164,6 +165,11 @@ static int launch_gather(Sac* h, int par, const mopo_pool_desc* env, const mopo_
 #ifndef MOPO_SAC_F2_DA
 #define MOPO_SAC_F2_DA 1  // the (s, pi) critics' action gradient in F2 (sac_rows.h step 7), not B1
 #endif
+#ifndef MOPO_SAC_F1_U
+// 1: Q1 / Q2(s, a) dh1 / dq partials in F1 (step 7), B1 only sums and scales them -- measured 50.7 vs
+// 46.7 us/step (same-box A/B): F1 grows by more than B1 saves (2 MB of partials written and re-read)
+#define MOPO_SAC_F1_U 0
+#endif
 
 // One SAC step on batch bt[par], reading parameters Pb[par] and writing the updated ones to
 // Pb[1 - par].  With `prefetch`, the policy weight-gradient launch also gathers the next step's batch
@@ -203,6 +209,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       q.w1 = Wq(qi, 0); q.b1 = Wq(qi, 1); q.w2 = Wq(qi, 2); q.b2 = Wq(qi, 3);
       q.h1 = h->h1[2 + qi]; q.h2 = h->h2[2 + qi];
       q.wo = Wq(qi, 4); q.wo2 = nullptr; q.nout = 1; q.split = 1; q.opart = h->opart[2 + qi];
+      q.upart = MOPO_SAC_F1_U ? h->upart[qi] : nullptr;
     }
     f.st = Stamps{h->stamps, 0};
     hipLaunchKernelGGL(sac_fwd_kernel<false>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
@@ -249,6 +256,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       q.h1 = h->h1[2 + i]; q.h2 = h->h2[2 + i]; q.w2 = Wq(qi, 2); q.w3 = Wq(qi, 4); q.kind = i;
       q.dh1 = i < 2 ? h->dh1[i] : nullptr; q.dq = i < 2 ? h->dq[i] : nullptr;
       q.w1a = i < 2 ? nullptr : Wq(qi, 0) + (int64_t)O * H; q.dapart = i < 2 ? nullptr : h->dapart[qi];
+      q.upart = (MOPO_SAC_F1_U && i < 2) ? h->upart[qi] : nullptr;
     }
     LossRows& L = d.L;
     for (int i = 0; i < 6; ++i) {
@@ -341,6 +349,7 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   const size_t npart = (size_t)ceil_div(H, RB_COLS) * n * OPW;
   for (int i = 0; i < 8; ++i) f(&h->opart[i], npart);
   for (int i = 0; i < 2; ++i) f(&h->dapart[i], npart);
+  for (int i = 0; i < 2; ++i) f(&h->upart[i], (size_t)ceil_div(H, RB_COLS) * n * H);
   reg.push_back({(void**)&h->rb_ready, (size_t)ceil_div(batch, 16) * 4});
 #if MOPO_SAC_STAMPS
   reg.push_back({(void**)&h->stamps, (size_t)4 * 1024 * 8 * 8});

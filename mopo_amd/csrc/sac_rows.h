@@ -41,6 +41,9 @@ struct FwdInst {
   // over its 64 columns (dq = 1; the policy-row consumer applies the min-Q selection and -1/n)
   const float* w1a;                  // W1[O:] = the action rows [A][H], or NULL
   float* dapart;                     // [ncq][n][OPW]
+  // F1 Q1 / Q2(s, a): the block's partial of dh1 / dq = (W3 * (h2 > 0)) W2^T * (h1 > 0) over its 64
+  // columns, all H hidden units ([ncq][n][H]); B1 sums them and scales by the row's dq
+  float* upart;
 };
 
 struct FwdHead {                     // F2: the squashed-Gaussian head of pi(s) / pi(s') (HeadCtx math)
@@ -185,7 +188,7 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
   __shared__ __attribute__((aligned(16))) float Ts[RB_LDS_T];
   __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_T];
   __shared__ float act_s[16][8];
-  __shared__ float da_s[HEAD ? 4 : 1][16][9];
+  __shared__ float da_s[4][16][9];
   stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // grid (ncq, nrb, ninst): the indices are SGPRs, so the instance's fields come from the kernel
@@ -315,12 +318,14 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
   lds_barrier();
   // ---- 6. partial output dots of the block's 64 columns (wave 0, MFMA)
   if (w == 0) rows_partial_out<RB_COLS>(Ts, Wo, li, lk, i0, n, p.nout, p.opart + (int64_t)cq * n * OPW);
-  // ---- 7. F2, Q1 / Q2 at (s, pi(s)): this block's share of the critic's action gradient (dq = 1), so the
-  //         policy's backward needs no critic backward at (s, pi) in the next launch.  Wave w: dh1 rows
-  //         k in [64 w, 64 w + 64) of D(k, r) = sum_c W2[k][c0 + c] G(r, c), G = W3[c0 + c] (h2 > 0) (K =
-  //         the block's 64 columns), masked by h1 > 0, then its partial of sum_k dh1(r, k) W1[O + a][k]
-  if constexpr (HEAD) {
-    if (p.dapart) {
+  // ---- 7. a critic's backward share of the block (dq = 1): wave w forms dh1 rows k in [64 w, 64 w + 64)
+  //         of D(k, r) = sum_c W2[k][c0 + c] G(r, c), G = W3[c0 + c] (h2 > 0) (K = the block's 64
+  //         columns), masked by h1 > 0.  F2, Q1 / Q2 at (s, pi(s)): then its partial of the action
+  //         gradient sum_k dh1(r, k) W1[O + a][k], so the policy's backward needs no critic backward at
+  //         (s, pi) in the next launch.  F1, Q1 / Q2(s, a): the masked tile itself (upart), which B1
+  //         sums over the column blocks and scales by the row's dq (no W2 operand burst there).
+  {
+    if (p.dapart || p.upart) {
       const int kw = 64 * w;
       // A(m = k, K = c): lane (li, lk) holds W2[kw + 16 t + li][c0 + 16 s + 4 lk + u] (one b128 per (t, s))
       const auto dw2 = rsrc(p.w2, (int64_t)H * H);
@@ -334,13 +339,13 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
                                                      dw2, ((k < H && c < H) ? k * H + c : -4) * 4, 0, 0));
         }
       // B(K = k, n = a) of the action contraction: W1[O + a = li][kw + 16 t + 4 lk .. + 3]
-      const auto dwa = rsrc(p.w1a, (int64_t)A * H);
+      const auto dwa = rsrc(p.w1a, p.w1a ? (int64_t)A * H : 0);
       f32x4 wb1[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int k = kw + 16 * t + 4 * lk;
         wb1[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               dwa, ((li < A && k < H) ? li * H + k : -4) * 4, 0, 0));
+                                               dwa, ((p.w1a && li < A && k < H) ? li * H + k : -4) * 4, 0, 0));
       }
       // G(r = li, c = 16 s + 4 lk + u) from the block's h2 tile and W3 (Wo row 0)
       float gb[4][4];
@@ -359,13 +364,18 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
         for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
           for (int u = 0; u < 4; ++u) d = mfma4(wa2[t][s2][u], gb[s2][u], d);
+        f32x4 um;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {                        // * (h1 > 0); A(m = r = li, K = k)
           const int k = kw + 16 * t + 4 * lk + i;
-          const float v = (k < H && As[li * RB_LD + k] > 0.f) ? d[i] : 0.f;
-          da = mfma4(v, wb1[t][i], da);
+          um[i] = (k < H && As[li * RB_LD + k] > 0.f) ? d[i] : 0.f;
+          da = mfma4(um[i], wb1[t][i], da);
         }
+        const int k0 = kw + 16 * t + 4 * lk;
+        if (p.upart && i0 + li < n && k0 < H)                // one b128 per lane: row li, k0 .. k0 + 3
+          *reinterpret_cast<f32x4*>(p.upart + ((int64_t)cq * n + i0 + li) * H + k0) = um;
       }
+      if (!p.dapart) goto done7;
 #pragma unroll
       for (int i = 0; i < 4; ++i)                            // D: r = 4 lk + i, a = li
         if (li < 8) da_s[w][4 * lk + i][li] = da[i];
@@ -377,6 +387,7 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
       }
     }
   }
+done7:
   stamp(a.st, 4);
 }
 
@@ -417,6 +428,7 @@ static __device__ __forceinline__ RowQ row_losses(const LossRows& L, int n, int 
 }
 
 struct Dh1Inst {
+  const float* upart;                // F1's dh1 / dq partials [ncq][n][H] (then only dq, dh1 are formed here)
   const float* h1; const float* h2; const float* w2; const float* w3;
   int kind;                          // dq of the row: 0 (q1 - y) / n, 1 (q2 - y) / n, 2 min-select Q1, 3 Q2
   float* dh1;                        // stored when non-NULL
@@ -565,6 +577,37 @@ static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const 
   const int n = a.n, H = a.H, A = a.A;
   const int i0 = rb * 16, c0 = cq * B1_COLS, jw = c0 + w * 16;
   const int li = lane & 15, lk = lane >> 4;
+  if (p.upart) {
+    // dh1 = dq * sum of F1's column-block partials (already masked by h1 > 0), in column-block order:
+    // thread t owns row t / 32, columns c0 + 4 (t % 32) .. + 3 of the block (one b128 per partial)
+    const int rr = tid >> 5, kq = c0 + 4 * (tid & 31), orow = i0 + rr;
+    const auto du = rsrc(p.upart, (int64_t)a.ncq * n * H);
+    f32x4 up[MAX_NCQ];
+#pragma unroll
+    for (int c = 0; c < MAX_NCQ; ++c)
+      up[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            du, ((c < a.ncq && orow < n && kq < H) ? (c * n + orow) * H + kq : -4) * 4, 0, 0));
+    if (tid < 16) {
+      const int r2 = i0 + tid;
+      float dq = 0.f;
+      if (r2 < n) {
+        const RowQ o = row_losses(a.L, n, a.ncq, r2);
+        dq = (p.kind == 0 ? o.q[0] : o.q[1]) - o.y;
+        dq *= 1.f / (float)n;
+        if (cq == 0 && p.dq) p.dq[r2] = dq;
+      }
+      dqs[tid] = dq;
+    }
+    lds_barrier();
+    if (orow < n && kq < H) {
+      f32x4 v = up[0];
+#pragma unroll
+      for (int c = 1; c < MAX_NCQ; ++c) v += up[c];
+      *reinterpret_cast<f32x4*>(p.dh1 + (int64_t)orow * H + kq) = v * dqs[rr];
+    }
+    stamp(a.st, 4);
+    return;
+  }
   // ---- 1. operands up front: this wave's W2^T operand straight into MFMA registers (B(m, c) = W2[c][m]:
   //         lane (li, lk) holds W2[jw + li][64 lk + 4 s .. + 3]), the A slab's h2 rows and W3 (waves
   //         0-3), the h1 mask of this lane's outputs, W1[O:] columns of the block (the (s, pi) instances)
