@@ -102,7 +102,14 @@ def test_sac_steps_vs_reference_graph(path):
                                  for j in range(nj)])
             tiny = np.abs(gr) < 1e-3 * np.abs(gr).max()
             assert d[~tiny].max() <= 1e-6 + 1e-6 * np.abs(p_ref).max(), d[~tiny].max()
-            assert d[tiny].max() <= 1e-6 + 2 * sum(lr_t[:k + 1])
+            # a small gradient moves its parameter by ~lr_t m/sqrt(v) whatever its size, so the device's
+            # gradient error (<= 1e-4 max|g| of the tensor, tests/test_gpu_sac.py) moves the update by
+            # ~lr_t err/|g|: a sign may flip only where |g| is at that error level, elsewhere the allowance
+            # shrinks with |g| (it was a flat 2 sum(lr_t) for every small gradient)
+            allow = 1e-6 + 1e-6 * np.abs(p_ref).max() + 2 * sum(lr_t[:k + 1]) * np.minimum(
+                1.0, 1e-4 * np.abs(gr).max() / np.maximum(np.abs(gr), 1e-30))
+            bad = tiny & (d > allow)
+            assert not bad.any(), (int(bad.sum()), d[bad].max(), np.abs(gr[bad]).max() / np.abs(gr).max())
         else:
             assert d.max() <= 1e-6 + 2 * sum(lr_t[:k + 1])
         assert abs(float(la.item()) - float(z['b%d_log_alpha_f32' % k])) < 1e-6

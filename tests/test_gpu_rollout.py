@@ -415,15 +415,18 @@ def test_f16x3_dynamic_range(scale):
     mean, var = make_model(mats, E, H, dtype='f16x3').predict(x)
     rm, rv = obnn.forward(p, x, dtype=np.float64)
     assert np.isfinite(mean).all() and np.isfinite(var).all()
-    # the same ~22-bit operand class as bf16x6: within 2x the worse of the fp32 and bf16x6 kernels' own
-    # errors (adversarial scales make cancellations that amplify every kernel's rounding alike)
+    # within 2x the exact-f32 MFMA kernel's own error against the f64 oracle (adversarial scales make
+    # cancellations that amplify every kernel's rounding alike), and at the fp32 parity tolerance (2e-5,
+    # test_bnn_predict_split_vs_oracle) outright wherever the fp32 kernel itself meets it
     err = lambda a, b: float(np.max(np.abs(np.float64(a) - b) / (1 + np.abs(b))))
-    ref_m, ref_v = 2e-6, 2e-6
-    for dt in ('fp32', 'bf16x6'):
-        mo, vo = make_model(mats, E, H, dtype=dt).predict(x)
-        ref_m, ref_v = max(ref_m, 2 * err(mo, rm)), max(ref_v, 2 * err(vo, rv))
-    assert err(mean, rm) <= ref_m, (err(mean, rm), ref_m)
-    assert err(var, rv) <= ref_v, (err(var, rv), ref_v)
+    mo, vo = make_model(mats, E, H, dtype='fp32').predict(x)
+    e32m, e32v = err(mo, rm), err(vo, rv)
+    assert err(mean, rm) <= max(2 * e32m, 2e-6), (err(mean, rm), e32m)
+    assert err(var, rv) <= max(2 * e32v, 2e-6), (err(var, rv), e32v)
+    if e32m <= 1e-5:
+        assert err(mean, rm) <= 2e-5, err(mean, rm)
+    if e32v <= 1e-5:
+        assert err(var, rv) <= 2e-5, err(var, rv)
 
 
 def test_fused_rollout_bf16_walker_runs():
