@@ -395,6 +395,7 @@ int step_impl(Train* h, int par, int M, bool use_bstep, hipStream_t s) {
 // multiples of 4 (b128 weight rows).  MOPO_TRAIN_ROWS=0 selects step_impl (twelve launches) instead.
 // the weight-gradient launch's tile width (MOPO_TRAIN_WGRAD_TILE: 16 or 32; default 32: 4,000 16x16
 // tiles of K = 256 re-read each operand panel 16x over, 32x32 tiles half as often)
+constexpr int TRAIN_WG_P = NHID + 1;   // weight-gradient problems of the fused step (one per layer)
 int train_wgrad_tile() {
   static const int v = [] {
     const char* e = std::getenv("MOPO_TRAIN_WGRAD_TILE");
@@ -413,6 +414,34 @@ bool use_rows(const Train* h) {
   const bool inst = (gh == 13 || gh == 16 || gh == 2) && ((g0 == 2 && gd == 3) || (g0 == 1 && gd == 2));  // step_rows
   return env != 0 && inst && L.H % 4 == 0 && L.D % 2 == 0;
 }
+
+// the batch-level tail's inputs (train_rows.h train_loss_tail) -- the weight-gradient launch's last block
+struct TrainTail {
+  int E, nrb, D;
+  const float* lpart;
+  int64_t mx, mn;
+  float* logs; float* beta_pow; int* bstep_inc; float lr; float* G; AdamCtx ad;
+};
+// the weight-gradient launch of the fused step: block 0 the tail, then the problems' 32x32 tiles (gemm32_body)
+struct TrainWgrad {
+  int n;
+  int prefix[TRAIN_WG_P + 1];
+  AdamCtx ad;
+  GemmProb p[TRAIN_WG_P];
+  TrainTail t;
+};
+static __global__ __launch_bounds__(256, 2) void train_wgrad_kernel(const TrainWgrad g) {
+  if (blockIdx.x == 0) {   // dispatched first: its serial chain runs beside the tiles
+    __shared__ float sh[64];
+    train_loss_tail(g.t, sh);
+    return;
+  }
+  gemm32_body(g, (int)blockIdx.x - 1);
+}
+
+#ifndef MOPO_TRAIN_FUSED
+#define MOPO_TRAIN_FUSED 1  // forward + backward rows in one launch, the loss tail in the weight-gradient launch
+#endif
 
 int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t* idx, int64_t stride, bool use_bstep,
               int batch, int M, hipStream_t s) {
@@ -434,6 +463,40 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
   a.lr = h->lr; a.G = h->G; a.ad = ad;
   const int grid = 8 * a.nrb * ceil_div(E, 8);   // train_rows.h tr_block: a member's row blocks on one XCD
   const int g0 = ceil_div(IN, 16), gh = ceil_div(H, 16), gd = ceil_div(D2, 16);
+  if (MOPO_TRAIN_FUSED) {
+#define MOPO_TRF(G0, GH, GD)                                                                                 \
+    if (g0 == G0 && gh == GH && gd == GD) {                                                                  \
+      hipLaunchKernelGGL((train_rows_kernel<G0, GH, GD>), dim3(grid), dim3(TR_WAVES * 64), 0, s, a);                  \
+      MOPO_HIP(hipGetLastError());                                                                           \
+    } else
+    MOPO_TRF(2, 13, 3) MOPO_TRF(1, 13, 2) MOPO_TRF(1, 2, 2) MOPO_TRF(2, 2, 3) MOPO_TRF(2, 16, 3) MOPO_TRF(1, 16, 2)
+    return fail("bnn train: no row-block instantiation for these widths (use_rows)");
+#undef MOPO_TRF
+    TrainWgrad g{};
+    g.n = NHID + 1;
+    g.ad = ad;
+    int tot = 0;
+    for (int l = NHID, i = 0; l >= 0; --l, ++i) {   // dW_l = X_in^T dY (+ db = colsum dY), decay + Adam; batch = member
+      const int K = l == 0 ? IN : H, N = l == NHID ? D2 : H;
+      const float* dY = l == NHID ? h->dOUT : h->dZ[l];
+      const float* Xin = l == 0 ? h->X : h->Hh[l - 1];
+      GemmProb w = mk(K, N, M, Xin, K, 1, dY, N, 0, h->G + L.W[l], N);
+      w.colsum = h->G + L.b[l];
+      w.adam = 1;
+      w.wd = WDECAY[l];
+      w.nb = E;
+      g.p[i] = w;
+      g.prefix[i] = tot;
+      tot += E * ceil_div(K, 32) * ceil_div(N, 32);
+    }
+    g.prefix[g.n] = tot;
+    TrainTail& t = g.t;
+    t.E = E; t.nrb = a.nrb; t.D = D; t.lpart = h->lpart; t.mx = L.mx; t.mn = L.mn;
+    t.logs = h->logs; t.beta_pow = h->beta_pow; t.bstep_inc = a.bstep_inc; t.lr = h->lr; t.G = h->G; t.ad = ad;
+    hipLaunchKernelGGL(train_wgrad_kernel, dim3(tot + 1), dim3(256), 0, s, g);
+    MOPO_HIP(hipGetLastError());
+    return 0;
+  }
 #define MOPO_TRR(G0, GH, GD)                                                                                 \
   if (g0 == G0 && gh == GH && gd == GD) {                                                                    \
     hipLaunchKernelGGL((train_fwd_rows_kernel<G0, GH>), dim3(grid), dim3(TR_WAVES * 64), 0, s, a);                     \

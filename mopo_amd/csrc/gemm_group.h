@@ -767,7 +767,10 @@ static __device__ __forceinline__ void epi_apply(const GemmProb& p, float* C, co
 // (16 per operand and thread), half the operand traffic per output of 16x16 tiles and a quarter of
 // the blocks.  Epilogue: the tile goes through LDS, 4 elements per thread (same fused operations).
 constexpr int GKC32 = 128;
-static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmGroup g) {
+// The 32x32 tile `bid` of a group; GG: GemmGroup or any struct with its n / prefix / p / ad members
+// (bnn_train.hip's weight-gradient launch with the loss tail as its last block)
+template <class GG>
+static __device__ __forceinline__ void gemm32_body(const GG& g, int bid) {
   __shared__ __attribute__((aligned(16))) float As[GKC32 * 32];
   __shared__ __attribute__((aligned(16))) float Bs[GKC32 * 32];
   __shared__ float tile[32][33];
@@ -775,9 +778,9 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
   __shared__ float red[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int pi = 0;
-  while (pi + 1 < g.n && (int)blockIdx.x >= g.prefix[pi + 1]) ++pi;
+  while (pi + 1 < g.n && bid >= g.prefix[pi + 1]) ++pi;
   const GemmProb& p = g.p[pi];
-  int t0 = blockIdx.x - g.prefix[pi];
+  int t0 = bid - g.prefix[pi];
   const int tn_cnt = ceil_div(p.N, 32);
   int64_t oA = 0, oB = 0, oC = 0, oCs = 0;   // a batched problem's batch (gemm_group_kernel)
   if (p.nb > 1) {
@@ -869,12 +872,14 @@ static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmG
     if (tid == 0) {
       const float b = red[0] + red[1] + red[2] + red[3];
       const int64_t off = p.adam ? (int64_t)(pC - ad.G) : -1;
-      float* np = ad.norm_part + 2 * (int64_t)(ad.slot0 + blockIdx.x);
+      float* np = ad.norm_part + 2 * (int64_t)(ad.slot0 + bid);
       np[0] = off >= 0 && off < ad.n_pi ? b : 0.f;
       np[1] = off >= ad.n_pi && off < ad.n_pi + ad.n_q ? b : 0.f;
     }
   }
 }
+
+static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmGroup g) { gemm32_body(g, (int)blockIdx.x); }
 
 // ---------------------------------------------------------------------------------------------
 static inline GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C,

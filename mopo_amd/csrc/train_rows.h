@@ -273,7 +273,9 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_fwd_rows_kernel
 }
 
 // ---- batch-level tail: partial sums in (member, row block) order, then train_loss_kernel's tail -----
-static __device__ __forceinline__ void train_loss_tail(const TrainRows& a, float* sh) {
+// TR: TrainRows or TrainTail (the fields used here)
+template <class TR>
+static __device__ __forceinline__ void train_loss_tail(const TR& a, float* sh) {
   const int D = a.D, n = a.E * a.nrb;
   const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];  // every thread reads them before thread 0 advances them
   const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
@@ -358,6 +360,161 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_bwd_rows_kernel
   };
   layer(std::integral_constant<int, GD>{}, TR_NHID);
   for (int l = TR_NHID - 1; l >= 1; --l) layer(std::integral_constant<int, GH>{}, l);
+}
+
+// ---- forward + backward rows in ONE launch (MOPO_TRAIN_FUSED) -------------------------------------
+// train_fwd_rows_kernel then train_bwd_rows_kernel's chain in the same workgroup: the pre-activations Z
+// stay in LDS (zb, 66 KB; no HBM round trip), the heads' output gradient goes straight into the
+// backward's input buffer, and the batch-level tail moves to the weight-gradient launch (bnn_train.hip
+// train_wgrad_kernel), which only needs this step's lr_t -- block 0 writes it here (the tail advances
+// the beta powers after every reader of them in this step).
+template <int G0, int GH, int GD>
+static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(const TrainRows a) {
+  __shared__ __attribute__((aligned(16))) float buf[2][16 * TR_LD];
+  __shared__ __attribute__((aligned(16))) float zb[TR_NHID][16 * TR_LD];
+  __shared__ float red[3][64][17];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15;
+  int e, rb;
+  if (blockIdx.x == 0 && tid == 0) {
+    const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
+    a.beta_pow[2] = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);          // this step's TF1 Adam step size
+  }
+  if (!tr_block(blockIdx.x, a.nrb, a.E, e, rb)) return;
+  const int M = a.M, IN = a.IN, H = a.H, D = a.D, i0 = rb * 16;
+  {  // gather (train_fwd_rows_kernel)
+    const int W = IN + D, KP = ((IN + 15) >> 4) << 4;
+    const int64_t base = a.bstep ? (int64_t)(*a.bstep) * a.batch : 0;
+    for (int i = tid; i < 16 * KP; i += TR_WAVES * 64) buf[0][(i / KP) * TR_LD + i % KP] = 0.f;
+    lds_barrier();
+    for (int i = tid; i < 16 * W; i += TR_WAVES * 64) {
+      const int r = i / W, c = i % W, row = i0 + r;
+      if (row >= M) continue;
+      const int64_t src = a.rows ? a.rows[e * a.stride + base + row] : row;
+      const int64_t er = (int64_t)e * M + row;
+      if (c < IN) {
+        const float x = (a.inputs[src * IN + c] - a.mu[c]) / a.sigma[c];   // utils.py:96
+        a.X[er * IN + c] = x;
+        buf[0][r * TR_LD + c] = x;
+      } else {
+        a.T[er * D + (c - IN)] = a.targets[src * D + (c - IN)];
+      }
+    }
+    lds_barrier();
+  }
+  const int c0 = 64 * (w & 3) + 4 * li + TR_TW * (w >> 2);   // this lane's first column
+  const int lk = lane >> 4;
+  auto fwd = [&](auto gtag, int l) {
+    constexpr int G = decltype(gtag)::value;
+    const int K = l == 0 ? IN : H, N = l == TR_NHID ? 2 * D : H;
+    const float* Wl = a.P + a.W[l] + (int64_t)e * K * N;
+    float bias[TR_TW] = {};
+    if (c0 < N) ld_tw<TR_TW>(a.P + a.b[l] + (int64_t)e * N + c0, bias);
+    f32x4 acc[TR_TW];
+    rows_gemm<false, G, TR_TW>(buf[l & 1], Wl, K, N, N, c0, lane, acc);
+    float* out = buf[(l + 1) & 1];
+    if (__builtin_amdgcn_readfirstlane(c0 - 4 * li) < N) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * lk + i, row = i0 + r;
+        const bool ok = row < M && c0 < N;
+        float v[TR_TW];
+#pragma unroll
+        for (int q = 0; q < TR_TW; ++q) v[q] = acc[q][i] + bias[q];
+        if (l < TR_NHID) {
+          st_tw<TR_TW>(zb[l] + r * TR_LD + c0, v);             // pre-activation, for swish' below
+#pragma unroll
+          for (int q = 0; q < TR_TW; ++q) v[q] = swish_fast(v[q]);
+          if (ok) st_tw<TR_TW>(a.Hh[l] + ((int64_t)e * M + row) * H + c0, v);
+        } else if (ok) {
+          st_tw<TR_TW>(a.OUT + ((int64_t)e * M + row) * 2 * D + c0, v);
+        }
+        if (!ok)
+#pragma unroll
+          for (int q = 0; q < TR_TW; ++q) v[q] = 0.f;
+        st_tw<TR_TW>(out + r * TR_LD + c0, v);
+      }
+    }
+    lds_barrier();
+  };
+  fwd(std::integral_constant<int, G0>{}, 0);
+  for (int l = 1; l <= TR_NHID; ++l) fwd(std::integral_constant<int, GH>{}, l);
+  // ---- output gradient and the block's partial sums (train_fwd_rows_kernel); dY of the heads also into
+  //      buf[0] (the backward's input; zero-padded to a multiple of 16 columns)
+  const float* o = buf[(TR_NHID + 1) & 1];
+  float* dy = buf[TR_NHID & 1];
+  const int N2 = 2 * D, NP = ((N2 + 15) >> 4) << 4;
+  const float s = 1.f / ((float)M * (float)D);
+  for (int i = tid; i < 16 * D; i += TR_WAVES * 64) {
+    const int r = i / D, d = i % D, row = i0 + r;
+    float c_mx = 0.f, c_mn = 0.f, c_loss = 0.f, g_mean = 0.f, g_lv = 0.f;
+    if (row < M) {
+      const int64_t er = (int64_t)e * M + row;
+      const float mx = a.P[a.mx + d], mn = a.P[a.mn + d];
+      const float mean = o[r * TR_LD + d], raw = o[r * TR_LD + D + d], y = a.T[er * D + d];
+      const float lv1 = mx - softplusf(mx - raw);
+      const float lv = mn + softplusf(lv1 - mn);
+      const float inv = expf(-lv);
+      const float err = mean - y;
+      const float dlv = (1.f - err * err * inv) * s;
+      const float sb = 1.f / (1.f + expf(-(lv1 - mn))), sa = 1.f / (1.f + expf(-(mx - raw)));
+      const float dlv1 = dlv * sb;
+      g_mean = 2.f * err * inv * s;
+      g_lv = dlv1 * sa;
+      a.dOUT[er * 2 * D + d] = g_mean;
+      a.dOUT[er * 2 * D + D + d] = g_lv;
+      c_mn = dlv * (1.f - sb);
+      c_mx = dlv1 * (1.f - sa);
+      c_loss = (err * err * inv + lv) * s;
+    }
+    dy[r * TR_LD + d] = g_mean;
+    dy[r * TR_LD + D + d] = g_lv;
+    red[0][d][r] = c_mx;
+    red[1][d][r] = c_mn;
+    red[2][d][r] = c_loss;
+  }
+  for (int i = tid; i < 16 * (NP - N2); i += TR_WAVES * 64) dy[(i / (NP - N2)) * TR_LD + N2 + i % (NP - N2)] = 0.f;
+  lds_barrier();
+  if (tid < D) {                                          // rows in order (deterministic)
+    float t3[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      for (int r = 0; r < 16; ++r) t3[k] += red[k][tid][r];
+    float* pp = a.lpart + (((int64_t)e * a.nrb + rb) * D + tid) * 4;
+    pp[0] = t3[0]; pp[1] = t3[1]; pp[2] = t3[2];
+  }
+  // ---- the activation-gradient chain (train_bwd_rows_kernel), swish'(Z) from LDS; dY of layer l sits in
+  //      buf[(TR_NHID - l) & 1] as in that kernel (dy = buf[TR_NHID & 1] = buf[0] for 4 hidden layers)
+  static_assert((TR_NHID & 1) == 0, "the backward's first input buffer is buf[0]");
+  auto bwd = [&](auto gtag, int l) {
+    constexpr int G = decltype(gtag)::value;
+    const int Kl = H, Nl = l == TR_NHID ? 2 * D : H;     // layer l: [Kl -> Nl]; dZ_{l-1} is 16 x Kl
+    const float* Wl = a.P + a.W[l] + (int64_t)e * Kl * Nl;
+    float zm[4][TR_TW];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int q = 0; q < TR_TW; ++q) zm[i][q] = 0.f;
+      if (c0 < Kl) ld_tw<TR_TW>(zb[l - 1] + (4 * lk + i) * TR_LD + c0, zm[i]);
+    }
+    f32x4 acc[TR_TW];
+    rows_gemm<true, G, TR_TW>(buf[(TR_NHID - l) & 1], Wl, Nl, Kl, Nl, c0, lane, acc);
+    float* out = buf[(TR_NHID - l + 1) & 1];
+    if (__builtin_amdgcn_readfirstlane(c0 - 4 * li) < Kl) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * lk + i, row = i0 + r;
+        const bool ok = row < M && c0 < Kl;
+        float v[TR_TW];
+#pragma unroll
+        for (int q = 0; q < TR_TW; ++q) v[q] = ok ? acc[q][i] * dswish_fast(zm[i][q]) : 0.f;
+        if (ok) st_tw<TR_TW>(a.dZ[l - 1] + ((int64_t)e * M + row) * H + c0, v);
+        st_tw<TR_TW>(out + r * TR_LD + c0, v);
+      }
+    }
+    lds_barrier();
+  };
+  bwd(std::integral_constant<int, GD>{}, TR_NHID);
+  for (int l = TR_NHID - 1; l >= 1; --l) bwd(std::integral_constant<int, GH>{}, l);
 }
 
 }  // namespace mopo
