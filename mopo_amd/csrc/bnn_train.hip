@@ -415,7 +415,7 @@ bool use_rows(const Train* h) {
   return env != 0 && inst && L.H % 4 == 0 && L.D % 2 == 0;
 }
 
-// the batch-level tail's inputs (train_rows.h train_loss_tail) -- the weight-gradient launch's last block
+// the batch-level tail's inputs (train_rows.h train_loss_tail) -- the weight-gradient launch's block 0
 struct TrainTail {
   int E, nrb, D;
   const float* lpart;
@@ -432,7 +432,7 @@ struct TrainWgrad {
 };
 static __global__ __launch_bounds__(256, 2) void train_wgrad_kernel(const TrainWgrad g) {
   if (blockIdx.x == 0) {   // dispatched first: its serial chain runs beside the tiles
-    __shared__ float sh[64];
+    __shared__ float sh[3 * TR_TAIL_CH * 128];   // D <= 128
     train_loss_tail(g.t, sh);
     return;
   }

@@ -272,7 +272,8 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_fwd_rows_kernel
   }
 }
 
-// ---- batch-level tail: partial sums in (member, row block) order, then train_loss_kernel's tail -----
+// ---- batch-level tail: the (member, row block) partial sums, then train_loss_kernel's tail ------------
+constexpr int TR_TAIL_CH = 8;   // sh: >= 3 TR_TAIL_CH D floats; blockDim >= TR_TAIL_CH D
 // TR: TrainRows or TrainTail (the fields used here)
 template <class TR>
 static __device__ __forceinline__ void train_loss_tail(const TR& a, float* sh) {
@@ -280,12 +281,28 @@ static __device__ __forceinline__ void train_loss_tail(const TR& a, float* sh) {
   const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];  // every thread reads them before thread 0 advances them
   const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   __syncthreads();
-  if ((int)threadIdx.x < D) {
-    const int dd = threadIdx.x;
-    float gmx = 0.f, gmn = 0.f, loss = 0.f;
-    for (int c = 0; c < n; ++c) {
+  // the E nrb partials of each d in TR_TAIL_CH interleaved chunks (thread (j, d): partials j, j + CH, ...
+  // in order, 8 independent loads in flight), then the chunk sums in chunk order: deterministic, and one
+  // memory latency instead of E nrb dependent ones (a serial loop made the tail ~30 us)
+  constexpr int CH = TR_TAIL_CH;
+  const int t = threadIdx.x;
+  if (t < CH * D) {
+    const int dd = t % D, j = t / D;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+    for (int c = j; c < n; c += CH) {
       const float* pp = a.lpart + ((int64_t)c * D + dd) * 4;
-      gmx += pp[0]; gmn += pp[1]; loss += pp[2];
+      s0 += pp[0]; s1 += pp[1]; s2 += pp[2];
+    }
+    sh[(j * D + dd) * 3 + 0] = s0; sh[(j * D + dd) * 3 + 1] = s1; sh[(j * D + dd) * 3 + 2] = s2;
+  }
+  __syncthreads();
+  float loss = 0.f;
+  if (t < D) {
+    const int dd = t;
+    float gmx = 0.f, gmn = 0.f;
+    for (int j = 0; j < CH; ++j) {
+      gmx += sh[(j * D + dd) * 3 + 0]; gmn += sh[(j * D + dd) * 3 + 1]; loss += sh[(j * D + dd) * 3 + 2];
     }
     gmx += 0.01f;                                                   // 0.01 * sum(max_logvar)
     gmn -= 0.01f;                                                   // -0.01 * sum(min_logvar)
@@ -293,8 +310,9 @@ static __device__ __forceinline__ void train_loss_tail(const TR& a, float* sh) {
     a.G[a.mn + dd] = gmn;
     adam_apply(a.ad, a.mx + dd, gmx, adam_load(a.ad, a.mx + dd), lr_t);
     adam_apply(a.ad, a.mn + dd, gmn, adam_load(a.ad, a.mn + dd), lr_t);
-    sh[dd] = loss;
   }
+  __syncthreads();                                                  // every chunk sum is read
+  if (t < D) sh[t] = loss;
   __syncthreads();
   if (threadIdx.x == 0) {
     float loss = 0.f;
