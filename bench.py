@@ -256,7 +256,7 @@ def roofline_of(dtype, rows, ms, flop_row=FLOP_BNN_ROW):
                 'flop_per_launch': rows * flop_row, 'avg_launch_ms': ms}
     parts, prods = SPLIT[dtype]
     if dtype == 'f16x3':
-        kern = ('bnn_fwd_f16q_kernel (ensemble forward on a 3-slot LDS ring, f16 MFMA 16x16x32, 3 products per f32 '
+        kern = ('bnn_fwd_ring_kernel<P=2> (ensemble forward on a 3-slot LDS ring, f16 MFMA 16x16x32, 3 products per f32 '
                 'product; bnn_fwd_f16s_kernel at H > 256)')
     else:
         kern = 'bnn_fwd_bf16_kernel<P=%d> (ensemble forward, bf16 MFMA 16x16x32, %d products per f32 product)' % (
