@@ -8,11 +8,12 @@
 // The loop control (holdout split, bootstrap indices, early stopping, elites) stays on the host
 // (mopo_amd/bnn.py), drawing from numpy's global stream in the reference's order.
 //
-// One minibatch step = 3 launches (step_rows, train_rows.h): the row-block forward (gather + scaler,
-// 4 swish layers + heads, output gradient, loss partials), the row-block activation-gradient chain
-// (+ the batch-level tail: max/min log-var gradients and their Adam, this step's lr_t), and one
-// grouped-GEMM launch whose weight-gradient tiles apply weight decay and the TF1 Adam in their
-// epilogue (gemm_group.h; parameters ping-pong between two buffers).  The previous 12-launch form
+// One minibatch step = 2 launches (step_rows, train_rows.h): the row blocks (gather + scaler, 4 swish
+// layers + heads, output gradient, loss partials, then the activation-gradient chain with the
+// pre-activations held in LDS), and one launch whose block 0 runs the batch-level tail (max/min log-var
+// gradients and their Adam) beside the weight-gradient tiles, which apply weight decay and the TF1
+// Adam in their epilogue (gemm_group.h; parameters ping-pong between two buffers).  MOPO_TRAIN_FUSED=0
+// keeps the 3-launch form (separate forward / backward row launches, the tail in the backward's).  The previous 12-launch form
 // (gather, 5 forward GEMM launches, loss kernel, 5 backward GEMM launches: step_impl) remains for
 // H > 256 and for the holdout evaluation's forward.  Full-batch steps are captured into hipGraphs
 // (8 / 2 / 1+copy-back steps); the epoch's partial last batch runs eagerly.
@@ -432,7 +433,7 @@ struct TrainWgrad {
 };
 static __global__ __launch_bounds__(256, 2) void train_wgrad_kernel(const TrainWgrad g) {
   if (blockIdx.x == 0) {   // dispatched first: its serial chain runs beside the tiles
-    __shared__ float sh[3 * TR_TAIL_CH * 128];   // D <= 128
+    __shared__ float sh[TR_TAIL_SH];   // small enough to keep 4 workgroups of the tiles per CU
     train_loss_tail(g.t, sh);
     return;
   }

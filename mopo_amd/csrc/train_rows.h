@@ -77,6 +77,11 @@ constexpr int TR_WAVES = TR_WAVES_CFG, TR_TW = 16 / TR_WAVES;
 // ds_read_b128 of A per k-group).  G = ceil(K / 16) at compile time: straight-line code with the loads
 // two k-groups ahead (a runtime k-group loop made the compiler wait for all but 2 of the prefetched
 // loads at its header).
+#ifndef TR_PF_CFG
+#define TR_PF_CFG 2
+#endif
+// k-groups of B loaded ahead of their MFMAs (4 / 7: 11.52k -> 11.41k / 11.10k grad-steps/s, same-box A/B)
+constexpr int TR_PF = TR_PF_CFG;
 template <bool KT, int G, int TW>
 static __device__ __forceinline__ void rows_gemm(const float* As, const float* Wv, int Kv, int Nv, int ldwv, int c,
                                                  int lane, f32x4 (&acc)[TW]) {
@@ -122,12 +127,12 @@ static __device__ __forceinline__ void rows_gemm(const float* As, const float* W
 #pragma unroll
       for (int q = 0; q < TW; ++q) acc[q] = mfma4(a4[u], bv[u][q], acc[q]);
   };
-  float bq[G + 2][4][TW];
-  ld(0, bq[0]);
-  if constexpr (G > 1) ld(1, bq[1]);
+  float bq[G + TR_PF][4][TW];
+#pragma unroll
+  for (int grp = 0; grp < TR_PF && grp < G; ++grp) ld(grp, bq[grp]);
 #pragma unroll
   for (int grp = 0; grp < G; ++grp) {
-    if (grp + 2 < G) ld(grp + 2, bq[grp + 2]);            // two k-groups ahead
+    if (grp + TR_PF < G) ld(grp + TR_PF, bq[grp + TR_PF]);   // TR_PF k-groups ahead
     // keep them there: left alone the scheduler sinks each load to just before its first use, leaving
     // one or two in flight
     __builtin_amdgcn_sched_barrier(0);
@@ -273,7 +278,8 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_fwd_rows_kernel
 }
 
 // ---- batch-level tail: the (member, row block) partial sums, then train_loss_kernel's tail ------------
-constexpr int TR_TAIL_CH = 8;   // sh: >= 3 TR_TAIL_CH D floats; blockDim >= TR_TAIL_CH D
+constexpr int TR_TAIL_CH = 8;     // chunks per output column, at most
+constexpr int TR_TAIL_SH = 512;   // floats of sh the tail may use (3 per (chunk, column))
 // TR: TrainRows or TrainTail (the fields used here)
 template <class TR>
 static __device__ __forceinline__ void train_loss_tail(const TR& a, float* sh) {
@@ -284,7 +290,7 @@ static __device__ __forceinline__ void train_loss_tail(const TR& a, float* sh) {
   // the E nrb partials of each d in TR_TAIL_CH interleaved chunks (thread (j, d): partials j, j + CH, ...
   // in order, 8 independent loads in flight), then the chunk sums in chunk order: deterministic, and one
   // memory latency instead of E nrb dependent ones (a serial loop made the tail ~30 us)
-  constexpr int CH = TR_TAIL_CH;
+  const int CH = max(1, min(TR_TAIL_CH, min(TR_TAIL_SH / (3 * D), (int)blockDim.x / D)));
   const int t = threadIdx.x;
   if (t < CH * D) {
     const int dd = t % D, j = t / D;
