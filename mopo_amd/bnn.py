@@ -175,10 +175,7 @@ class BNN:
         return self
 
     def get_params(self):
-        if self._mats is None:
-            raise RuntimeError('BNN.get_params: this rank holds only the packed device image (import_packed); '
-                               'the .mat arrays live on the broadcasting rank')
-        return [m.copy() for m in self._mats]
+        return [m.copy() for m in self._require_mats('get_params')]
 
     # -- packed device image (multi-GPU broadcast) ------------------------------------------------------
     def packed_nbytes(self):
@@ -195,11 +192,53 @@ class BNN:
         L.check(L.lib().mopo_bnn_packed_copy(self._h, 0, L.ptr(out), n, L.stream_ptr(stream)))
         return out
 
-    def import_packed(self, buf, stream=None):
-        """Load a packed image exported by a handle of the same shapes and dtype.  The host copy of
-        the .mat arrays is dropped (it no longer describes the device weights)."""
+    def import_packed(self, buf, stream=None, mats=None, holdout_losses=None):
+        """Load a packed image exported by a handle of the same shapes and dtype.  ``mats``: the
+        sender's .mat arrays (``flat_params``) -- with them this handle's host state (``get_params``,
+        ``scaler``, ``save``, ``train``, ``validate``) describes the imported weights; without them
+        the host state is dropped and those methods raise."""
         L.check(L.lib().mopo_bnn_packed_copy(self._h, 1, L.ptr(buf), int(buf.numel()), L.stream_ptr(stream)))
         self._mats = None
+        self.scaler = None
+        self._holdout_losses = None if holdout_losses is None else np.asarray(holdout_losses, np.float64)
+        if mats is not None:
+            mats = [np.ascontiguousarray(np.asarray(m, np.float32)) for m in mats]
+            shapes = [m.shape for m in self._mat_shapes()]
+            if [m.shape for m in mats] != shapes:
+                raise ValueError('import_packed: .mat arrays do not match this ensemble')
+            self._mats = mats
+            self.scaler = _Scaler(mats[0], mats[1])
+
+    def _mat_shapes(self):
+        """Zero arrays of the .mat shapes (set_params' expectation)."""
+        E, IN, H, D = self.num_nets, self.obs_dim + self.act_dim, self.hidden_dim, self.obs_dim + 1
+        exp = [(1, IN), (1, IN)]
+        dims = [IN] + [H] * N_HIDDEN + [D if self.separate_mean_var else 2 * D]
+        for i in range(len(dims) - 1):
+            exp += [(E, dims[i], dims[i + 1]), (E, 1, dims[i + 1])]
+        if self.separate_mean_var:
+            exp += [(E, H, D), (E, 1, D)]
+        exp += [(1, D), (1, D)]
+        return [np.zeros(s, np.float32) for s in exp]
+
+    def flat_params(self):
+        """The .mat arrays concatenated (f32), the broadcast form of ``import_packed(mats=...)``."""
+        return np.concatenate([m.ravel() for m in self._require_mats('flat_params')])
+
+    def unflatten_params(self, flat):
+        out, off = [], 0
+        for z in self._mat_shapes():
+            out.append(np.asarray(flat[off:off + z.size], np.float32).reshape(z.shape))
+            off += z.size
+        if off != len(flat):
+            raise ValueError('unflatten_params: %d values for %d parameters' % (len(flat), off))
+        return out
+
+    def _require_mats(self, what):
+        if self._mats is None:
+            raise RuntimeError('BNN.%s: this handle holds only a packed device image (import_packed without '
+                               'mats); the .mat arrays live on the broadcasting rank' % what)
+        return self._mats
 
     def load_params(self, path=None):
         """bnn.py:276-281: loadmat('<model_dir>/<name>.mat'), keys '0'..'15'."""
@@ -218,6 +257,7 @@ class BNN:
             # the reference's joint-head branch (bnn.py:571-576) writes the halved last layer once per
             # hidden layer, a file its own _load_structure cannot read back; only smv is written here
             raise NotImplementedError('BNN.save: structure files are written for separate_mean_var=True only')
+        self._require_mats('save')
         savedir = self.model_dir if savedir is None else savedir
         mean, var = structure_lines(self.num_nets, self.obs_dim, self.act_dim, self.hidden_dim)
         for suffix, lines in (('', mean), ('_var', var)):

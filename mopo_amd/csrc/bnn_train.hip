@@ -520,7 +520,7 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
     w.nb = E;
     g.push_back(w);
   }
-  return launch_group(g, s, &ad, nullptr, nullptr, nullptr, nullptr, nullptr, 0, train_wgrad_tile());
+  return launch_group(g, s, &ad, nullptr, nullptr, train_wgrad_tile());
 }
 
 int copy_back(Train* h, hipStream_t s) {

@@ -1,7 +1,6 @@
 // Grouped small-GEMM kernel with fused epilogues (activation, activation-derivative masks,
-// bias-gradient column sums, TF1 Adam + Polyak), shared by the SAC step's weight-gradient launches
-// (sac.hip; plus the policy's row-local backward chain and the next batch's gather as extra blocks)
-// and the ensemble training step (bnn_train.hip).
+// bias-gradient column sums, TF1 Adam), used by the ensemble training step (bnn_train.hip); the
+// Adam context, the range-checked buffer loads and the stamps are shared with the SAC step (sac.hip).
 //
 // One 16x16 output tile per 256-thread block; K is split over the four waves and reduced through
 // LDS.  f32 MFMA (v_mfma_f32_16x16x4_f32).  The shapes these updates see are small (batch 256,
@@ -94,7 +93,6 @@ struct AdamCtx {
 enum {
   LOG_Q1_LOSS = 0, LOG_Q2_LOSS, LOG_Q1, LOG_Q2, LOG_ALPHA, LOG_ENTROPY, LOG_LOGP, LOG_PI_GNORM, LOG_Q_GNORM,
   LOG_PI_LOSS, LOG_PI_GSQ, LOG_Q_GSQ,
-  LOG_HANDOFF,                       // sticky: 1 once an in-launch hand-off wait timed out (sac.py raises)
   LOG_N = 16
 };
 
@@ -107,282 +105,11 @@ static __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t d, int idx)
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(d, idx * 4, 0, 0));
 }
 
-// ---- SAC batch gather (_training_batch, mopo.py:801-821): rows [0, n_env) from the env pool, rest
-// from the model pool; each index uniform over the pool's live size (Philox) unless injected.  One
-// thread per (row, field column): every thread derives its row's source index itself (the Philox
-// draw is cheap), so the work is two dependent memory latencies (pool size + counter, then the field)
-// with no barrier.  Run by sac_gather_kernel (sac.hip) and by the gather blocks of a GemmGroup launch.
-struct Batch {
-  float *sa, *xpi, *xn, *rew, *term;  // [s, a], [s, pi(s)], [s', pi(s')], r, done
-  int64_t* idx;                       // [n] sampled rows
-};
-
-struct GatherArgs {
-  mopo_pool_desc env, mod;
-  int n, n_env, O, A;                // n: batch rows
-  const int64_t* idx_in;             // injected rows or NULL (Philox draw)
-  uint64_t seed;
-  const int64_t* iter;
-  Batch out;
-};
-
-// field c of batch row r (obs | act | next_obs | rew | term)
-static __device__ __forceinline__ void gather_elem(const GatherArgs& g, int r, int c) {
-  const int O = g.O, A = g.A, W = O + A;
-  const bool fe = r < g.n_env;
-  const mopo_pool_desc& p = fe ? g.env : g.mod;
-  int64_t src;
-  if (g.idx_in) {
-    src = g.idx_in[r];
-  } else {
-    const uint64_t size = (uint64_t)p.d_state[1];
-    const int64_t it = *g.iter;
-    u32x4 cc{(uint32_t)r, (uint32_t)it, (uint32_t)((uint64_t)it >> 32), RNG_SAC};
-    u32x4 q = philox(cc, (uint32_t)g.seed, (uint32_t)(g.seed >> 32));
-    src = (int64_t)(((uint64_t)q.x * size) >> 32);
-  }
-  const Batch& b = g.out;
-  if (c == 0) b.idx[r] = src;
-  if (c < O) {
-    const float v = p.d_obs[src * O + c];
-    b.sa[r * W + c] = v;
-    b.xpi[r * W + c] = v;
-  } else if (c < O + A) {
-    b.sa[r * W + c] = p.d_act[src * A + (c - O)];
-  } else if (c < 2 * O + A) {
-    b.xn[r * W + (c - O - A)] = p.d_next_obs[src * O + (c - O - A)];
-  } else if (c == 2 * O + A) {
-    b.rew[r] = p.d_rew[src];
-  } else {
-    b.term[r] = (float)p.d_term[src];
-  }
-}
-
-// ---- the policy's row-local backward chain (mopo.py:337-377 through the critics at (s, pi(s))),
-// run by extra blocks of the critic weight-gradient launch: block (rb, cq) owns batch rows
-// [16 rb, 16 rb + 16) and columns [64 cq, 64 cq + 64) of the policy's first hidden layer.
-//   dx_a   = dh1_Q1(s,pi) W1_Q1[O:]^T + dh1_Q2(s,pi) W1_Q2[O:]^T      (-d min Q / d action)
-//            -- the sum of the per-column-block partials the critic dh1 launch wrote (sac_rows.h)
-//   dhead  = squashed-Gaussian head backward (mean, log_std; alpha / n on the log-prob)
-//   dh2p   = (dhead_mu Wm^T + dhead_ls Wl^T) * (h2p > 0)               (all H columns, in LDS)
-//   dh1p   = dh2p W2p^T * (h1p > 0)                                     (this block's 64 columns, MFMA)
-// Every quantity before dh1p is row-local, so each column block recomputes it (cheap: ncq partials
-// per action, K = 2A per dh2p value) and only cq == 0 stores dhead and dh2p, which the policy weight
-// gradients of the next launch read with dh1p.
-constexpr int OPW = 16;              // floats per (column block, row) partial record (sac_rows.h)
-constexpr int MAX_NCQ = 4;           // column blocks of 64 (H <= 256)
-constexpr int DH2_TILES = 4;         // dh2p column tiles per wave (H <= 256 over >= 4 waves)
-
-struct PolicyRows {
-  int nblk;                          // 0: none; ceil(n / 16) * ceil(H / 64)
-  int n, O, A, H, ncq;
-  const float* dapart[2];            // Q1 / Q2 at (s, pi(s)): [ncq][n][OPW] partials of dh1 W1[O:]^T
-  // non-NULL: the partials are unselected (dq = 1, sac_fwd_kernel<true> step 7) and the consumer applies
-  // the min-Q selection (mopo.py:367-377; tf.minimum's gradient to x where x <= y) and -1/n itself, from
-  // Q1 / Q2(s, pi) = b3 + the critics' forward partials [qncq][n][OPW] (element 0)
-  const float* qpart[2]; const float* b3[2]; int qncq;
-  const float* head_s;               // [n][2A] mean | raw log_std
-  const float* eps_s;                // [n][A]
-  const float* log_alpha;
-  const float* Wm; const float* Wl;  // [H][A]
-  const float* h2p; const float* h1p;// [n][H]
-  const float* W2p;                  // [H][H]
-  float* dhead; float* dh2p; float* dh1p;
-};
-
-constexpr int PR_COLS = 64;          // dh1p columns per 4-wave policy-row block (one 16-wide tile per wave)
-constexpr int PR_LDS = 2 * 256 * 16; // floats the grouped kernel's panel LDS offers it (H <= 508)
-
-// Latency layout: every global operand of the chain is loaded in ONE burst of unconditional
-// (range-checked) loads at the start -- the action-gradient partials and head inputs, Wm / Wl / h2p at
-// this thread's dh2p column, this wave's W2p operands of the dh1p tile and the h1p mask -- so the
-// block pays one memory latency, then computes.
-// S: >= 16 (H + 4) floats of LDS (PR_LDS); hs: >= 3 * 128 floats.  Blocks of 4 or 8 waves (64 or 128
-// dh1p columns).  H % 16 == 0, H <= 256 (one dh2p column per thread), A <= 8.
-// WAIT: called after every other operand of the chain is in flight, before the action-gradient
-// partials are loaded; SC1: load them with agent-scope (sc1) loads -- the partials were written by
-// other workgroups of the SAME launch (the in-launch hand-off of sac_dh1_kernel).
-// UNSEL: the partials are the unselected ones of sac_fwd_kernel<true> (PolicyRows::qpart)
-template <bool SC1 = false, bool UNSEL = false, typename Wait>
-static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs, Wait wait,
-                                                         const Stamps& st = Stamps{nullptr, 0}) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int H = c.H, A = c.A, HS = H + 4, n = c.n;
-  const int pcols = 16 * (int)(blockDim.x >> 6);   // dh1p columns of the block: one 16-wide tile per wave
-  const int ncq = (H + pcols - 1) / pcols;
-  const int rb = x / ncq, cq = x % ncq, r0 = rb * 16;
-  const int li = lane & 15, lk = lane >> 4;
-  // ---- the burst: head inputs, Wm / Wl / h2p at this thread's dh2p column, this wave's W2p operands of
-  //      the dh1p tile and the h1p mask; then (after wait()) the action-gradient partials
-  const int hr = tid >> 3, hj = tid & 7, hrow = r0 + hr;
-  const bool hon = tid < 128 && hj < A && hrow < n;
-  const auto dh = rsrc(c.head_s, (int64_t)n * 2 * A), de = rsrc(c.eps_s, (int64_t)n * A);
-  const float mu = bload(dh, hon ? hrow * 2 * A + hj : -1);
-  const float raw = bload(dh, hon ? hrow * 2 * A + A + hj : -1);
-  const float ep = bload(de, hon ? hrow * A + hj : -1);
-  const float la = *c.log_alpha;
-  // dh2p tiles of this wave: 16 columns each, tiles w, w + nw, ... (at most DH2_TILES)
-  const int nw = (int)(blockDim.x >> 6), nt2 = (H + 15) >> 4;
-  const auto dwm = rsrc(c.Wm, (int64_t)H * A), dwl = rsrc(c.Wl, (int64_t)H * A), dh2 = rsrc(c.h2p, (int64_t)n * H);
-  float wb[DH2_TILES][4], h2v[DH2_TILES][4];   // B(k, c) = k < 8 ? Wm[c][k] : Wl[c][k - 8]; lane k = 4 s + lk
-#pragma unroll
-  for (int q = 0; q < DH2_TILES; ++q) {
-    const int c2 = (w + q * nw) * 16 + li;
-    const bool on = w + q * nw < nt2 && c2 < H;
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) {
-      const int k = 4 * (s2 & 1) + lk;
-      wb[q][s2] = bload(s2 < 2 ? dwm : dwl, (on && k < A) ? c2 * A + k : -1);
-      h2v[q][s2] = bload(dh2, on ? (r0 + 4 * lk + s2) * H + c2 : -1);     // rows >= n: past the extent
-    }
-  }
-  const int j0 = cq * pcols + w * 16, col = j0 + li;
-  const bool tile_on = j0 < H;
-  const auto dw2 = rsrc(c.W2p, (int64_t)H * H);
-  const int boff = (tile_on ? col : 0) * H;
-  f32x4 bq[16];                       // B(k, j) = W2p[j][k]: lane (li, lk) contracts k = 64 lk + 4 t + u
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    const int k = 64 * lk + 4 * t;
-    bq[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dw2, (k < H ? boff + k : -4) * 4, 0, 0));
-  }
-  const auto dm1 = rsrc(c.h1p, (int64_t)n * H);
-  float m1[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
-  float qv[2][MAX_NCQ] = {};           // Q1 / Q2(s, pi) partials of this thread's row (UNSEL)
-  if constexpr (UNSEL) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const auto dq = rsrc(c.qpart[i], (int64_t)c.qncq * n * OPW);
-#pragma unroll
-      for (int q = 0; q < MAX_NCQ; ++q) qv[i][q] = bload(dq, (hon && q < c.qncq) ? (q * n + hrow) * OPW : -1);
-    }
-  }
-  wait();
-  stamp(st, 1);
-  float dap[2][MAX_NCQ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    if constexpr (SC1) {
-#pragma unroll
-      for (int q = 0; q < MAX_NCQ; ++q)
-        dap[i][q] = (hon && q < c.ncq) ? __hip_atomic_load(c.dapart[i] + ((int64_t)q * n + hrow) * OPW + hj,
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                       : 0.f;
-    } else {
-      const auto dp = rsrc(c.dapart[i], (int64_t)c.ncq * n * OPW);
-#pragma unroll
-      for (int q = 0; q < MAX_NCQ; ++q) dap[i][q] = bload(dp, (hon && q < c.ncq) ? (q * n + hrow) * OPW + hj : -1);
-    }
-  }
-  // ---- squashed-Gaussian head backward (mopo.py:282-308 differentiated; pi_loss mopo.py:371-377)
-  float* dmu_s = hs + 128;
-  float* dls_s = hs + 256;
-  if (tid < 128) {
-    float dmu = 0.f, dls = 0.f;
-    if (hon) {
-      float da = 0.f;                                               // -dmin q / da through Q1 / Q2:
-      if constexpr (UNSEL) {                                        // the selected critic's partials, x -1/n
-        float q12[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          float qs = *c.b3[i];
-#pragma unroll
-          for (int q = 0; q < MAX_NCQ; ++q) qs += qv[i][q];
-          q12[i] = qs;
-        }
-        const int sel = q12[0] <= q12[1] ? 0 : 1;
-#pragma unroll
-        for (int q = 0; q < MAX_NCQ; ++q) da += sel == 0 ? dap[0][q] : dap[1][q];
-        da *= -1.f / (float)n;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)                                 // partials in a fixed order
-#pragma unroll
-          for (int q = 0; q < MAX_NCQ; ++q) da += dap[i][q];
-      }
-      const float g = expf(la) / (float)n;                         // d L_pi / d logp (stop_gradient(alpha))
-      const float ls = fminf(fmaxf(raw, -20.f), 2.f);
-      const float sd = expf(ls);
-      const float u = mu + ep * sd;
-      const float a = tanhf(u);
-      const float inv = 1.f / (sd + 1e-8f);
-      const float zz = (u - mu) * inv;
-      float du = da * (1.f - a * a);                                // tanh grad (y-based)
-      du += g * (-zz * inv);                                        // gaussian_likelihood wrt x
-      du += g * (2.f - 4.f / (1.f + expf(2.f * u)));                // squash correction: 2 - 4 sigmoid(-2u)
-      dmu = g * zz * inv + du;
-      const float dstd = g * zz * zz * inv + du * ep;
-      dls = -g + dstd * sd;
-      if (!(raw >= -20.f && raw <= 2.f)) dls = 0.f;                 // clip_by_value grad
-      if (cq == 0) {
-        c.dhead[(int64_t)hrow * 2 * A + hj] = dmu;
-        c.dhead[(int64_t)hrow * 2 * A + A + hj] = dls;
-      }
-    }
-    dmu_s[tid] = dmu;
-    dls_s[tid] = dls;
-  }
-  lds_barrier();
-  stamp(st, 2);
-  // ---- dh2p = dhead [dWm; dWl]^T (K = 16: mu parts 0..7, log-std parts 8..15) masked by h2p > 0 ->
-  //      LDS rows of stride HS (and dh2p in HBM from the cq == 0 blocks)
-  {
-    float av[4];
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) av[s2] = (s2 < 2 ? dmu_s : dls_s)[li * 8 + 4 * (s2 & 1) + lk];
-#pragma unroll
-    for (int q = 0; q < DH2_TILES; ++q) {
-      if (w + q * nw >= nt2) break;
-      f32x4 d = zero4();
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) d = mfma4(av[s2], wb[q][s2], d);
-      const int c2 = (w + q * nw) * 16 + li;
-      if (c2 < H) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {                                // D: row 4 lk + i, col li
-          const int row = 4 * lk + i;
-          const float v = h2v[q][i] > 0.f ? d[i] : 0.f;
-          S[row * HS + c2] = v;
-          if (cq == 0 && r0 + row < n) c.dh2p[(int64_t)(r0 + row) * H + c2] = v;
-        }
-      }
-    }
-  }
-  lds_barrier();
-  stamp(st, 3);
-  // ---- dh1p tile = dh2p W2p^T * (h1p > 0): rows r0.., columns j0.. (wave w)
-  if (!tile_on) return;
-  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    const int k = 64 * lk + 4 * t;
-    const f32x4 a = k < H ? *reinterpret_cast<const f32x4*>(S + li * HS + k) : zero4();
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = mfma4(a[u], bq[t][u], acc[u]);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = r0 + 4 * lk + i;                                // D: col li, row 4 lk + i
-    if (row < n && col < H) {
-      const float v = acc[0][i] + acc[1][i] + acc[2][i] + acc[3][i];
-      c.dh1p[(int64_t)row * H + col] = m1[i] > 0.f ? v : 0.f;
-    }
-  }
-}
-
-// Blocks of a launch: [pr.nblk policy-row blocks] [the problems' tiles (prefix[n])] [gather_blocks
-// blocks of the next step's batch gather (ga)].
 struct GemmGroup {
   int n;
   int prefix[MAXP + 1];
   AdamCtx ad;
-  PolicyRows pr;
-  int* zero; int nzero;              // block 0 zeroes zero[0, nzero) (SAC: the next step's hand-off counters)
   Stamps st;                         // diagnostic builds (MOPO_SAC_STAMPS): per-block phase stamps
-  int gather_blocks;
-  GatherArgs ga;
   GemmProb p[MAXP];
 };
 
@@ -392,16 +119,24 @@ static __device__ __forceinline__ AdamIn adam_load(const AdamCtx& ad, int64_t i)
   return AdamIn{ad.Pc[i], ad.M[i], ad.V[i], ad.T ? ad.T[i] : 0.f};
 }
 
-// TF1 Adam (m += (g - m)(1 - b1), v += (g^2 - v)(1 - b2), p -= lr_t m / (sqrt(v) + eps)) + Polyak
-static __device__ __forceinline__ void adam_apply(const AdamCtx& ad, int64_t i, float g, AdamIn a, float lr_t) {
+// TF1 Adam (m += (g - m)(1 - b1), v += (g^2 - v)(1 - b2), p -= lr_t m / (sqrt(v) + eps)) + Polyak.
+// Returns the new parameter; *t_new (when given) the new target, or the old one where it did not move.
+static __device__ __forceinline__ float adam_apply(const AdamCtx& ad, int64_t i, float g, AdamIn a, float lr_t,
+                                                   float* t_new = nullptr) {
   const float m = a.m + (g - a.m) * (1.f - 0.9f);
   const float v = a.v + (g * g - a.v) * (1.f - 0.999f);
   const float p = a.p - (m * lr_t) / (sqrtf(v) + 1e-8f);
   ad.M[i] = m;
   ad.V[i] = v;
   ad.Pn[i] = p;
+  float t = a.t;
   // mopo.py:446-447 (after the updates), on the steps whose timestep % target_update_interval == 0 (:843-845)
-  if (ad.T && i < ad.total && (!ad.tgt_on || *ad.tgt_on != 0.f)) ad.T[i] = (1.f - ad.tau) * a.t + ad.tau * p;
+  if (ad.T && i < ad.total && (!ad.tgt_on || *ad.tgt_on != 0.f)) {
+    t = (1.f - ad.tau) * a.t + ad.tau * p;
+    ad.T[i] = t;
+  }
+  if (t_new) *t_new = t;
+  return p;
 }
 
 
@@ -560,35 +295,20 @@ static __device__ __forceinline__ void stage_dispatch(const GemmProb& p, int i0,
 // of LDS; partial tiles are summed through LDS and the epilogue fuses bias / activation / the
 // activation-derivative mask, and (for weight gradients) the optimizer.
 static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGroup g) {
-  __shared__ __attribute__((aligned(16))) float ABs[2 * GKC * 16];  // the A and B panels (one array: the policy-row blocks use it whole)
+  __shared__ __attribute__((aligned(16))) float ABs[2 * GKC * 16];  // the A and B panels
   float (*As)[16] = reinterpret_cast<float (*)[16]>(ABs);
   float (*Bs)[16] = reinterpret_cast<float (*)[16]>(ABs + GKC * 16);
   __shared__ __attribute__((aligned(16))) float part[4][256];
   __shared__ float csum[16][17];
-  // block order: [pr.nblk policy-row blocks (first: the longest chain starts at once)] [the problems'
-  // tiles (prefix[n])] [gather blocks]
   stamp(g.st, 0);
-  if (blockIdx.x == 0 && (int)threadIdx.x < g.nzero) g.zero[threadIdx.x] = 0;
-  if ((int)blockIdx.x < g.pr.nblk) {
-    policy_rows_block(g.pr, blockIdx.x, ABs, &part[0][0], [] {});
-    stamp(g.st, 4);
-    return;
-  }
-  const int bid = (int)blockIdx.x - g.pr.nblk;
-  if (bid >= g.prefix[g.n]) {  // the gather blocks after the tiles
-    const int x = bid - g.prefix[g.n];
-    const int C = 2 * g.ga.O + g.ga.A + 2, e = x * 256 + (int)threadIdx.x;
-    if (e < g.ga.n * C) gather_elem(g.ga, e / C, e % C);
-    stamp(g.st, 4);
-    return;
-  }
+  const int bid = (int)blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int pi = 0;
   while (pi + 1 < g.n && bid >= g.prefix[pi + 1]) ++pi;
   const GemmProb& p = g.p[pi];
   int t = bid - g.prefix[pi];
   const int tn_cnt = ceil_div(p.N, 16);
-  int first = g.pr.nblk + g.prefix[pi];   // block id of this (batch's) tile 0
+  int first = g.prefix[pi];   // block id of this (batch's) tile 0
   // batched problem: batch b's operands are dense-packed at these offsets (floats)
   int64_t oA = 0, oB = 0, oC = 0, oCs = 0;
   if (p.nb > 1) {
@@ -903,12 +623,9 @@ static inline int gemm_tile_override() {
 
 // tile: 0 the policy above; 32 the 32x32 kernel whatever the problem sizes (partial tiles are range-checked)
 static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const AdamCtx* ad = nullptr, int* slot = nullptr,
-                               const PolicyRows* pr = nullptr, const GatherArgs* ga = nullptr,
-                               const Stamps* st = nullptr, int* zero = nullptr, int nzero = 0, int tile = 0) {
+                               const Stamps* st = nullptr, int tile = 0) {
   GemmGroup g{};
   if (st) g.st = *st;
-  if (nzero > 256) return fail("gemm group: at most 256 words to zero");
-  g.zero = zero; g.nzero = zero ? nzero : 0;
   g.n = (int)ps.size();
   if (g.n > MAXP) return fail("gemm group too large");
   bool big = true;
@@ -936,22 +653,8 @@ static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const Ad
     g.ad.slot0 = slot ? *slot : 0;
     if (slot) *slot += tot;
   }
-  int extra = 0;
-  if (pr) {
-    if (TW != 16 || pr->A > 8 || pr->H % 16 || pr->H > 256 || 16 * (pr->H + 4) > PR_LDS)
-      return fail("gemm group: bad policy rows (A <= 8, H <= 256, H % 16 == 0)");
-    g.pr = *pr;
-    g.pr.nblk = ceil_div(pr->n, 16) * ceil_div(pr->H, PR_COLS);
-    extra += g.pr.nblk;  // leading blocks (gemm_group_kernel)
-  }
-  if (ga) {
-    if (TW != 16) return fail("gemm group: gather blocks need the 16-wide kernel");
-    g.ga = *ga;
-    g.gather_blocks = ceil_div(ga->n * (2 * ga->O + ga->A + 2), 256);
-    extra += g.gather_blocks;
-  }
   if (TW == 32) hipLaunchKernelGGL(gemm32_group_kernel, dim3(tot), dim3(256), 0, s, g);
-  else hipLaunchKernelGGL(gemm_group_kernel, dim3(tot + extra), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL(gemm_group_kernel, dim3(tot), dim3(256), 0, s, g);
   MOPO_HIP(hipGetLastError());
   return 0;
 }

@@ -10,17 +10,16 @@
 // row-block launches (sac_rows.h) that hand each other per-column-block partial dot products instead
 // of full rows: F1 the hidden layers of pi(s), pi(s'), Q1/Q2(s,a) + partial output layers; F2 the
 // policy head (from F1's partials) feeding the hidden layers of Q1/Q2(s,pi) and the target critics +
-// partial output layers; B1 each row's TD target and dq (from the partials), the critics' dh1, the
-// action-gradient partials of Q1/Q2(s,pi), the batch loss tail, and -- handed those partials inside
-// the launch through per-row-block counters -- the policy's row-local backward chain (head backward
-// -> dh2p -> dh1p).  Then ONE grouped-GEMM launch (gemm_group.h) computes every weight gradient with
-// its TF1 Adam (+ Polyak for the critics) fused into the epilogue, reading parameters Pb[p] and
-// writing Pb[1 - p] (every gradient of the step sees pre-step parameters), and gathers the next
-// step's batch.
+// partial output layers, and the (s, pi) critics' action-gradient partials; B1 each row's TD target
+// and dq (from the partials), the critics' dh1, the policy's row-local backward chain (head backward
+// -> dh2p -> dh1p), the step control (lr_t) and the gather of the next step's batch.  Then ONE launch
+// (sac_wgrad.h) computes every weight gradient with its TF1 Adam (+ Polyak for the critics) fused
+// into the epilogue, reading parameters Pb[p] and writing Pb[1 - p] (every gradient of the step sees
+// pre-step parameters), beside the batch loss tail (logs, the alpha update, the step counter).
 #include <vector>
 #include <cstring>
 
-#include "sac_rows.h"
+#include "sac_wgrad.h"
 
 namespace mopo {
 
@@ -73,9 +72,7 @@ struct Sac {
   float *dh1[4];
   float *opart[8];                // [ncq][n][OPW] output-layer partials of the 8 instances (sac_rows.h)
   float *dapart[2];               // [ncq][n][OPW] action-gradient partials of Q1 / Q2 at (s, pi(s))
-  float *upart[2];                // [ncq][n][H] F1's dh1 / dq partials of Q1 / Q2(s, a) (sac_rows.h step 7)
   uint64_t* stamps = nullptr;     // MOPO_SAC_STAMPS builds: [slot][block][8]
-  int* rb_ready = nullptr;        // [ceil(n / 16)] B1's in-launch hand-off counters (zeroed by B2)
   float *dhead, *dh2p, *dh1p;
   // graph
   bool use_graph = true;
@@ -162,18 +159,9 @@ static int launch_gather(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   return 0;
 }
 
-#ifndef MOPO_SAC_F2_DA
-#define MOPO_SAC_F2_DA 1  // the (s, pi) critics' action gradient in F2 (sac_rows.h step 7), not B1
-#endif
-#ifndef MOPO_SAC_F1_U
-// 1: Q1 / Q2(s, a) dh1 / dq partials in F1 (step 7), B1 only sums and scales them -- measured 50.7 vs
-// 46.7 us/step (same-box A/B): F1 grows by more than B1 saves (2 MB of partials written and re-read)
-#define MOPO_SAC_F1_U 0
-#endif
-
 // One SAC step on batch bt[par], reading parameters Pb[par] and writing the updated ones to
-// Pb[1 - par].  With `prefetch`, the policy weight-gradient launch also gathers the next step's batch
-// into bt[1 - par] (a separate gather launch, or a forked graph branch, costs more than it hides).
+// Pb[1 - par].  With `prefetch`, B1 also gathers the next step's batch into bt[1 - par] (a separate
+// gather launch, or a forked graph branch, costs more than it hides).
 static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
                          const float* eps_in_s, const float* eps_in_n, hipStream_t s, bool prefetch) {
   const SacDims& d = h->d;
@@ -185,13 +173,19 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   ad.lr_t = h->beta_pow + 2; ad.tau = h->tau; ad.total = o.total; ad.n_pi = o.n_pi; ad.n_q = o.n_q;
   ad.norm_part = h->norm_part;
   ad.tgt_on = h->beta_pow + 3;
-  int slot = 0;
   const float* T = h->T;
   float* G = h->G;
   const Batch& bt = h->bt[par];
   auto Wq = [&](int qi, int k) { return P + o.q[qi][k]; };
   auto Tq = [&](int qi, int k) { return T + o.q[qi][k]; };
   const int ncq = ceil_div(H, RB_COLS), nrb = ceil_div(n, 16);
+  LossRows L{};
+  for (int i = 0; i < 6; ++i) {
+    L.qpart[i] = h->opart[2 + i];
+    L.b3[i] = i < 4 ? Wq(i & 1, 5) : Tq(i & 1, 5);
+  }
+  L.logp_s = h->logp_s; L.logp_n = h->logp_n; L.head_s = h->out[0]; L.rew = bt.rew; L.term = bt.term;
+  L.log_alpha = P + o.total; L.gamma = h->gamma; L.rscale = h->rscale;
   // ---- F1: pi(s), pi(s'), Q1(s,a), Q2(s,a) hidden layers + partial output layers
   {
     FwdArgsR f{};
@@ -209,29 +203,30 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       q.w1 = Wq(qi, 0); q.b1 = Wq(qi, 1); q.w2 = Wq(qi, 2); q.b2 = Wq(qi, 3);
       q.h1 = h->h1[2 + qi]; q.h2 = h->h2[2 + qi];
       q.wo = Wq(qi, 4); q.wo2 = nullptr; q.nout = 1; q.split = 1; q.opart = h->opart[2 + qi];
-      q.upart = MOPO_SAC_F1_U ? h->upart[qi] : nullptr;
     }
+    f.hd.iter = h->iter; f.hd.seed = seed; f.hd.eps_out[0] = h->eps_s; f.hd.eps_out[1] = h->eps_n;
+    f.hd.gen_eps = (eps_in_s ? 0 : 1) | (eps_in_n ? 0 : 2);   // the heads whose noise is not injected
     f.st = Stamps{h->stamps, 0};
     hipLaunchKernelGGL(sac_fwd_kernel<false>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
     MOPO_HIP(hipGetLastError());
   }
-  // ---- F2: the policy head from F1's partials -> Q1/Q2(s, pi(s)) (main), Qt1/Qt2(s', pi(s')) (target)
+  // ---- F2: the policy head from F1's partials -> Q1/Q2(s, pi(s)) (main), Qt1/Qt2(s', pi(s')) (target);
+  //      the main critics' blocks also emit their action-gradient partials (dq = 1)
   {
     FwdArgsR f{};
     f.ninst = 4; f.n = n; f.H = H; f.A = A; f.ncq = ncq; f.nrb = nrb;
     for (int i = 0; i < 4; ++i) {
       const int qi = i & 1;
       const bool tgt = i >= 2;
-      auto L = [&](int k) { return tgt ? Tq(qi, k) : Wq(qi, k); };
+      auto Lw = [&](int k) { return tgt ? Tq(qi, k) : Wq(qi, k); };
       FwdInst& q = f.in[i];
       q.x = tgt ? bt.xn : bt.sa; q.ldx = W; q.kx = O; q.k1 = W;
-      q.w1 = L(0); q.b1 = L(1); q.w2 = L(2); q.b2 = L(3);
-      q.h1 = tgt ? nullptr : h->h1[4 + i]; q.h2 = tgt ? nullptr : h->h2[4 + i];
-      q.wo = L(4); q.wo2 = nullptr; q.nout = 1; q.split = 1; q.opart = h->opart[4 + i];
+      q.w1 = Lw(0); q.b1 = Lw(1); q.w2 = Lw(2); q.b2 = Lw(3);
+      q.h1 = nullptr; q.h2 = nullptr;
+      q.wo = Lw(4); q.wo2 = nullptr; q.nout = 1; q.split = 1; q.opart = h->opart[4 + i];
       q.head = tgt ? 1 : 0;
-      // Q1 / Q2(s, pi): the blocks' (unselected) action-gradient partials for the policy backward
-      q.w1a = (MOPO_SAC_F2_DA && !tgt) ? Wq(qi, 0) + (int64_t)O * H : nullptr;
-      q.dapart = (MOPO_SAC_F2_DA && !tgt) ? h->dapart[qi] : nullptr;
+      q.w1a = tgt ? nullptr : Wq(qi, 0) + (int64_t)O * H;
+      q.dapart = tgt ? nullptr : h->dapart[qi];
     }
     FwdHead& hd = f.hd;
     hd.opart[0] = h->opart[0]; hd.opart[1] = h->opart[1]; hd.bm = P + o.pbm; hd.bl = P + o.pbl;
@@ -242,85 +237,82 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     hipLaunchKernelGGL(sac_fwd_kernel<true>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
     MOPO_HIP(hipGetLastError());
   }
-  // ---- B1: per-row TD targets and dq -> the critics' dh1 (Q1/Q2 at (s,a) and (s,pi)), the action-
-  //      gradient partials of the (s, pi) instances, and the batch loss tail (one extra block)
+  // ---- B1: per-row TD targets and dq -> Q1/Q2(s,a) dh1; the policy's row-local backward chain; the
+  //      step control; the gather of the next step's batch (with `prefetch`)
   {
     Dh1Args d{};
     const int ncq1 = ceil_div(H, B1_COLS);
-    // MOPO_SAC_F2_DA: the (s, pi) critics' backward ran in F2 (their action-gradient partials), so only
-    // Q1 / Q2(s, a) get a dh1 here and the policy-row blocks start at once (no in-launch hand-off)
-    d.ninst = MOPO_SAC_F2_DA ? 2 : 4; d.n = n; d.H = H; d.A = A; d.ncq = ncq; d.ncq1 = ncq1; d.nrb = nrb;
-    for (int i = 0; i < 4; ++i) {
-      const int qi = i & 1;
+    d.n = n; d.H = H; d.A = A; d.ncq = ncq; d.ncq1 = ncq1; d.nrb = nrb;
+    for (int i = 0; i < 2; ++i) {
       Dh1Inst& q = d.in[i];
-      q.h1 = h->h1[2 + i]; q.h2 = h->h2[2 + i]; q.w2 = Wq(qi, 2); q.w3 = Wq(qi, 4); q.kind = i;
-      q.dh1 = i < 2 ? h->dh1[i] : nullptr; q.dq = i < 2 ? h->dq[i] : nullptr;
-      q.w1a = i < 2 ? nullptr : Wq(qi, 0) + (int64_t)O * H; q.dapart = i < 2 ? nullptr : h->dapart[qi];
-      q.upart = (MOPO_SAC_F1_U && i < 2) ? h->upart[qi] : nullptr;
+      q.h1 = h->h1[2 + i]; q.h2 = h->h2[2 + i]; q.w2 = Wq(i, 2); q.w3 = Wq(i, 4); q.kind = i;
+      q.dh1 = h->dh1[i]; q.dq = h->dq[i];
     }
-    LossRows& L = d.L;
-    for (int i = 0; i < 6; ++i) {
-      L.qpart[i] = h->opart[2 + i];
-      L.b3[i] = i < 4 ? Wq(i & 1, 5) : Tq(i & 1, 5);
-    }
-    L.logp_s = h->logp_s; L.logp_n = h->logp_n; L.head_s = h->out[0]; L.rew = bt.rew; L.term = bt.term;
-    L.log_alpha = P + o.total; L.gamma = h->gamma; L.rscale = h->rscale;
-    d.ad = ad; d.tent = h->tent; d.lr = h->lr; d.logs = h->logs; d.beta_pow = h->beta_pow; d.iter = h->iter; d.tctl = h->tctl;
+    d.L = L;
+    d.lr = h->lr; d.beta_pow = h->beta_pow; d.iter = h->iter; d.tctl = h->tctl;
     PolicyRows& pr = d.pr;
-    pr.n = n; pr.O = O; pr.A = A; pr.H = H; pr.ncq = MOPO_SAC_F2_DA ? ncq : ncq1;
+    pr.n = n; pr.O = O; pr.A = A; pr.H = H; pr.ncq = ncq;
     pr.dapart[0] = h->dapart[0]; pr.dapart[1] = h->dapart[1];
-    if (MOPO_SAC_F2_DA) {
-      pr.qpart[0] = h->opart[4]; pr.qpart[1] = h->opart[5]; pr.qncq = ncq;
-      pr.b3[0] = Wq(0, 5); pr.b3[1] = Wq(1, 5);
-    }
+    pr.qpart[0] = h->opart[4]; pr.qpart[1] = h->opart[5];
+    pr.b3[0] = Wq(0, 5); pr.b3[1] = Wq(1, 5);
     pr.head_s = h->out[0]; pr.eps_s = h->eps_s; pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
     pr.h2p = h->h2[0]; pr.h1p = h->h1[0]; pr.W2p = P + o.pW2;
     pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p;
-    d.rb_ready = h->rb_ready;
+    d.gather = prefetch ? 1 : 0;
+    if (prefetch) {
+      d.ga = gather_args(h, 1 - par, env, mod, seed, nullptr);
+      d.ga.iter_add = 1;                       // the next step's batch (the counter advances in B2)
+    }
     d.st = Stamps{h->stamps, 2};
-    hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq1, nrb, d.ninst + 2), dim3(B1_WAVES * 64), 0, s, d);
+    if (ncq1 * nrb < 2 && prefetch) return fail("sac: B1 needs at least one gather block");
+    hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq1, nrb, 4), dim3(B1_WAVES * 64), 0, s, d);
     MOPO_HIP(hipGetLastError());
   }
-  // ---- B2: every weight gradient with its fused TF1 Adam (+ Polyak for the critics), the next step's
-  //      batch gather (with `prefetch`; the step counter was advanced by this step's loss tail), and
-  //      the zeroing of the next step's hand-off counters
+  // ---- B2: every weight gradient with its fused TF1 Adam (+ Polyak for the critics), beside the batch
+  //      loss tail (block 0)
   {
-    std::vector<GemmProb> g;
-    for (int qi = 0; qi < 2; ++qi) {  // critics: dW2 = h1^T dh2 (+db2), dW3 = h2^T dq (+db3)
-      auto w2 = mk(H, H, n, h->h1[2 + qi], H, 1, nullptr, H, 0, G + o.q[qi][2], H); w2.colsum = G + o.q[qi][3];
-      w2.adam = 1;
-      w2.b_u = h->dq[qi]; w2.b_v = Wq(qi, 4); w2.b_m = h->h2[2 + qi]; w2.b_ldm = H;
-      g.push_back(w2);
-      auto w3 = mk(H, 1, n, h->h2[2 + qi], H, 1, h->dq[qi], 1, 0, G + o.q[qi][4], 1); w3.colsum = G + o.q[qi][5];
-      w3.adam = 1;
-      g.push_back(w3);
+    WgradArgs g{};
+    std::vector<WgProb> ps;
+    for (int qi = 0; qi < 2; ++qi) {  // critics: dW2 = h1^T dh2 (+db2), dh2 = dq (x) W3 * (h2 > 0); dW3 = h2^T dq (+db3)
+      WgProb w2 = wprob(H, H, h->h1[2 + qi], H, nullptr, H, G + o.q[qi][2], H, G + o.q[qi][3]);
+      w2.bu = h->dq[qi]; w2.bv = Wq(qi, 4); w2.bm = h->h2[2 + qi]; w2.bldm = H;
+      ps.push_back(w2);
+      ps.push_back(wprob(H, 1, h->h2[2 + qi], H, h->dq[qi], 1, G + o.q[qi][4], 1, G + o.q[qi][5]));
     }
-    for (int qi = 0; qi < 2; ++qi) {  // critics: dW1 = [s,a]^T dh1 (+db1)
-      auto w1 = mk(W, H, n, bt.sa, W, 1, h->dh1[qi], H, 0, G + o.q[qi][0], H); w1.colsum = G + o.q[qi][1];
-      w1.adam = 1;
-      g.push_back(w1);
-    }
+    for (int qi = 0; qi < 2; ++qi)    // critics: dW1 = [s,a]^T dh1 (+db1)
+      ps.push_back(wprob(W, H, bt.sa, W, h->dh1[qi], H, G + o.q[qi][0], H, G + o.q[qi][1]));
     // the policy (dh2p, dh1p, dhead from the policy-row blocks of B1)
-    auto w2 = mk(H, H, n, h->h1[0], H, 1, h->dh2p, H, 0, G + o.pW2, H); w2.colsum = G + o.pb2; w2.adam = 1; g.push_back(w2);
-    auto wm = mk(H, A, n, h->h2[0], H, 1, h->dhead, 2 * A, 0, G + o.pWm, A); wm.colsum = G + o.pbm; wm.adam = 1;
-    g.push_back(wm);
-    auto wl = mk(H, A, n, h->h2[0], H, 1, h->dhead + A, 2 * A, 0, G + o.pWl, A); wl.colsum = G + o.pbl; wl.adam = 1;
-    g.push_back(wl);
-    auto w1 = mk(O, H, n, bt.sa, W, 1, h->dh1p, H, 0, G + o.pW1, H); w1.colsum = G + o.pb1; w1.adam = 1; g.push_back(w1);
-    const GatherArgs ga = gather_args(h, 1 - par, env, mod, seed, nullptr);
-    const Stamps st{h->stamps, 3};
-    if (launch_group(g, s, &ad, &slot, nullptr, prefetch ? &ga : nullptr, &st, h->rb_ready, nrb)) return -1;
+    ps.push_back(wprob(H, H, h->h1[0], H, h->dh2p, H, G + o.pW2, H, G + o.pb2));
+    ps.push_back(wprob(H, A, h->h2[0], H, h->dhead, 2 * A, G + o.pWm, A, G + o.pbm));
+    ps.push_back(wprob(H, A, h->h2[0], H, h->dhead + A, 2 * A, G + o.pWl, A, G + o.pbl));
+    ps.push_back(wprob(O, H, bt.sa, W, h->dh1p, H, G + o.pW1, H, G + o.pb1));
+    if ((int)ps.size() > WG_MAXP) return fail("sac: too many weight-gradient problems");
+    int tot = 0;
+    for (size_t i = 0; i < ps.size(); ++i) {
+      g.p[i] = ps[i];
+      g.prefix[i] = tot;
+      tot += wgrad_tiles(ps[i].M, ps[i].N);
+    }
+    g.np = (int)ps.size();
+    g.prefix[g.np] = tot;
+    g.n = n;
+    g.ad = ad;
+    g.ad.slot0 = 0;
+    g.L = L; g.A = A; g.ncq = ncq; g.tent = h->tent; g.logs = h->logs; g.iter = h->iter;
+    g.st = Stamps{h->stamps, 3};
+    if (tot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
+    h->nslots = tot;
+    hipLaunchKernelGGL(sac_wgrad_kernel, dim3(1 + tot), dim3(1024), 0, s, g);
+    MOPO_HIP(hipGetLastError());
   }
-  if (slot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
-  h->nslots = slot;  // tiles of the weight-gradient launch (tile choice: launch_group)
   return 0;
 }
 
-// the GEMM tiles of the weight-gradient launch (16x16 tiles; one grad-norm slot each)
+// the tiles of the weight-gradient launch (32 x 32; one grad-norm slot each)
 static int count_slots(const SacDims& d) {
-  auto t = [](int M, int N) { return ceil_div(M, 16) * ceil_div(N, 16); };
   const int H = d.H, O = d.O, A = d.A, W = O + A;
-  return 2 * t(H, H) + 2 * t(H, 1) + 2 * t(W, H) + t(H, H) + 2 * t(H, A) + t(O, H);
+  return 2 * wgrad_tiles(H, H) + 2 * wgrad_tiles(H, 1) + 2 * wgrad_tiles(W, H) + wgrad_tiles(H, H) +
+         2 * wgrad_tiles(H, A) + wgrad_tiles(O, H);
 }
 
 }  // namespace mopo
@@ -349,8 +341,6 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   const size_t npart = (size_t)ceil_div(H, RB_COLS) * n * OPW;
   for (int i = 0; i < 8; ++i) f(&h->opart[i], npart);
   for (int i = 0; i < 2; ++i) f(&h->dapart[i], npart);
-  for (int i = 0; i < 2; ++i) f(&h->upart[i], (size_t)ceil_div(H, RB_COLS) * n * H);
-  reg.push_back({(void**)&h->rb_ready, (size_t)ceil_div(batch, 16) * 4});
 #if MOPO_SAC_STAMPS
   reg.push_back({(void**)&h->stamps, (size_t)4 * 1024 * 8 * 8});
 #endif

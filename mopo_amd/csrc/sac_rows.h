@@ -9,21 +9,258 @@
 //       ([W_mean | W_log_std] for the policy, W3 for a critic)                   (mopo.py:298-324)
 //   F2  sac_fwd_kernel<true>: Q1/Q2(s, pi(s)) with the main critics, Qt1/Qt2(s', pi(s')) with the
 //       targets; the prologue sums pi's partials of its 16 rows into the squashed-Gaussian head
-//       (action, log-prob, noise: mopo.py:282-308) -- the action is the critic's layer-1 input
-//   B1  sac_dh1_kernel: dh1 = (dq (x) W3 * (h2 > 0)) W2^T * (h1 > 0) for Q1/Q2(s,a) and Q1/Q2(s,pi), the
-//       prologue forming each row's dq from the critics' partials (the TD target y, mopo.py:380-404;
-//       the min-Q selection, :367-377); the (s, pi) instances emit partials of d(-min Q)/d action
-//       (dh1 W1[O:]^T) for the policy backward; one extra block reduces the batch losses (logs,
-//       alpha Adam, lr_t, beta powers, step counter: mopo.py:403-443); the policy's row-local
-//       backward chain runs in the same launch, each row block's 4 workgroups starting as soon as the
-//       8 workgroups that produce its action-gradient partials have published them
-//
-// Replaces the previous 4-launch chain (forward hidden layers / output layers + head / (s, pi) hidden
-// layers / losses + critic output layers) + the critic dh1 launch: 5 -> 3 launches.
+//       (action, log-prob, noise: mopo.py:282-308) -- the action is the critic's layer-1 input; the
+//       main critics' blocks also emit their share of d Q / d action (dq = 1) for the policy backward
+//   B1  sac_dh1_kernel: dh1 = (dq (x) W3 * (h2 > 0)) W2^T * (h1 > 0) for Q1/Q2(s,a), the prologue forming
+//       each row's dq from the critics' partials (the TD target y, mopo.py:380-404); the policy's
+//       row-local backward chain (policy_rows_block, from F2's partials with the min-Q selection,
+//       mopo.py:367-377); the step control (lr_t, beta powers, target-update flag: mopo.py:407-447); and
+//       the gather of the next step's batch
+// The weight gradients and the batch loss tail follow in one more launch (sac_wgrad.h).
 #pragma once
 #include "gemm_group.h"
 
 namespace mopo {
+
+// ---- SAC batch gather (_training_batch, mopo.py:801-821): rows [0, n_env) from the env pool, rest
+// from the model pool; each index uniform over the pool's live size (Philox) unless injected.  One
+// thread per (row, field column): every thread derives its row's source index itself (the Philox
+// draw is cheap), so the work is two dependent memory latencies (pool size + counter, then the field)
+// with no barrier.  Run by sac_gather_kernel (sac.hip) and by the gather blocks of sac_dh1_kernel.
+struct Batch {
+  float *sa, *xpi, *xn, *rew, *term;  // [s, a], [s, pi(s)], [s', pi(s')], r, done
+  int64_t* idx;                       // [n] sampled rows
+};
+
+struct GatherArgs {
+  mopo_pool_desc env, mod;
+  int n, n_env, O, A;                // n: batch rows
+  const int64_t* idx_in;             // injected rows or NULL (Philox draw)
+  uint64_t seed;
+  const int64_t* iter;
+  int iter_add;                      // the step the batch is for: *iter + iter_add (B1 gathers the next step's)
+  Batch out;
+};
+
+// field c of batch row r (obs | act | next_obs | rew | term)
+static __device__ __forceinline__ void gather_elem(const GatherArgs& g, int r, int c) {
+  const int O = g.O, A = g.A, W = O + A;
+  const bool fe = r < g.n_env;
+  const mopo_pool_desc& p = fe ? g.env : g.mod;
+  int64_t src;
+  if (g.idx_in) {
+    src = g.idx_in[r];
+  } else {
+    const uint64_t size = (uint64_t)p.d_state[1];
+    const int64_t it = *g.iter + g.iter_add;
+    u32x4 cc{(uint32_t)r, (uint32_t)it, (uint32_t)((uint64_t)it >> 32), RNG_SAC};
+    u32x4 q = philox(cc, (uint32_t)g.seed, (uint32_t)(g.seed >> 32));
+    src = (int64_t)(((uint64_t)q.x * size) >> 32);
+  }
+  const Batch& b = g.out;
+  if (c == 0) b.idx[r] = src;
+  if (c < O) {
+    const float v = p.d_obs[src * O + c];
+    b.sa[r * W + c] = v;
+    b.xpi[r * W + c] = v;
+  } else if (c < O + A) {
+    b.sa[r * W + c] = p.d_act[src * A + (c - O)];
+  } else if (c < 2 * O + A) {
+    b.xn[r * W + (c - O - A)] = p.d_next_obs[src * O + (c - O - A)];
+  } else if (c == 2 * O + A) {
+    b.rew[r] = p.d_rew[src];
+  } else {
+    b.term[r] = (float)p.d_term[src];
+  }
+}
+
+// ---- the policy's row-local backward chain (mopo.py:337-377 through the critics at (s, pi(s))), run by
+// the policy-row blocks of sac_dh1_kernel: block (rb, cq) owns batch rows [16 rb, 16 rb + 16) and
+// columns [128 cq, 128 cq + 128) of the policy's first hidden layer.
+//   dx_a   = -1/n d Q_sel(s, pi) / d action                            (Q_sel = the smaller critic per row)
+//            -- the sum of the per-column-block partials sac_fwd_kernel<true> wrote (dq = 1), of the
+//            critic tf.minimum selects (mopo.py:367-377; its gradient goes to x where x <= y)
+//   dhead  = squashed-Gaussian head backward (mean, log_std; alpha / n on the log-prob)
+//   dh2p   = (dhead_mu Wm^T + dhead_ls Wl^T) * (h2p > 0)               (all H columns, in LDS)
+//   dh1p   = dh2p W2p^T * (h1p > 0)                                     (this block's columns, MFMA)
+// Every quantity before dh1p is row-local, so each column block recomputes it (cheap: ncq partials
+// per action, K = 2A per dh2p value) and only cq == 0 stores dhead and dh2p, which the policy weight
+// gradients of the next launch read with dh1p.
+constexpr int OPW = 16;              // floats per (column block, row) record of the policy's output partials
+constexpr int DPW = 8;               // ... of the action-gradient partials (A <= 8); a critic's is 1 float
+constexpr int MAX_NCQ = 4;           // column blocks of 64 (H <= 256)
+constexpr int DH2_TILES = 4;         // dh2p column tiles per wave (H <= 256 over >= 4 waves)
+
+struct PolicyRows {
+  int n, O, A, H, ncq;
+  const float* dapart[2];            // Q1 / Q2 at (s, pi(s)): [ncq][n][DPW] partials of dh1 W1[O:]^T (dq = 1)
+  // Q1 / Q2(s, pi) = b3 + the critics' forward partials [ncq][n]: the min-Q selection
+  const float* qpart[2]; const float* b3[2];
+  const float* head_s;               // [n][2A] mean | raw log_std
+  const float* eps_s;                // [n][A]
+  const float* log_alpha;
+  const float* Wm; const float* Wl;  // [H][A]
+  const float* h2p; const float* h1p;// [n][H]
+  const float* W2p;                  // [H][H]
+  float* dhead; float* dh2p; float* dh1p;
+};
+
+
+// Latency layout: every global operand of the chain is loaded in ONE burst of unconditional
+// (range-checked) loads at the start -- the action-gradient partials and head inputs, Wm / Wl / h2p at
+// this thread's dh2p column, this wave's W2p operands of the dh1p tile and the h1p mask -- so the
+// block pays one memory latency, then computes.
+// S: >= 16 (H + 4) floats of LDS; hs: >= 3 * 128 floats.  Blocks of 4 or 8 waves (64 or 128 dh1p
+// columns).  H % 16 == 0, H <= 256 (one dh2p column per thread), A <= 8.
+static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs,
+                                                         const Stamps& st) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int H = c.H, A = c.A, HS = H + 4, n = c.n;
+  const int pcols = 16 * (int)(blockDim.x >> 6);   // dh1p columns of the block: one 16-wide tile per wave
+  const int ncq = (H + pcols - 1) / pcols;
+  const int rb = x / ncq, cq = x % ncq, r0 = rb * 16;
+  const int li = lane & 15, lk = lane >> 4;
+  // ---- the burst: head inputs, Wm / Wl / h2p at this thread's dh2p column, this wave's W2p operands of
+  //      the dh1p tile and the h1p mask, the critics' partials
+  const int hr = tid >> 3, hj = tid & 7, hrow = r0 + hr;
+  const bool hon = tid < 128 && hj < A && hrow < n;
+  const auto dh = rsrc(c.head_s, (int64_t)n * 2 * A), de = rsrc(c.eps_s, (int64_t)n * A);
+  const float mu = bload(dh, hon ? hrow * 2 * A + hj : -1);
+  const float raw = bload(dh, hon ? hrow * 2 * A + A + hj : -1);
+  const float ep = bload(de, hon ? hrow * A + hj : -1);
+  const float la = *c.log_alpha;
+  float qv[2][MAX_NCQ];                // Q1 / Q2(s, pi) partials of this thread's row: the chain's first link
+  float dap[2][MAX_NCQ];
+  float b3v[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const auto dq = rsrc(c.qpart[i], (int64_t)c.ncq * n);
+    const auto dp = rsrc(c.dapart[i], (int64_t)c.ncq * n * DPW);
+#pragma unroll
+    for (int q = 0; q < MAX_NCQ; ++q) {
+      qv[i][q] = bload(dq, (hon && q < c.ncq) ? q * n + hrow : -1);
+      dap[i][q] = bload(dp, (hon && q < c.ncq) ? (q * n + hrow) * DPW + hj : -1);
+    }
+    b3v[i] = *c.b3[i];
+  }
+  // dh2p tiles of this wave: 16 columns each, tiles w, w + nw, ... (at most DH2_TILES)
+  const int nw = (int)(blockDim.x >> 6), nt2 = (H + 15) >> 4;
+  const auto dwm = rsrc(c.Wm, (int64_t)H * A), dwl = rsrc(c.Wl, (int64_t)H * A), dh2 = rsrc(c.h2p, (int64_t)n * H);
+  float wb[DH2_TILES][4], h2v[DH2_TILES][4];   // B(k, c) = k < 8 ? Wm[c][k] : Wl[c][k - 8]; lane k = 4 s + lk
+#pragma unroll
+  for (int q = 0; q < DH2_TILES; ++q) {
+    const int c2 = (w + q * nw) * 16 + li;
+    const bool on = w + q * nw < nt2 && c2 < H;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int k = 4 * (s2 & 1) + lk;
+      wb[q][s2] = bload(s2 < 2 ? dwm : dwl, (on && k < A) ? c2 * A + k : -1);
+      h2v[q][s2] = bload(dh2, on ? (r0 + 4 * lk + s2) * H + c2 : -1);     // rows >= n: past the extent
+    }
+  }
+  const int j0 = cq * pcols + w * 16, col = j0 + li;
+  const bool tile_on = j0 < H;
+  const auto dw2 = rsrc(c.W2p, (int64_t)H * H);
+  const int boff = (tile_on ? col : 0) * H;
+  f32x4 bq[16];                       // B(k, j) = W2p[j][k]: lane (li, lk) contracts k = 64 lk + 4 t + u
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int k = 64 * lk + 4 * t;
+    bq[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dw2, (k < H ? boff + k : -4) * 4, 0, 0));
+  }
+  const auto dm1 = rsrc(c.h1p, (int64_t)n * H);
+  float m1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
+  stamp(st, 1);
+  // ---- squashed-Gaussian head backward (mopo.py:282-308 differentiated; pi_loss mopo.py:371-377)
+  float* dmu_s = hs + 128;
+  float* dls_s = hs + 256;
+  if (tid < 128) {
+    float dmu = 0.f, dls = 0.f;
+    if (hon) {
+      float da = 0.f;                                               // -dmin q / da through Q1 / Q2:
+      float q12[2];                                                 // the selected critic's partials, x -1/n
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float qs = b3v[i];
+#pragma unroll
+        for (int q = 0; q < MAX_NCQ; ++q) qs += qv[i][q];
+        q12[i] = qs;
+      }
+      const int sel = q12[0] <= q12[1] ? 0 : 1;
+#pragma unroll
+      for (int q = 0; q < MAX_NCQ; ++q) da += sel == 0 ? dap[0][q] : dap[1][q];
+      da *= -1.f / (float)n;
+      const float g = expf(la) / (float)n;                         // d L_pi / d logp (stop_gradient(alpha))
+      const float ls = fminf(fmaxf(raw, -20.f), 2.f);
+      const float sd = expf(ls);
+      const float u = mu + ep * sd;
+      const float a = tanhf(u);
+      const float inv = 1.f / (sd + 1e-8f);
+      const float zz = (u - mu) * inv;
+      float du = da * (1.f - a * a);                                // tanh grad (y-based)
+      du += g * (-zz * inv);                                        // gaussian_likelihood wrt x
+      du += g * (2.f - 4.f / (1.f + expf(2.f * u)));                // squash correction: 2 - 4 sigmoid(-2u)
+      dmu = g * zz * inv + du;
+      const float dstd = g * zz * zz * inv + du * ep;
+      dls = -g + dstd * sd;
+      if (!(raw >= -20.f && raw <= 2.f)) dls = 0.f;                 // clip_by_value grad
+      if (cq == 0) {
+        c.dhead[(int64_t)hrow * 2 * A + hj] = dmu;
+        c.dhead[(int64_t)hrow * 2 * A + A + hj] = dls;
+      }
+    }
+    dmu_s[tid] = dmu;
+    dls_s[tid] = dls;
+  }
+  lds_barrier();
+  stamp(st, 2);
+  // ---- dh2p = dhead [dWm; dWl]^T (K = 16: mu parts 0..7, log-std parts 8..15) masked by h2p > 0 ->
+  //      LDS rows of stride HS (and dh2p in HBM from the cq == 0 blocks)
+  {
+    float av[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) av[s2] = (s2 < 2 ? dmu_s : dls_s)[li * 8 + 4 * (s2 & 1) + lk];
+#pragma unroll
+    for (int q = 0; q < DH2_TILES; ++q) {
+      if (w + q * nw >= nt2) break;
+      f32x4 d = zero4();
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) d = mfma4(av[s2], wb[q][s2], d);
+      const int c2 = (w + q * nw) * 16 + li;
+      if (c2 < H) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {                                // D: row 4 lk + i, col li
+          const int row = 4 * lk + i;
+          const float v = h2v[q][i] > 0.f ? d[i] : 0.f;
+          S[row * HS + c2] = v;
+          if (cq == 0 && r0 + row < n) c.dh2p[(int64_t)(r0 + row) * H + c2] = v;
+        }
+      }
+    }
+  }
+  lds_barrier();
+  stamp(st, 3);
+  // ---- dh1p tile = dh2p W2p^T * (h1p > 0): rows r0.., columns j0.. (wave w)
+  if (!tile_on) return;
+  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int k = 64 * lk + 4 * t;
+    const f32x4 a = k < H ? *reinterpret_cast<const f32x4*>(S + li * HS + k) : zero4();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = mfma4(a[u], bq[t][u], acc[u]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = r0 + 4 * lk + i;                                // D: col li, row 4 lk + i
+    if (row < n && col < H) {
+      const float v = acc[0][i] + acc[1][i] + acc[2][i] + acc[3][i];
+      c.dh1p[(int64_t)row * H + col] = m1[i] > 0.f ? v : 0.f;
+    }
+  }
+}
 
 constexpr int RB_COLS = 64;  // second-layer columns per workgroup (4 waves x 16); OPW: gemm_group.h
 
@@ -35,15 +272,12 @@ struct FwdInst {
   float* h1; float* h2;              // stored for the backward pass when non-NULL
   const float* wo; const float* wo2; // output layer [H][nout]: columns [0, split) from wo (ld split),
   int nout, split;                   //   [split, nout) from wo2 (ld nout - split)
-  float* opart;                      // [ncq][n][OPW] partial dots of the block's 64 outputs
+  float* opart;                      // [ncq][n][OPW] (policy) / [ncq][n] (critic) partial dots of the block's 64 outputs
   int head;                          // F2: 0 = pi(s) head (s, pi(s)), 1 = pi(s') head
   // F2 (s, pi) critics: the block's partial of d Q / d action = (W3 * (h2 > 0)) W2^T * (h1 > 0) W1[O:]^T
   // over its 64 columns (dq = 1; the policy-row consumer applies the min-Q selection and -1/n)
   const float* w1a;                  // W1[O:] = the action rows [A][H], or NULL
-  float* dapart;                     // [ncq][n][OPW]
-  // F1 Q1 / Q2(s, a): the block's partial of dh1 / dq = (W3 * (h2 > 0)) W2^T * (h1 > 0) over its 64
-  // columns, all H hidden units ([ncq][n][H]); B1 sums them and scales by the row's dq
-  float* upart;
+  float* dapart;                     // [ncq][n][DPW]
 };
 
 struct FwdHead {                     // F2: the squashed-Gaussian head of pi(s) / pi(s') (HeadCtx math)
@@ -52,6 +286,7 @@ struct FwdHead {                     // F2: the squashed-Gaussian head of pi(s) 
   const float* eps_in[2];            // injected noise [n][A] or NULL (Philox)
   float* eps_out[2]; float* head_out[2]; float* logp[2];   // written by the designated blocks
   uint64_t seed; const int64_t* iter;
+  int gen_eps;                       // F1: bit i draws head i's noise into eps_out[i] (not injected; F2 loads it)
 };
 
 struct FwdArgsR {
@@ -61,44 +296,53 @@ struct FwdArgsR {
   Stamps st;
 };
 
-// the head of row r, action j (8 lanes per row; every lane of the 8 calls it): pre-activation
-// mean / raw log_std from the partials, then head_fwd_elem's math; returns the action (tanh u)
-static __device__ __forceinline__ float rows_head(const FwdHead& h, int nxt, int n, int A, int ncq, int r, int j,
+// the head of row r, action j (8 lanes per row; every lane of the 8 calls both halves): the loads (issued
+// before every other operand of the launch: the head is the first link of the launch's chain), then the
+// pre-activation mean / raw log_std from the partials and head_fwd_elem's math; returns the action (tanh u)
+struct HeadIn { float pm[MAX_NCQ], pl[MAX_NCQ], bm, bl, z; };
+
+// the policy noise of row r, action j (mopo.py:306 tf.random_normal): Philox keyed by (seed, step, row,
+// which head, action block) -- generated by F1 (it depends on nothing F1 computes), so F2's head only loads it
+static __device__ __forceinline__ float head_noise(uint64_t seed, int64_t it, int r, int nxt, int j) {
+  const int blk = j >> 2;
+  u32x4 c{(uint32_t)r | ((uint32_t)nxt << 31), (uint32_t)it ^ ((uint32_t)blk << 24), (uint32_t)((uint64_t)it >> 32),
+          RNG_SAC + 16};
+  u32x4 q = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  float z0, z1;
+  if (j & 2) box_muller(q.z, q.w, z0, z1);
+  else box_muller(q.x, q.y, z0, z1);
+  return (j & 1) ? z1 : z0;
+}
+
+static __device__ __forceinline__ HeadIn rows_head_load(const FwdHead& h, int nxt, int n, int A, int ncq, int r,
+                                                        int j, bool ok) {
+  HeadIn o;
+  const bool on = ok && j < A;
+  const auto dp = rsrc(h.opart[nxt], (int64_t)ncq * n * OPW);
+#pragma unroll
+  for (int c = 0; c < MAX_NCQ; ++c) {     // unconditional loads (out-of-range ones return 0)
+    o.pm[c] = bload(dp, (on && c < ncq) ? (c * n + r) * OPW + j : -1);
+    o.pl[c] = bload(dp, (on && c < ncq) ? (c * n + r) * OPW + A + j : -1);
+  }
+  o.bm = bload(rsrc(h.bm, A), on ? j : -1);
+  o.bl = bload(rsrc(h.bl, A), on ? j : -1);
+  const float* ein = h.eps_in[nxt] ? h.eps_in[nxt] : h.eps_out[nxt];   // injected, or F1's draws
+  o.z = bload(rsrc(ein, (int64_t)n * A), on ? r * A + j : -1);
+  return o;
+}
+
+static __device__ __forceinline__ float rows_head(const FwdHead& h, const HeadIn& in, int nxt, int A, int r, int j,
                                                   bool ok, bool store) {
   const bool on = ok && j < A;
-  float mu = 0.f, raw = 0.f, z = 0.f;
-  if (on) {
-    const auto dp = rsrc(h.opart[nxt], (int64_t)ncq * n * OPW);
-    float pm[MAX_NCQ], pl[MAX_NCQ];
-#pragma unroll
-    for (int c = 0; c < MAX_NCQ; ++c) {   // unconditional loads, then the sums in column-block order
-      pm[c] = bload(dp, c < ncq ? (c * n + r) * OPW + j : -1);
-      pl[c] = bload(dp, c < ncq ? (c * n + r) * OPW + A + j : -1);
-    }
-    mu = h.bm[j];
-    raw = h.bl[j];
-#pragma unroll
-    for (int c = 0; c < MAX_NCQ; ++c) {
-      mu += pm[c];
-      raw += pl[c];
-    }
-    const float* ein = h.eps_in[nxt];
-    if (ein) {
-      z = ein[r * A + j];
-    } else {
-      const int64_t it = *h.iter;
-      const int blk = j >> 2;
-      u32x4 c{(uint32_t)r | ((uint32_t)nxt << 31), (uint32_t)it ^ ((uint32_t)blk << 24), (uint32_t)((uint64_t)it >> 32),
-              RNG_SAC + 16};
-      u32x4 q = philox(c, (uint32_t)h.seed, (uint32_t)(h.seed >> 32));
-      float z0, z1;
-      if (j & 2) box_muller(q.z, q.w, z0, z1);
-      else box_muller(q.x, q.y, z0, z1);
-      z = (j & 1) ? z1 : z0;
-    }
-  }
   float v = 0.f, act = 0.f;
   if (on) {
+    float mu = in.bm, raw = in.bl;
+    const float z = in.z;
+#pragma unroll
+    for (int c = 0; c < MAX_NCQ; ++c) {   // the sums in column-block order
+      mu += in.pm[c];
+      raw += in.pl[c];
+    }
     const float ls = fminf(fmaxf(raw, -20.f), 2.f);               // mopo.py:304
     const float sd = expf(ls);
     const float u = mu + z * sd;                                    // mopo.py:306
@@ -107,7 +351,7 @@ static __device__ __forceinline__ float rows_head(const FwdHead& h, int nxt, int
         - 2.f * (0.6931471805599453f - u - softplusf(-2.f * u));    // squash correction (:292)
     act = tanhf(u);
     if (store) {
-      h.eps_out[nxt][r * A + j] = z;
+      if (h.eps_in[nxt]) h.eps_out[nxt][r * A + j] = z;
       h.head_out[nxt][r * 2 * A + j] = mu;
       h.head_out[nxt][r * 2 * A + A + j] = raw;
     }
@@ -158,10 +402,10 @@ static __device__ __forceinline__ void rows_contract(const float* As, const f32x
 }
 
 // wave 0: partial output dots of the block's tile, Out[r][j] = sum_{c < COLS} T[r][c] WT[j][c] (COLS / 4
-// MFMAs; row stride COLS + 4); rows r < n and j < nout are stored to part[row][OPW]
-template <int COLS, bool SC1 = false>
+// MFMAs; row stride COLS + 4); rows r < n and j < nout are stored to part[row][ldp]
+template <int COLS>
 static __device__ __forceinline__ void rows_partial_out(const float* T, const float* WT, int li, int lk, int i0, int n,
-                                                        int nout, float* part) {
+                                                        int nout, int ldp, float* part) {
   constexpr int LD = COLS + 4;
   f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
@@ -175,9 +419,38 @@ static __device__ __forceinline__ void rows_partial_out(const float* T, const fl
     const int orow = i0 + 4 * lk + rr;
     if (li < nout && orow < n) {
       const float v = acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr];
-      if constexpr (SC1) __hip_atomic_store(part + (int64_t)orow * OPW + li, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else part[(int64_t)orow * OPW + li] = v;
+      part[(int64_t)orow * ldp + li] = v;
     }
+  }
+}
+
+#ifndef MOPO_SAC_S7_EARLY
+// 1: issue step 7's operand loads right after the layer-2 MFMAs instead of in step 7 -- measured 45.4 vs
+// 43.6 us/step (same-box A/B): they delay the epilogue's own loads and stores more than they hide
+#define MOPO_SAC_S7_EARLY 0
+#endif
+
+// F2 (s, pi) critics: step 7's operands.  A(m = k, K = c): lane (li, lk) holds W2[64 w + 16 t + li][c0 +
+// 16 s + 4 lk + u] (one b128 per (t, s)); B(K = k, n = a) of the action contraction: W1[O + a = li][64 w +
+// 16 t + 4 lk .. + 3]
+static __device__ __forceinline__ void step7_loads(const FwdInst& p, int w, int li, int lk, int c0, int H, int A,
+                                                   f32x4 (&wa2)[4][4], f32x4 (&wb1)[4]) {
+  const int kw = 64 * w;
+  const auto dw2 = rsrc(p.w2, (int64_t)H * H);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int k = kw + 16 * t + li, c = c0 + 16 * s2 + 4 * lk;
+      wa2[t][s2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 dw2, ((k < H && c < H) ? k * H + c : -4) * 4, 0, 0));
+    }
+  const auto dwa = rsrc(p.w1a, p.w1a ? (int64_t)A * H : 0);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int k = kw + 16 * t + 4 * lk;
+    wb1[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           dwa, ((p.w1a && li < A && k < H) ? li * H + k : -4) * 4, 0, 0));
   }
 }
 
@@ -198,35 +471,16 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
   const FwdInst p = pick4(a.in, ii);
   const int n = a.n, H = a.H, A = a.A;
   const int i0 = rb * 16, c0 = cq * RB_COLS, jw = c0 + w * 16;
-  // ---- 1. every global operand, issued up front: this wave's W2 operand straight into MFMA registers
-  //         (lane (li, lk): W2[64 lk + 4 s + u][jw + li]; 16 lanes read 64 contiguous bytes of a row),
-  //         the output-layer columns of the block's 64 rows, layer 1
+  // ---- 0. F2: the head's operands first (the head is the first link of this launch's chain)
+  const int hr = tid >> 3, hj = tid & 7, hrow = i0 + hr;
+  HeadIn hin{};
+  if (HEAD && tid < 128) hin = rows_head_load(a.hd, p.head, n, A, a.ncq, hrow, hj, hrow < n);
+  // ---- 1. every global operand, issued up front in the order the chain consumes them: layer 1 (its
+  //         MFMAs then run while the layer-2 operand is still arriving -- loads return in order, so
+  //         layer-1 operands queued behind it waited for all of it), this wave's W2 operand straight into
+  //         MFMA registers (lane (li, lk): W2[64 lk + 4 s + u][jw + li]; 16 lanes read 64 contiguous bytes
+  //         of a row), the output-layer columns of the block's 64 rows
   const int li = lane & 15, lk = lane >> 4;
-  f32x4 bp[16];
-  {
-    const auto dbw = rsrc(p.w2, (int64_t)H * H);
-    const bool con = jw + li < H;
-#pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = 64 * lk + 4 * s2 + u;
-        bp[s2][u] = bload(dbw, (con && k < H) ? k * H + jw + li : -1);
-      }
-  }
-  float wov[4];
-  {
-    const int ld2 = p.nout - p.split;
-    const auto d1 = rsrc(p.wo, (int64_t)H * p.split), d2 = rsrc(p.wo2, (int64_t)H * (ld2 > 0 ? ld2 : 1));
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {           // element e = c * OPW + j of Wo: c = e / 16, j = e % 16
-      const int e = tid + 256 * q, c = c0 + (e >> 4), j = e & 15;
-      const bool in1 = j < p.split, on = c < H && j < p.nout;
-      const float v1 = bload(d1, on && in1 ? c * p.split + j : -1);
-      const float v2 = bload(d2, on && !in1 ? c * ld2 + (j - p.split) : -1);
-      wov[q] = in1 ? v1 : v2;
-    }
-  }
   const int r = lane & 15, q4 = lane >> 4;
   const int row = i0 + r;
   const int k1 = p.k1, ns = (k1 + 4) >> 2, sb = k1 >> 2;
@@ -252,13 +506,41 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
       bv[kt] = bload(db, k < H ? k : -1);
     }
   }
+  f32x4 bp[16];
+  {
+    const auto dbw = rsrc(p.w2, (int64_t)H * H);
+    const bool con = jw + li < H;
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = 64 * lk + 4 * s2 + u;
+        bp[s2][u] = bload(dbw, (con && k < H) ? k * H + jw + li : -1);
+      }
+  }
+  float wov[4];
+  {
+    const int ld2 = p.nout - p.split;
+    const auto d1 = rsrc(p.wo, (int64_t)H * p.split), d2 = rsrc(p.wo2, (int64_t)H * (ld2 > 0 ? ld2 : 1));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {           // element e = c * OPW + j of Wo: c = e / 16, j = e % 16
+      const int e = tid + 256 * q, c = c0 + (e >> 4), j = e & 15;
+      const bool in1 = j < p.split, on = c < H && j < p.nout;
+      const float v1 = bload(d1, on && in1 ? c * p.split + j : -1);
+      const float v2 = bload(d2, on && !in1 ? c * ld2 + (j - p.split) : -1);
+      wov[q] = in1 ? v1 : v2;
+    }
+  }
   float b2v = bload(rsrc(p.b2, H), jw + (lane & 15) < H ? jw + (lane & 15) : -1);
+  // ---- F1, pi(s) / pi(s') blocks of column block 0: this step's policy noise of their 16 rows (while the
+  //      operands arrive), which F2's head loads
+  if (!HEAD && ii < 2 && cq == 0 && ((a.hd.gen_eps >> ii) & 1) && tid < 128 && hj < A && hrow < n)
+    a.hd.eps_out[ii][hrow * A + hj] = head_noise(a.hd.seed, *a.hd.iter, hrow, ii, hj);
   // ---- 2. F2: the policy head of the block's 16 rows (its action feeds layer 1)
   if (HEAD) {
     if (tid < 128) {
-      const int hr = tid >> 3, hj = tid & 7, hrow = i0 + hr;
       const bool store = cq == 0 && (ii == 0 || ii == 2);  // Q1(s,pi) / Qt1(s',pi') blocks publish the head
-      act_s[hr][hj] = rows_head(a.hd, p.head, n, A, a.ncq, hrow, hj, hrow < n, store);
+      act_s[hr][hj] = rows_head(a.hd, hin, p.head, A, hrow, hj, hrow < n, store);
     }
     lds_barrier();
 #pragma unroll
@@ -305,6 +587,10 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
   // ---- 4. layer 2: the wave's 16 x 16 tile over the whole K
   f32x4 acc[4];
   rows_contract(As, bp, li, lk, acc);
+  f32x4 wa2[4][4], wb1[4];
+#if MOPO_SAC_S7_EARLY
+  if (HEAD && p.dapart) step7_loads(p, w, li, lk, c0, H, A, wa2, wb1);
+#endif
   stamp(a.st, 3);
   // ---- 5. bias + relu (D: column li, rows 4 lk + rr); h2 store; the tile into LDS
   const int col = jw + li;
@@ -317,36 +603,21 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
   }
   lds_barrier();
   // ---- 6. partial output dots of the block's 64 columns (wave 0, MFMA)
-  if (w == 0) rows_partial_out<RB_COLS>(Ts, Wo, li, lk, i0, n, p.nout, p.opart + (int64_t)cq * n * OPW);
-  // ---- 7. a critic's backward share of the block (dq = 1): wave w forms dh1 rows k in [64 w, 64 w + 64)
-  //         of D(k, r) = sum_c W2[k][c0 + c] G(r, c), G = W3[c0 + c] (h2 > 0) (K = the block's 64
-  //         columns), masked by h1 > 0.  F2, Q1 / Q2 at (s, pi(s)): then its partial of the action
+  if (w == 0) {                     // a critic's records are 1 float (dense rows: the loss reads stay coalesced)
+    const int ldp = p.nout == 1 ? 1 : OPW;
+    rows_partial_out<RB_COLS>(Ts, Wo, li, lk, i0, n, p.nout, ldp, p.opart + (int64_t)cq * n * ldp);
+  }
+  // ---- 7. F2, Q1 / Q2 at (s, pi(s)): the critic's backward share of the block (dq = 1): wave w forms
+  //         dh1 rows k in [64 w, 64 w + 64) of D(k, r) = sum_c W2[k][c0 + c] G(r, c), G = W3[c0 + c]
+  //         (h2 > 0) (K = the block's 64 columns), masked by h1 > 0, then its partial of the action
   //         gradient sum_k dh1(r, k) W1[O + a][k], so the policy's backward needs no critic backward at
-  //         (s, pi) in the next launch.  F1, Q1 / Q2(s, a): the masked tile itself (upart), which B1
-  //         sums over the column blocks and scales by the row's dq (no W2 operand burst there).
+  //         (s, pi) in the next launch
   {
-    if (p.dapart || p.upart) {
+    if (HEAD && p.dapart) {
+#if !MOPO_SAC_S7_EARLY
+      step7_loads(p, w, li, lk, c0, H, A, wa2, wb1);
+#endif
       const int kw = 64 * w;
-      // A(m = k, K = c): lane (li, lk) holds W2[kw + 16 t + li][c0 + 16 s + 4 lk + u] (one b128 per (t, s))
-      const auto dw2 = rsrc(p.w2, (int64_t)H * H);
-      f32x4 wa2[4][4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          const int k = kw + 16 * t + li, c = c0 + 16 * s2 + 4 * lk;
-          wa2[t][s2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     dw2, ((k < H && c < H) ? k * H + c : -4) * 4, 0, 0));
-        }
-      // B(K = k, n = a) of the action contraction: W1[O + a = li][kw + 16 t + 4 lk .. + 3]
-      const auto dwa = rsrc(p.w1a, p.w1a ? (int64_t)A * H : 0);
-      f32x4 wb1[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int k = kw + 16 * t + 4 * lk;
-        wb1[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               dwa, ((p.w1a && li < A && k < H) ? li * H + k : -4) * 4, 0, 0));
-      }
       // G(r = li, c = 16 s + 4 lk + u) from the block's h2 tile and W3 (Wo row 0)
       float gb[4][4];
 #pragma unroll
@@ -371,11 +642,7 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
           um[i] = (k < H && As[li * RB_LD + k] > 0.f) ? d[i] : 0.f;
           da = mfma4(um[i], wb1[t][i], da);
         }
-        const int k0 = kw + 16 * t + 4 * lk;
-        if (p.upart && i0 + li < n && k0 < H)                // one b128 per lane: row li, k0 .. k0 + 3
-          *reinterpret_cast<f32x4*>(p.upart + ((int64_t)cq * n + i0 + li) * H + k0) = um;
       }
-      if (!p.dapart) goto done7;
 #pragma unroll
       for (int i = 0; i < 4; ++i)                            // D: r = 4 lk + i, a = li
         if (li < 8) da_s[w][4 * lk + i][li] = da[i];
@@ -383,11 +650,10 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
       if (tid < 128) {                                       // waves' partials in wave order
         const int rr = tid >> 3, aa = tid & 7, orow = i0 + rr;
         const float v = da_s[0][rr][aa] + da_s[1][rr][aa] + da_s[2][rr][aa] + da_s[3][rr][aa];
-        if (aa < A && orow < n) p.dapart[((int64_t)cq * n + orow) * OPW + aa] = v;
+        if (aa < A && orow < n) p.dapart[((int64_t)cq * n + orow) * DPW + aa] = v;
       }
     }
   }
-done7:
   stamp(a.st, 4);
 }
 
@@ -396,7 +662,7 @@ done7:
 // partials + b3, in column-block order.  Instances of the partial arrays: 0 Q1(s,a) 1 Q2(s,a)
 // 2 Q1(s,pi) 3 Q2(s,pi) 4 Qt1(s',pi') 5 Qt2(s',pi').
 struct LossRows {
-  const float* qpart[6];             // [ncq][n][OPW] (element 0)
+  const float* qpart[6];             // [ncq][n]
   const float* b3[6];
   const float* logp_s; const float* logp_n; const float* head_s; const float* rew; const float* term;
   const float* log_alpha;
@@ -405,220 +671,127 @@ struct LossRows {
 
 struct RowQ { float q[6]; float y, alpha; };
 
-static __device__ __forceinline__ RowQ row_losses(const LossRows& L, int n, int ncq, int r) {
-  RowQ o;
-  float pv[6][MAX_NCQ];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {           // unconditional loads, then the sums in column-block order
-    const auto dp = rsrc(L.qpart[i], (int64_t)ncq * n * OPW);
-#pragma unroll
-    for (int c = 0; c < MAX_NCQ; ++c) pv[i][c] = bload(dp, c < ncq ? (c * n + r) * OPW : -1);
-  }
+// The loads of row r's loss terms, all issued at once (out-of-range rows read 0), and the terms from them:
+// q = sum of the column-block partials + b3, in column-block order.
+struct RowIn { float pv[6][MAX_NCQ]; float b3[6]; float la, rew, term, logp_n; };
+
+static __device__ __forceinline__ RowIn row_losses_load(const LossRows& L, int n, int ncq, int r, bool on) {
+  RowIn o;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    float s = *L.b3[i];
+    const auto dp = rsrc(L.qpart[i], (int64_t)ncq * n);
 #pragma unroll
-    for (int c = 0; c < MAX_NCQ; ++c) s += pv[i][c];
+    for (int c = 0; c < MAX_NCQ; ++c) o.pv[i][c] = bload(dp, (on && c < ncq) ? c * n + r : -1);
+    o.b3[i] = *L.b3[i];
+  }
+  o.la = *L.log_alpha;
+  o.rew = bload(rsrc(L.rew, n), on ? r : -1);
+  o.term = bload(rsrc(L.term, n), on ? r : -1);
+  o.logp_n = bload(rsrc(L.logp_n, n), on ? r : -1);
+  return o;
+}
+
+static __device__ __forceinline__ RowQ row_losses(const LossRows& L, const RowIn& in) {
+  RowQ o;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float s = in.b3[i];
+#pragma unroll
+    for (int c = 0; c < MAX_NCQ; ++c) s += in.pv[i][c];
     o.q[i] = s;
   }
-  o.alpha = expf(*L.log_alpha);                                       // mopo.py:361
+  o.alpha = expf(in.la);                                              // mopo.py:361
   const float qt = fminf(o.q[4], o.q[5]);                             // mopo.py:368
-  o.y = L.rscale * L.rew[r] + L.gamma * ((1.f - L.term[r]) * (qt - o.alpha * L.logp_n[r]));  // :380-386
+  o.y = L.rscale * in.rew + L.gamma * ((1.f - in.term) * (qt - o.alpha * in.logp_n));  // :380-386
   return o;
 }
 
 struct Dh1Inst {
-  const float* upart;                // F1's dh1 / dq partials [ncq][n][H] (then only dq, dh1 are formed here)
   const float* h1; const float* h2; const float* w2; const float* w3;
-  int kind;                          // dq of the row: 0 (q1 - y) / n, 1 (q2 - y) / n, 2 min-select Q1, 3 Q2
-  float* dh1;                        // stored when non-NULL
-  float* dq;                         // stored by the column-block-0 workgroups when non-NULL
-  const float* w1a;                  // (s, pi) instances: W1[O:] = the action rows [A][H]; NULL otherwise
-  float* dapart;                     // [ncq1][n][OPW]: partial dh1 W1[O:]^T of the block's 128 columns
+  int kind;                          // dq of the row: 0 (q1 - y) / n, 1 (q2 - y) / n
+  float* dh1;
+  float* dq;                         // stored by the column-block-0 workgroups
 };
 
-constexpr int B1_WAVES = 8, B1_COLS = 16 * B1_WAVES;   // B1 workgroups: 16 rows x 128 columns
+#ifndef MOPO_SAC_B1_WAVES
+// 4: 16 rows x 64 columns per workgroup (twice the workgroups of the 8-wave form, half the W2 panel each):
+// 41.4 vs 43.5 us/step (same-box A/B, profiles/r04_sac_ab.txt)
+#define MOPO_SAC_B1_WAVES 4
+#endif
+constexpr int B1_WAVES = MOPO_SAC_B1_WAVES, B1_COLS = 16 * B1_WAVES;   // B1 workgroups: 16 rows x 16 B1_WAVES columns
 constexpr int B1_TLD = B1_COLS + 4;
 
 struct Dh1Args {
-  int ninst, n, H, A;
+  int n, H, A;
   int ncq;                           // column blocks of the forward partials (64 wide)
-  int ncq1;                          // B1's column blocks (128 wide): its action-gradient partials
+  int ncq1;                          // B1's column blocks (128 wide)
   int nrb;
-  Dh1Inst in[4];
+  Dh1Inst in[2];
   LossRows L;
-  // the loss tail (last block): batch means -> logs, the alpha gradient + Adam, lr_t, beta powers, step
-  AdamCtx ad;
-  float tent, lr;
-  float* logs; float* beta_pow; int64_t* iter;
+  // step control (block 0): lr_t, beta powers, the target-update flag of this step
+  float lr;
+  float* beta_pow; const int64_t* iter;
   const int64_t* tctl;               // target schedule {base, n_train_repeat, interval} (sac.hip mopo_sac_set_target_schedule)
-  // the policy's row-local backward chain (gemm_group.h policy_rows_block) as blocks z = ninst + 1 of
-  // this launch: block (cq, rb) waits until the 2 ncq1 (s, pi) workgroups of row block rb published
-  // their action-gradient partials (agent-scope counter rb_ready[rb], zeroed by the step's last launch)
-  PolicyRows pr;
-  int* rb_ready;
+  PolicyRows pr;                     // the policy's row-local backward chain (blocks z = 3)
+  int gather;                        // 1: the other z = 0 blocks gather the next step's batch (ga)
+  GatherArgs ga;
   Stamps st;
 };
 
-constexpr int PR_SPIN_LIMIT = 1 << 22;   // ~ 0.2 s of polling: a hang guard, never reached in a sane launch
-
-// the extra block: per-row loss terms of all n rows (thread t: rows t, t + 256, ...), block sums in a
-// fixed order (deterministic), then thread 0 applies the batch-level updates (loss_tail_block's tail)
-static __device__ __forceinline__ void loss_tail_rows(const Dh1Args& a, float* sh) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
-  const int n = a.n, A = a.A;
-  // the alpha Adam state and the beta powers, fetched up front (thread 0; used after the reduction)
-  AdamIn al{0.f, 0.f, 0.f, 0.f};
-  float b1p = 0.f, b2p = 0.f;
-  if (tid == 0) {
-    al = adam_load(a.ad, a.ad.total);                                 // log_alpha = the last parameter
-    b1p = a.beta_pow[0];
-    b2p = a.beta_pow[1];
-  }
-  float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int r = tid; r < n; r += blockDim.x) {
-    const RowQ o = row_losses(a.L, n, a.ncq, r);
-    const float q1 = o.q[0], q2 = o.q[1], q1p = o.q[2], q2p = o.q[3];
-    const float lps = a.L.logp_s[r];
-    float ent = 0.f;                                                  // pi_entropy terms (mopo.py:341)
-    for (int j = 0; j < A; ++j) {
-      const float ls = fminf(fmaxf(a.L.head_s[(int64_t)r * 2 * A + A + j], -20.f), 2.f);
-      ent += logf(expf(ls) + 1e-8f) + 0.5f * logf(2.f * 3.14159265358979f * 2.718281828459045f);
-    }
-    red[0] += (q1 - o.y) * (q1 - o.y); red[1] += (q2 - o.y) * (q2 - o.y); red[2] += q1; red[3] += q2;
-    red[4] += lps; red[5] += ent; red[6] += o.alpha * lps - fminf(q1p, q2p);
-  }
-#pragma unroll
-  for (int i = 0; i < 7; ++i)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) red[i] += __shfl_xor(red[i], off);
-  if (lane == 0)
-#pragma unroll
-    for (int i = 0; i < 7; ++i) sh[w * 8 + i] = red[i];
-  lds_barrier();
-  if (tid != 0) return;
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {                                       // wave partials in wave order
-    float t = 0.f;
-    for (int q = 0; q < nw; ++q) t += sh[8 * q + i];
-    red[i] = t;
-  }
-  const AdamCtx& ad = a.ad;
-  const float fn = (float)n;
-  const float l1 = red[0] / fn * 0.5f, l2 = red[1] / fn * 0.5f;       // mopo.py:403-404
-  const float m1 = red[2] / fn, m2 = red[3] / fn, mlp = red[4] / fn, ment = red[5] / fn;
-  const float pil = red[6] / fn;                                      // mopo.py:371-377
-  const float ga = -(mlp + a.tent);                                   // d/dlog_alpha of -mean(la*(logp+H))
-  const_cast<float*>(ad.G)[ad.total] = ga;
-  float* logs = a.logs;
-  logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;
-  logs[LOG_ALPHA] = expf(al.p); logs[LOG_ENTROPY] = ment; logs[LOG_LOGP] = mlp; logs[LOG_PI_LOSS] = pil;
-  const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);           // TF1 Adam step size
-  a.beta_pow[2] = lr_t;
+// Block 0: the step's scalar control -- TF1 Adam's step size from the beta powers (every Adam of the step
+// shares it: identical step counts), the beta powers of the next step, and whether this step's timestep
+// moves the targets (mopo.py:780-799, 843-845: n_train_repeat steps share one timestep).  The step counter
+// itself advances in the loss tail of the next launch (sac_wgrad.h), after every reader of this step's.
+static __device__ __forceinline__ void step_control(const Dh1Args& a) {
+  if (threadIdx.x != 0) return;
+  const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
+  const int64_t it = *a.iter, base = a.tctl[0];
+  const int64_t rep = a.tctl[1] > 0 ? a.tctl[1] : 1, every = a.tctl[2] > 0 ? a.tctl[2] : 1;
+  a.beta_pow[2] = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);             // TF1 Adam step size
   a.beta_pow[0] = b1p * 0.9f;
   a.beta_pow[1] = b2p * 0.999f;
-  {  // the step's timestep (mopo.py:780-799: n_train_repeat steps share one) and its target-update flag
-    const int64_t rep = a.tctl[1] > 0 ? a.tctl[1] : 1, every = a.tctl[2] > 0 ? a.tctl[2] : 1;
-    const int64_t ts = (*a.iter - a.tctl[0]) / rep;
-    a.beta_pow[3] = ((ts % every) + every) % every == 0 ? 1.f : 0.f;
-  }
-  *a.iter += 1;
-  adam_apply(ad, ad.total, ga, al, lr_t);
+  const int64_t ts = (it - base) / rep;
+  a.beta_pow[3] = ((ts % every) + every) % every == 0 ? 1.f : 0.f;
 }
 
-// Grid (column block, row block, 2 + ninst): z = 0, block (0, 0): the loss tail; z = 1 .. ninst: the
-// instances; z = ninst + 1: the policy-row blocks (they wait on the (s, pi) instances' partials).
-// B1 runs 8-wave workgroups (16 rows x 128 columns), one per CU: the 1 + 4 x 32 + 32 busy workgroups
-// of a batch-256 step then all start at once on their own CUs -- the policy-row blocks prefetch their
-// operands beside the producers instead of queueing for a CU or sharing one with them.
+// Grid (column block, row block, 4): z = 0: block (0, 0) the step control, the other blocks the gather of
+// the next step's batch; z = 1, 2: Q1 / Q2(s, a) dh1 tiles; z = 3: the policy-row blocks.
+// B1 runs 8-wave workgroups (16 rows x 128 columns), one per CU.
 static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const Dh1Args a) {
   __shared__ __attribute__((aligned(16))) float As[RB_LDS_A];
   __shared__ __attribute__((aligned(16))) float Ts[16 * B1_TLD];
-  __shared__ __attribute__((aligned(16))) float Wo[16 * B1_TLD];
   __shared__ float dqs[16];
   stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // grid (ncq1, nrb, ninst + 2): SGPR indices (see sac_fwd_kernel); z = 0 holds the loss tail (block
-  // (0, 0, 0), dispatched first: its ~6 us chain runs beside the tiles instead of after them), the
-  // instances are z = 1 .. ninst, the policy-row blocks z = ninst + 1
   if (blockIdx.z == 0) {
-    if (blockIdx.x == 0 && blockIdx.y == 0) {
-      loss_tail_rows(a, Ts);
-      stamp(a.st, 4);
+    const int zb = blockIdx.x + gridDim.x * blockIdx.y;
+    if (zb == 0) {
+      step_control(a);
+    } else if (a.gather) {
+      const GatherArgs& g = a.ga;
+      const int C = 2 * g.O + g.A + 2, tot = g.n * C, stride = (gridDim.x * gridDim.y - 1) * blockDim.x;
+      for (int e = (zb - 1) * blockDim.x + tid; e < tot; e += stride) gather_elem(g, e / C, e % C);
     }
-    return;
-  }
-  if ((int)blockIdx.z > a.ninst) {    // the policy-row blocks
-    const int rb = blockIdx.y, cq = blockIdx.x;
-    if (a.pr.qpart[0]) {                // the action-gradient partials come from F2 (the previous launch)
-      policy_rows_block<false, true>(a.pr, rb * a.ncq1 + cq, As, Ts, [] {}, a.st);
-      stamp(a.st, 4);
-      return;
-    }
-    const int need = 2 * a.ncq1;
-    bool late = false;
-    auto wait = [&] {
-      if (threadIdx.x == 0) {
-        int spins = 0;
-        while (__hip_atomic_load(a.rb_ready + rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > PR_SPIN_LIMIT) { late = true; break; }
-        }
-      }
-      __syncthreads();   // a full fence: the partials' agent-scope loads must not move above it
-    };
-    policy_rows_block<true>(a.pr, rb * a.ncq1 + cq, As, Ts, wait, a.st);
-    if (late) a.logs[LOG_HANDOFF] = 1.f;   // hand-off timed out: sac.py raises on the flag
     stamp(a.st, 4);
     return;
   }
-  const int ii = blockIdx.z - 1, rb = blockIdx.y, cq = blockIdx.x;
-  const Dh1Inst p = pick4(a.in, ii);
-  const int n = a.n, H = a.H, A = a.A;
+  if (blockIdx.z == 3) {              // the policy-row blocks: the action-gradient partials came from F2
+    policy_rows_block(a.pr, blockIdx.y * a.ncq1 + blockIdx.x, As, Ts, a.st);
+    stamp(a.st, 4);
+    return;
+  }
+  const int rb = blockIdx.y, cq = blockIdx.x;
+  const Dh1Inst p = blockIdx.z == 1 ? a.in[0] : a.in[1];
+  const int n = a.n, H = a.H;
   const int i0 = rb * 16, c0 = cq * B1_COLS, jw = c0 + w * 16;
   const int li = lane & 15, lk = lane >> 4;
-  if (p.upart) {
-    // dh1 = dq * sum of F1's column-block partials (already masked by h1 > 0), in column-block order:
-    // thread t owns row t / 32, columns c0 + 4 (t % 32) .. + 3 of the block (one b128 per partial)
-    const int rr = tid >> 5, kq = c0 + 4 * (tid & 31), orow = i0 + rr;
-    const auto du = rsrc(p.upart, (int64_t)a.ncq * n * H);
-    f32x4 up[MAX_NCQ];
-#pragma unroll
-    for (int c = 0; c < MAX_NCQ; ++c)
-      up[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            du, ((c < a.ncq && orow < n && kq < H) ? (c * n + orow) * H + kq : -4) * 4, 0, 0));
-    if (tid < 16) {
-      const int r2 = i0 + tid;
-      float dq = 0.f;
-      if (r2 < n) {
-        const RowQ o = row_losses(a.L, n, a.ncq, r2);
-        dq = (p.kind == 0 ? o.q[0] : o.q[1]) - o.y;
-        dq *= 1.f / (float)n;
-        if (cq == 0 && p.dq) p.dq[r2] = dq;
-      }
-      dqs[tid] = dq;
-    }
-    lds_barrier();
-    if (orow < n && kq < H) {
-      f32x4 v = up[0];
-#pragma unroll
-      for (int c = 1; c < MAX_NCQ; ++c) v += up[c];
-      *reinterpret_cast<f32x4*>(p.dh1 + (int64_t)orow * H + kq) = v * dqs[rr];
-    }
-    stamp(a.st, 4);
-    return;
-  }
-  // ---- 1. operands up front: this wave's W2^T operand straight into MFMA registers (B(m, c) = W2[c][m]:
-  //         lane (li, lk) holds W2[jw + li][64 lk + 4 s .. + 3]), the A slab's h2 rows and W3 (waves
-  //         0-3), the h1 mask of this lane's outputs, W1[O:] columns of the block (the (s, pi) instances)
-  const auto dw2 = rsrc(p.w2, (int64_t)H * H);
-  f32x4 bp[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int m = 64 * lk + 4 * i, c = jw + li;
-    bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                          dw2, ((m < H && c < H) ? c * H + m : -4) * 4, 0, 0));
-  }
+  // ---- 0. the dq of the block's 16 rows first (the partials of F1 / F2; one lane per row): the A slab
+  //         below waits on it
+  RowIn rin{};
+  if (tid < 16) rin = row_losses_load(a.L, n, a.ncq, i0 + tid, i0 + tid < n);
+  // ---- 1. operands in the order the chain consumes them: the A slab's h2 rows and W3, the h1 mask of this
+  //         lane's outputs, then this wave's W2^T operand straight into MFMA registers (B(m, c) = W2[c][m]:
+  //         lane (li, lk) holds W2[jw + li][64 lk + 4 s .. + 3])
   // A slab: thread (m-quad tid % 64, rows 4 (tid / 64) .. + 3), waves 0-3
   const bool slab = w < 4;
   const int am = 4 * (tid & 63), ar = 4 * (w & 3);
@@ -636,26 +809,21 @@ static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const 
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) m1[rr] = bload(dm1, (jw + li < H && i0 + 4 * lk + rr < n) ? (i0 + 4 * lk + rr) * H + jw + li : -1);
   }
-  float wov[4] = {0.f, 0.f, 0.f, 0.f};
-  if (p.w1a) {
-    const auto d1 = rsrc(p.w1a, (int64_t)A * H);
+  const auto dw2 = rsrc(p.w2, (int64_t)H * H);
+  f32x4 bp[16];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {     // Wo[c][j] = W1[O + j][c0 + c]: element e = c * 16 + j
-      const int e = tid + B1_WAVES * 64 * q, c = c0 + (e >> 4), j = e & 15;
-      wov[q] = bload(d1, (c < H && j < A) ? j * H + c : -1);
-    }
+  for (int i = 0; i < 16; ++i) {
+    const int m = 64 * lk + 4 * i, c = jw + li;
+    bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          dw2, ((m < H && c < H) ? c * H + m : -4) * 4, 0, 0));
   }
   // ---- 2. dq of the block's 16 rows (one lane per row)
   if (tid < 16) {
-    const int rr = i0 + tid;
     float dq = 0.f;
-    if (rr < n) {
-      const RowQ o = row_losses(a.L, n, a.ncq, rr);
-      const float inv_n = 1.f / (float)n;
-      const bool sel1 = o.q[2] <= o.q[3];                             // tf.minimum grad -> x where x <= y
-      dq = p.kind == 0 ? (o.q[0] - o.y) * inv_n : p.kind == 1 ? (o.q[1] - o.y) * inv_n
-         : p.kind == 2 ? (sel1 ? -inv_n : 0.f) : (sel1 ? 0.f : -inv_n);
-      if (cq == 0 && p.dq) p.dq[rr] = dq;
+    if (i0 + tid < n) {
+      const RowQ rq = row_losses(a.L, rin);
+      dq = ((p.kind == 0 ? rq.q[0] : rq.q[1]) - rq.y) * (1.f / (float)n);
+      if (cq == 0) p.dq[i0 + tid] = dq;
     }
     dqs[tid] = dq;
   }
@@ -672,35 +840,19 @@ static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const 
       *reinterpret_cast<f32x4*>(As + (ar + q) * RB_LD + am) = v;
     }
   }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {     // Wo[j][c]
-    const int e = tid + B1_WAVES * 64 * q;
-    Wo[(e & 15) * B1_TLD + (e >> 4)] = wov[q];
-  }
   lds_barrier();
   stamp(a.st, 2);
   // ---- 4. dh1 tile of the wave: 16 rows x 16 columns over the whole K
   f32x4 acc[4];
   rows_contract(As, bp, li, lk, acc);
   stamp(a.st, 3);
-  // ---- 5. relu mask from h1; store; the (s, pi) instances' action-gradient partials
+  // ---- 5. relu mask from h1; store
   const int col = jw + li;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int orow = i0 + 4 * lk + rr;
     const float v = (col < H && orow < n && m1[rr] > 0.f) ? acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr] : 0.f;
-    if (p.dh1 && orow < n && col < H) p.dh1[(int64_t)orow * H + col] = v;
-    Ts[(4 * lk + rr) * B1_TLD + w * 16 + li] = v;
-  }
-  if (p.w1a) {
-    lds_barrier();
-    if (w == 0) {
-      // the policy-row blocks of this launch read these partials: agent-scope (sc1) stores, the wave's
-      // vmcnt(0), then one lane's agent-scope counter add (MI355X_MICROARCH.md hand-off, row 1)
-      rows_partial_out<B1_COLS, true>(Ts, Wo, li, lk, i0, n, A, p.dapart + (int64_t)cq * n * OPW);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(a.rb_ready + rb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (orow < n && col < H) p.dh1[(int64_t)orow * H + col] = v;
   }
   stamp(a.st, 4);
 }

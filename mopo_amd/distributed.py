@@ -10,6 +10,7 @@ ranks (SAC samples from them locally).  ``pack_rows`` / ``assemble_global`` /
 ``allgather_transitions`` are the host-orchestrated form of the same order (CPU gloo tests).
 No reference counterpart (the reference is single-process); see SURVEY §8(e).
 """
+import numpy as np
 import torch
 
 
@@ -124,6 +125,27 @@ class DistributedRollout:
 # (SURVEY 8(e)), and the replicated learners stay identical even if some float reduction on the device
 # were not bit-reproducible.
 
+WAIT_TIMEOUT_S = 30 * 24 * 3600   # rank 0's model training has no time bound (max_model_t=None)
+
+
+def wait_group():
+    """A CPU (gloo) process group with a month-long timeout, for the ranks that wait while rank 0 alone
+    trains the ensemble: a collective of the default group (RCCL, 10-minute watchdog by default) would
+    abort the job when training outlasts that timeout.  Collective: every rank calls it, in the same
+    order (``MOPO.__init__``)."""
+    import datetime
+    import torch.distributed as dist
+    return dist.new_group(backend='gloo', timeout=datetime.timedelta(seconds=WAIT_TIMEOUT_S))
+
+
+def wait_for_src(group):
+    """Every rank blocks here until all ranks arrive -- the training rank after its training, the others
+    at once -- on ``group`` (``wait_group``), so the default group's next collective starts only when
+    every rank is ready for it."""
+    import torch.distributed as dist
+    dist.barrier(group=group)
+
+
 def world_info(group=None):
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
@@ -133,9 +155,10 @@ def world_info(group=None):
 
 def broadcast_model(model, src=0, group=None):
     """The ensemble from ``src`` to every rank as its packed device image (weights in the kernels'
-    fragment layout, biases, scaler, log-var bounds, f16x3 scales: mopo_bnn_packed_copy) plus the
-    elite indices -- one device-to-device broadcast, no host copy and no repack.  Receiving ranks keep
-    no host .mat arrays afterwards (``BNN.get_params`` is rank ``src``'s)."""
+    fragment layout, biases, scaler, log-var bounds, f16x3 scales: mopo_bnn_packed_copy) -- one
+    device-to-device broadcast, no repack -- plus the elite indices, the holdout losses and the .mat
+    arrays (so every rank's host state -- ``get_params``, ``scaler``, ``save``, ``train`` -- describes
+    the same model)."""
     import torch.distributed as dist
     rank = dist.get_rank(group)
     dev = torch.device('cuda', torch.cuda.current_device())
@@ -146,10 +169,19 @@ def broadcast_model(model, src=0, group=None):
     dist.broadcast(ne, src, group=group)
     if rank != src:
         el = torch.empty(int(ne.item()), dtype=torch.int64, device=dev)
+    n_flat = sum(z.size for z in model._mat_shapes())
+    if rank == src:
+        hl = getattr(model, '_holdout_losses', None)
+        hl = np.full(model.num_nets, np.nan) if hl is None else np.asarray(hl, np.float64)
+        host = torch.from_numpy(np.concatenate([model.flat_params().astype(np.float64), hl])).to(dev)
+    else:
+        host = torch.empty(n_flat + model.num_nets, dtype=torch.float64, device=dev)
     dist.broadcast(buf, src, group=group)
     dist.broadcast(el, src, group=group)
+    dist.broadcast(host, src, group=group)
     if rank != src:
-        model.import_packed(buf)
+        h = host.cpu().numpy()
+        model.import_packed(buf, mats=model.unflatten_params(h[:n_flat]), holdout_losses=h[n_flat:])
         model.set_elites(el.cpu().tolist())
     torch.cuda.current_stream().synchronize()
 

@@ -72,8 +72,10 @@ class MOPO:
         self._rollout_length = rollout_length
         # multi-GPU (torch.distributed initialised, one process per GPU): the rollout rows are sharded
         # over the ranks and all-gathered into every rank's model pool; SAC runs replicated
-        from .distributed import world_info
+        from .distributed import wait_group, world_info
         self._rank, self._world = world_info()
+        # the ranks that wait while rank 0 trains the ensemble wait on this long-timeout CPU group
+        self._wait_group = wait_group() if self._world > 1 else None
         if self._rollout_batch_size % self._world:
             raise ValueError('rollout_batch_size must be a multiple of the world size')
         self._max_model_t = max_model_t
@@ -164,7 +166,8 @@ class MOPO:
     # -- mopo.py:780-799 + 834-853: n steps of (_training_batch, _do_training, _update_target); the first
     #    is timestep `first_timestep` of the epoch, each timestep n_train_repeat steps
     def _do_training_repeats(self, n_steps, first_timestep=0):
-        self._sac._do_training(first_timestep, self._pool, self._model_pool, n_steps=n_steps,
+        # real_ratio = 1.0: no model pool (mopo.py:554 skips the rollouts); every row comes from the env pool
+        self._sac._do_training(first_timestep, self._pool, getattr(self, '_model_pool', None), n_steps=n_steps,
                                seed=self._seed + 7919 * self._epoch, n_train_repeat=self._n_train_repeat)
         self._num_train_steps += n_steps
         return self._sac.logs()
@@ -181,10 +184,12 @@ class MOPO:
         t_roll = t_train = 0.0
         for k, ts in enumerate(range(0, self._epoch_length, f)):
             t0 = time.perf_counter()
-            self._set_rollout_length()
-            self._reallocate_model_pool()
-            metrics.update(self._rollout_model(self._rollout_batch_size, rollout_key=self._epoch * per_epoch + k))
-            torch.cuda.synchronize()
+            if self._real_ratio < 1.0:                                                  # mopo.py:554
+                self._set_rollout_length()
+                self._reallocate_model_pool()
+                metrics.update(self._rollout_model(self._rollout_batch_size,
+                                                   rollout_key=self._epoch * per_epoch + k))
+                torch.cuda.synchronize()
             t1 = time.perf_counter()
             logs = self._do_training_repeats(min(f, self._epoch_length - ts) * self._n_train_repeat, first_timestep=ts)
             t_roll, t_train = t_roll + t1 - t0, t_train + time.perf_counter() - t1
@@ -223,7 +228,8 @@ class MOPO:
                 self._model_train_metrics = self._train_model(batch_size=256, max_epochs=max_epochs,
                                                               holdout_ratio=0.2, max_t=self._max_model_t)
             if self._world > 1:
-                from .distributed import broadcast_model, broadcast_numpy_rng, broadcast_metrics
+                from .distributed import broadcast_model, broadcast_numpy_rng, broadcast_metrics, wait_for_src
+                wait_for_src(self._wait_group)   # no RCCL collective is pending while rank 0 trains
                 broadcast_model(self._model)
                 broadcast_numpy_rng()       # the training loop drew from numpy's global stream on rank 0 only
                 self._model_train_metrics = broadcast_metrics(self._model_train_metrics)

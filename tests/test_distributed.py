@@ -117,3 +117,38 @@ def test_numpy_stream_and_metrics_follow_rank0_world2():
         np.testing.assert_array_equal(res[r][0], ref[0])
         np.testing.assert_array_equal(res[r][1], ref[1])
         assert res[r][2] == {'val_loss': 0.25, 'epochs': 7.0}
+
+
+def _slow_src_worker(rank, world, port, q):
+    """Rank 0 'trains' for longer than the default group's timeout; the others wait on wait_group."""
+    import datetime
+    import time
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world, timeout=datetime.timedelta(seconds=3))
+    from mopo_amd.distributed import wait_for_src, wait_group
+    g = wait_group()
+    if rank == 0:
+        time.sleep(6)                     # longer than the default group's 3 s timeout
+    wait_for_src(g)
+    t = torch.tensor([7.0 if rank == 0 else 0.0])
+    dist.broadcast(t, 0)                  # the default group's collective, after the wait
+    q.put((rank, float(t[0])))
+    dist.destroy_process_group()
+
+
+def test_slow_training_rank_does_not_time_out_waiters():
+    """while rank 0 alone trains the ensemble (no time bound), the other ranks must not sit in a
+    default-group collective (RCCL's watchdog would abort the job): MOPO.train waits on a long-timeout
+    gloo group first (mopo_amd/distributed.py wait_group / wait_for_src)."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slow_src_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: 7.0, 1: 7.0}

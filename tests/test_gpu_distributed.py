@@ -95,6 +95,9 @@ def _state(algo):
     mp_ = algo._model_pool
     return dict(sac=p.cpu().numpy(), log_alpha=np.float32(la.item()), target=algo._sac.get_target().cpu().numpy(),
                 bnn=algo._model.export_packed().cpu().numpy(), elites=np.array(algo._model._model_inds),
+                # every rank's host model state (import_packed used to leave it stale / None)
+                bnn_mats=algo._model.flat_params(), bnn_holdout=np.asarray(algo._model._holdout_losses),
+                bnn_scaler_mu=np.asarray(algo._model.scaler.cached_mu),
                 **{'pool_' + k: v[:mp_.size].cpu().numpy() for k, v in mp_.fields.items()})
 
 

@@ -143,3 +143,24 @@ def test_mopo_rollouts_every_model_train_freq_steps():
     assert all(np.isfinite(v) for v in d[-1].values())
     rows = algo._model_pool.fields['observations'][:algo._model_pool.size].reshape(6, 500, 17)
     assert not torch.equal(rows[0], rows[1])          # distinct start-row draws per rollout
+
+
+def test_mopo_real_ratio_one_skips_rollouts():
+    """real_ratio = 1.0 (mopo.py:554): no model rollout and no model pool; SAC trains on env rows only."""
+    from mopo_amd.mopo import MOPO
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.static import static_fns
+    rs = np.random.RandomState(3)
+    n = 2000
+    obs = rs.normal(size=(n, 17)).astype(np.float32)
+    pool = SimpleReplayPool(obs_dim=17, act_dim=6, max_size=n)
+    pool.add_samples({'observations': obs, 'actions': rs.uniform(-1, 1, (n, 6)), 'rewards': rs.normal(size=(n, 1)),
+                      'terminals': np.zeros((n, 1), bool), 'next_observations': obs + 0.1})
+    algo = MOPO(pool, static_fns['halfcheetah'], 17, 6, rollout_batch_size=500, rollout_length=1, epoch_length=50,
+                model_train_freq=25, separate_mean_var=True, real_ratio=1.0, target_entropy=-3, max_model_t=3)
+    calls = []
+    orig = algo._rollout_model
+    algo._rollout_model = lambda *a, **k: calls.append(k) or orig(*a, **k)
+    d = list(algo.train(1))
+    assert calls == [] and not hasattr(algo, '_model_pool')
+    assert algo._num_train_steps == 50 and all(np.isfinite(v) for v in d[-1].values())
