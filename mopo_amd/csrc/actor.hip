@@ -293,7 +293,10 @@ __device__ __forceinline__ void actor_finish(const ActorArgs& a, float (&head)[A
 // TQ0: k-steps in the last k-group of the observation (tail_steps(O); 4 = all)
 template <int KG0, int NBP, int TQ0 = 4>
 #ifndef ACT_F32_OCC
-#define ACT_F32_OCC 4  // fp32 actor workgroups per CU at H = 256 (4: 128 VGPRs)
+// fp32 actor workgroups per CU at H = 256.  4 caps the kernel at 128 VGPRs and spilled 22-26 of them (88 B
+// of scratch per lane); 3 needs no scratch, runs 0.101 vs 0.092 ms per 50k rows alone and the fp32 rollout
+// the same or faster (59.2 vs 58.9M transitions/s, same-box A/B, profiles/r04_actor_ab.txt)
+#define ACT_F32_OCC 3
 #endif
 __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? ACT_F32_OCC : 2) void actor_kernel(const ActorArgs a) {
   constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
@@ -472,8 +475,9 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16_kernel(const Acto
 // head ([mu | log_std], 2 KG fragments) prefetched during layer 2's last slice, so no layer starts on
 // an exposed copy and the head runs behind ONE barrier instead of 2 KG.
 #ifndef ACT_F16_R
-#define ACT_F16_R 0  // 0: actor_f16_kernel; R >= 1: actor_f16r_kernel<R>
+#define ACT_F16_R 0  // 0: actor_f16_kernel; R >= 1: actor_f16r_kernel<R> (A/B builds only: not compiled at 0)
 #endif
+#if ACT_F16_R > 0
 template <int NBP, int R>
 __global__ __launch_bounds__(ACT_WAVES * 64, R == 1 ? 2 : 1) void actor_f16r_kernel(const ActorArgs a) {
   constexpr int KG = NBP / 2;
@@ -555,6 +559,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64, R == 1 ? 2 : 1) void actor_f16r_ker
     actor_finish(a, head, wv, m, g, row, row < count);
   }
 }
+#endif
 
 // f16x3 policy forward over a 3-slot LDS ring (ACT_F16_RING; bnn.hip bnn_fwd_f16q_kernel's pipeline):
 // actor_f16_kernel's arithmetic, product for product, with the weight slices as ONE stream -- layer 1
@@ -563,8 +568,10 @@ __global__ __launch_bounds__(ACT_WAVES * 64, R == 1 ? 2 : 1) void actor_f16r_ker
 // hidden biases ride into LDS once, ahead of the first slices; the head's output rows reuse a ring slot.
 #ifndef ACT_F16_RING
 #define ACT_F16_RING 0  // same-box A/B: actor 0.062 -> 0.054 ms alone, but the rollout 1.6 % slower (203 VGPRs
-                        // beside the concurrent ensemble launch of the other row part), so it stays off
+                        // beside the concurrent ensemble launch of the other row part), so it stays off (and
+                        // is compiled only in ACT_F16_RING = 1 A/B builds)
 #endif
+#if ACT_F16_RING
 template <int NBP>
 __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16q_kernel(const ActorArgs a) {
   static_assert(NBP == 16, "ring actor: hidden 256");
@@ -714,6 +721,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16q_kernel(const Act
   __syncthreads();
   actor_finish(a, head, wv, m, g, row, ok);
 }
+#endif
 
 int launch_actor(const ActorArgs& a, hipStream_t s) {
   if (a.B == 0) return 0;
@@ -723,8 +731,9 @@ int launch_actor(const ActorArgs& a, hipStream_t s) {
   MOPO_REQUIRE(a.O >= 1 && a.O <= 32, "actor: obs_dim must be in [1, 32]");
   MOPO_REQUIRE(a.Wpk, "actor: packed weights required");
   dim3 grid(ceil_div((int)a.B, 16 * ACT_WAVES)), block(64 * ACT_WAVES);
-  if (a.dtype == DT_F16X3 && ACT_F16_R > 0) {
-    constexpr int R = ACT_F16_R > 0 ? ACT_F16_R : 1;
+#if ACT_F16_R > 0
+  if (a.dtype == DT_F16X3) {
+    constexpr int R = ACT_F16_R;
     const dim3 gr(ceil_div((int)a.B, 16 * ACT_WAVES * R));
     if (a.Hp == 256) hipLaunchKernelGGL((actor_f16r_kernel<16, R>), gr, block, 0, s, a);
     else if (a.Hp == 32) hipLaunchKernelGGL((actor_f16r_kernel<2, R>), gr, block, 0, s, a);
@@ -732,9 +741,13 @@ int launch_actor(const ActorArgs& a, hipStream_t s) {
     MOPO_HIP(hipGetLastError());
     return 0;
   }
+#endif
   if (a.dtype == DT_F16X3) {
-    if (a.Hp == 256 && ACT_F16_RING) hipLaunchKernelGGL(actor_f16q_kernel<16>, grid, block, 0, s, a);
-    else if (a.Hp == 256) hipLaunchKernelGGL(actor_f16_kernel<16>, grid, block, 0, s, a);
+#if ACT_F16_RING
+    if (a.Hp == 256) hipLaunchKernelGGL(actor_f16q_kernel<16>, grid, block, 0, s, a);
+    else
+#endif
+    if (a.Hp == 256) hipLaunchKernelGGL(actor_f16_kernel<16>, grid, block, 0, s, a);
     else if (a.Hp == 32) hipLaunchKernelGGL(actor_f16_kernel<2>, grid, block, 0, s, a);
     else return fail("actor f16x3: unsupported hidden size (256 or 32)");
     MOPO_HIP(hipGetLastError());

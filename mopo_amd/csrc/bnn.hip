@@ -1039,11 +1039,15 @@ static int launch_bf16_p(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   a.ntiles = (int)ceil_div((int)a.B, 16);
   if (a.ntiles == 0) return 0;
   dim3 grid(ceil_div(a.ntiles, WV) * h->E), block(64 * WV);
-  if (h->dev.NBH == NB2 - 1) {  // odd hidden-block count: the last block is padding (e.g. H = 200)
-    if (mode == FWD_PREDICT)
-      hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_PREDICT, WV, P, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
-    else
-      hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+  // odd hidden-block count (e.g. H = 200): the last block is padding and is skipped (NBU = NB2 - 1); not at
+  // H = 400 (25 of 26), where the skipping variant takes 256 VGPRs and spills
+  if (NB2 <= 16 && h->dev.NBH == NB2 - 1) {
+    if constexpr (NB2 <= 16) {
+      if (mode == FWD_PREDICT)
+        hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_PREDICT, WV, P, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+      else
+        hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+    }
   } else if (mode == FWD_PREDICT) {
     hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_PREDICT, WV, P, PS>), grid, block, 0, s, h->dev, a);
   } else {
@@ -1086,14 +1090,23 @@ static int launch_f16s(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
 #endif
   // NBU: hidden blocks in use (NB2 - 1 when the block count is odd, e.g. H = 200 -> 13 of 14).  Not at
   // H = 400 (25 of 26): the register allocation it gets there (VGPR + AGPR split) measured 17 % slower.
-  if constexpr (BNN_F16_RING && NB2 <= 16)
+  // H <= 256 runs the ring kernel (every supported hidden size there has a ring shape); the f16s kernel
+  // is compiled for H = 400 only (and for H <= 256 in BNN_F16_RING = 0 A/B builds)
+  if constexpr (BNN_F16_RING && NB2 <= 16) {
     if (ring_shape<NB2>(h)) return launch_ring<NB2, NBO, 2, BNN_RING_DEPTH_F16>(h, mode, a, s);
-  if (NB2 <= 16 && h->dev.NBH == NB2 - 1) {
-    if (mode == FWD_PREDICT)
-      hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_PREDICT, WV, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
-    else
-      hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_ROLLOUT, WV, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
-  } else if (mode == FWD_PREDICT) {
+    return fail("bnn f16x3: unsupported hidden size");
+  }
+  if constexpr (NB2 <= 16) {
+    if (h->dev.NBH == NB2 - 1) {
+      if (mode == FWD_PREDICT)
+        hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_PREDICT, WV, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+      else
+        hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_ROLLOUT, WV, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+      MOPO_HIP(hipGetLastError());
+      return 0;
+    }
+  }
+  if (mode == FWD_PREDICT) {
     hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_PREDICT, WV, PS>), grid, block, 0, s, h->dev, a);
   } else {
     hipLaunchKernelGGL((bnn_fwd_f16s_kernel<NB2, NBO, FWD_ROLLOUT, WV, PS>), grid, block, 0, s, h->dev, a);
@@ -1107,7 +1120,11 @@ static int launch_bf16_t(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s
   if (h->dtype == DT_F16X3) return launch_f16s<NB2, NBO>(h, mode, a, s);
   switch (bf16_parts(h->dtype)) {
     case 2: return launch_bf16_p<NB2, NBO, 2>(h, mode, a, s);
-    case 3: return launch_bf16_p<NB2, NBO, 3>(h, mode, a, s);
+    case 3:
+      // bf16x6 at H > 256: its 39-slice layer loop does not unroll (the part index goes dynamic: 432 B of
+      // scratch per lane, a ~70x cliff) -- f16x3 is the f32-accurate 16-bit mode there
+      if constexpr (NB2 > 16) return fail("bnn bf16x6: hidden sizes <= 256 only (use f16x3 or fp32 at H = 400)");
+      else return launch_bf16_p<NB2, NBO, 3>(h, mode, a, s);
   }
   return launch_bf16_p<NB2, NBO, 1>(h, mode, a, s);
 }
@@ -1163,6 +1180,10 @@ extern "C" int mopo_bnn_create(mopo_bnn_t* out, int E, int obs_dim, int act_dim,
   d.NBO = ceil_div(2 * d.D, 16);
   d.NB2 = (d.NBH + 1) / 2 * 2;
   d.BS = d.NB2 * 16;
+  if (dtype == 3 && d.NB2 > 16) {   // launch_bf16_t: no bf16x6 kernel above H = 256
+    delete h;
+    return fail("mopo_bnn_create: bf16x6 supports hidden sizes <= 256 (use f16x3 or fp32)");
+  }
   *out = reinterpret_cast<mopo_bnn_t>(h);
   return 0;
 }

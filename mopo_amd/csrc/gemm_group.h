@@ -294,6 +294,10 @@ static __device__ __forceinline__ void stage_dispatch(const GemmProb& p, int i0,
 // one memory latency per chunk), then the four waves split K and run v_mfma_f32_16x16x4_f32 out
 // of LDS; partial tiles are summed through LDS and the epilogue fuses bias / activation / the
 // activation-derivative mask, and (for weight gradients) the optimizer.
+#ifndef MOPO_GEMM_KERNELS
+#define MOPO_GEMM_KERNELS 1   // 0: a translation unit that uses only the shared helpers (sac.hip)
+#endif
+#if MOPO_GEMM_KERNELS
 static __global__ __launch_bounds__(256, 4) void gemm_group_kernel(const GemmGroup g) {
   __shared__ __attribute__((aligned(16))) float ABs[2 * GKC * 16];  // the A and B panels
   float (*As)[16] = reinterpret_cast<float (*)[16]>(ABs);
@@ -600,6 +604,7 @@ static __device__ __forceinline__ void gemm32_body(const GG& g, int bid) {
 }
 
 static __global__ __launch_bounds__(256, 2) void gemm32_group_kernel(const GemmGroup g) { gemm32_body(g, (int)blockIdx.x); }
+#endif
 
 // ---------------------------------------------------------------------------------------------
 static inline GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb, float* C,
@@ -609,6 +614,7 @@ static inline GemmProb mk(int M, int N, int K, const float* A, int lda, int ta, 
   return p;
 }
 
+#if MOPO_GEMM_KERNELS
 // Tile policy: 16x16 (gemm_group_kernel).  MOPO_GEMM_TILE=32 selects gemm32_group_kernel for launches
 // whose problems are all >= 32 x 32.  Measured on MI355X: 32x32 tiles are slower
 // for both users (SAC step 115.7 vs 99.8 us, BNN.train 6.09k vs 6.51k steps/s): these launches are
@@ -658,5 +664,7 @@ static inline int launch_group(std::vector<GemmProb> ps, hipStream_t s, const Ad
   MOPO_HIP(hipGetLastError());
   return 0;
 }
+
+#endif
 
 }  // namespace mopo

@@ -19,6 +19,7 @@
 #include <vector>
 #include <cstring>
 
+#define MOPO_GEMM_KERNELS 0   // the grouped-GEMM kernels are bnn_train.hip's; this file uses the helpers only
 #include "sac_wgrad.h"
 
 namespace mopo {

@@ -38,7 +38,8 @@ class MOPO:
         """``ensemble_dtype``: the ensemble forward's arithmetic (``mopo_amd.bnn.DTYPES``), default
         ``DEFAULT_ENSEMBLE_DTYPE`` ('f16x3': f32 operands as two fp16 parts, f32 accumulate, held to
         the fp32 parity tolerances); 'fp32' runs exact-f32 MFMA.  ``actor_dtype``: the rollout
-        policy forward ('fp32' / 'f16x3'; default f16x3 with an f16x3 ensemble, else fp32)."""
+        policy forward ('fp32' / 'f16x3'; default fp32 with the fp32 ensemble, else f16x3:
+        ``rollout.default_actor_dtype``)."""
         self._pool = pool                                   # device SimpleReplayPool of env data
         self._static_fns = static_fns
         self._obs_dim, self._act_dim = obs_dim, act_dim

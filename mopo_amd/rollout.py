@@ -50,6 +50,13 @@ def split_params(flat, O, A, H=256):
 _ACTOR_DTYPES = {'fp32': 0, 'f16x3': 4}
 
 
+def default_actor_dtype(ensemble_dtype):
+    """The rollout policy's arithmetic for an ensemble dtype: exact f32 beside the exact-f32 ensemble,
+    else the f16x3 actor (f32-class operands on the f16 MFMA, held to the fp32 actor tolerances) -- a
+    16-bit ensemble (f16x3, bf16x6, bf16x3, bf16) gets a 16-bit-MFMA actor, not the 9x slower f32 one."""
+    return 'fp32' if ensemble_dtype == 'fp32' else 'f16x3'
+
+
 class ModelRollout:
     """Owns the rollout workspace for up to ``max_batch`` rows x ``max_horizon`` steps."""
 
@@ -99,7 +106,7 @@ class ModelRollout:
             d_model_inds=dptr(model_inds, torch.int32), d_steps=L.ptr(steps),
             penalty_learned_var=int(bool(penalty_learned_var)), deterministic=int(bool(deterministic)),
             rollout_random=int(bool(rollout_random)), d_act_uniform=dptr(act_uniform, torch.float32),
-            actor_dtype=_ACTOR_DTYPES[actor_dtype or ('f16x3' if self.model.dtype == 'f16x3' else 'fp32')])
+            actor_dtype=_ACTOR_DTYPES[actor_dtype or default_actor_dtype(self.model.dtype)])
         if step_hook is not None:
             # one call per horizon step into the staging block step_hook(i) names; step_hook(i, steps)
             # is then called after step i is enqueued (multi-GPU: gather step i while i + 1 computes)

@@ -42,6 +42,11 @@ def test_bnn_predict_vs_reference_graph(path, dtype):
     z = dict(np.load(path))
     E, H, smv = int(z['E']), int(z['H']), bool(z['smv'])
     p = ref_bnn_params(z)
+    if dtype == 'bf16x6' and H > 256:   # refused at construction (mopo_bnn_create): f16x3 covers H = 400
+        with pytest.raises(RuntimeError, match='bf16x6'):
+            BNN({'name': 'ref', 'num_networks': E, 'num_elites': min(5, E), 'separate_mean_var': smv, 'obs_dim': 17,
+                 'act_dim': 6, 'hidden_dim': H, 'dtype': dtype})
+        return
     m = BNN({'name': 'ref', 'num_networks': E, 'num_elites': min(5, E), 'separate_mean_var': smv, 'obs_dim': 17,
              'act_dim': 6, 'hidden_dim': H, 'dtype': dtype}).set_params(obnn.to_mat_list(p))
     mean, var = m.predict(z['x'], factored=True)

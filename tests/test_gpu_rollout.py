@@ -365,6 +365,10 @@ def test_bnn_predict_split_vs_oracle(E, H, B, dtype, tol):
     mats = obnn.to_mat_list(obnn.init_params(E, 17, 6, hidden=H, seed=3, inputs=rs.normal(size=(300, 23)) * 3))
     p = obnn.from_mat_list(mats)
     x = (rs.normal(size=(B, 23)) * 2).astype(np.float32)
+    if dtype == 'bf16x6' and H > 256:   # no bf16x6 kernel above H = 256 (its layer loop would not unroll)
+        with pytest.raises(RuntimeError, match='bf16x6'):
+            make_model(mats, E, H, dtype=dtype)
+        return
     mean, var = make_model(mats, E, H, dtype=dtype).predict(x)
     rm, rv = obnn.forward(p, x, dtype=np.float64)
     close(mean, rm, tol)
