@@ -68,10 +68,11 @@ def parse():
     p.add_argument('--batch', type=int, default=50000)
     p.add_argument('--horizon', type=int, default=5)
     p.add_argument('--no-cpu-baseline', action='store_true')
-    p.add_argument('--cpu-batch', type=int, default=50000,
-                   help='rows of the CPU baseline rollout (default: the headline batch, same workload)')
+    p.add_argument('--cpu-batch', type=int, default=10000,
+                   help='rows of the C2 CPU-baseline rollout sample (the headline workload at fewer rows; each of '
+                        'the 6 runs takes a few seconds)')
     p.add_argument('--sac-steps', type=int, default=1000)
-    p.add_argument('--cpu-sac-steps', type=int, default=500)
+    p.add_argument('--cpu-sac-steps', type=int, default=1000)
     p.add_argument('--no-c3', action='store_true', help='skip the secondary C3 (bf16 walker2d) line')
     p.add_argument('--train-epochs', type=int, default=2, help='timed BNN.train epochs (0: skip)')
     p.add_argument('--cpu-train-steps', type=int, default=10)
@@ -186,51 +187,85 @@ def blas_threads():
         return 1
 
 
-def cpu_baseline(args):
-    """Oracle (numpy port of the reference rollout) on a bounded sample, BLAS threads as configured."""
+CPU_RUNS = 5   # the median of >= 5 runs after 1 warm-up, fixed seeds
+
+
+def median_runs(fn, runs=CPU_RUNS):
+    """One warm-up call, then ``runs`` timed calls of ``fn() -> (units, seconds)``; returns the median rate,
+    the per-run rates and the total sample."""
+    fn()
+    rates, units, secs = [], 0, 0.0
+    for _ in range(runs):
+        u, dt = fn()
+        rates.append(u / dt)
+        units += u
+        secs += dt
+    return float(np.median(rates)), [float(r) for r in rates], units, secs
+
+
+def cpu_rollout_leg(B, horizon, domain='halfcheetah', penalty=1.0, env_rows=20000, seed=0):
+    """The oracle's ``_rollout_model`` (numpy port of mopo.py:723-765 with the fp32 ensemble, FakeEnv and
+    the static termination fns): start-state gather through the final pool append, fixed seed per run."""
     from oracle import bnn as obnn
     from oracle import fake_env as ofe
     from oracle import replay_pool as opool
     from oracle import rollout as orollout
     from oracle import sac as osac
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get('num_threads', 1) for i in threadpool_info() if i.get('user_api') == 'blas'] or [1])
-    except Exception:
-        threads = 1
-    rs = np.random.RandomState(0)
-    n_env = 20000
-    env_obs = rs.normal(size=(n_env, O)).astype(np.float32)
-    p = obnn.init_params(E, O, A, hidden=H, seed=1, inputs=np.concatenate([env_obs, rs.uniform(-1, 1, (n_env, A))], 1))
+    rs = np.random.RandomState(seed)
+    env_obs = rs.normal(size=(env_rows, O)).astype(np.float32)
+    if domain == 'walker2d':
+        env_obs[:, 0] = rs.uniform(0.9, 1.9, env_rows)
+        env_obs[:, 1] = rs.uniform(-0.9, 0.9, env_rows)
+    fit = min(env_rows, 20000)
+    p = obnn.init_params(E, O, A, hidden=H, seed=1, inputs=np.concatenate([env_obs[:fit], rs.uniform(-1, 1, (fit, A))], 1))
     P = osac.init_params(O, A, HP, seed=2)[:8]
-    envp = opool.Pool(O, A, n_env)
-    envp.add_samples({'observations': env_obs, 'actions': np.zeros((n_env, A)), 'rewards': np.zeros((n_env, 1)),
-                      'terminals': np.zeros((n_env, 1), bool), 'next_observations': env_obs})
-    B = args.cpu_batch
-    mp = opool.Pool(O, A, B * args.horizon)
-    np.random.seed(88)
-    t0 = time.perf_counter()
-    out = orollout.rollout(envp, mp, p, [0, 1, 2, 3, 4], P, B, args.horizon, ofe.term_halfcheetah, 1.0,
-                           eps_act=lambda n: np.random.normal(size=(n, A)))
-    dt = time.perf_counter() - t0
-    trans = sum(out['steps_added'])
-    return {'value': trans / dt, 'unit': 'transitions/s', 'cores': int(threads), 'kind': 'port',
-            'sample': 'oracle numpy rollout (mopo.py:723-765 restated), B=%d, horizon=%d, E=%d, H=%d: '
-                      '%d transitions in %.2f s' % (B, args.horizon, E, H, trans, dt)}
+    envp = opool.Pool(O, A, env_rows)
+    envp.add_samples({'observations': env_obs, 'actions': np.zeros((env_rows, A)), 'rewards': np.zeros((env_rows, 1)),
+                      'terminals': np.zeros((env_rows, 1), bool), 'next_observations': env_obs})
+
+    def run():
+        mp = opool.Pool(O, A, B * horizon)
+        np.random.seed(88)
+        t0 = time.perf_counter()
+        out = orollout.rollout(envp, mp, p, [0, 1, 2, 3, 4], P, B, horizon, ofe.TERMINATION[domain], penalty,
+                               eps_act=lambda n: np.random.normal(size=(n, A)))
+        return sum(out['steps_added']), time.perf_counter() - t0
+    return run
+
+
+def cpu_baseline(args):
+    """The CPU baseline of BASELINE.md section 3: the numpy restatement of the reference rollout (fp32
+    ensemble; the reference's own TF path cannot run here), BLAS on the host's cores, the median of 5 runs
+    after a warm-up, on bounded samples of each BASELINE config's workload (same E, H, horizon, domain,
+    penalty and env-pool size; fewer rows, so the default bench stays within minutes)."""
+    threads = blas_threads()
+    legs = {}
+    for key, B, h, dom, pen, env_rows, what in (
+            ('C1', 1000, 1, 'halfcheetah', 1.0, 20000, 'halfcheetah_mixed plumbing config, B=1k, h=1'),
+            ('C2', args.cpu_batch, args.horizon, 'halfcheetah', 1.0, 20000, 'halfcheetah-mixed, B=50k, h=5'),
+            ('C3', 20000, 1, 'walker2d', 1.0, 20000, 'walker2d-medium-replay, B=100k, h=1 (fp32 on CPU)'),
+            ('C4', 5000, 5, 'halfcheetah', 5.0, 1000000, 'halfcheetah-medium-expert, penalty 5, 1e6-row env pool')):
+        med, runs, units, secs = median_runs(cpu_rollout_leg(B, h, dom, pen, env_rows))
+        legs[key] = {'value': med, 'unit': 'transitions/s', 'runs': runs, 'median': med, 'cores': int(threads),
+                     'sample': '%s: B=%d, h=%d, E=%d, H=%d; %d timed runs (%d transitions in %.2f s) after 1 warm-up'
+                               % (what, B, h, E, H, CPU_RUNS, units, secs)}
+    c2 = legs['C2']
+    return {'value': c2['median'], 'unit': 'transitions/s', 'cores': int(threads), 'kind': 'port',
+            'runs': c2['runs'], 'median': c2['median'],
+            'sample': 'oracle numpy rollout (mopo.py:723-765 restated), ' + c2['sample'], 'configs': legs}
 
 
 def cpu_baseline_1core(args):
-    """The same oracle rollout with BLAS limited to one thread, on a smaller sample."""
+    """The same oracle rollout with BLAS limited to one thread (the C2 workload on a smaller sample)."""
     try:
         from threadpoolctl import threadpool_limits
     except Exception:
         return None
-    a1 = argparse.Namespace(**vars(args))
-    a1.cpu_batch = 15000
     with threadpool_limits(limits=1):
-        r = cpu_baseline(a1)
-    r['cores'] = 1
-    return r
+        med, runs, units, secs = median_runs(cpu_rollout_leg(3000, args.horizon))
+    return {'value': med, 'unit': 'transitions/s', 'cores': 1, 'kind': 'port', 'runs': runs, 'median': med,
+            'sample': 'oracle numpy rollout, 1 BLAS thread, B=3000, h=%d, E=%d, H=%d: %d timed runs (%d transitions '
+                      'in %.2f s) after 1 warm-up' % (args.horizon, E, H, CPU_RUNS, units, secs)}
 
 
 BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense MFMA
@@ -389,7 +424,8 @@ def train_leg(args, env):
 
 
 def cpu_baseline_train(args):
-    """Oracle BNN training steps (numpy restatement of the TF graph, f32 arrays) on the host."""
+    """Oracle BNN training steps (numpy restatement of the TF graph, f32 arrays) on the host: median of 5
+    runs of ``cpu_train_steps`` minibatch steps after a warm-up."""
     from oracle import bnn as obnn
     from oracle import bnn_train as ot
     rs = np.random.RandomState(0)
@@ -397,15 +433,17 @@ def cpu_baseline_train(args):
     st = ot.TrainState(p, dtype=np.float32)
     X = rs.normal(size=(E, 256, O + A)).astype(np.float32)
     Y = rs.normal(size=(E, 256, O + 1)).astype(np.float32)
-    st.step(X, Y, np.float32)
     n = args.cpu_train_steps
-    t0 = time.perf_counter()
-    for _ in range(n):
-        st.step(X, Y, np.float32)
-    dt = time.perf_counter() - t0
-    return {'value': n / dt, 'unit': 'grad-steps/s', 'cores': blas_threads(), 'kind': 'port',
+
+    def run():
+        t0 = time.perf_counter()
+        for _ in range(n):
+            st.step(X, Y, np.float32)
+        return n, time.perf_counter() - t0
+    med, runs, units, secs = median_runs(run)
+    return {'value': med, 'unit': 'grad-steps/s', 'cores': blas_threads(), 'kind': 'port', 'runs': runs, 'median': med,
             'sample': 'oracle numpy BNN train step (bnn.py:241-249 loss, hand backward, TF1 Adam), E=7, H=200, '
-                      'batch 256: %d steps in %.2f s' % (n, dt)}
+                      'batch 256: %d timed runs of %d steps (%.2f s) after 1 warm-up' % (CPU_RUNS, n, secs)}
 
 
 SAC_DIAG = {}
@@ -462,13 +500,10 @@ def sac_leg(args, pool, env, dev, world):
 
 
 def cpu_baseline_sac(args):
-    """Oracle SAC step (numpy restatement of mopo.py:204-466, 834-853) on the host."""
+    """Oracle SAC steps (numpy restatement of mopo.py:204-466, 834-853) on the host, BASELINE.md section 3:
+    ``cpu_sac_steps`` (1000) consecutive steps at batch 256, timed as 5 runs of a fifth each after a
+    warm-up run; the median run's rate."""
     from oracle import sac as osac
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get('num_threads', 1) for i in threadpool_info() if i.get('user_api') == 'blas'] or [1])
-    except Exception:
-        threads = 1
     rs = np.random.RandomState(0)
     st = osac.SACState(osac.init_params(O, A, HP, seed=2, dtype=np.float32))
     for k in ('params', 'target'):
@@ -477,12 +512,17 @@ def cpu_baseline_sac(args):
     batch = {'observations': rs.normal(size=(n, O)).astype(np.float32), 'actions': rs.uniform(-1, 1, (n, A)).astype(np.float32),
              'next_observations': rs.normal(size=(n, O)).astype(np.float32), 'rewards': rs.normal(size=(n, 1)).astype(np.float32),
              'terminals': np.zeros((n, 1), bool)}
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_sac_steps):
-        osac.sac_step(st, batch, rs.normal(size=(n, A)).astype(np.float32), rs.normal(size=(n, A)).astype(np.float32))
-    dt = time.perf_counter() - t0
-    return {'value': args.cpu_sac_steps / dt, 'unit': 'grad-steps/s', 'cores': int(threads), 'kind': 'port',
-            'sample': 'oracle numpy SAC step (fp32 arrays), batch 256, %d steps in %.2f s' % (args.cpu_sac_steps, dt)}
+    per = max(args.cpu_sac_steps // CPU_RUNS, 1)
+
+    def run():
+        t0 = time.perf_counter()
+        for _ in range(per):
+            osac.sac_step(st, batch, rs.normal(size=(n, A)).astype(np.float32), rs.normal(size=(n, A)).astype(np.float32))
+        return per, time.perf_counter() - t0
+    med, runs, units, secs = median_runs(run)
+    return {'value': med, 'unit': 'grad-steps/s', 'cores': blas_threads(), 'kind': 'port', 'runs': runs, 'median': med,
+            'sample': 'oracle numpy SAC step (fp32 arrays), batch 256: %d consecutive steps as %d timed runs of %d '
+                      '(%.2f s) after a warm-up run' % (units, CPU_RUNS, per, secs)}
 
 
 def main():

@@ -28,3 +28,19 @@ def test_committed_pmc_summary_prices_the_measured_workloads(monkeypatch):
         # HBM bytes per ensemble launch: at least the algorithmic bytes, far below 1 GB
         alg = bench.ensemble_bytes(args.batch, bench.CONFIGS[args.config], args.ensemble_dtype)
         assert alg >= lo * 0.9 and alg * 0.9 <= t < 1e9, (bench.workload_key(args), alg, t)
+
+
+def test_cpu_baseline_median_of_five_after_warmup():
+    """every CPU-baseline figure is the median of >= 5 timed runs after 1 warm-up."""
+    import bench
+    calls = []
+
+    def fn():
+        calls.append(1)
+        return 10, 0.5 + 0.1 * len(calls)
+    med, runs, units, secs = bench.median_runs(fn)
+    assert len(calls) == 1 + bench.CPU_RUNS and len(runs) == bench.CPU_RUNS >= 5
+    assert med == sorted(runs)[len(runs) // 2] and units == 10 * bench.CPU_RUNS
+    run = bench.cpu_rollout_leg(64, 2, 'walker2d', 5.0, env_rows=500)   # the oracle rollout leg, tiny
+    n, dt = run()
+    assert 0 < n <= 128 and dt > 0
