@@ -111,7 +111,7 @@ class SAC:
 
     def __del__(self):
         h = getattr(self, '_h', None)
-        if h is not None and h.value:
+        if h is not None and h.value and L is not None and L.lib is not None:   # not at interpreter teardown
             L.lib().mopo_sac_destroy(h)
             self._h = None
 

@@ -87,3 +87,35 @@ def model_choice(uid, seed, step, elites):
     x = _words(uid, seed, step, RNG_MODEL)[0]
     elites = np.asarray(elites, np.int32)
     return elites[((x.astype(np.uint64) * np.uint64(len(elites))) >> np.uint64(32)).astype(np.int64)]
+
+
+# ---- the SAC step's perf-mode streams (csrc/sac_rows.h gather_elem / head_noise), keyed by the device
+# step counter ``it`` (0 for a fresh handle, +1 per step) and the call's seed (MOPO: seed + 7919 * epoch)
+RNG_SAC = 5
+
+
+def _sac_words(r, seed, c1, c2, stream):
+    return philox4x32_10(np.asarray(r, np.uint64), c1, c2, stream, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+
+
+def sac_batch_indices(n, n_env, env_size, model_size, seed, it):
+    """_training_batch (mopo.py:801-821) in perf mode: row r < n_env indexes the env pool, the rest the
+    model pool, uniform over the pool's live size: counter {r, it lo, it hi, RNG_SAC}."""
+    r = np.arange(n, dtype=np.uint64)
+    x = _sac_words(r, seed, np.uint64(it & 0xFFFFFFFF), np.uint64((it >> 32) & 0xFFFFFFFF), RNG_SAC)[0]
+    size = np.where(r < n_env, env_size, model_size).astype(np.uint64)
+    return ((x.astype(np.uint64) * size) >> np.uint64(32)).astype(np.int64)
+
+
+def sac_noise(n, A, seed, it, nxt):
+    """The policy noise of the SAC step (mopo.py:306) for pi(s) (nxt 0) / pi(s') (nxt 1): action j of row r
+    from the Philox block j // 4 with counter {r | nxt << 31, it ^ (block << 24), it hi, RNG_SAC + 16};
+    actions 4b, 4b+1 from words (x, y), 4b+2, 4b+3 from (z, w)."""
+    r = np.arange(n, dtype=np.uint64) | (np.uint64(nxt) << np.uint64(31))
+    out = np.empty((n, 4 * ((A + 3) // 4)), np.float32)
+    for blk in range((A + 3) // 4):
+        x, y, z, w = _sac_words(r, seed, np.uint64((it & 0xFFFFFFFF) ^ (blk << 24)),
+                                np.uint64((it >> 32) & 0xFFFFFFFF), RNG_SAC + 16)
+        out[:, 4 * blk], out[:, 4 * blk + 1] = box_muller(x, y)
+        out[:, 4 * blk + 2], out[:, 4 * blk + 3] = box_muller(z, w)
+    return out[:, :A]

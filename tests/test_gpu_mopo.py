@@ -164,3 +164,104 @@ def test_mopo_real_ratio_one_skips_rollouts():
     d = list(algo.train(1))
     assert calls == [] and not hasattr(algo, '_model_pool')
     assert algo._num_train_steps == 50 and all(np.isfinite(v) for v in d[-1].values())
+
+
+@pytest.mark.parametrize('K', [50, 200])
+def test_mopo_epoch_vs_oracle_epoch(K):
+    """One whole MOPO epoch (mopo.py:536-573: the model rollout into the model pool, then epoch_length
+    _do_training_repeats steps over the mixed env / model batch, mopo.py:723-765, 780-853) through
+    MOPO.train itself, in perf mode, against an oracle epoch run from the restated streams (oracle/rng.py:
+    the rollout's start rows, policy noise, member choice and observation noise; SAC's batch indices and
+    policy noise): oracle.rollout fills the oracle's model pool, oracle.sac steps on batches drawn from the
+    oracle's own pools (a true end-to-end recompute, no device state shared).
+    Tolerances: the model pool as the rollout parity cases (5e-5 (1 + |ref|); terminals, size bit-exact).
+    SAC after K steps, scaled error |dev - ref| / (1 + |ref|) of every parameter, target, Adam m / v and
+    log_alpha against the f64 oracle.  SAC's training dynamics amplify the f32 rounding of the device (f32
+    storage and sums) over the steps (scripts/dbg/sac_drift.py, the same streams on other pools: max 4e-7
+    after 10 steps, 1.4e-6 after 50, 9e-4 after 200 with p50 2.4e-7), so the bounds are on the distribution:
+    K = 50: p50 <= 1e-6, p99 <= 1e-4, max <= 1e-3 (measured 1e-8 / 2e-6 / 9e-5); K = 200: p50 <= 2e-6,
+    p99 <= 1e-3, max <= 2e-2; and the last step's losses (logs) within 1e-3 relative."""
+    import torch
+    from oracle import fake_env as ofe
+    from oracle import replay_pool as opool
+    from oracle import rng as orng
+    from oracle import rollout as orl
+    from oracle import sac as osac
+    from oracle import bnn as obnn
+    from mopo_amd.mopo import MOPO
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.static import static_fns
+    O, A, E, H = 17, 6, 7, 200
+    B, h, seed = 1000, 5, 0x5eed
+    rs = np.random.RandomState(31)
+    n_env = 3000
+    env = {'observations': rs.normal(size=(n_env, O)).astype(np.float32),
+           'actions': rs.uniform(-1, 1, (n_env, A)).astype(np.float32),
+           'rewards': rs.normal(size=(n_env, 1)).astype(np.float32),
+           'terminals': rs.uniform(size=(n_env, 1)) < 0.05}
+    env['next_observations'] = (env['observations'] + 0.1 * rs.normal(size=(n_env, O))).astype(np.float32)
+    pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=n_env)
+    pool.add_samples(env)
+    algo = MOPO(pool, static_fns['halfcheetah'], O, A, rollout_batch_size=B, rollout_length=h, epoch_length=K,
+                model_train_freq=250, real_ratio=0.05, target_entropy=-3, ensemble_dtype='fp32', actor_dtype='fp32',
+                num_networks=E, num_elites=5, hidden_dim=H, separate_mean_var=True, penalty_coeff=1.0,
+                penalty_learned_var=True, seed=seed)
+    mats = obnn.to_mat_list(obnn.init_params(E, O, A, hidden=H, seed=32,
+                                             inputs=np.concatenate([env['observations'], env['actions']], 1)))
+    elites = [3, 0, 6, 1, 4]
+    algo._model.set_params(mats)
+    algo._model.set_elites(elites)
+    algo._model_train_metrics = {}                     # the model is given (no BNN.train in this epoch)
+    p0, la0 = algo._sac.get_params()
+    flat0 = p0.cpu().numpy().astype(np.float64)
+    list(algo.train(1))
+    torch.cuda.synchronize()
+    # ---- the oracle epoch: rollout (epoch 0: start rows at step 0, horizon step i at 1 + i)
+    bnn = obnn.from_mat_list(mats)
+    shapes = osac.param_shapes(O, A, 256)
+    P0, off = [], 0
+    for s in shapes:
+        P0.append(flat0[off:off + int(np.prod(s))].reshape(s))
+        off += int(np.prod(s))
+    envp = opool.Pool(O, A, n_env)
+    envp.add_samples(env)
+    modp = opool.Pool(O, A, algo._model_pool._max_size)
+    uid = np.arange(B)
+    orl.rollout(envp, modp, bnn, elites, P0[:8], B, h, ofe.TERMINATION['halfcheetah'], 1.0,
+                eps_act=[orng.act_noise(uid, seed, 1 + i, A).astype(np.float64) for i in range(h)],
+                start_idx=orng.start_rows(uid, seed, 0, n_env),
+                noise=[np.broadcast_to(orng.obs_noise(uid, seed, 1 + i, O + 1).astype(np.float64), (E, B, O + 1))
+                       for i in range(h)],
+                model_inds=[orng.model_choice(uid, seed, 1 + i, elites) for i in range(h)])
+    mp = algo._model_pool
+    assert mp.size == modp.size == B * h
+    got = {k: v[:mp.size].cpu().numpy() for k, v in mp.fields.items()}
+    for k in ('observations', 'actions', 'next_observations', 'rewards'):
+        err = np.abs(got[k].astype(np.float64) - modp.fields[k][:mp.size]) / (1 + np.abs(modp.fields[k][:mp.size]))
+        assert err.max() <= 5e-5, (k, err.max())
+    np.testing.assert_array_equal(got['terminals'], modp.fields['terminals'][:mp.size])
+    # ---- the oracle epoch: K SAC steps on batches of the oracle's pools (step counter k, seed + 7919 * 0)
+    st = osac.SACState(P0, log_alpha=float(la0.item()))
+    n, n_env_b = 256, int(256 * 0.05)
+    for k in range(K):
+        idx = orng.sac_batch_indices(n, n_env_b, envp.size, modp.size, seed, k)
+        e_b, m_b = envp.batch_by_indices(idx[:n_env_b]), modp.batch_by_indices(idx[n_env_b:])
+        batch = {f: np.concatenate([e_b[f], m_b[f]]).astype(np.float64) for f in e_b}
+        lg = osac.sac_step(st, batch, orng.sac_noise(n, A, seed, k, 0).astype(np.float64),
+                           orng.sac_noise(n, A, seed, k, 1).astype(np.float64), target_entropy=-3.0)
+    flat = lambda xs: np.concatenate([np.asarray(x, np.float64).ravel() for x in xs])
+    ref = {'params': np.append(flat(st.params), st.log_alpha), 'target': flat(st.target),
+           'adam_m': np.concatenate([flat(st.opt_pi.m), flat(st.opt_q1.m), flat(st.opt_q2.m), flat(st.opt_a.m)]),
+           'adam_v': np.concatenate([flat(st.opt_pi.v), flat(st.opt_q1.v), flat(st.opt_q2.v), flat(st.opt_a.v)])}
+    dev = {k: v.cpu().numpy().astype(np.float64) for k, v in algo._sac.state_dict().items()}
+    errs = {}
+    for k in ref:
+        assert dev[k].shape == ref[k].shape, k
+        errs[k] = np.abs(dev[k] - ref[k]) / (1 + np.abs(ref[k]))
+    q = {k: [float(np.quantile(e, x)) for x in (0.5, 0.99, 1.0)] for k, e in errs.items()}
+    print('K=%d: epoch vs oracle epoch, scaled error p50 / p99 / max:' % K, q)
+    p50, p99, mx = (1e-6, 1e-4, 1e-3) if K <= 50 else (2e-6, 1e-3, 2e-2)
+    assert all(v[0] <= p50 and v[1] <= p99 and v[2] <= mx for v in q.values()), q
+    dl = algo._sac.logs()
+    for dk, rk in (('Q/q1_loss', 'Q/q1_loss'), ('sac_Q/q2_loss', 'sac_Q/q2_loss'), ('policy_loss', 'pi_loss')):
+        assert abs(dl[dk] - lg[rk]) <= 1e-3 * (1 + abs(lg[rk])), (dk, dl[dk], lg[rk])
