@@ -724,15 +724,24 @@ __global__ __launch_bounds__(WAVES * 64, R == 1 ? 2 : 1) void bnn_fwd_f16r_kerne
 #ifndef BNN_RING_DEPTH_BF16
 #define BNN_RING_DEPTH_BF16 3
 #endif
+#ifndef BNN_F16_FOLD
+#define BNN_F16_FOLD 1   // with BNN_F16Q_DEFER: the ring kernel's row scale folded into the swish (bnn_fwd_ring_kernel)
+#endif
 #ifndef BNN_F16Q_DEFER
-#define BNN_F16Q_DEFER 0  // 1: the swish of k-group c in the MFMA gaps of k-group c - 1 (see below)
+// 1: the swish of k-group c in the MFMA gaps of k-group c - 1 (see below).  Alone within noise of 0; with
+// the folded scale (BNN_F16_FOLD) +1.4 % on the headline rollout (131.2 vs 129.4M/s, ensemble 0.331 vs
+// 0.334 ms, same-box A/B, profiles/r04_ens_ab_fold.txt), so both are on
+#define BNN_F16Q_DEFER 1
 #endif
 
 #ifndef BNN_RING_WAVES
 #define BNN_RING_WAVES 4  // waves per workgroup (16 rows each) sharing one ring
 #endif
+#ifndef BNN_RING_MINB
+#define BNN_RING_MINB 3  // 4-wave workgroups per CU the ring kernel's registers are capped for (LDS admits 3)
+#endif
 template <int NB2, int NBO, int MODE, int WAVES, int P, int DEPTH, int NBU = NB2>
-__global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES > 0 ? BNN_F16_MINB * 4 / WAVES : 1) void bnn_fwd_ring_kernel(const BnnDev w,
+__global__ __launch_bounds__(WAVES * 64, BNN_RING_MINB * 4 / WAVES > 0 ? BNN_RING_MINB * 4 / WAVES : 1) void bnn_fwd_ring_kernel(const BnnDev w,
                                                                                             const FwdArgs a) {
   static_assert(P == 1 || P == 2, "1: bf16, 2: f16x3");
   static_assert(DEPTH >= 3, "ring of at least 3 slots");
@@ -835,6 +844,11 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES > 0 ? BNN_F16_
   // the activation y' = u / (1 + 2^u) of k-group c is made during the MFMAs of k-group c - 1 of the next
   // layer (its exp / rcp in the MFMA issue gaps).
   constexpr bool DEF = BNN_F16Q_DEFER;
+  // Folded scale (BNN_F16_FOLD with the deferred swish, f16x3): the row scale already comes from max |u|
+  // (|y'| = |u| / (1 + 2^u) <= |u|, so y' s stays below 2^15), so the swish produces y' s directly as
+  // u / ((1 + 2^u) / s) -- its 1 + 2^u add becomes an fma with 1 / s -- and the split needs no multiply:
+  // one VALU op per value less, in a kernel whose vector issue, not its MFMAs, is the bound
+  constexpr bool FOLD = F16 && DEF && BNN_F16_FOLD;
   auto to_input = [&](float f) {
     float mx = 0.f;
 #pragma unroll
@@ -853,16 +867,20 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES > 0 ? BNN_F16_
     }
     if constexpr (F16) row_scale(row_max(mx), s_in, inv_row);
   };
-  auto act = [&](int c, int j) {  // y' of value j of k-group c (the padding block of an odd count stays 0)
-    if (j < 4 || 2 * c + 1 < NBU) hf[c][j] = swish_log2(hf[c][j]);
+  auto act = [&](int c, int j) {  // y' (FOLD: y' s) of value j of k-group c (the padding block stays 0)
+    if (j < 4 || 2 * c + 1 < NBU) {
+      const float u = hf[c][j];
+      hf[c][j] = FOLD ? u * __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(u), inv_row, inv_row)) : swish_log2(u);
+    }
   };
   // the operand parts of k-group kg of `in`: f16x3 the two scaled fp16 parts, bf16 the RN bf16 values
-  auto parts = [&](const float (&v)[8]) {
+  auto parts = [&](const float (&v)[8], auto prescaled) {
     if constexpr (F16) {
       u32x4v h4, l4;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const F16Pair pr = split_f16_pair(v[2 * q], v[2 * q + 1], s_in);
+        const F16Pair pr = decltype(prescaled)::value ? split_f16_pair_prescaled(v[2 * q], v[2 * q + 1])
+                                                      : split_f16_pair(v[2 * q], v[2 * q + 1], s_in);
         h4[q] = pr.hi;
         l4[q] = pr.lo;
       }
@@ -888,7 +906,8 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16_MINB * 4 / WAVES > 0 ? BNN_F16_
     }
     RingRun<J0, J0 + P * KGL>::run([&](auto jc) {
       constexpr int J = decltype(jc)::value, s = J - J0, kg = s / P, p = s % P;
-      if constexpr (p == 0) parts(in[kg]);   // made when the k-group is first consumed
+      // made when the k-group is first consumed (layers > 0 under FOLD hold y' s already)
+      if constexpr (p == 0) parts(in[kg], std::integral_constant<bool, FOLD && (L > 0)>{});
       // slice J landed (every later slice still in flight may stay so) ... for every wave, and every wave
       // is done with the buffer slice J + DEPTH - 1 goes into (slice J - 1's)
       constexpr int N = [] {

@@ -374,6 +374,17 @@ __device__ __forceinline__ F16Pair split_f16_pair(float a, float b, float s) {
   return {h, l};
 }
 
+// the same split of two values already multiplied by their row scale
+__device__ __forceinline__ F16Pair split_f16_pair_prescaled(float as, float bs) {
+  uint32_t h;
+  asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h) : "v"(as), "v"(bs));
+  const float ah = (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
+  const float bh = (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16));
+  uint32_t l;
+  asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(l) : "v"(as - ah), "v"(bs - bh));
+  return {h, l};
+}
+
 // power-of-two scale s with max |v| * s in [2^14, 2^15) (mx >= 0; zero / tiny rows clamp, inf / NaN
 // stay inf / NaN as in f32) and its exact inverse
 __device__ __forceinline__ void row_scale(float mx, float& s, float& inv) {
