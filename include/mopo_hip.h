@@ -283,6 +283,11 @@ int mopo_sac_set_graph(mopo_sac_t h, int enable);
  * targets iff ((c - base) / n_train_repeat) % interval == 0.  Enqueued on `stream` (it orders with
  * mopo_sac_step); the default {0, 1, 1} updates on every step. */
 int mopo_sac_set_target_schedule(mopo_sac_t h, int64_t base, int64_t n_train_repeat, int64_t interval, void* stream);
+
+/* softlearning SAC's action_prior (softlearning/algorithms/sac.py:42, 285-289): 0 'uniform' (MOPO's own
+ * graph, mopo.py:364; the default), 1 'normal' -- the policy loss subtracts the standard-normal log-prob
+ * of the policy's action. */
+int mopo_sac_set_action_prior(mopo_sac_t h, int normal);
 /* device<->device copy of a handle buffer (which: 0 params, 1 target, 2 adam_m, 3 adam_v, 4 grads,
  * 5 logs); to_handle=1 writes the handle's buffer from d_buf (e.g. loading a checkpoint). */
 int mopo_sac_copy(mopo_sac_t h, int which, int to_handle, void* d_buf, int64_t count, void* stream);

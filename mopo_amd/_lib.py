@@ -92,6 +92,7 @@ SIGNATURES = {
                               c_void_p, c_void_p, c_void_p]),
     'mopo_sac_set_graph': (c_int, [c_void_p, c_int]),
     'mopo_sac_set_target_schedule': (c_int, [c_void_p, c_i64, c_i64, c_i64, c_void_p]),
+    'mopo_sac_set_action_prior': (c_int, [c_void_p, c_int]),
     'mopo_sac_copy': (c_int, [c_void_p, c_int, c_int, c_void_p, c_i64, c_void_p]),
     'mopo_sac_debug_stamps': (c_int, [c_void_p, c_void_p, c_i64]),
     'mopo_mt_create': (c_int, [C.POINTER(c_void_p), c_u32]),

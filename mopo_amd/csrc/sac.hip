@@ -79,6 +79,7 @@ struct Sac {
   bool use_graph = true;
   hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
   hipGraph_t graph[3] = {nullptr, nullptr, nullptr};
+  int prior = 0;                  // action_prior 'normal' (mopo_sac_set_action_prior)
   mopo_pool_desc genv{}, gmod{};
   hipStream_t gstream = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
@@ -258,7 +259,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     pr.b3[0] = Wq(0, 5); pr.b3[1] = Wq(1, 5);
     pr.head_s = h->out[0]; pr.eps_s = h->eps_s; pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
     pr.h2p = h->h2[0]; pr.h1p = h->h1[0]; pr.W2p = P + o.pW2;
-    pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p;
+    pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p; pr.prior = h->prior;
     d.gather = prefetch ? 1 : 0;
     if (prefetch) {
       d.ga = gather_args(h, 1 - par, env, mod, seed, nullptr);
@@ -300,6 +301,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     g.ad = ad;
     g.ad.slot0 = 0;
     g.L = L; g.A = A; g.ncq = ncq; g.tent = h->tent; g.logs = h->logs; g.iter = h->iter;
+    g.prior = h->prior; g.eps_s = h->eps_s;
     g.st = Stamps{h->stamps, 3};
     if (tot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
     h->nslots = tot;
@@ -543,6 +545,15 @@ extern "C" int mopo_sac_set_target_schedule(mopo_sac_t hh, int64_t base, int64_t
   hipLaunchKernelGGL(sac_set_tctl_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, h->tctl, base, n_train_repeat,
                      interval);
   MOPO_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int mopo_sac_set_action_prior(mopo_sac_t hh, int normal) {
+  Sac* h = reinterpret_cast<Sac*>(hh);
+  MOPO_REQUIRE(h, "mopo_sac_set_action_prior: NULL handle");
+  MOPO_REQUIRE(normal == 0 || normal == 1, "mopo_sac_set_action_prior: 0 (uniform) or 1 (normal)");
+  if (h->prior != normal) drop_graphs(h);   // the flag is a kernel argument of the captured steps
+  h->prior = normal;
   return 0;
 }
 

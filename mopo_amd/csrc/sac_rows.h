@@ -103,6 +103,7 @@ struct PolicyRows {
   const float* h2p; const float* h1p;// [n][H]
   const float* W2p;                  // [H][H]
   float* dhead; float* dh2p; float* dh1p;
+  int prior;                         // 1: action_prior 'normal' (softlearning sac.py:285-289): + a / n on d L / d a
 };
 
 
@@ -199,6 +200,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
       const float a = tanhf(u);
       const float inv = 1.f / (sd + 1e-8f);
       const float zz = (u - mu) * inv;
+      if (c.prior) da += a * (1.f / (float)n);                       // -mean(log N(a; 0, I))' = a / n
       float du = da * (1.f - a * a);                                // tanh grad (y-based)
       du += g * (-zz * inv);                                        // gaussian_likelihood wrt x
       du += g * (2.f - 4.f / (1.f + expf(2.f * u)));                // squash correction: 2 - 4 sigmoid(-2u)

@@ -48,6 +48,8 @@ struct WgradArgs {
   float tent;
   float* logs;
   int64_t* iter;
+  int prior;                         // action_prior 'normal': the policy loss logs - log N(a; 0, I)
+  const float* eps_s;                // [n][A] the step's policy noise of pi(s) (for the action)
   Stamps st;
 };
 
@@ -72,9 +74,14 @@ static __device__ __forceinline__ void wgrad_loss_tail(const WgradArgs& a, float
     // every load of the row first (one memory latency), then the terms
     const RowIn in = row_losses_load(a.L, n, a.ncq, r, on);
     const float lps = bload(dlp, on ? r : -1);
-    float lsv[8];
+    float lsv[8], muv[8], epv[8];
+    const auto dep = rsrc(a.eps_s, (int64_t)n * A);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) lsv[j] = bload(dls, (on && j < A) ? r * 2 * A + A + j : -1);
+    for (int j = 0; j < 8; ++j) {
+      lsv[j] = bload(dls, (on && j < A) ? r * 2 * A + A + j : -1);
+      muv[j] = bload(dls, (a.prior && on && j < A) ? r * 2 * A + j : -1);
+      epv[j] = bload(dep, (a.prior && on && j < A) ? r * A + j : -1);
+    }
     if (!on) continue;
     const RowQ o = row_losses(a.L, in);
     const float q1 = o.q[0], q2 = o.q[1], q1p = o.q[2], q2p = o.q[3];
@@ -86,7 +93,17 @@ static __device__ __forceinline__ void wgrad_loss_tail(const WgradArgs& a, float
       ent += logf(expf(ls) + 1e-8f) + 0.5f * logf(2.f * 3.14159265358979f * 2.718281828459045f);
     }
     red[0] += (q1 - o.y) * (q1 - o.y); red[1] += (q2 - o.y) * (q2 - o.y); red[2] += q1; red[3] += q2;
-    red[4] += lps; red[5] += ent; red[6] += o.alpha * lps - fminf(q1p, q2p);
+    float lprior = 0.f;                                               // log N(a; 0, I) of pi(s)'s action
+    if (a.prior) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j >= A) break;
+        const float act = tanhf(muv[j] + epv[j] * expf(fminf(fmaxf(lsv[j], -20.f), 2.f)));
+        lprior -= 0.5f * act * act;
+      }
+      lprior -= 0.5f * (float)A * 1.8378770664093453f;
+    }
+    red[4] += lps; red[5] += ent; red[6] += o.alpha * lps - fminf(q1p, q2p) - lprior;
   }
 #pragma unroll
   for (int i = 0; i < 7; ++i)

@@ -40,6 +40,8 @@ class MOPO:
         the fp32 parity tolerances); 'fp32' runs exact-f32 MFMA.  ``actor_dtype``: the rollout
         policy forward ('fp32' / 'f16x3'; default fp32 with the fp32 ensemble, else f16x3:
         ``rollout.default_actor_dtype``)."""
+        if kwargs.get('action_prior', 'uniform') != 'uniform':   # mopo.py:364 asserts the uniform prior
+            raise AssertionError("MOPO's policy loss supports action_prior='uniform' only (mopo.py:364)")
         self._pool = pool                                   # device SimpleReplayPool of env data
         self._static_fns = static_fns
         self._obs_dim, self._act_dim = obs_dim, act_dim

@@ -52,8 +52,8 @@ class SAC:
                            discount=0.99, tau=5e-3, target_update_interval=1, action_prior='uniform',
                            reparameterize=False, store_extra_policy_info=False, save_full_state=False,
                            batch_size=256, real_ratio=1.0, **kwargs):
-        if action_prior != 'uniform':
-            raise NotImplementedError("action_prior must be 'uniform' (sac.py:255-262 normal prior not on this path)")
+        if action_prior not in ('uniform', 'normal'):
+            raise NotImplementedError("action_prior must be 'uniform' or 'normal' (sac.py:285-289)")
         if store_extra_policy_info:
             raise NotImplementedError('store_extra_policy_info')
         env = training_environment
@@ -71,11 +71,12 @@ class SAC:
         self._policy, self._Qs, self._pool, self._plotter = policy, Qs, pool, plotter
         self._init(obs_dim, act_dim, hidden=hs[0], batch_size=batch_size, real_ratio=real_ratio, lr=lr,
                    discount=discount, tau=tau, reward_scale=reward_scale, target_entropy=target_entropy,
-                   reparameterize=reparameterize, target_update_interval=target_update_interval, **kwargs)
+                   reparameterize=reparameterize, target_update_interval=target_update_interval,
+                   action_prior=action_prior, **kwargs)
 
     def _init(self, obs_dim, act_dim, hidden=256, batch_size=256, real_ratio=0.05, lr=3e-4, discount=0.99,
               tau=5e-3, reward_scale=1.0, target_entropy='auto', params=None, log_alpha=0.0, seed=2,
-              reparameterize=True, use_graph=True, target_update_interval=1):
+              reparameterize=True, use_graph=True, target_update_interval=1, action_prior='uniform'):
         if not reparameterize:
             raise NotImplementedError('only the reparameterized policy loss is implemented (mopo.py:370-374; '
                                       'every config sets reparameterize=True, examples/config/d4rl/base.py)')
@@ -103,6 +104,10 @@ class SAC:
         self._h = h
         self.n_params = n
         L.check(L.lib().mopo_sac_set_graph(h, int(bool(use_graph))))
+        if action_prior not in ('uniform', 'normal'):
+            raise NotImplementedError("action_prior must be 'uniform' or 'normal' (sac.py:285-289)")
+        self._action_prior = action_prior
+        L.check(L.lib().mopo_sac_set_action_prior(h, int(action_prior == 'normal')))
         bufs = [C.c_void_p() for _ in range(6)]
         npar = C.c_int64()
         L.check(L.lib().mopo_sac_buffers(h, *[C.byref(b) for b in bufs], C.byref(npar)))

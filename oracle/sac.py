@@ -156,9 +156,18 @@ class SACState:
         self.opt_a = Adam([self.log_alpha], lr)
 
 
-def sac_step(st, batch, eps_s, eps_s2, gamma=0.99, tau=5e-3, reward_scale=1.0, target_entropy=-3.0, grads_out=None):
+def prior_log_prob(a):
+    """softlearning sac.py:285-289: MultivariateNormalDiag(0, 1).log_prob(actions), per row."""
+    return -0.5 * np.sum(a * a, axis=-1) - 0.5 * a.shape[-1] * np.log(2 * np.pi)
+
+
+def sac_step(st, batch, eps_s, eps_s2, gamma=0.99, tau=5e-3, reward_scale=1.0, target_entropy=-3.0, grads_out=None,
+             action_prior='uniform'):
     """One ``_do_training`` + ``_update_target`` (mopo.py:834-853). Mutates ``st``; returns logs.
-    ``grads_out`` (dict): receives the pre-step gradients 'pi', 'q1', 'q2' (lists) and 'alpha'."""
+    ``grads_out`` (dict): receives the pre-step gradients 'pi', 'q1', 'q2' (lists) and 'alpha'.
+    ``action_prior='normal'``: softlearning's SAC (sac.py:285-289, 304-306) subtracts the standard-normal
+    log-prob of the policy's action from the policy loss (MOPO's own graph asserts 'uniform',
+    mopo.py:364)."""
     s, a, s2 = batch['observations'], batch['actions'], batch['next_observations']
     r, d = batch['rewards'][:, 0], batch['terminals'][:, 0].astype(np.float64)
     n = s.shape[0]
@@ -177,7 +186,8 @@ def sac_step(st, batch, eps_s, eps_s2, gamma=0.99, tau=5e-3, reward_scale=1.0, t
     y = reward_scale * r + gamma * ((1 - d) * (np.minimum(q1_t, q2_t) - alpha * logp_next))  # :380-386
     q1_loss = 0.5 * np.mean((q1 - y) ** 2)
     q2_loss = 0.5 * np.mean((q2 - y) ** 2)
-    pi_loss = np.mean(alpha * logp_pi - np.minimum(q1_pi, q2_pi))
+    prior = prior_log_prob(a_pi) if action_prior == 'normal' else 0.0
+    pi_loss = np.mean(alpha * logp_pi - np.minimum(q1_pi, q2_pi) - prior)
     # gradients
     g_q1, _ = q_backward(Q1, c1, (q1 - y) / n)
     g_q2, _ = q_backward(Q2, c2, (q2 - y) / n)
@@ -186,6 +196,8 @@ def sac_step(st, batch, eps_s, eps_s2, gamma=0.99, tau=5e-3, reward_scale=1.0, t
     _, dx2 = q_backward(Q2, c2p, np.where(sel1, 0.0, -1.0 / n), need_params=False)
     O = s.shape[1]
     da = dx1[:, O:] + dx2[:, O:]
+    if action_prior == 'normal':
+        da = da + a_pi / n                                          # d/da of -mean(log N(a; 0, I))
     g_pi = pi_backward(P, cpi, np.full(n, alpha / n), da)
     g_alpha = -np.mean(logp_pi + target_entropy)                    # d/dlog_alpha of :437-438
     if grads_out is not None:

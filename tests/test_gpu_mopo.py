@@ -271,10 +271,12 @@ def test_mopo_epoch_vs_oracle_epoch(K):
 def test_f16x3_product_default_tracks_fp32_over_epochs():
     """the product default (f16x3 ensemble and actor) against exact-f32 MFMA over a whole
     multi-epoch MOPO.train (3 epochs: rollout + 100 SAC steps each, same seeds, same given model), so the
-    end-to-end effect of the 22-bit operands on what SAC learns is pinned, not only per step.  Bounds on
-    the scaled difference |f16x3 - fp32| / (1 + |fp32|) of the SAC parameters after the 3 epochs: p50 <= 1e-5,
-    p99 <= 2e-3 (the same order as the f32 device's own drift from the f64 oracle over 200 steps,
-    test_mopo_epoch_vs_oracle_epoch), and the last losses within 1e-2 relative."""
+    end-to-end effect of the 22-bit operands on what SAC learns is pinned, not only per step.  SAC's
+    training dynamics amplify any rounding difference (test_mopo_epoch_vs_oracle_epoch: the f32 device
+    against the f64 oracle reaches p50 3e-5 / p99 5e-4 after 200 steps), so the yardstick is another
+    f32-accurate arithmetic: bf16x6 (3 bf16 parts, 6 products) against the same fp32 run.  The scaled SAC
+    parameter difference |x - fp32| / (1 + |fp32|) of f16x3 must stay within 3x bf16x6's at the median and
+    the 99th percentile (floor 1e-6), and the last losses within 1e-2 relative of fp32's."""
     import torch
     from oracle import bnn as obnn
     from mopo_amd.mopo import MOPO
@@ -291,7 +293,7 @@ def test_f16x3_product_default_tracks_fp32_over_epochs():
     mats = obnn.to_mat_list(obnn.init_params(E, O, A, hidden=H, seed=42,
                                              inputs=np.concatenate([env['observations'], env['actions']], 1)))
     out = {}
-    for dt in ('f16x3', 'fp32'):
+    for dt in ('f16x3', 'bf16x6', 'fp32'):
         pool = SimpleReplayPool(obs_dim=O, act_dim=A, max_size=n_env)
         pool.add_samples(env)
         algo = MOPO(pool, static_fns['halfcheetah'], O, A, rollout_batch_size=1000, rollout_length=5, epoch_length=100,
@@ -304,10 +306,14 @@ def test_f16x3_product_default_tracks_fp32_over_epochs():
         diags = list(algo.train(3))
         torch.cuda.synchronize()
         out[dt] = (algo._sac.state_dict()['params'].cpu().numpy().astype(np.float64), diags[-1])
-    (p16, d16), (p32, d32) = out['f16x3'], out['fp32']
-    err = np.abs(p16 - p32) / (1 + np.abs(p32))
-    q = [float(np.quantile(err, x)) for x in (0.5, 0.99, 1.0)]
-    print('f16x3 vs fp32 after 3 epochs, scaled param difference p50 / p99 / max:', q)
-    assert q[0] <= 1e-5 and q[1] <= 2e-3, q
+    p32, d32 = out['fp32']
+    q = {}
+    for dt in ('f16x3', 'bf16x6'):
+        err = np.abs(out[dt][0] - p32) / (1 + np.abs(p32))
+        q[dt] = [float(np.quantile(err, x)) for x in (0.5, 0.99, 1.0)]
+    print('after 3 epochs, scaled SAC parameter difference from fp32, p50 / p99 / max:', q)
+    for i in (0, 1):
+        assert q['f16x3'][i] <= max(3 * q['bf16x6'][i], 1e-6), q
+    d16 = out['f16x3'][1]
     for k in ('Q_loss', 'training/policy_loss'):
         assert abs(d16[k] - d32[k]) <= 1e-2 * (1 + abs(d32[k])), (k, d16[k], d32[k])

@@ -282,3 +282,41 @@ def test_sac_one_step_gradients_odd_shapes(o, a, h, n):
         err = np.abs(g[off:off + m] - gr.ravel()).max()
         assert err <= 1e-4 * scale + 1e-7, 'grad tensor %d: err %.3g scale %.3g' % (i, err, scale)
         off += m
+
+
+def test_sac_normal_action_prior_one_step_vs_oracle():
+    """softlearning SAC's action_prior='normal' (sac.py:285-289) through the device step: the policy loss
+    log and every gradient against the fp64 oracle with the prior (tolerances as test_sac_one_step_parity),
+    then a graph-replayed second run of the same step equals the eager one (the flag is captured)."""
+    from mopo_amd.sac import SAC
+    rs = np.random.RandomState(8)
+    (env_p, env_op), (mod_p, mod_op) = pools(rs)
+    params = [p + rs.normal(size=p.shape) * 0.02 for p in osac.init_params(O, A, H, seed=5)]
+    fl = flat(params).astype(np.float32)
+    sac = SAC(O, A, H, batch_size=256, real_ratio=0.05, target_entropy=-3, params=fl, log_alpha=0.1,
+              action_prior='normal')
+    idx, e1, e2 = draw(rs, env_p.size, mod_p.size)
+    st = osac.SACState([p.astype(np.float32).astype(np.float64) for p in params], log_alpha=np.float32(0.1))
+    batch = host_batch(env_op, mod_op, idx)
+    got = {}
+    logs_ref = osac.sac_step(st, batch, e1.astype(np.float64), e2.astype(np.float64), grads_out=got,
+                             action_prior='normal')
+    sac._do_training(0, env_p, mod_p, idx=idx, eps_s=e1, eps_n=e2)
+    lg = sac.logs()
+    np.testing.assert_allclose(lg['policy_loss'], logs_ref['pi_loss'], rtol=2e-4, atol=1e-6)
+    np.testing.assert_allclose(lg['Q/q1_loss'], logs_ref['Q/q1_loss'], rtol=2e-4, atol=1e-6)
+    g = sac.get_grads()[0].cpu().numpy()
+    off = 0
+    for i, gr in enumerate(got['pi'] + got['q1'] + got['q2']):
+        n = gr.size
+        err = np.abs(g[off:off + n] - gr.ravel()).max()
+        assert err <= 1e-4 * (np.abs(gr).max() + 1e-12) + 1e-7, 'grad tensor %d: err %.3g' % (i, err)
+        off += n
+    # perf mode: graph replay with the prior equals the eager path
+    outs = []
+    for use_graph in (True, False):
+        s2 = SAC(O, A, H, batch_size=256, real_ratio=0.05, target_entropy=-3, params=fl, log_alpha=0.1,
+                 action_prior='normal', use_graph=use_graph)
+        s2._do_training(0, env_p, mod_p, n_steps=3, seed=11)
+        outs.append(s2.get_params()[0].cpu().numpy())
+    np.testing.assert_array_equal(outs[0], outs[1])

@@ -224,3 +224,44 @@ def test_model_pool_size_configs():
     assert orl.model_pool_size(50000, 1000, 1000, 5, 5) == 1250000
     assert orl.model_pool_size(50000, 1000, 1000, 1, 5) == 250000
     assert orl.model_pool_size(100000, 1000, 250, 1, 20) == 8000000
+
+
+def test_sac_oracle_normal_action_prior_matches_torch_autograd():
+    """softlearning SAC's action_prior='normal' (sac.py:285-289): the policy loss subtracts the standard-
+    normal log-prob of pi's action; the oracle's policy gradient and loss against torch autograd."""
+    torch = pytest.importorskip('torch')
+    O, A, H, n = 11, 3, 32, 48
+    rs = np.random.RandomState(4)
+    params = [p + rs.normal(size=p.shape) * 0.05 for p in osac.init_params(O, A, H, seed=6)]
+    st = osac.SACState(params, log_alpha=-0.2)
+    batch = {'observations': rs.normal(size=(n, O)), 'actions': rs.uniform(-1, 1, (n, A)),
+             'next_observations': rs.normal(size=(n, O)), 'rewards': rs.normal(size=(n, 1)),
+             'terminals': rs.uniform(size=(n, 1)) < 0.2}
+    e1, e2 = rs.normal(size=(n, A)), rs.normal(size=(n, A))
+    T = [torch.tensor(p, dtype=torch.float64, requires_grad=True) for p in params]
+    s = torch.tensor(batch['observations'])
+
+    def pi(P, x, eps):
+        h = torch.relu(x @ P[0] + P[1]); h = torch.relu(h @ P[2] + P[3])
+        mu = h @ P[4] + P[5]
+        ls = torch.clamp(h @ P[6] + P[7], -20, 2)
+        std = torch.exp(ls); u = mu + torch.tensor(eps) * std
+        logp = torch.sum(-0.5 * (((u - mu) / (std + 1e-8)) ** 2 + 2 * ls + np.log(2 * np.pi)), -1)
+        logp = logp - torch.sum(2 * (np.log(2) - u - torch.nn.functional.softplus(-2 * u)), -1)
+        return torch.tanh(u), logp
+
+    def q(Q, x, act):
+        z = torch.cat([x, act], -1)
+        h = torch.relu(z @ Q[0] + Q[1]); h = torch.relu(h @ Q[2] + Q[3])
+        return (h @ Q[4] + Q[5])[:, 0]
+
+    P, Q1, Q2 = T[0:8], T[8:14], T[14:20]
+    api, logp = pi(P, s, e1)
+    prior = -0.5 * torch.sum(api * api, -1) - 0.5 * A * np.log(2 * np.pi)
+    lpi = torch.mean(np.exp(-0.2) * logp - torch.minimum(q(Q1, s, api), q(Q2, s, api)) - prior)
+    gpi = torch.autograd.grad(lpi, P)
+    got = {}
+    logs = osac.sac_step(st, batch, e1, e2, grads_out=got, action_prior='normal')
+    np.testing.assert_allclose(logs['pi_loss'], lpi.item(), rtol=1e-12)
+    for go, gt in zip(got['pi'], gpi):
+        np.testing.assert_allclose(go, gt.numpy(), rtol=1e-9, atol=1e-12)
