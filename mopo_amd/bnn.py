@@ -84,6 +84,16 @@ def structure_lines(E, obs_dim, act_dim, hidden):
     return mean, [fc_repr(D, hidden, None, VAR_WEIGHT_DECAY, E)]
 
 
+def structure_files(E, obs_dim, act_dim, hidden, smv):
+    """BNN.save's structure files (bnn.py:572-585) as {suffix: text}: smv writes '' (mean layers)
+    and '_var'; the joint branch as written writes the halved last layer (output D, activation
+    None) after EVERY hidden layer -- a file the reference's own _load_structure cannot read back
+    (nor load_model=True here)."""
+    mean, var = structure_lines(E, obs_dim, act_dim, hidden)
+    files = {'': mean, '_var': var} if smv else {'': [ln for hid in mean[:-1] for ln in (hid, mean[-1])]}
+    return {k: ''.join('%s\n' % ln for ln in v) for k, v in files.items()}
+
+
 def parse_structure(path):
     """BNN._load_structure's line parser (bnn.py:594-625): a list of FC keyword dicts."""
     layers = []
@@ -95,6 +105,29 @@ def parse_structure(path):
                            'activation': None if kw['activation'] == 'None' else kw['activation'][1:-1],
                            'ensemble_size': int(kw['ensemble_size'])})
     return layers
+
+
+def _smv_shapes(shapes):
+    """.mat shapes of the smv layout for a (joint or smv) list of shapes."""
+    if len(shapes) == 16:
+        return shapes
+    W, b = shapes[10], shapes[11]
+    D = W[-1] // 2
+    half_w, half_b = W[:-1] + (D,), b[:-1] + (D,)
+    return shapes[:10] + [half_w, half_b, half_w, half_b] + shapes[12:]
+
+
+def _joint_to_smv(mats):
+    """14 joint arrays -> 16 smv arrays: head [E, H, 2D] split into mean / log-var columns."""
+    W, b = mats[10], mats[11]
+    D = W.shape[-1] // 2
+    c = np.ascontiguousarray
+    return list(mats[:10]) + [c(W[..., :D]), c(b[..., :D]), c(W[..., D:]), c(b[..., D:])] + list(mats[12:])
+
+
+def _smv_to_joint(mats):
+    return list(mats[:10]) + [np.concatenate([mats[10], mats[12]], -1),
+                              np.concatenate([mats[11], mats[13]], -1)] + list(mats[14:])
 
 
 class BNN:
@@ -250,19 +283,16 @@ class BNN:
         self.model_loaded = True
 
     def save(self, savedir, timestep):
-        """BNN.save (bnn.py:559-592): '<name>_<t>.nns' + '<name>_<t>_var.nns' (the structure, one
-        repr(FC) per line) and '<name>_<t>.mat' (keys '0'..'15' = nonoptvars + optvars)."""
+        """BNN.save (bnn.py:559-592): '<name>_<t>.nns' (+ '<name>_<t>_var.nns' for smv; the
+        structure, one repr(FC) per line, ``structure_files``) and '<name>_<t>.mat' (keys '0'..'15',
+        joint '0'..'13' = nonoptvars + optvars)."""
         from scipy.io import savemat
-        if not self.separate_mean_var:
-            # the reference's joint-head branch (bnn.py:571-576) writes the halved last layer once per
-            # hidden layer, a file its own _load_structure cannot read back; only smv is written here
-            raise NotImplementedError('BNN.save: structure files are written for separate_mean_var=True only')
         self._require_mats('save')
         savedir = self.model_dir if savedir is None else savedir
-        mean, var = structure_lines(self.num_nets, self.obs_dim, self.act_dim, self.hidden_dim)
-        for suffix, lines in (('', mean), ('_var', var)):
+        files = structure_files(self.num_nets, self.obs_dim, self.act_dim, self.hidden_dim, self.separate_mean_var)
+        for suffix, text in files.items():   # joint: one file, the reference's interleaved text
             with open(os.path.join(savedir, '{}_{}{}.nns'.format(self.name, timestep, suffix)), 'w+') as f:
-                f.write(''.join('%s\n' % ln for ln in lines))
+                f.write(text)
         savemat(os.path.join(savedir, '{}_{}.mat'.format(self.name, timestep)),
                 {str(i): m for i, m in enumerate(self._mats)})
 
@@ -303,14 +333,19 @@ class BNN:
         return t
 
     def _train_params(self, t, mats=None):
+        """Move the .mat arrays into / out of the trainer.  The trainer holds the smv layout; a
+        joint head (bnn.py:183-189) goes in as its mean / log-var column halves, which carry the
+        same 0.0001 decay (constructor.py:34-36), so the loss and every Adam update are the
+        joint model's (oracle: tests/test_oracle_train.py::test_joint_head_equals_split_heads)."""
         if mats is not None:
+            mats = mats if self.separate_mean_var else _joint_to_smv(mats)
             arr = (C.c_void_p * 16)(*[m.ctypes.data for m in mats])
             L.check(L.lib().mopo_bnn_train_set_params(t, arr))
             return None
-        out = [np.empty_like(m) for m in self._mats]
+        out = [np.empty(s, np.float32) for s in _smv_shapes([z.shape for z in self._mat_shapes()])]
         arr = (C.c_void_p * 16)(*[m.ctypes.data for m in out])
         L.check(L.lib().mopo_bnn_train_get_params(t, arr))
-        return out
+        return out if self.separate_mean_var else _smv_to_joint(out)
 
     def train(self, inputs, targets, batch_size=32, max_epochs=None, max_epochs_since_update=5,
               hide_progress=False, holdout_ratio=0.0, max_logging=1000, max_grad_updates=None, timer=None,
@@ -320,8 +355,6 @@ class BNN:
         ``np.random.permutation`` order (the permutation was drawn by the caller, as
         ``MOPO._train_model`` does when it formats the device pool in that order)."""
         import torch
-        if not self.separate_mean_var:
-            raise NotImplementedError('training is implemented for separate_mean_var=True (all D4RL configs)')
         E = self.num_nets
         N = int(inputs.shape[0])
         num_holdout = min(int(N * holdout_ratio), max_logging)

@@ -4,6 +4,9 @@ Follows (reference xionghuichen/mopo):
   * train loss (not deterministic)     mopo/models/bnn.py:241-249 -- sum over members of
       mean((mu - y)^2 exp(-lv)) + mean(lv), + sum of decays, + 0.01 sum(maxlv) - 0.01 sum(minlv)
   * _compile_losses                    mopo/models/bnn.py:677-701 (mse_loss = inc_var_loss False)
+  * joint head (separate_mean_var=False) bnn.py:183-189 (last layer widened to 2D outputs, one
+      weight_decay 0.0001 on the whole [H, 2D] matrix), bnn.py:644-654 (mean = out[..., :D],
+      log-var raw = out[..., D:])
   * 3-D forward (per-member batches)   mopo/models/fc.py:99-104 (matmul), bnn.py:656-675
   * weight decay                       mopo/models/fc.py:156-157 (wd * tf.nn.l2_loss(W)),
                                        rates constructor.py:30-36
@@ -30,12 +33,19 @@ def _sigmoid(x):
     return one / (one + np.exp(-x))
 
 
+def _smv(p):
+    return p.get('smv', True)
+
+
 def optvars(p):
-    """The optimised variables in bnn.py optvars order (mean layers W,b; var layer W,b; maxlv, minlv)."""
+    """The optimised variables in bnn.py optvars order (mean layers W,b; var layer W,b (smv only);
+    maxlv, minlv) -- bnn.py:199-222."""
     out = []
     for w, b in zip(p['W'], p['b']):
         out += [w, b]
-    out += [p['Wv'], p['bv'], p['max_logvar'], p['min_logvar']]
+    if _smv(p):
+        out += [p['Wv'], p['bv']]
+    out += [p['max_logvar'], p['min_logvar']]
     return out
 
 
@@ -44,7 +54,10 @@ def set_optvars(p, vals):
     q['W'] = [vals[2 * i] for i in range(N_HIDDEN + 1)]
     q['b'] = [vals[2 * i + 1] for i in range(N_HIDDEN + 1)]
     k = 2 * (N_HIDDEN + 1)
-    q['Wv'], q['bv'], q['max_logvar'], q['min_logvar'] = vals[k], vals[k + 1], vals[k + 2], vals[k + 3]
+    if _smv(p):
+        q['Wv'], q['bv'] = vals[k], vals[k + 1]
+        k += 2
+    q['max_logvar'], q['min_logvar'] = vals[k], vals[k + 1]
     return q
 
 
@@ -58,8 +71,13 @@ def forward3d(p, X, dtype=np.float64):
         h = z * _sigmoid(z)
         zs.append(z)
         hs.append(h)
-    mean = np.matmul(h, p['W'][N_HIDDEN].astype(dtype)) + p['b'][N_HIDDEN].astype(dtype)
-    raw = np.matmul(h, p['Wv'].astype(dtype)) + p['bv'].astype(dtype)
+    out = np.matmul(h, p['W'][N_HIDDEN].astype(dtype)) + p['b'][N_HIDDEN].astype(dtype)
+    if _smv(p):
+        mean = out
+        raw = np.matmul(h, p['Wv'].astype(dtype)) + p['bv'].astype(dtype)
+    else:                                                                   # bnn.py:644-654
+        D = out.shape[-1] // 2
+        mean, raw = out[..., :D], out[..., D:]
     mx, mn = p['max_logvar'].astype(dtype), p['min_logvar'].astype(dtype)
     lv1 = mx - softplus(mx - raw)                                           # bnn.py:669
     lv = mn + softplus(lv1 - mn)                                            # bnn.py:670
@@ -81,8 +99,11 @@ def loss_and_grads(p, X, Y, dtype=np.float64):
     err = mean - y
     loss = np.sum(np.mean(np.mean(err * err * inv, -1), -1) + np.mean(np.mean(lv, -1), -1))
     Ws = [w.astype(dtype) for w in p['W']]
-    Wv = p['Wv'].astype(dtype)
-    decay = sum(wd * 0.5 * np.sum(w * w) for wd, w in zip(WD, Ws)) + WD_VAR * 0.5 * np.sum(Wv * Wv)
+    smv = _smv(p)
+    decay = sum(wd * 0.5 * np.sum(w * w) for wd, w in zip(WD, Ws))
+    if smv:
+        Wv = p['Wv'].astype(dtype)
+        decay = decay + WD_VAR * 0.5 * np.sum(Wv * Wv)
     mx, mn = p['max_logvar'].astype(dtype), p['min_logvar'].astype(dtype)
     loss = loss + decay + 0.01 * np.sum(mx) - 0.01 * np.sum(mn)
     s = 1.0 / (B * D)
@@ -97,11 +118,17 @@ def loss_and_grads(p, X, Y, dtype=np.float64):
     h4 = c['hs'][N_HIDDEN]
     gW = [None] * (N_HIDDEN + 1)
     gb = [None] * (N_HIDDEN + 1)
-    gW[N_HIDDEN] = np.matmul(h4.transpose(0, 2, 1), dmean) + WD[N_HIDDEN] * Ws[N_HIDDEN]
-    gb[N_HIDDEN] = np.sum(dmean, 1, keepdims=True)
-    gWv = np.matmul(h4.transpose(0, 2, 1), draw) + WD_VAR * Wv
-    gbv = np.sum(draw, 1, keepdims=True)
-    dh = np.matmul(dmean, Ws[N_HIDDEN].transpose(0, 2, 1)) + np.matmul(draw, Wv.transpose(0, 2, 1))
+    if smv:
+        gW[N_HIDDEN] = np.matmul(h4.transpose(0, 2, 1), dmean) + WD[N_HIDDEN] * Ws[N_HIDDEN]
+        gb[N_HIDDEN] = np.sum(dmean, 1, keepdims=True)
+        gWv = np.matmul(h4.transpose(0, 2, 1), draw) + WD_VAR * Wv
+        gbv = np.sum(draw, 1, keepdims=True)
+        dh = np.matmul(dmean, Ws[N_HIDDEN].transpose(0, 2, 1)) + np.matmul(draw, Wv.transpose(0, 2, 1))
+    else:                        # one [H, 2D] head: d out = [d mean | d raw]
+        dout = np.concatenate([dmean, draw], -1)
+        gW[N_HIDDEN] = np.matmul(h4.transpose(0, 2, 1), dout) + WD[N_HIDDEN] * Ws[N_HIDDEN]
+        gb[N_HIDDEN] = np.sum(dout, 1, keepdims=True)
+        dh = np.matmul(dout, Ws[N_HIDDEN].transpose(0, 2, 1))
     for l in range(N_HIDDEN - 1, -1, -1):
         z = c['zs'][l]
         sg = _sigmoid(z)
@@ -113,7 +140,9 @@ def loss_and_grads(p, X, Y, dtype=np.float64):
     grads = []
     for l in range(N_HIDDEN + 1):
         grads += [gW[l], gb[l]]
-    grads += [gWv, gbv, dmx, dmn]
+    if smv:
+        grads += [gWv, gbv]
+    grads += [dmx, dmn]
     return loss, grads
 
 
@@ -196,7 +225,8 @@ def _member_vars(p):
     out = []
     for w, b in zip(p['W'], p['b']):
         out += [np.array(w), np.array(b)]
-    out += [np.array(p['Wv']), np.array(p['bv'])]
+    if _smv(p):
+        out += [np.array(p['Wv']), np.array(p['bv'])]
     return out
 
 
@@ -204,5 +234,6 @@ def _set_member_vars(p, vals):
     q = dict(p)
     q['W'] = [vals[2 * i] for i in range(N_HIDDEN + 1)]
     q['b'] = [vals[2 * i + 1] for i in range(N_HIDDEN + 1)]
-    q['Wv'], q['bv'] = vals[-2], vals[-1]
+    if _smv(p):
+        q['Wv'], q['bv'] = vals[-2], vals[-1]
     return q

@@ -124,6 +124,7 @@ def build_bnn(refs, p, E, O, A, H, smv, dtype):
     if not smv:  # bnn.py:186-193
         obj.layers[-1].set_output_dim(2 * obj.layers[-1].get_output_dim())
         obj.end_act = obj.layers[-1].get_activation()
+        obj.end_act_name = obj.layers[-1].get_activation(as_func=False)
         obj.layers[-1].unset_activation()
     # variable values (names as finalize's scopes create them, bnn.py:196-227)
     iv = tfstub.S.init_values
@@ -179,20 +180,20 @@ def bnn_forward_case(refs, name, E, H, B, smv, seed, store_weights, x_f64=False)
     return out
 
 
-def bnn_loss_case(refs, name, E, H, n, seed):
+def bnn_loss_case(refs, name, E, H, n, seed, smv=True):
     """train_loss = sum(_compile_losses(inc_var_loss=True)) + add_n(decays) + 0.01 sum maxlv - 0.01 sum minlv
     (bnn.py:241-246) and mse_loss (bnn.py:248), 3-D inputs [E, n, IN]; gradients w.r.t. optvars."""
     O, A = 17, 6
     rs = np.random.RandomState(seed + 200)
-    p = obnn.init_params(E, O, A, hidden=H, seed=seed, smv=True, inputs=rs.normal(size=(300, O + A)))
+    p = obnn.init_params(E, O, A, hidden=H, seed=seed, smv=smv, inputs=rs.normal(size=(300, O + A)))
     X = rs.normal(size=(E, n, O + A)).astype(np.float32)
     Y = (rs.normal(size=(E, n, O + 1)) * 0.5).astype(np.float32)
-    out = dict(E=E, H=H, n=n, seed=seed, X=X, Y=Y)
+    out = dict(E=E, H=H, n=n, seed=seed, X=X, Y=Y, smv=int(smv))
     for i, m in enumerate(obnn.to_mat_list(p)):
         out['w%d' % i] = m
     bnn = refs[2]
     for tag, dt in (('f32', torch.float32), ('f64', torch.float64)):
-        obj = build_bnn(refs, p, E, O, A, H, True, dt)
+        obj = build_bnn(refs, p, E, O, A, H, smv, dt)
         xin, yin = tfstub.w(torch.as_tensor(X, dtype=dt)), tfstub.w(torch.as_tensor(Y, dtype=dt))
         loss = tfstub.reduce_sum(bnn.BNN._compile_losses(obj, xin, yin, inc_var_loss=True))
         loss = loss + tfstub.add_n(obj.decays)
@@ -327,15 +328,15 @@ def sac_case(refs, name, O, A, H, n, seed, steps=3, term_frac=0.2, compact=False
     np.savez_compressed(os.path.join(HERE, 'ref_sac_%s.npz' % name), **out)
 
 
-def bnn_save_case(refs, E=3, H=32, seed=41):
+def bnn_save_case(refs, E=3, H=32, seed=41, smv=True, dirname='ref_save'):
     """BNN.save (bnn.py:559-592) executed from the reference on a stand-in model: the structure files
     ('<name>_<t>.nns', '<name>_<t>_var.nns': one repr(FC) per line) and the '.mat' of nonoptvars +
     optvars, written to tests/golden/ref_save/."""
     utils, fc, bnn, _ = refs
     O, A = 17, 6
     rs = np.random.RandomState(seed)
-    p = obnn.init_params(E, O, A, hidden=H, seed=seed, smv=True, inputs=rs.normal(size=(200, O + A)))
-    obj = build_bnn(refs, p, E, O, A, H, True, torch.float32)
+    p = obnn.init_params(E, O, A, hidden=H, seed=seed, smv=smv, inputs=rs.normal(size=(200, O + A)))
+    obj = build_bnn(refs, p, E, O, A, H, smv, torch.float32)
     obj.finalized, obj.name, obj.model_dir = True, 'BNN', None
     obj.nonoptvars = obj.scaler.get_vars()
     obj.optvars = []
@@ -343,7 +344,7 @@ def bnn_save_case(refs, E=3, H=32, seed=41):
         obj.optvars.extend(layer.get_vars())
     obj.optvars += [obj.max_logvar, obj.min_logvar]
     obj._sess = tfstub.Session()   # BNN.sess is a property over _sess
-    out = os.path.join(HERE, 'ref_save')
+    out = os.path.join(HERE, dirname)
     os.makedirs(out, exist_ok=True)
     bnn.BNN.save(obj, out, 0)
     # the inputs / outputs of one predict with these weights, for the load test
@@ -354,8 +355,13 @@ def bnn_save_case(refs, E=3, H=32, seed=41):
                         var=tfstub.u(var).detach().numpy())
 
 
-def main():
+def main(argv):
     refs = load_reference()
+    if argv[1:] == ['joint']:   # the joint-head (separate_mean_var=False) training and save cases only
+        bnn_loss_case(refs, 'E3_H32_joint', 3, 32, 40, 22, smv=False)
+        bnn_save_case(refs, seed=42, smv=False, dirname='ref_save_joint')
+        print('ok')
+        return
     bnn_save_case(refs)
     # ensemble forward: the headline shapes and the stress shape (weights regenerated from the seed
     # for the large ones), the joint-head branch, f64 inputs (the rollout feeds f64 next_obs)
@@ -371,4 +377,4 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    main(sys.argv)

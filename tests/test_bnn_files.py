@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 REF = os.path.join(os.path.dirname(__file__), 'golden', 'ref_save')
+REF_JOINT = os.path.join(os.path.dirname(__file__), 'golden', 'ref_save_joint')
 
 
 def _lines(path):
@@ -15,10 +16,30 @@ def _lines(path):
 
 
 def test_structure_text_matches_reference_save():
-    from mopo_amd.bnn import structure_lines
-    mean, var = structure_lines(3, 17, 6, 32)
-    assert _lines(os.path.join(REF, 'BNN_0.nns')) == ''.join(l + '\n' for l in mean)
-    assert _lines(os.path.join(REF, 'BNN_0_var.nns')) == ''.join(l + '\n' for l in var)
+    from mopo_amd.bnn import structure_files
+    files = structure_files(3, 17, 6, 32, smv=True)
+    assert sorted(files) == ['', '_var']
+    assert _lines(os.path.join(REF, 'BNN_0.nns')) == files['']
+    assert _lines(os.path.join(REF, 'BNN_0_var.nns')) == files['_var']
+
+
+def test_joint_structure_text_matches_reference_save():
+    """bnn.py:572-579 as the reference writes it: the halved head after every hidden layer."""
+    from mopo_amd.bnn import structure_files
+    files = structure_files(3, 17, 6, 32, smv=False)
+    assert list(files) == ['']
+    assert _lines(os.path.join(REF_JOINT, 'BNN_0.nns')) == files['']
+    assert not os.path.exists(os.path.join(REF_JOINT, 'BNN_0_var.nns'))
+
+
+def test_reference_joint_mat_keys():
+    from scipy.io import loadmat
+    d = loadmat(os.path.join(REF_JOINT, 'BNN_0.mat'))
+    assert '14' not in d
+    shapes = [d[str(i)].shape for i in range(14)]
+    assert shapes[:2] == [(1, 23), (1, 23)]
+    assert shapes[2:12:2] == [(3, 23, 32), (3, 32, 32), (3, 32, 32), (3, 32, 32), (3, 32, 36)]
+    assert shapes[12:] == [(1, 18), (1, 18)]
 
 
 def test_parse_reference_structure():
@@ -64,3 +85,27 @@ def test_load_reference_save_and_round_trip(tmp_path):
     mean2, var2 = m2.predict(z['x'])
     np.testing.assert_array_equal(mean2, mean)
     np.testing.assert_array_equal(var2, var)
+
+
+@pytest.mark.gpu
+def test_joint_reference_save_predict_and_round_trip(tmp_path):
+    """The reference's joint .mat loaded into a joint handle (shapes given: its .nns is unreadable by
+    design, bnn.py:572-579) predicts as the reference graph did; save writes the same two files."""
+    from mopo_amd.bnn import BNN
+    from scipy.io import loadmat
+    m = BNN({'name': 'BNN_0', 'model_dir': REF_JOINT, 'num_elites': 3, 'separate_mean_var': False,
+             'num_networks': 3, 'obs_dim': 17, 'act_dim': 6, 'hidden_dim': 32})
+    m.load_params()
+    z = np.load(os.path.join(REF_JOINT, 'predict.npz'))
+    mean, var = m.predict(z['x'])
+    assert np.max(np.abs(mean - z['mean']) / (1 + np.abs(z['mean']))) < 2e-5
+    assert np.max(np.abs(var - z['var']) / z['var']) < 5e-5
+    m.save(str(tmp_path), 3)
+    assert _lines(str(tmp_path / 'BNN_0_3.nns')) == _lines(os.path.join(REF_JOINT, 'BNN_0.nns'))
+    assert not (tmp_path / 'BNN_0_3_var.nns').exists()
+    a, b = loadmat(str(tmp_path / 'BNN_0_3.mat')), loadmat(os.path.join(REF_JOINT, 'BNN_0.mat'))
+    for i in range(14):
+        np.testing.assert_array_equal(a[str(i)], b[str(i)])
+    with pytest.raises(ValueError):        # the reference's own _load_structure cannot read it either
+        os.rename(str(tmp_path / 'BNN_0_3.nns'), str(tmp_path / 'again.nns'))
+        BNN({'name': 'again', 'model_dir': str(tmp_path), 'load_model': True, 'num_elites': 3})

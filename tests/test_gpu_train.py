@@ -187,3 +187,39 @@ def test_train_loop_matches_oracle():
     mean, var = m.predict(X[:20])
     rm, rv = obnn.forward(obnn.from_mat_list(got, smv=True), X[:20])
     np.testing.assert_allclose(mean, rm, rtol=1e-4, atol=1e-5)
+
+
+def test_train_loop_joint_head_matches_oracle():
+    """separate_mean_var=False: the joint [H, 2D] head trains through the smv trainer on its column
+    halves (same 0.0001 decay, constructor.py:34-36); the oracle trains the joint head directly
+    (bnn.py:644-654, pinned by tests/golden/ref_bnn_loss_E3_H32_joint.npz)."""
+    from mopo_amd.bnn import construct_model
+    m = construct_model(obs_dim=O, act_dim=A, hidden_dim=H, num_networks=E, num_elites=2, separate_mean_var=False,
+                        seed=9)
+    mats = m.get_params()
+    assert len(mats) == 14 and mats[10].shape == (E, H, 2 * D)
+    rs = np.random.RandomState(109)
+    for i in range(3, 12, 2):
+        mats[i] = (rs.normal(size=mats[i].shape) * 0.1).astype(np.float32)
+    mats[12] = np.full_like(mats[12], 0.5)
+    mats[13] = np.full_like(mats[13], -3.0)
+    m.set_params(mats)
+    X, Y = data(300, seed=10)
+    np.random.seed(12)
+    out = m.train(X, Y, batch_size=32, max_epochs=10, holdout_ratio=0.2, max_epochs_since_update=3)
+    np.random.seed(12)
+    p0 = obnn.from_mat_list([x.astype(np.float64) for x in mats], smv=False)
+    q, elites, hl, epochs, updates = ot.train(p0, X, Y, num_elites=2, batch_size=32, max_epochs=10,
+                                              holdout_ratio=0.2, max_epochs_since_update=3)
+    assert m._train_epochs == epochs and m._train_grad_updates == updates
+    np.testing.assert_allclose(m._holdout_losses, hl, rtol=1e-3)
+    assert m._model_inds == elites
+    assert out['val_loss'] == pytest.approx(np.sort(hl)[:2].mean(), rel=1e-3)
+    got = m.get_params()
+    assert len(got) == 14
+    for i, (g, r) in enumerate(zip(got, obnn.to_mat_list(q))):
+        np.testing.assert_allclose(g, np.asarray(r).reshape(g.shape), rtol=1e-3, atol=1e-4, err_msg=str(i))
+    mean, var = m.predict(X[:20])
+    rm, rv = obnn.forward(obnn.from_mat_list(got, smv=False), X[:20])
+    np.testing.assert_allclose(mean, rm, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(var, rv, rtol=1e-4, atol=1e-6)

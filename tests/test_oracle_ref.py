@@ -77,6 +77,21 @@ def test_bnn_train_loss_oracle_vs_reference_graph():
     np.testing.assert_allclose(obt.mse_losses(p, z['X'], z['Y']), z['mse_f64'], rtol=1e-12)
 
 
+def test_bnn_train_loss_joint_head_vs_reference_graph():
+    """The joint head (separate_mean_var=False, bnn.py:183-189 / 644-654) through the reference's
+    _compile_losses + decays: 14 .mat arrays, one [H, 2D] head with one decay."""
+    z = dict(np.load(os.path.join(GOLD, 'ref_bnn_loss_E3_H32_joint.npz')))
+    assert int(z['smv']) == 0
+    p = obnn.from_mat_list([z['w%d' % i] for i in range(14)], smv=False)
+    loss, grads = obt.loss_and_grads(p, z['X'], z['Y'])
+    assert rel(loss, z['loss_f64']) < 1e-12
+    assert len(grads) == 12
+    for i, g in enumerate(grads):   # optvars: layers (W, b) x5 (head [H, 2D]), maxlv, minlv
+        ref = z['grad%d_f64' % i]
+        assert np.max(np.abs(g - ref)) <= 1e-12 * max(1.0, np.max(np.abs(ref))), i
+    np.testing.assert_allclose(obt.mse_losses(p, z['X'], z['Y']), z['mse_f64'], rtol=1e-12)
+
+
 def _sac_batch(z, k):
     return {kk: z['b%d_%s' % (k, kk)] for kk in ('observations', 'actions', 'next_observations', 'rewards',
                                                   'terminals')}

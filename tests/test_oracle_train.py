@@ -7,17 +7,18 @@ from oracle import bnn as obnn
 from oracle import bnn_train as ot
 
 
-def _tiny(E=2, O=3, A=1, H=6, seed=0):
-    p = obnn.init_params(E, O, A, hidden=H, seed=seed, bias_std=0.1)
+def _tiny(E=2, O=3, A=1, H=6, seed=0, smv=True):
+    p = obnn.init_params(E, O, A, hidden=H, seed=seed, bias_std=0.1, smv=smv)
     p['max_logvar'] = p['max_logvar'] * 0 + 0.3
     p['min_logvar'] = p['min_logvar'] * 0 - 2.0
     return {k: (v.astype(np.float64) if isinstance(v, np.ndarray) else
                 [x.astype(np.float64) for x in v] if isinstance(v, list) else v) for k, v in p.items()}
 
 
-def test_loss_gradient_matches_finite_differences():
+@pytest.mark.parametrize('smv', [True, False])
+def test_loss_gradient_matches_finite_differences(smv):
     rs = np.random.RandomState(1)
-    p = _tiny()
+    p = _tiny(smv=smv)
     E, IN, D = 2, 4, 4
     X = rs.normal(size=(E, 5, IN))
     Y = rs.normal(size=(E, 5, D))
@@ -80,3 +81,36 @@ def test_train_loop_early_stops_and_picks_elites():
                                       max_epochs_since_update=2)
     assert elites2 == elites
     np.testing.assert_array_equal(hl2, hl)
+
+
+def _split_joint(p):
+    """The joint head [H, 2D] as an smv pair (mean columns, log-var columns)."""
+    q = dict(p, smv=True, W=list(p['W']), b=list(p['b']))
+    W, b = p['W'][-1], p['b'][-1]
+    D = W.shape[-1] // 2
+    q['W'][-1], q['b'][-1], q['Wv'], q['bv'] = W[..., :D], b[..., :D], W[..., D:], b[..., D:]
+    return q
+
+
+def test_joint_head_equals_split_heads():
+    """bnn.py:183-189 + constructor.py:34-36: the joint head carries the same 0.0001 decay as the
+    smv mean and var heads, so its loss and gradients are the smv ones on the split columns (the
+    identity the device trainer uses for separate_mean_var=False)."""
+    rs = np.random.RandomState(5)
+    p = _tiny(smv=False)
+    X = rs.normal(size=(2, 9, 4))
+    Y = rs.normal(size=(2, 9, 4))
+    lj, gj = ot.loss_and_grads(p, X, Y)
+    q = _split_joint(p)
+    ls, gs = ot.loss_and_grads(q, X, Y)
+    assert lj == pytest.approx(ls, rel=1e-13)
+    for a, b in zip(gj[:8], gs[:8]):
+        np.testing.assert_allclose(a, b, rtol=1e-13)
+    np.testing.assert_allclose(gj[8], np.concatenate([gs[8], gs[10]], -1), rtol=1e-13)
+    np.testing.assert_allclose(gj[9], np.concatenate([gs[9], gs[11]], -1), rtol=1e-13)
+    np.testing.assert_allclose(gj[10], gs[12], rtol=1e-13)
+    np.testing.assert_allclose(gj[11], gs[13], rtol=1e-13)
+    _, mj, vj = ot.forward3d(p, X)
+    _, ms, vs = ot.forward3d(q, X)
+    np.testing.assert_allclose(mj, ms, rtol=1e-13)
+    np.testing.assert_allclose(vj, vs, rtol=1e-13)
