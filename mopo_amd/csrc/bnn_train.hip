@@ -73,6 +73,9 @@ struct Train {
   float *mu = nullptr, *sigma = nullptr;
   float *X = nullptr, *T = nullptr, *Z[NHID] = {}, *Hh[NHID] = {}, *OUT = nullptr, *dOUT = nullptr, *dZ[NHID] = {};
   std::vector<int> snap;       // members with a snapshot
+  int32_t* wlist = nullptr;    // weight-gradient tiles per XCD (train_wgrad2_kernel): [8][wl_per_x], counts [8]
+  int32_t* wcnt = nullptr;
+  int wl_per_x = 0;
   // graphs (full-batch steps), keyed by the epoch's data pointers
   hipStream_t gs = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
@@ -440,6 +443,278 @@ static __global__ __launch_bounds__(256, 2) void train_wgrad_kernel(const TrainW
   gemm32_body(g, (int)blockIdx.x - 1);
 }
 
+// ---- the weight-gradient launch, persistent XCD-local form -------------------------------------------
+// Every weight gradient dW_l = X_in^T dY (+ db = colsum dY, decay, TF1 Adam) of every member as 32 x 32
+// output tiles over the minibatch rows k < M (sac_wgrad.h's tile: 1024 threads, wave w the 16 x 16 quadrant
+// w & 3 over the K quarter w >> 2, K in chunks of 256 staged [row][k]).  The tiles are dealt to XCDs on the
+// host (build_wlist): member e's tiles go to XCD e mod 8 -- the XCD whose CUs ran its row blocks
+// (train_rows.h tr_block), so its X_in / dY panels, parameters and Adam slots are that L2's -- up to an even
+// share, the overflow to the least-loaded XCDs.  Each XCD's workgroups walk its list (workgroup j: entries
+// j, j + nwx, ...) and load the next tile's panels and Adam inputs into registers while the current tile's
+// MFMAs and epilogue run, so a workgroup has two tiles in flight instead of one memory latency per tile.
+// The last block runs the batch-level tail (train_loss_tail).
+constexpr int TW2_T = 32, TW2_KC = 256, TW2_KP = TW2_KC + 4;
+struct TrainWg2 {
+  int M;                               // minibatch rows per member (the contraction length)
+  int nwx, per_x;                      // tile workgroups per XCD; list stride per XCD
+  const int32_t* list;                 // [8][per_x]: l | e << 3 | tm << 7 | tn << 12
+  const int32_t* cnt;                  // [8] entries per XCD
+  const float* A[NHID + 1];            // X_in of layer l, member 0 ([E][M][K_l])
+  const float* B[NHID + 1];            // dY of layer l, member 0 ([E][M][N_l])
+  int K[NHID + 1], N[NHID + 1];
+  int64_t W[NHID + 1], b[NHID + 1];
+  float wd[NHID + 1];
+  AdamCtx ad;
+  TrainTail t;
+};
+
+struct Wg2Tile {
+  const float* A; const float* B;
+  int K, N, i0, j0;
+  int64_t w0, b0;                      // parameter index of W(0, 0) / b(0) of the tile's member and layer
+  float wd;
+  bool cs;                             // tile-row 0: also the bias column sums
+};
+
+static __device__ __forceinline__ Wg2Tile wg2_tile(const TrainWg2& g, int v) {
+  Wg2Tile t;
+  const int l = v & 7, e = (v >> 3) & 15, tm = (v >> 7) & 31, tn = (v >> 12) & 31;
+  t.K = g.K[l]; t.N = g.N[l];
+  t.A = g.A[l] + (int64_t)e * g.M * t.K;
+  t.B = g.B[l] + (int64_t)e * g.M * t.N;
+  t.i0 = TW2_T * tm; t.j0 = TW2_T * tn;
+  t.w0 = g.W[l] + (int64_t)e * t.K * t.N;
+  t.b0 = g.b[l] + (int64_t)e * t.N;
+  t.wd = g.wd[l];
+  t.cs = tm == 0;
+  return t;
+}
+
+// Workgroups of NT threads (512 or 1024): wave w owns quadrant w & 3 of the tile over the K part w >> 2 of
+// KW = 256 / (NT / 256) rows.  Thread t stages elements (row 4 (t % 8) + u, k (t / 8) + NT / 8 q), u < 4,
+// q < NQ: one b128 load per (operand, q) where the operand's row length is a multiple of 4 floats (b32
+// loads otherwise -- the 14 / 23-wide inputs of layer 0).  k >= M read 0 (buffer range); rows past the
+// operand's width read the next minibatch row's values, which only reach outputs that are not stored.
+template <int NT>
+struct Wg2 {
+  static constexpr int NQ = TW2_T * TW2_KC / (4 * NT);   // b128 loads per operand and chunk
+  static constexpr int NKQ = NT / 256, KW = TW2_KC / NKQ;
+  static constexpr int NE = TW2_T * TW2_T / NT;          // output elements per thread
+  static constexpr int CT = NT / TW2_T, CK = TW2_KC / CT; // colsum: threads per column, k per thread
+};
+
+template <int NT>
+static __device__ __forceinline__ void wg2_issue(const Wg2Tile& t, int M, int kc, int tid, f32x4 (&va)[Wg2<NT>::NQ],
+                                                 f32x4 (&vb)[Wg2<NT>::NQ]) {
+  const auto dA = rsrc(t.A, (int64_t)M * t.K), dB = rsrc(t.B, (int64_t)M * t.N);
+  const int r0 = 4 * (tid & 7), k0 = kc + (tid >> 3);
+  const bool a4 = (t.K & 3) == 0, b4 = (t.N & 3) == 0;   // wave-uniform
+#pragma unroll
+  for (int q = 0; q < Wg2<NT>::NQ; ++q) {
+    const int k = k0 + (NT / 8) * q;
+    const int ia = k * t.K + t.i0 + r0, ib = k * t.N + t.j0 + r0;
+    if (a4) va[q] = bload4(dA, ia);
+    else va[q] = f32x4{bload(dA, ia), bload(dA, ia + 1), bload(dA, ia + 2), bload(dA, ia + 3)};
+    if (b4) vb[q] = bload4(dB, ib);
+    else vb[q] = f32x4{bload(dB, ib), bload(dB, ib + 1), bload(dB, ib + 2), bload(dB, ib + 3)};
+  }
+}
+
+template <int NT>
+static __device__ __forceinline__ void wg2_adam_in(const AdamCtx& ad, const Wg2Tile& t, int tid,
+                                                   AdamIn (&a)[Wg2<NT>::NE], AdamIn& c) {
+#pragma unroll
+  for (int h = 0; h < Wg2<NT>::NE; ++h) {
+    const int e = tid + NT * h;
+    const int gi = min(t.i0 + (e >> 5), t.K - 1), gj = min(t.j0 + (e & 31), t.N - 1);
+    const int64_t ix = t.w0 + (int64_t)gi * t.N + gj;
+    a[h] = AdamIn{ad.Pc[ix], ad.M[ix], ad.V[ix], 0.f};   // no target copy in training (ad.T == NULL)
+  }
+  c = AdamIn{0.f, 0.f, 0.f, 0.f};
+  if (t.cs && tid % Wg2<NT>::CT == 0) {
+    const int64_t ix = t.b0 + min(t.j0 + tid / Wg2<NT>::CT, t.N - 1);
+    c = AdamIn{ad.Pc[ix], ad.M[ix], ad.V[ix], 0.f};
+  }
+}
+
+template <int NT>
+static __global__ __launch_bounds__(NT, NT / 128) void train_wgrad2_kernel(const TrainWg2 g) {
+  using C = Wg2<NT>;
+  __shared__ __attribute__((aligned(16))) float As[TW2_T * TW2_KP];   // [i][k]; later the K-part partials
+  __shared__ __attribute__((aligned(16))) float Bs[TW2_T * TW2_KP];   // [j][k]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (blockIdx.x == gridDim.x - 1) {   // the batch-level tail
+    train_loss_tail(g.t, As);
+    return;
+  }
+  const int x = blockIdx.x & 7, j = blockIdx.x >> 3;   // workgroups are dealt round-robin over the XCDs
+  const int cnt = g.cnt[x];
+  if (j >= cnt) return;
+  const int32_t* lst = g.list + (int64_t)x * g.per_x;
+  const int M = g.M;
+  const AdamCtx& ad = g.ad;
+  const float lr_t = *ad.lr_t;
+  const int qd = w & 3, qi = qd >> 1, qj = qd & 1, kq = w >> 2, li = lane & 15, lk = lane >> 4;
+  int i = j;
+  Wg2Tile cur = wg2_tile(g, __builtin_amdgcn_readfirstlane(lst[i]));
+  f32x4 va[C::NQ], vb[C::NQ];
+  wg2_issue<NT>(cur, M, 0, tid, va, vb);
+  AdamIn a_in[C::NE], c_in;
+  wg2_adam_in<NT>(ad, cur, tid, a_in, c_in);
+  while (true) {
+    const int inx = i + g.nwx;
+    const bool has_nx = inx < cnt;
+    const Wg2Tile nx = wg2_tile(g, has_nx ? __builtin_amdgcn_readfirstlane(lst[inx]) : 0);
+    AdamIn a_nx[C::NE], c_nx{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < C::NE; ++h) a_nx[h] = AdamIn{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc0 = zero4(), acc1 = zero4();
+    float cs = 0.f;
+    for (int kc = 0; kc < M; kc += TW2_KC) {
+      // re-derive the thread index here: otherwise the per-thread LDS / buffer offsets are hoisted out of
+      // the loops and held in registers across them
+      int tt = tid;
+      asm volatile("" : "+v"(tt));
+      {
+        const int r0 = 4 * (tt & 7), k0 = tt >> 3;
+#pragma unroll
+        for (int q = 0; q < C::NQ; ++q)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            As[(r0 + u) * TW2_KP + k0 + (NT / 8) * q] = va[q][u];
+            Bs[(r0 + u) * TW2_KP + k0 + (NT / 8) * q] = vb[q][u];
+          }
+      }
+      lds_barrier();
+      // the next chunk, or the next tile's first chunk and Adam inputs, in flight during this one
+      if (kc + TW2_KC < M) {
+        wg2_issue<NT>(cur, M, kc + TW2_KC, tt, va, vb);
+      } else if (has_nx) {
+        wg2_issue<NT>(nx, M, 0, tt, va, vb);
+        wg2_adam_in<NT>(ad, nx, tt, a_nx, c_nx);
+      }
+#pragma unroll
+      for (int s = 0; s < C::KW / 16; ++s) {         // k = KW kq + (KW / 4) lk + 4 s + u
+        const int k = C::KW * kq + (C::KW / 4) * lk + 4 * s;
+        const f32x4 a4 = ld4(As + (16 * qi + li) * TW2_KP + k), b4 = ld4(Bs + (16 * qj + li) * TW2_KP + k);
+        acc0 = mfma4(a4[0], b4[0], acc0);
+        acc1 = mfma4(a4[1], b4[1], acc1);
+        acc0 = mfma4(a4[2], b4[2], acc0);
+        acc1 = mfma4(a4[3], b4[3], acc1);
+      }
+      if (cur.cs) {                                  // column tid / CT, k = CK (tid % CT) .. + CK - 1
+        const float* bp = Bs + (tid / C::CT) * TW2_KP + C::CK * (tid % C::CT);
+#pragma unroll
+        for (int v = 0; v < C::CK; v += 4) {
+          const f32x4 x0 = ld4(bp + v);
+          cs += (x0[0] + x0[1]) + (x0[2] + x0[3]);
+        }
+      }
+      lds_barrier();
+    }
+    // ---- K parts through LDS (As reused), then decay + Adam per element
+    float* part = As;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[kq * 1024 + (16 * qi + 4 * lk + r) * 32 + 16 * qj + li] = acc0[r] + acc1[r];
+    if (cur.cs) {
+#pragma unroll
+      for (int off = C::CT / 2; off > 0; off >>= 1) cs += __shfl_xor(cs, off);
+    }
+    lds_barrier();
+#pragma unroll
+    for (int h = 0; h < C::NE; ++h) {
+      const int e = tid + NT * h;
+      float v = part[e];
+#pragma unroll
+      for (int q = 1; q < C::NKQ; ++q) v += part[1024 * q + e];
+      const int gi = cur.i0 + (e >> 5), gj = cur.j0 + (e & 31);
+      if (gi < cur.K && gj < cur.N)
+        adam_apply(ad, cur.w0 + (int64_t)gi * cur.N + gj, v + cur.wd * a_in[h].p, a_in[h], lr_t);   // fc.py:156-157
+    }
+    {
+      const int cj = cur.j0 + tid / C::CT;
+      if (cur.cs && tid % C::CT == 0 && cj < cur.N) adam_apply(ad, cur.b0 + cj, cs, c_in, lr_t);
+    }
+    if (!has_nx) break;
+    lds_barrier();                                   // the partials are read before the next panels land
+    i = inx;
+    cur = nx;
+#pragma unroll
+    for (int h = 0; h < C::NE; ++h) a_in[h] = a_nx[h];
+    c_in = c_nx;
+  }
+}
+
+// MOPO_TRAIN_WG2 (default 1): the persistent XCD-local weight-gradient launch; 0: train_wgrad_kernel
+int train_wg2() {
+  static const int v = [] {
+    const char* e = std::getenv("MOPO_TRAIN_WG2");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
+// tiles of member e to XCD e mod 8 up to ceil(total / 8) per XCD, the rest to the least-loaded XCDs; within
+// an XCD in (member, layer NHID .. 0, tile row, tile column) order, so a round's workgroups share panels
+int build_wlist(Train* h) {
+  const Layout& L = h->L;
+  std::vector<std::vector<int32_t>> xl(8);
+  std::vector<int32_t> over;
+  int total = 0;
+  for (int l = 0; l <= NHID; ++l) {
+    const int K = l == 0 ? L.IN : L.H, N = l == NHID ? 2 * L.D : L.H;
+    total += L.E * ceil_div(K, TW2_T) * ceil_div(N, TW2_T);
+  }
+  const int target = ceil_div(total, 8);
+  for (int e = 0; e < L.E; ++e) {
+    auto& home = xl[e % 8];
+    for (int l = NHID; l >= 0; --l) {
+      const int K = l == 0 ? L.IN : L.H, N = l == NHID ? 2 * L.D : L.H;
+      for (int tm = 0; tm < ceil_div(K, TW2_T); ++tm)
+        for (int tn = 0; tn < ceil_div(N, TW2_T); ++tn) {
+          const int32_t v = l | (e << 3) | (tm << 7) | (tn << 12);
+          if ((int)home.size() < target) home.push_back(v);
+          else over.push_back(v);
+        }
+    }
+  }
+  for (int32_t v : over) {
+    int best = 0;
+    for (int x = 1; x < 8; ++x)
+      if (xl[x].size() < xl[best].size()) best = x;
+    xl[best].push_back(v);
+  }
+  int per = 1;
+  for (auto& v : xl) per = std::max(per, (int)v.size());
+  std::vector<int32_t> host((size_t)8 * per + 8, -1);
+  for (int x = 0; x < 8; ++x) {
+    std::copy(xl[x].begin(), xl[x].end(), host.begin() + (size_t)x * per);
+    host[(size_t)8 * per + x] = (int32_t)xl[x].size();
+  }
+  if (hipMalloc(&h->wlist, host.size() * 4) != hipSuccess) return fail("bnn train: out of device memory (tile list)");
+  h->wcnt = h->wlist + (size_t)8 * per;
+  h->wl_per_x = per;
+  MOPO_HIP(hipMemcpy(h->wlist, host.data(), host.size() * 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
+// threads per tile workgroup (MOPO_TRAIN_WG2_NT: 512, two per CU; or 1024, one per CU) and tile
+// workgroups per XCD (MOPO_TRAIN_WG2_NWX; default: the CUs' resident workgroups)
+int train_wg2_nt() {
+  static const int v = [] {
+    const char* e = std::getenv("MOPO_TRAIN_WG2_NT");
+    return e && std::atoi(e) == 1024 ? 1024 : 512;
+  }();
+  return v;
+}
+int train_wg2_nwx() {
+  static const int v = [] {
+    const char* e = std::getenv("MOPO_TRAIN_WG2_NWX");
+    return e ? std::max(1, std::atoi(e)) : 64;   // two workgroups per CU (LDS: 2 x 66.5 KB)
+  }();
+  return v;
+}
+
 #ifndef MOPO_TRAIN_FUSED
 #define MOPO_TRAIN_FUSED 1  // forward + backward rows in one launch, the loss tail in the weight-gradient launch
 #endif
@@ -473,6 +748,31 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
     MOPO_TRF(2, 13, 3) MOPO_TRF(1, 13, 2) MOPO_TRF(1, 2, 2) MOPO_TRF(2, 2, 3) MOPO_TRF(2, 16, 3) MOPO_TRF(1, 16, 2)
     return fail("bnn train: no row-block instantiation for these widths (use_rows)");
 #undef MOPO_TRF
+    if (train_wg2()) {
+      TrainWg2 g{};
+      g.M = M;
+      g.nwx = train_wg2_nwx();
+      g.per_x = h->wl_per_x;
+      g.list = h->wlist;
+      g.cnt = h->wcnt;
+      for (int l = 0; l <= NHID; ++l) {
+        g.K[l] = l == 0 ? IN : H;
+        g.N[l] = l == NHID ? D2 : H;
+        g.A[l] = l == 0 ? h->X : h->Hh[l - 1];
+        g.B[l] = l == NHID ? h->dOUT : h->dZ[l];
+        g.W[l] = L.W[l];
+        g.b[l] = L.b[l];
+        g.wd[l] = WDECAY[l];
+      }
+      g.ad = ad;
+      TrainTail& t = g.t;
+      t.E = E; t.nrb = a.nrb; t.D = D; t.lpart = h->lpart; t.mx = L.mx; t.mn = L.mn;
+      t.logs = h->logs; t.beta_pow = h->beta_pow; t.bstep_inc = a.bstep_inc; t.lr = h->lr; t.G = h->G; t.ad = ad;
+      if (train_wg2_nt() == 1024) hipLaunchKernelGGL(train_wgrad2_kernel<1024>, dim3(8 * g.nwx + 1), dim3(1024), 0, s, g);
+      else hipLaunchKernelGGL(train_wgrad2_kernel<512>, dim3(8 * g.nwx + 1), dim3(512), 0, s, g);
+      MOPO_HIP(hipGetLastError());
+      return 0;
+    }
     TrainWgrad g{};
     g.n = NHID + 1;
     g.ad = ad;
@@ -599,6 +899,7 @@ extern "C" int mopo_bnn_train_create(mopo_bnn_train_t* out, int E, int obs_dim, 
   for (auto& r : reg) { *r.first = m; m += (r.second + 255) & ~(size_t)255; }
   const float bp[3] = {0.9f, 0.999f, 0.f};
   MOPO_HIP(hipMemcpy(h->beta_pow, bp, sizeof(bp), hipMemcpyHostToDevice));
+  if (build_wlist(h)) { (void)hipFree(h->mem); delete h; return -1; }
   std::vector<float> one(L.IN, 1.f);
   MOPO_HIP(hipMemcpy(h->sigma, one.data(), L.IN * 4, hipMemcpyHostToDevice));
   *out = reinterpret_cast<mopo_bnn_train_t>(h);
@@ -613,6 +914,7 @@ extern "C" int mopo_bnn_train_destroy(mopo_bnn_train_t hh) {
   if (h->ev_out) (void)hipEventDestroy(h->ev_out);
   if (h->gs) (void)hipStreamDestroy(h->gs);
   if (h->sort_keys) (void)hipFree(h->sort_keys);  // one allocation (keys | values | offsets | temp)
+  if (h->wlist) (void)hipFree(h->wlist);
   if (h->mem) (void)hipFree(h->mem);
   delete h;
   return 0;
