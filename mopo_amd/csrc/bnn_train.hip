@@ -666,6 +666,11 @@ int build_wlist(Train* h) {
     total += L.E * ceil_div(K, TW2_T) * ceil_div(N, TW2_T);
   }
   const int target = ceil_div(total, 8);
+  static const int order = [] {   // MOPO_TRAIN_WG2_ORDER=1: tiles dealt round-robin, no member -> XCD grouping (A/B)
+    const char* e = std::getenv("MOPO_TRAIN_WG2_ORDER");
+    return e ? std::atoi(e) : 0;
+  }();
+  int rr = 0;
   for (int e = 0; e < L.E; ++e) {
     auto& home = xl[e % 8];
     for (int l = NHID; l >= 0; --l) {
@@ -673,7 +678,8 @@ int build_wlist(Train* h) {
       for (int tm = 0; tm < ceil_div(K, TW2_T); ++tm)
         for (int tn = 0; tn < ceil_div(N, TW2_T); ++tn) {
           const int32_t v = l | (e << 3) | (tm << 7) | (tn << 12);
-          if ((int)home.size() < target) home.push_back(v);
+          if (order == 1) xl[rr++ % 8].push_back(v);
+          else if ((int)home.size() < target) home.push_back(v);
           else over.push_back(v);
         }
     }
