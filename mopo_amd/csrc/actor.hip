@@ -293,10 +293,11 @@ __device__ __forceinline__ void actor_finish(const ActorArgs& a, float (&head)[A
 // TQ0: k-steps in the last k-group of the observation (tail_steps(O); 4 = all)
 template <int KG0, int NBP, int TQ0 = 4>
 #ifndef ACT_F32_OCC
-// fp32 actor workgroups per CU at H = 256.  4 caps the kernel at 128 VGPRs and spilled 22-26 of them (88 B
-// of scratch per lane); 3 needs no scratch, runs 0.101 vs 0.092 ms per 50k rows alone and the fp32 rollout
-// the same or faster (59.2 vs 58.9M transitions/s, same-box A/B, profiles/r04_actor_ab.txt)
-#define ACT_F32_OCC 3
+// fp32 actor waves per SIMD at H = 256 (launch bound).  4 caps the kernel at 128 VGPRs and spilled 22-26 of
+// them (88 B of scratch per lane); 3 (168 VGPRs) still spills 10-11 (44-48 B); 2 holds its 178 VGPRs with
+// no scratch.  Measured at 4 / 3: 0.092 / 0.101 ms per 50k rows alone, the fp32 rollout 58.9 / 59.2M
+// transitions/s (same-box A/B, profiles/r04_actor_ab.txt)
+#define ACT_F32_OCC 2
 #endif
 __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? ACT_F32_OCC : 2) void actor_kernel(const ActorArgs a) {
   constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;

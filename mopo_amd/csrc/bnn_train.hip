@@ -639,7 +639,6 @@ static __global__ __launch_bounds__(NT, NT / 128) void train_wgrad2_kernel(const
     lds_barrier();                                   // the partials are read before the next panels land
     i = inx;
     cur = nx;
-#pragma unroll
     for (int h = 0; h < C::NE; ++h) a_in[h] = a_nx[h];
     c_in = c_nx;
   }

@@ -11,42 +11,40 @@ namespace mopo {
 
 constexpr int MAXD = 32;
 
+// Every per-row quantity is re-read from the (L1/L2-resident) inputs where it is used instead of being
+// held in per-thread arrays indexed by the runtime D: such arrays live in scratch (528 B per lane).
 __global__ __launch_bounds__(256) void fakeenv_post_kernel(const mopo_fakeenv_args a, int E, int O, int A) {
   const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (b >= a.B) return;
   const int D = O + 1;
   const int64_t B = a.B;
-  double obs[MAXD];
-  for (int d = 0; d < O; ++d)
-    obs[d] = a.obs_f64 ? reinterpret_cast<const double*>(a.d_obs)[b * O + d]
-                       : (double)reinterpret_cast<const float*>(a.d_obs)[b * O + d];
+  auto obs_at = [&](int d) -> double {
+    return a.obs_f64 ? reinterpret_cast<const double*>(a.d_obs)[b * O + d]
+                     : (double)reinterpret_cast<const float*>(a.d_obs)[b * O + d];
+  };
   auto mean_at = [&](int e, int d) -> float {  // fake_env.py:66 (f64 add, stored back to f32)
     float m = a.d_ens_mean[((int64_t)e * B + b) * D + d];
-    return d >= 1 ? (float)((double)m + obs[d - 1]) : m;
+    return d >= 1 ? (float)((double)m + obs_at(d - 1)) : m;
   };
-  double sample[MAXD];
-  float mmean[MAXD], mstd[MAXD];
-  if (!a.deterministic) {
-    const int sel = (int)a.d_model_inds[b];  // bnn.py:343 / fake_env.py:77-81
-    for (int d = 0; d < D; ++d) {
-      float m = mean_at(sel, d);
-      float s = sqrtf(a.d_ens_var[((int64_t)sel * B + b) * D + d]);
-      mmean[d] = m;
-      mstd[d] = s;
-      sample[d] = (double)m + a.d_noise_sel[b * D + d] * (double)s;  // fake_env.py:72 (f64)
-    }
-  } else {  // fake_env.py:69-70, 84-86: plain f32 means over all members
-    for (int d = 0; d < D; ++d) {
-      float sm = 0.f, ss = 0.f;
-      for (int e = 0; e < E; ++e) {
-        sm += mean_at(e, d);
-        ss += sqrtf(a.d_ens_var[((int64_t)e * B + b) * D + d]);
-      }
-      mmean[d] = sm / (float)E;
-      mstd[d] = ss / (float)E;
-      sample[d] = (double)mmean[d];
-    }
-  }
+  auto var_at = [&](int e, int d) -> float { return a.d_ens_var[((int64_t)e * B + b) * D + d]; };
+  const int sel = a.deterministic ? 0 : (int)a.d_model_inds[b];  // bnn.py:343 / fake_env.py:77-81
+  // the selected mean / std (fake_env.py:77-81) or, deterministic, the plain f32 member means (:69-70, 84-86)
+  auto mmean_at = [&](int d) -> float {
+    if (!a.deterministic) return mean_at(sel, d);
+    float sm = 0.f;
+    for (int e = 0; e < E; ++e) sm += mean_at(e, d);
+    return sm / (float)E;
+  };
+  auto mstd_at = [&](int d) -> float {
+    if (!a.deterministic) return sqrtf(var_at(sel, d));
+    float ss = 0.f;
+    for (int e = 0; e < E; ++e) ss += sqrtf(var_at(e, d));
+    return ss / (float)E;
+  };
+  auto sample_at = [&](int d) -> double {  // fake_env.py:72 (f64); deterministic: the mean
+    if (a.deterministic) return (double)mmean_at(d);
+    return (double)mean_at(sel, d) + a.d_noise_sel[b * D + d] * (double)sqrtf(var_at(sel, d));
+  };
   // _get_logprob (fake_env.py:20-35): log-sum-exp over ALL members, naive exp then log
   if (a.d_log_prob || a.d_dev) {
     double prob = 0.0;
@@ -54,9 +52,9 @@ __global__ __launch_bounds__(256) void fakeenv_post_kernel(const mopo_fakeenv_ar
     for (int e = 0; e < E; ++e) {
       double slv = 0.0, sq = 0.0;
       for (int d = 0; d < D; ++d) {
-        float v = a.d_ens_var[((int64_t)e * B + b) * D + d];
+        float v = var_at(e, d);
         slv += (double)logf(v);
-        double df = sample[d] - (double)mean_at(e, d);
+        double df = sample_at(d) - (double)mean_at(e, d);
         sq += df * df / (double)v;
       }
       prob += exp(-0.5 * (k_log2pi + slv + sq));
@@ -79,7 +77,7 @@ __global__ __launch_bounds__(256) void fakeenv_post_kernel(const mopo_fakeenv_ar
     }
   }
   // termination on the f64 next_obs (fake_env.py:90-91)
-  const bool term = term_fn(a.term_kind, sample + 1, O);
+  const bool term = term_fn_at(a.term_kind, [&](int d) { return sample_at(d + 1); }, O);
   // penalty (fake_env.py:97-115)
   float pen = 0.f;
   if (a.penalty_coeff != 0.f) {
@@ -87,31 +85,27 @@ __global__ __launch_bounds__(256) void fakeenv_post_kernel(const mopo_fakeenv_ar
       for (int e = 0; e < E; ++e) {
         float s2 = 0.f;
         for (int d = 0; d < D; ++d) {
-          float s = sqrtf(a.d_ens_var[((int64_t)e * B + b) * D + d]);
+          float s = sqrtf(var_at(e, d));
           s2 += s * s;
         }
         pen = fmaxf(pen, sqrtf(s2));
       }
-    } else {
-      float mu[MAXD];
-      for (int d = 1; d < D; ++d) {
-        float sm = 0.f;
-        for (int e = 0; e < E; ++e) sm += mean_at(e, d);
-        mu[d] = sm / (float)E;
-      }
+    } else {  // max over members of || mean_e - mean over members || over the obs dims
       for (int e = 0; e < E; ++e) {
         float s2 = 0.f;
         for (int d = 1; d < D; ++d) {
-          float df = mean_at(e, d) - mu[d];
+          float sm = 0.f;
+          for (int f = 0; f < E; ++f) sm += mean_at(f, d);
+          const float df = mean_at(e, d) - sm / (float)E;
           s2 += df * df;
         }
         pen = fmaxf(pen, sqrtf(s2));
       }
     }
   }
-  const double rew = sample[0];
+  const double rew = sample_at(0);
   const double pen_rew = a.penalty_coeff != 0.f ? rew - (double)a.penalty_coeff * (double)pen : rew;
-  for (int d = 0; d < O; ++d) a.d_next_obs[b * O + d] = sample[d + 1];
+  for (int d = 0; d < O; ++d) a.d_next_obs[b * O + d] = sample_at(d + 1);
   a.d_rewards[b] = pen_rew;
   a.d_terminals[b] = term ? 1 : 0;
   if (a.d_penalty) a.d_penalty[b] = pen;
@@ -119,9 +113,9 @@ __global__ __launch_bounds__(256) void fakeenv_post_kernel(const mopo_fakeenv_ar
   if (a.d_info_mean) {  // fake_env.py:94-95
     float* im = a.d_info_mean + b * (D + 1);
     float* is = a.d_info_std + b * (D + 1);
-    im[0] = mmean[0]; im[1] = term ? 1.f : 0.f;
-    is[0] = mstd[0]; is[1] = 0.f;
-    for (int d = 1; d < D; ++d) { im[d + 1] = mmean[d]; is[d + 1] = mstd[d]; }
+    im[0] = mmean_at(0); im[1] = term ? 1.f : 0.f;
+    is[0] = mstd_at(0); is[1] = 0.f;
+    for (int d = 1; d < D; ++d) { im[d + 1] = mmean_at(d); is[d + 1] = mstd_at(d); }
   }
   (void)A;
 }

@@ -86,24 +86,30 @@ int launch_bnn_fwd(const Bnn* h, int mode, const FwdArgs& a, hipStream_t s);
 int pack_frags(const float* src, float* dst, int E, int K, int N, int KG, int NB, hipStream_t s, int perm_k = 0);
 
 // termination kinds (mopo/static)
-__device__ __forceinline__ bool term_fn(int kind, const double* nobs, int O) {
+// nobs: next_obs[d] for d < O -- an array or any accessor callable with d
+template <class F>
+__device__ __forceinline__ bool term_fn_at(int kind, const F& nobs, int O) {
   if (kind == MOPO_TERM_WALKER2D) {  // walker2d.py:10-16
-    double hh = nobs[0], an = nobs[1];
+    double hh = nobs(0), an = nobs(1);
     bool not_done = (hh > 0.8) && (hh < 2.0) && (an > -1.0) && (an < 1.0);
     return !not_done;
   }
   if (kind == MOPO_TERM_HOPPER) {  // hopper.py:10-17 (np.abs(bool) == bool)
     bool fin = true, small = true;
     for (int d = 0; d < O; ++d) {
-      double v = nobs[d];
+      double v = nobs(d);
       fin = fin && isfinite(v);
       if (d >= 1) small = small && (v < 100.0);
     }
-    double hh = nobs[0], an = nobs[1];
+    double hh = nobs(0), an = nobs(1);
     bool not_done = fin && small && (hh > 0.7) && (fabs(an) < 0.2);
     return !not_done;
   }
   return false;  // halfcheetah.py:9-10
+}
+
+__device__ __forceinline__ bool term_fn(int kind, const double* nobs, int O) {
+  return term_fn_at(kind, [&](int d) { return nobs[d]; }, O);
 }
 
 }  // namespace mopo
