@@ -191,6 +191,11 @@ int mopo_bnn_train_snapshot(mopo_bnn_train_t h, int member, void* stream);
 int mopo_bnn_train_restore(mopo_bnn_train_t h, void* stream);
 /* h_logs[0] = data term of the last minibatch's training loss. */
 int mopo_bnn_train_logs(mopo_bnn_train_t h, float* h_logs, int n);
+/* Host only (no device call): the per-XCD tile lists of the training step's weight-gradient launch.
+ * Writes 8 lists of `per` packed tiles (layer | member << 3 | tile row << 7 | tile column << 12, -1 padded)
+ * followed by the 8 list lengths into out (8 per + 8 ints; out may be NULL) and returns per (< 0: error).
+ * No reference counterpart: a layout detail of bnn.py:425-432's minibatch op on this device. */
+int mopo_bnn_train_tile_lists(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap);
 
 /* ---- fused model rollout (MOPO._rollout_model) ----------------------------------------- */
 typedef struct mopo_rollout_s* mopo_rollout_t;

@@ -655,25 +655,21 @@ int train_wg2() {
 
 // tiles of member e to XCD e mod 8 up to ceil(total / 8) per XCD, the rest to the least-loaded XCDs; within
 // an XCD in (member, layer NHID .. 0, tile row, tile column) order, so a round's workgroups share panels
-int build_wlist(Train* h) {
-  const Layout& L = h->L;
+// host image: [8][per] tile lists (-1 padded) then the 8 counts; *per = the list stride
+std::vector<int32_t> make_wlist(int E, int IN, int H, int D, int order, int* per_out) {
   std::vector<std::vector<int32_t>> xl(8);
   std::vector<int32_t> over;
   int total = 0;
   for (int l = 0; l <= NHID; ++l) {
-    const int K = l == 0 ? L.IN : L.H, N = l == NHID ? 2 * L.D : L.H;
-    total += L.E * ceil_div(K, TW2_T) * ceil_div(N, TW2_T);
+    const int K = l == 0 ? IN : H, N = l == NHID ? 2 * D : H;
+    total += E * ceil_div(K, TW2_T) * ceil_div(N, TW2_T);
   }
   const int target = ceil_div(total, 8);
-  static const int order = [] {   // MOPO_TRAIN_WG2_ORDER=1: tiles dealt round-robin, no member -> XCD grouping (A/B)
-    const char* e = std::getenv("MOPO_TRAIN_WG2_ORDER");
-    return e ? std::atoi(e) : 0;
-  }();
   int rr = 0;
-  for (int e = 0; e < L.E; ++e) {
+  for (int e = 0; e < E; ++e) {
     auto& home = xl[e % 8];
     for (int l = NHID; l >= 0; --l) {
-      const int K = l == 0 ? L.IN : L.H, N = l == NHID ? 2 * L.D : L.H;
+      const int K = l == 0 ? IN : H, N = l == NHID ? 2 * D : H;
       for (int tm = 0; tm < ceil_div(K, TW2_T); ++tm)
         for (int tn = 0; tn < ceil_div(N, TW2_T); ++tn) {
           const int32_t v = l | (e << 3) | (tm << 7) | (tn << 12);
@@ -696,6 +692,18 @@ int build_wlist(Train* h) {
     std::copy(xl[x].begin(), xl[x].end(), host.begin() + (size_t)x * per);
     host[(size_t)8 * per + x] = (int32_t)xl[x].size();
   }
+  *per_out = per;
+  return host;
+}
+
+int build_wlist(Train* h) {
+  const Layout& L = h->L;
+  static const int order = [] {   // MOPO_TRAIN_WG2_ORDER=1: tiles dealt round-robin, no member -> XCD grouping (A/B)
+    const char* e = std::getenv("MOPO_TRAIN_WG2_ORDER");
+    return e ? std::atoi(e) : 0;
+  }();
+  int per = 0;
+  const std::vector<int32_t> host = make_wlist(L.E, L.IN, L.H, L.D, order, &per);
   if (hipMalloc(&h->wlist, host.size() * 4) != hipSuccess) return fail("bnn train: out of device memory (tile list)");
   h->wcnt = h->wlist + (size_t)8 * per;
   h->wl_per_x = per;
@@ -909,6 +917,19 @@ extern "C" int mopo_bnn_train_create(mopo_bnn_train_t* out, int E, int obs_dim, 
   MOPO_HIP(hipMemcpy(h->sigma, one.data(), L.IN * 4, hipMemcpyHostToDevice));
   *out = reinterpret_cast<mopo_bnn_train_t>(h);
   return 0;
+}
+
+// host only (no device call): the weight-gradient launch's per-XCD tile lists, for tests and tools
+extern "C" int mopo_bnn_train_tile_lists(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap) {
+  MOPO_REQUIRE(E >= 1 && E <= 16 && obs_dim >= 1 && act_dim >= 1 && hidden >= 1 && obs_dim + 1 <= 64,
+               "mopo_bnn_train_tile_lists: bad dims");
+  int per = 0;
+  const std::vector<int32_t> host = make_wlist(E, obs_dim + act_dim, hidden, obs_dim + 1, 0, &per);
+  if (out) {
+    MOPO_REQUIRE(cap >= (int64_t)host.size(), "mopo_bnn_train_tile_lists: output too small (8 per + 8 ints)");
+    std::copy(host.begin(), host.end(), out);
+  }
+  return per;
 }
 
 extern "C" int mopo_bnn_train_destroy(mopo_bnn_train_t hh) {
