@@ -88,7 +88,7 @@ typedef struct {
   int penalty_learned_var;  /* 1: max_e ||std_e||  0: max_e ||mean_e - mean|| (fake_env.py:98-110) */
   int term_kind;            /* MOPO_TERM_* */
   /* outputs (device) */
-  double* d_next_obs;       /* [B, O] f64 */
+  double* d_next_obs;       /* [B, O] f64; must not alias d_obs */
   double* d_rewards;        /* [B] penalized rewards f64 */
   uint8_t* d_terminals;     /* [B] */
   float* d_penalty;         /* [B] f32, may be NULL */

@@ -977,27 +977,20 @@ static int launch_ring(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   a.ntiles = (int)ceil_div((int)a.B, 16);
   if (a.ntiles == 0) return 0;
   dim3 grid(8 * ceil_div(ceil_div(a.ntiles, WV), 8) * h->E), block(64 * WV);
-  if constexpr (NB2 == 14) {  // H = 200: an odd hidden-block count, the last block is padding (NBU = 13)
-    if (h->dev.NBH == NB2 - 1) {
-      if (mode == FWD_PREDICT)
-        hipLaunchKernelGGL((bnn_fwd_ring_kernel<NB2, NBO, FWD_PREDICT, WV, P, DEPTH, NB2 - 1>), grid, block, 0, s, h->dev, a);
-      else
-        hipLaunchKernelGGL((bnn_fwd_ring_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, DEPTH, NB2 - 1>), grid, block, 0, s, h->dev, a);
-      MOPO_HIP(hipGetLastError());
-      return 0;
-    }
-  }
+  // NB2 = 14 is H = 200 only: an odd hidden-block count, the last block is padding (NBU = 13); the
+  // whole-block NB2 = 14 form (H = 209..224, no config) is not instantiated (it spilled 8-12 B)
+  constexpr int NBU = NB2 == 14 ? NB2 - 1 : NB2;
   if (mode == FWD_PREDICT) {
-    hipLaunchKernelGGL((bnn_fwd_ring_kernel<NB2, NBO, FWD_PREDICT, WV, P, DEPTH>), grid, block, 0, s, h->dev, a);
+    hipLaunchKernelGGL((bnn_fwd_ring_kernel<NB2, NBO, FWD_PREDICT, WV, P, DEPTH, NBU>), grid, block, 0, s, h->dev, a);
   } else {
-    hipLaunchKernelGGL((bnn_fwd_ring_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, DEPTH>), grid, block, 0, s, h->dev, a);
+    hipLaunchKernelGGL((bnn_fwd_ring_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, DEPTH, NBU>), grid, block, 0, s, h->dev, a);
   }
   MOPO_HIP(hipGetLastError());
   return 0;
 }
-// the ring kernel's shapes: H = 200 (NB2 14, 13 used), or a whole even block count (NBH = NB2)
+// the ring kernel's shapes: H = 200 (NB2 14, 13 used), or a whole even block count (NBH = NB2) other than 14
 template <int NB2>
-static bool ring_shape(const Bnn* h) { return NB2 <= 16 && (h->dev.NBH == NB2 || (NB2 == 14 && h->dev.NBH == 13)); }
+static bool ring_shape(const Bnn* h) { return NB2 <= 16 && (NB2 == 14 ? h->dev.NBH == 13 : h->dev.NBH == NB2); }
 
 #ifndef BNN_R13
 #define BNN_R13 1  // row blocks per wave at H = 200
@@ -1060,7 +1053,14 @@ static int launch_bf16_p(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   dim3 grid(ceil_div(a.ntiles, WV) * h->E), block(64 * WV);
   // odd hidden-block count (e.g. H = 200): the last block is padding and is skipped (NBU = NB2 - 1); not at
   // H = 400 (25 of 26), where the skipping variant takes 256 VGPRs and spills
-  if (NB2 <= 16 && h->dev.NBH == NB2 - 1) {
+  // NB2 = 14: H = 200 only (13 blocks used); the whole-block form is not instantiated (it spilled 8-12 B)
+  if constexpr (NB2 == 14) {
+    if (h->dev.NBH != NB2 - 1) return fail("bnn bf16: unsupported hidden size (H in (192, 224] runs at H <= 208 only)");
+    if (mode == FWD_PREDICT)
+      hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_PREDICT, WV, P, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+    else
+      hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_ROLLOUT, WV, P, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
+  } else if (NB2 <= 16 && h->dev.NBH == NB2 - 1) {
     if constexpr (NB2 <= 16) {
       if (mode == FWD_PREDICT)
         hipLaunchKernelGGL((bnn_fwd_bf16_kernel<NB2, NBO, FWD_PREDICT, WV, P, PS, NB2 - 1>), grid, block, 0, s, h->dev, a);
@@ -1199,6 +1199,11 @@ extern "C" int mopo_bnn_create(mopo_bnn_t* out, int E, int obs_dim, int act_dim,
   d.NBO = ceil_div(2 * d.D, 16);
   d.NB2 = (d.NBH + 1) / 2 * 2;
   d.BS = d.NB2 * 16;
+  if (dtype != 0 && d.NB2 == 14 && d.NBH != 13) {   // the 16-bit kernels' NB2 = 14 shape is H = 200's 13 blocks
+    delete h;
+    return fail("mopo_bnn_create: the 16-bit dtypes do not support hidden sizes 209..224 (got " +
+                std::to_string(hidden) + "; use fp32)");
+  }
   if (dtype == 3 && d.NB2 > 16) {   // launch_bf16_t: no bf16x6 kernel above H = 256
     delete h;
     return fail("mopo_bnn_create: bf16x6 supports hidden sizes <= 256 (use f16x3 or fp32)");

@@ -923,6 +923,10 @@ extern "C" int mopo_bnn_train_create(mopo_bnn_train_t* out, int E, int obs_dim, 
 extern "C" int mopo_bnn_train_tile_lists(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap) {
   MOPO_REQUIRE(E >= 1 && E <= 16 && obs_dim >= 1 && act_dim >= 1 && hidden >= 1 && obs_dim + 1 <= 64,
                "mopo_bnn_train_tile_lists: bad dims");
+  // a packed tile id holds the tile row and column in 5 bits each (make_wlist): K, N <= 32 tiles of 32
+  MOPO_REQUIRE(ceil_div(obs_dim + act_dim, TW2_T) <= 32 && ceil_div(hidden, TW2_T) <= 32 &&
+               ceil_div(2 * (obs_dim + 1), TW2_T) <= 32,
+               "mopo_bnn_train_tile_lists: hidden and obs_dim + act_dim must be <= 1024 (5-bit tile ids)");
   int per = 0;
   const std::vector<int32_t> host = make_wlist(E, obs_dim + act_dim, hidden, obs_dim + 1, 0, &per);
   if (out) {

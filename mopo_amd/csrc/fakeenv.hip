@@ -134,6 +134,8 @@ extern "C" int mopo_fakeenv_step(mopo_bnn_t hh, const mopo_fakeenv_args* a, void
   MOPO_REQUIRE(a->deterministic || (a->d_noise_sel && a->d_model_inds),
                "mopo_fakeenv_step: noise and model_inds required unless deterministic");
   MOPO_REQUIRE(a->d_next_obs && a->d_rewards && a->d_terminals, "mopo_fakeenv_step: NULL output");
+  // the post kernel re-reads a row's obs (info_mean / info_std) after storing its next_obs
+  MOPO_REQUIRE((const void*)a->d_next_obs != a->d_obs, "mopo_fakeenv_step: d_next_obs must not alias d_obs");
   MOPO_REQUIRE(!a->d_info_mean == !a->d_info_std, "mopo_fakeenv_step: info_mean/info_std go together");
   hipStream_t s = (hipStream_t)stream;
   FwdArgs f{};

@@ -172,16 +172,18 @@ def broadcast_model(model, src=0, group=None):
     n_flat = sum(z.size for z in model._mat_shapes())
     if rank == src:
         hl = getattr(model, '_holdout_losses', None)
-        hl = np.full(model.num_nets, np.nan) if hl is None else np.asarray(hl, np.float64)
-        host = torch.from_numpy(np.concatenate([model.flat_params().astype(np.float64), hl])).to(dev)
+        has = np.array([0.0 if hl is None else 1.0])   # a has-holdout flag: None stays None on every rank
+        hl = np.zeros(model.num_nets) if hl is None else np.asarray(hl, np.float64)
+        host = torch.from_numpy(np.concatenate([model.flat_params().astype(np.float64), hl, has])).to(dev)
     else:
-        host = torch.empty(n_flat + model.num_nets, dtype=torch.float64, device=dev)
+        host = torch.empty(n_flat + model.num_nets + 1, dtype=torch.float64, device=dev)
     dist.broadcast(buf, src, group=group)
     dist.broadcast(el, src, group=group)
     dist.broadcast(host, src, group=group)
     if rank != src:
         h = host.cpu().numpy()
-        model.import_packed(buf, mats=model.unflatten_params(h[:n_flat]), holdout_losses=h[n_flat:])
+        hl = h[n_flat:n_flat + model.num_nets] if h[-1] != 0 else None
+        model.import_packed(buf, mats=model.unflatten_params(h[:n_flat]), holdout_losses=hl)
         model.set_elites(el.cpu().tolist())
     torch.cuda.current_stream().synchronize()
 

@@ -1,0 +1,71 @@
+#!/bin/bash
+# One gpurun call, any sequence of steps (each under its own time limit; the call stops at the first
+# failing step):
+#   tests       the whole -m gpu suite                                  -> gpurun_out/pytest_gpu.log
+#   tests:EXPR  the -m gpu tests selected by -k EXPR                    -> gpurun_out/pytest_k.log
+#   bench       the default bench line                                  -> gpurun_out/bench_full.json
+#   profile     kernel traces + PMC passes of every leg (gpu_profile.sh) -> gpurun_out/prof_$TAG/
+#   probe       XCD placement / L2 persistence probe (scripts/micro/xcc_probe)
+#   ab          headline A/B over abv/<v>.so for v in $AB (scripts/ab.sh)
+#   sac_ab      SAC parity on each abv/<v>.so of $AB, then the step-time A/B (scripts/ab_sac.sh)
+#   train_ab    BNN.train parity, then the train leg under each env setting of $VARS
+#   stamps      SAC phase stamps from abv/sac_stamps.so (scripts/sac_stamps.py)
+# usage: bash scripts/gpu.sh tests bench ;  AB="new old" bash scripts/gpu.sh sac_ab
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+PYT="python -u -m pytest -p no:cacheprovider --timeout 300 --timeout-method thread"
+keep() { cp mopo_amd/libmopo_hip.so /tmp/lib_keep.so; }
+restore() { cp /tmp/lib_keep.so mopo_amd/libmopo_hip.so; }
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 1100 $PYT tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+      tail -4 gpurun_out/pytest_gpu.log ;;
+    tests:*)
+      timeout -k 10 900 $PYT tests -m gpu -x -q -k "${step#tests:}" > gpurun_out/pytest_k.log 2>&1; rc=$?
+      tail -4 gpurun_out/pytest_k.log ;;
+    bench)
+      timeout -k 10 400 python bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err; rc=$?
+      [ $rc -eq 0 ] && python scripts/bench_brief.py gpurun_out/bench_full.json || tail -5 gpurun_out/bench_full.err ;;
+    profile)
+      bash scripts/gpu_profile.sh; rc=$? ;;
+    probe)
+      timeout -k 10 60 ./scripts/micro/xcc_probe > gpurun_out/xcc_probe.txt 2>&1; rc=$?
+      cat gpurun_out/xcc_probe.txt ;;
+    ab)
+      keep; bash scripts/ab.sh; rc=$?; restore ;;
+    sac_ab)
+      keep; rc=0
+      for v in $AB; do
+        cp abv/$v.so mopo_amd/libmopo_hip.so
+        timeout -k 10 300 $PYT tests/test_gpu_sac.py tests/test_gpu_ref.py -q -x -k "sac or SAC" > gpurun_out/sac_tests_$v.log 2>&1
+        rc=$?; echo "== $v parity rc=$rc: $(tail -1 gpurun_out/sac_tests_$v.log)"
+        [ $rc -ne 0 ] && break
+      done
+      [ $rc -eq 0 ] && { AB="$AB_EXTRA $AB" bash scripts/ab_sac.sh; rc=$?; }
+      restore ;;
+    train_ab)
+      timeout -k 10 300 $PYT tests/test_gpu_train.py -q -x > gpurun_out/train_tests.log 2>&1; rc=$?
+      tail -3 gpurun_out/train_tests.log
+      if [ $rc -eq 0 ]; then
+        : > gpurun_out/ab_train.txt
+        for i in 1 2; do
+          for v in ${VARS:-"MOPO_TRAIN_WG2=1 MOPO_TRAIN_WG2=0"}; do
+            env ${v//,/ } timeout -k 10 200 python bench.py --no-cpu-baseline --no-c3 --no-alt-dtypes --sac-steps 16 --steps 3 \
+              --warmup 1 --train-epochs 3 > gpurun_out/abt_cur.json 2> gpurun_out/abt_cur.err || { rc=1; tail -5 gpurun_out/abt_cur.err; break 2; }
+            python -c "import json; d=json.load(open('gpurun_out/abt_cur.json')); t=d['model_train']; print('$v', round(t['value']), 'steps/s', round(t['ms_per_epoch'], 2), 'ms/epoch')" >> gpurun_out/ab_train.txt
+          done
+        done
+        cat gpurun_out/ab_train.txt
+      fi ;;
+    stamps)
+      keep; cp abv/sac_stamps.so mopo_amd/libmopo_hip.so
+      timeout -k 10 120 python scripts/sac_stamps.py > gpurun_out/sac_stamps.txt 2>&1; rc=$?
+      restore; cat gpurun_out/sac_stamps.txt ;;
+    *) echo "unknown step $step"; rc=2 ;;
+  esac
+  echo "== step $step rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+done
+exit 0

@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run, --kernel-trace only besides --pmc) over a short
-# bench: HBM bytes (FETCH_SIZE, WRITE_SIZE separately, per MI355X_MICROARCH.md §HBM) and MFMA busy.
+# bench: HBM bytes (FETCH_SIZE, WRITE_SIZE separately, per MI355X_MICROARCH.md §HBM), MFMA busy, wait share,
+# L2 hit rate and the VALU / MFMA / LDS instruction mix.
 # usage: scripts/pmc.sh OUT.json [extra bench.py args selecting the workload, e.g. --ensemble-dtype fp32]
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD
@@ -15,7 +16,8 @@ TAG=$(echo "$KEY" | tr ' =' '__')
 export MOPO_ROLLOUT_SPLIT=1
 cd /tmp
 i=0
-for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" "SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY"; do
+for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" "SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY" \
+         "TCC_HIT_sum TCC_MISS_sum SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"; do
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_$TAG/pmc$i" -o run -- python "$R/bench.py" $ARGS > "$R/gpurun_out/pmc_${TAG}_$i.log" 2>&1
   rc=$?
