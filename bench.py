@@ -69,8 +69,9 @@ def parse():
     p.add_argument('--horizon', type=int, default=5)
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-batch', type=int, default=10000,
-                   help='rows of the C2 CPU-baseline rollout sample (the headline workload at fewer rows; each of '
-                        'the 6 runs takes a few seconds)')
+                   help='rows of the C2 CPU-baseline rollout sample (the headline workload at fewer rows, labelled '
+                        'as a sample in the bench line; each of the 6 runs takes a few seconds; 50000 = the whole '
+                        'config, about a minute)')
     p.add_argument('--sac-steps', type=int, default=1000)
     p.add_argument('--cpu-sac-steps', type=int, default=1000)
     p.add_argument('--no-c3', action='store_true', help='skip the secondary C3 (bf16 walker2d) line')
@@ -240,18 +241,23 @@ def cpu_baseline(args):
     penalty and env-pool size; fewer rows, so the default bench stays within minutes)."""
     threads = blas_threads()
     legs = {}
-    for key, B, h, dom, pen, env_rows, what in (
-            ('C1', 1000, 1, 'halfcheetah', 1.0, 20000, 'halfcheetah_mixed plumbing config, B=1k, h=1'),
-            ('C2', args.cpu_batch, args.horizon, 'halfcheetah', 1.0, 20000, 'halfcheetah-mixed, B=50k, h=5'),
-            ('C3', 20000, 1, 'walker2d', 1.0, 20000, 'walker2d-medium-replay, B=100k, h=1 (fp32 on CPU)'),
-            ('C4', 5000, 5, 'halfcheetah', 5.0, 1000000, 'halfcheetah-medium-expert, penalty 5, 1e6-row env pool')):
+    # (config, sample rows, horizon, domain, penalty, env rows, config description, the config's own rows)
+    for key, B, h, dom, pen, env_rows, what, full in (
+            ('C1', 1000, 1, 'halfcheetah', 1.0, 20000, 'halfcheetah_mixed plumbing config, h=1', 1000),
+            ('C2', args.cpu_batch, args.horizon, 'halfcheetah', 1.0, 20000, 'halfcheetah-mixed, h=5', 50000),
+            ('C3', 20000, 1, 'walker2d', 1.0, 20000, 'walker2d-medium-replay, h=1 (fp32 on CPU)', 100000),
+            ('C4', 5000, 5, 'halfcheetah', 5.0, 1000000, 'halfcheetah-medium-expert, penalty 5, 1e6-row env pool, h=5',
+             400000)):
         med, runs, units, secs = median_runs(cpu_rollout_leg(B, h, dom, pen, env_rows))
+        scope = 'the whole config' if B == full else 'a sample of %d rollout rows (the config runs %d)' % (B, full)
         legs[key] = {'value': med, 'unit': 'transitions/s', 'runs': runs, 'median': med, 'cores': int(threads),
-                     'sample': '%s: B=%d, h=%d, E=%d, H=%d; %d timed runs (%d transitions in %.2f s) after 1 warm-up'
-                               % (what, B, h, E, H, CPU_RUNS, units, secs)}
+                     'rows_sampled': B, 'rows_config': full,
+                     'sample': '%s, E=%d, H=%d: %s; %d timed runs (%d transitions in %.2f s) after 1 warm-up'
+                               % (what, E, H, scope, CPU_RUNS, units, secs)}
     c2 = legs['C2']
     return {'value': c2['median'], 'unit': 'transitions/s', 'cores': int(threads), 'kind': 'port',
             'runs': c2['runs'], 'median': c2['median'],
+            'rows_sampled': c2['rows_sampled'], 'rows_config': c2['rows_config'],
             'sample': 'oracle numpy rollout (mopo.py:723-765 restated), ' + c2['sample'], 'configs': legs}
 
 
@@ -500,9 +506,10 @@ def sac_leg(args, pool, env, dev, world):
 
 
 def cpu_baseline_sac(args):
-    """Oracle SAC steps (numpy restatement of mopo.py:204-466, 834-853) on the host, BASELINE.md section 3:
-    ``cpu_sac_steps`` (1000) consecutive steps at batch 256, timed as 5 runs of a fifth each after a
-    warm-up run; the median run's rate."""
+    """Oracle SAC steps (numpy restatement of mopo.py:204-466, 834-853) on the host: ``cpu_sac_steps``
+    (1000) consecutive steps at batch 256 on one SAC state, timed as 5 consecutive runs of a fifth each
+    after a warm-up run (a bounded sample: BASELINE.md section 3 asks for 5 runs of 1000 steps, about 40 s
+    here); the median run's rate."""
     from oracle import sac as osac
     rs = np.random.RandomState(0)
     st = osac.SACState(osac.init_params(O, A, HP, seed=2, dtype=np.float32))
@@ -521,8 +528,10 @@ def cpu_baseline_sac(args):
         return per, time.perf_counter() - t0
     med, runs, units, secs = median_runs(run)
     return {'value': med, 'unit': 'grad-steps/s', 'cores': blas_threads(), 'kind': 'port', 'runs': runs, 'median': med,
-            'sample': 'oracle numpy SAC step (fp32 arrays), batch 256: %d consecutive steps as %d timed runs of %d '
-                      '(%.2f s) after a warm-up run' % (units, CPU_RUNS, per, secs)}
+            'steps_consecutive': units, 'steps_per_run': per,
+            'sample': 'oracle numpy SAC step (fp32 arrays), batch 256: %d consecutive steps on one SAC state, timed as '
+                      '%d runs of %d (%.2f s) after a warm-up run of %d; BASELINE.md section 3 times 5 runs of 1000'
+                      % (units, CPU_RUNS, per, secs, per)}
 
 
 def main():

@@ -215,7 +215,7 @@ def broadcast_metrics(metrics, src=0, group=None):
 def broadcast_sac(sac, src=0, group=None):
     """The SAC state (params + log_alpha, targets, Adam m / v) from ``src`` to every rank."""
     import torch.distributed as dist
-    n = sac.n_params
+    n = sac._n_dev     # the raw device buffers (padded layout of a [H1, H2] network)
     parts = [(0, n + 1), (1, n), (2, n + 1), (3, n + 1)]
     buf = torch.cat([sac._copy(w, c) for w, c in parts])
     dist.broadcast(buf, src, group=group)

@@ -64,13 +64,11 @@ class MOPO:
         self._epoch = 0
         self._num_train_steps = 0
         self._seed = seed
-        hs = (network_kwargs or {}).get('hidden_sizes', [256, 256])
-        if len(hs) != 2 or hs[0] != hs[1]:
-            raise NotImplementedError('policy/Q hidden_sizes must be [H, H] (reference: [256, 256])')
-        self._sac = SAC(obs_dim, act_dim, hidden=hs[0], batch_size=batch_size, real_ratio=real_ratio, lr=lr,
+        hs = list((network_kwargs or {}).get('hidden_sizes', [256, 256]))   # mopo.py:275-280, base.py:60-66
+        self._sac = SAC(obs_dim, act_dim, hidden=hs, batch_size=batch_size, real_ratio=real_ratio, lr=lr,
                         discount=discount, tau=tau, reward_scale=reward_scale, target_entropy=target_entropy,
                         seed=seed, reparameterize=reparameterize, target_update_interval=target_update_interval)
-        self._pi_hidden = hs[0]
+        self._pi_hidden = self._sac.hidden   # the device width the rollout actor runs (rollout.device_hidden)
         self._rollout = None
         self._rollout_length = rollout_length
         # multi-GPU (torch.distributed initialised, one process per GPU): the rollout rows are sharded

@@ -16,15 +16,38 @@ import numpy as np
 from . import _lib as L
 
 
+def hidden_pair(H):
+    """The two hidden widths of the policy / Q MLPs (mopo.py:275-280, 311-325: ``hidden_sizes``): an int
+    H means [H, H]."""
+    if isinstance(H, (int, np.integer)):
+        return int(H), int(H)
+    hs = [int(x) for x in H]
+    if len(hs) != 2 or min(hs) < 1:
+        raise NotImplementedError('policy / Q hidden_sizes must be two widths [H1, H2] (got %r)' % (H,))
+    return hs[0], hs[1]
+
+
+def device_hidden(H):
+    """The square width the device kernels run a [H1, H2] network at: max(H1, H2) rounded up to 16.
+    A narrower layer is embedded with zero weights and biases, which is exact for the relu MLPs: a
+    padded unit is relu(0) = 0 forward, its relu mask is off backward, so its weights' gradients, Adam
+    moments and updates stay exactly 0 (and the Polyak average of zeros is 0)."""
+    h1, h2 = hidden_pair(H)
+    return (max(h1, h2) + 15) // 16 * 16
+
+
 def sac_param_shapes(O, A, H=256):
-    """Creation order of get_vars('main') (mopo.py:32-33, 298-324): pi, q1, q2 in TF [in,out] layout."""
-    pi = [(O, H), (H,), (H, H), (H,), (H, A), (A,), (H, A), (A,)]
-    q = [(O + A, H), (H,), (H, H), (H,), (H, 1), (1,)]
+    """Creation order of get_vars('main') (mopo.py:32-33, 298-324): pi, q1, q2 in TF [in,out] layout;
+    ``H`` an int or [H1, H2]."""
+    h1, h2 = hidden_pair(H)
+    pi = [(O, h1), (h1,), (h1, h2), (h2,), (h2, A), (A,), (h2, A), (A,)]
+    q = [(O + A, h1), (h1,), (h1, h2), (h2,), (h2, 1), (1,)]
     return pi + q + q
 
 
 def init_sac_params(O, A, H=256, seed=2):
-    """tf.layers.dense defaults: glorot_uniform kernels, zero biases; returns a flat float32 array."""
+    """tf.layers.dense defaults: glorot_uniform kernels, zero biases; returns a flat float32 array in
+    the [H1, H2] network's own layout."""
     rng = np.random.RandomState(seed)
     parts = []
     for shp in sac_param_shapes(O, A, H):
@@ -34,8 +57,26 @@ def init_sac_params(O, A, H=256, seed=2):
         else:
             parts.append(np.zeros(shp, np.float32))
     flat = np.concatenate(parts)
-    assert flat.size == L.lib().mopo_sac_param_count(O, A, H)
+    if hidden_pair(H)[0] == hidden_pair(H)[1]:
+        assert flat.size == L.lib().mopo_sac_param_count(O, A, hidden_pair(H)[0])
     return flat
+
+
+def sac_pad_index(O, A, H):
+    """Positions of a [H1, H2] network's flat parameters inside the flat layout of the square
+    device_hidden(H) network (each tensor's [:rows, :cols] corner); None when H is already square."""
+    h1, h2 = hidden_pair(H)
+    hd = device_hidden(H)
+    if h1 == h2 == hd:
+        return None
+    idx, off = [], 0
+    for ls, ds in zip(sac_param_shapes(O, A, (h1, h2)), sac_param_shapes(O, A, hd)):
+        if len(ls) == 2:
+            idx.append((off + np.arange(ls[0])[:, None] * ds[1] + np.arange(ls[1])[None, :]).ravel())
+        else:
+            idx.append(off + np.arange(ls[0]))
+        off += int(np.prod(ds))
+    return np.concatenate(idx).astype(np.int64)
 
 
 def split_params(flat, O, A, H=256):

@@ -16,7 +16,7 @@ from collections import OrderedDict
 import numpy as np
 
 from . import _lib as L
-from .rollout import init_sac_params
+from .rollout import device_hidden, hidden_pair, init_sac_params, sac_pad_index, sac_param_shapes
 
 LOG_KEYS = ['Q/q1_loss', 'sac_Q/q2_loss', 'sac_Q/q1', 'sac_Q/q2', 'sac_pi/alpha', 'sac_pi/pi_entropy',
             'sac_pi/logp_pi', 'sac_pi/pi_global_norm', 'sac_Q/q_global_norm', 'policy_loss']
@@ -32,7 +32,8 @@ def _space_dim(space):
 class SAC:
     """Two constructor forms:
 
-    * ``SAC(obs_dim, act_dim, hidden=256, ...)`` -- the dims directly;
+    * ``SAC(obs_dim, act_dim, hidden=256, ...)`` -- the dims directly (``hidden`` an int H for [H, H], or the
+      two widths [H1, H2] of mopo.py:275-280's ``hidden_sizes``);
     * ``SAC(training_environment, evaluation_environment, policy, Qs, pool, plotter=None,
       tf_summaries=False, lr=3e-4, reward_scale=1.0, target_entropy='auto', discount=0.99, tau=5e-3,
       target_update_interval=1, action_prior='uniform', reparameterize=False, store_extra_policy_info=False,
@@ -64,12 +65,10 @@ class SAC:
         for src in (policy, *(Qs or ())):
             hs = hs or getattr(src, 'hidden_layer_sizes', None) or getattr(src, '_hidden_layer_sizes', None) or \
                 getattr(src, 'hidden_sizes', None)
-        hs = list(hs or [256, 256])
-        if len(hs) != 2 or hs[0] != hs[1]:
-            raise NotImplementedError('policy / Q hidden sizes must be [H, H]')
+        hs = hidden_pair(list(hs or [256, 256]))
         self._training_environment, self._evaluation_environment = training_environment, evaluation_environment
         self._policy, self._Qs, self._pool, self._plotter = policy, Qs, pool, plotter
-        self._init(obs_dim, act_dim, hidden=hs[0], batch_size=batch_size, real_ratio=real_ratio, lr=lr,
+        self._init(obs_dim, act_dim, hidden=hs, batch_size=batch_size, real_ratio=real_ratio, lr=lr,
                    discount=discount, tau=tau, reward_scale=reward_scale, target_entropy=target_entropy,
                    reparameterize=reparameterize, target_update_interval=target_update_interval,
                    action_prior=action_prior, **kwargs)
@@ -80,7 +79,12 @@ class SAC:
         if not reparameterize:
             raise NotImplementedError('only the reparameterized policy loss is implemented (mopo.py:370-374; '
                                       'every config sets reparameterize=True, examples/config/d4rl/base.py)')
-        self.obs_dim, self.act_dim, self.hidden = obs_dim, act_dim, hidden
+        # a [H1, H2] network runs on the device as the square device_hidden() one with the narrower
+        # layer zero-padded (exact: rollout.device_hidden); every accessor speaks the [H1, H2] layout
+        self.hidden_sizes = hidden_pair(hidden)
+        self.obs_dim, self.act_dim, self.hidden = obs_dim, act_dim, device_hidden(hidden)
+        self._pad = sac_pad_index(obs_dim, act_dim, self.hidden_sizes)
+        self._pad_t = None
         self._pool = getattr(self, '_pool', None)
         self.batch_size = int(batch_size)
         self._real_ratio = real_ratio
@@ -92,13 +96,18 @@ class SAC:
             raise ValueError('target_update_interval must be >= 1')
         self._target_update_interval = int(target_update_interval)
         self._schedule = (0, 1, 1)       # the device's target schedule (mopo_sac_set_target_schedule)
-        flat = init_sac_params(obs_dim, act_dim, hidden, seed=seed) if params is None else \
-            np.ascontiguousarray(params, np.float32)
-        n = L.lib().mopo_sac_param_count(obs_dim, act_dim, hidden)
+        flat = init_sac_params(obs_dim, act_dim, self.hidden_sizes, seed=seed) if params is None else \
+            np.ascontiguousarray(params, np.float32).ravel()
+        n = sum(int(np.prod(s)) for s in sac_param_shapes(obs_dim, act_dim, self.hidden_sizes))
         if flat.size != n:
             raise ValueError('expected %d parameters, got %d' % (n, flat.size))
+        self._n_dev = L.lib().mopo_sac_param_count(obs_dim, act_dim, self.hidden)
+        if self._pad is not None:
+            dev_flat = np.zeros(self._n_dev, np.float32)
+            dev_flat[self._pad] = flat
+            flat = dev_flat
         h = C.c_void_p()
-        L.check(L.lib().mopo_sac_create(C.byref(h), obs_dim, act_dim, hidden, self.batch_size, self.n_env,
+        L.check(L.lib().mopo_sac_create(C.byref(h), obs_dim, act_dim, self.hidden, self.batch_size, self.n_env,
                                         flat.ctypes.data, float(log_alpha), float(lr), float(discount), float(tau),
                                         float(reward_scale), float(self._target_entropy)))
         self._h = h
@@ -122,37 +131,64 @@ class SAC:
 
     @property
     def policy_params_ptr(self):
-        """Device pointer of the live policy parameters (pi block at offset 0) for rollouts."""
+        """Device pointer of the live policy parameters (pi block at offset 0, the device_hidden layout)
+        for rollouts (run them with pi_hidden = self.hidden)."""
         return self._ptrs['params']
 
     def _copy(self, which, count, tensor=None, to_handle=False, stream=None):
+        """Raw copy of a device buffer (the device layout: self._n_dev parameters)."""
         import torch
         if tensor is None:
             tensor = torch.empty(count, dtype=torch.float32, device='cuda')
         L.check(L.lib().mopo_sac_copy(self._h, which, int(to_handle), L.ptr(tensor), count, L.stream_ptr(stream)))
         return tensor
 
+    def _index(self):
+        import torch
+        if self._pad_t is None:
+            self._pad_t = torch.from_numpy(self._pad).cuda()
+        return self._pad_t
+
+    def _get(self, which, extra):
+        """Buffer ``which`` in the [H1, H2] layout (+ ``extra`` trailing elements: log_alpha)."""
+        import torch
+        t = self._copy(which, self._n_dev + extra)
+        if self._pad is None:
+            return t
+        return torch.cat([t[self._index()], t[self._n_dev:]])
+
+    def _put(self, which, t, extra):
+        """Buffer ``which`` from the [H1, H2] layout; the padding stays 0."""
+        import torch
+        t = t.reshape(-1).float().contiguous()
+        if self._pad is not None:
+            d = torch.zeros(self._n_dev + extra, dtype=torch.float32, device=t.device)
+            d[self._index()] = t[:self.n_params]
+            d[self._n_dev:] = t[self.n_params:]
+            t = d
+        self._copy(which, self._n_dev + extra, t, to_handle=True)
+
     def get_params(self):
         """(flat params [n_params], log_alpha) as torch CUDA tensors (copies)."""
-        t = self._copy(0, self.n_params + 1)
+        t = self._get(0, 1)
         return t[:-1], t[-1]
 
     def get_target(self):
-        return self._copy(1, self.n_params)
+        return self._get(1, 0)
 
     def get_grads(self):
-        t = self._copy(4, self.n_params + 1)
+        t = self._get(4, 1)
         return t[:-1], t[-1]
 
     def get_adam(self):
-        return self._copy(2, self.n_params + 1), self._copy(3, self.n_params + 1)
+        return self._get(2, 1), self._get(3, 1)
 
     def set_params(self, flat, log_alpha=None):
         import torch
         t = torch.as_tensor(np.asarray(flat, np.float32) if not torch.is_tensor(flat) else flat).cuda().float()
         la = float(self.get_params()[1].item()) if log_alpha is None else float(log_alpha)
         t = torch.cat([t.reshape(-1), torch.tensor([la], device=t.device)])
-        self._copy(0, self.n_params + 1, t, to_handle=True)
+        self._put(0, t, 1)
 
     def logs(self):
         """Fetches of the last step (mopo.py:453-463 names, plus policy_loss); synchronises."""
@@ -226,15 +262,14 @@ class SAC:
         return self.logs()
 
     def state_dict(self):
-        """Device copies of everything a step reads (the saveables of sac.py:418-427 and the targets)."""
-        n = self.n_params
-        return {'params': self._copy(0, n + 1), 'target': self._copy(1, n), 'adam_m': self._copy(2, n + 1),
-                'adam_v': self._copy(3, n + 1)}
+        """Device copies of everything a step reads (the saveables of sac.py:418-427 and the targets), in
+        the [H1, H2] layout."""
+        return {'params': self._get(0, 1), 'target': self._get(1, 0), 'adam_m': self._get(2, 1),
+                'adam_v': self._get(3, 1)}
 
     def load_state_dict(self, state):
-        n = self.n_params
-        for w, (k, c) in enumerate((('params', n + 1), ('target', n), ('adam_m', n + 1), ('adam_v', n + 1))):
-            self._copy(w, c, state[k].contiguous(), to_handle=True)
+        for w, (k, x) in enumerate((('params', 1), ('target', 0), ('adam_m', 1), ('adam_v', 1))):
+            self._put(w, state[k], x)
 
     def _training_batch(self, env_pool, model_pool, batch_size=None, as_numpy=False):
         """mopo.py:801-821 as a host-visible batch (the device step assembles the same batch itself):

@@ -19,12 +19,19 @@ import numpy as np
 LOG_STD_MAX, LOG_STD_MIN, EPS = 2.0, -20.0, 1e-8          # mopo.py:271-273
 LOG2PI = np.log(2 * np.pi)
 
-PI_SHAPES = lambda O, A, H: [(O, H), (H,), (H, H), (H,), (H, A), (A,), (H, A), (A,)]
-Q_SHAPES = lambda O, A, H: [(O + A, H), (H,), (H, H), (H,), (H, 1), (1,)]
+def _hs(H):
+    """hidden_sizes (mopo.py:275-280): an int H is [H, H]."""
+    return (H, H) if np.isscalar(H) else tuple(H)
+
+
+PI_SHAPES = lambda O, A, H: [(O, _hs(H)[0]), (_hs(H)[0],), _hs(H), (_hs(H)[1],), (_hs(H)[1], A), (A,),
+                             (_hs(H)[1], A), (A,)]
+Q_SHAPES = lambda O, A, H: [(O + A, _hs(H)[0]), (_hs(H)[0],), _hs(H), (_hs(H)[1],), (_hs(H)[1], 1), (1,)]
 
 
 def param_shapes(O, A, H=256):
-    """Creation order of get_vars('main') (mopo.py:32-33): pi (dense..dense_3), q1, q2."""
+    """Creation order of get_vars('main') (mopo.py:32-33): pi (dense..dense_3), q1, q2; ``H`` an int or
+    the two hidden widths [H1, H2]."""
     return PI_SHAPES(O, A, H) + Q_SHAPES(O, A, H) + Q_SHAPES(O, A, H)
 
 

@@ -222,11 +222,13 @@ def test_training_batch_mirror():
         np.testing.assert_array_equal(np.asarray(got[k], np.float64), ref[k], err_msg=k)
 
 
-@pytest.mark.parametrize('o,a,h,n', [(11, 3, 32, 100), (17, 6, 64, 250), (8, 8, 256, 40)])
+@pytest.mark.parametrize('o,a,h,n', [(11, 3, 32, 100), (17, 6, 64, 250), (8, 8, 256, 40), (17, 6, (256, 128), 256),
+                                     (11, 3, (48, 200), 100)])
 def test_sac_one_step_gradients_odd_shapes(o, a, h, n):
     """One step's gradients at shapes the headline never uses: a batch that is not a multiple of 16
     (the policy-row blocks' and tiles' out-of-range rows), H < 256 (the policy-row MFMA's partial
-    K split, column tiles not divisible by the 8 XCDs) and A = 8 (the widest head)."""
+    K split, column tiles not divisible by the 8 XCDs), A = 8 (the widest head), and non-square
+    hidden_sizes [H1, H2] (mopo.py:275-280; run as the zero-padded square network, rollout.device_hidden)."""
     from mopo_amd.replay_pool import SimpleReplayPool
     from mopo_amd.sac import SAC
     import torch
@@ -320,3 +322,44 @@ def test_sac_normal_action_prior_one_step_vs_oracle():
         s2._do_training(0, env_p, mod_p, n_steps=3, seed=11)
         outs.append(s2.get_params()[0].cpu().numpy())
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_sac_nonsquare_hidden_steps_vs_oracle():
+    """hidden_sizes [256, 128] (mopo.py:275-280, 311-325) over 30 perf-mode steps (graph replay, device
+    Philox batches and noise) against the fp64 oracle run on the same restated streams (oracle/rng.py):
+    losses within 1e-3 relative at the last step, parameters / targets / Adam moments scaled error p99
+    <= 1e-4; and the zero padding of the device's square network stays exactly 0 in every buffer."""
+    import torch
+    from oracle import rng as orng
+    from mopo_amd.sac import SAC
+    hs = (256, 128)
+    rs = np.random.RandomState(12)
+    (env_p, env_op), (mod_p, mod_op) = pools(rs)
+    params = [p + rs.normal(size=p.shape) * 0.02 for p in osac.init_params(O, A, hs, seed=13)]
+    fl = flat(params).astype(np.float32)
+    sac = SAC(O, A, list(hs), batch_size=256, real_ratio=0.05, target_entropy=-3, params=fl)
+    assert sac.hidden == 256 and sac.hidden_sizes == hs and sac.n_params == fl.size
+    K, seed = 30, 77
+    sac._do_training(0, env_p, mod_p, n_steps=K, seed=seed)
+    torch.cuda.synchronize()
+    st = osac.SACState([p.astype(np.float32).astype(np.float64) for p in params])
+    for k in range(K):
+        idx = orng.sac_batch_indices(256, 12, env_p.size, mod_p.size, seed, k)
+        lg = osac.sac_step(st, host_batch(env_op, mod_op, idx), orng.sac_noise(256, A, seed, k, 0).astype(np.float64),
+                           orng.sac_noise(256, A, seed, k, 1).astype(np.float64), target_entropy=-3.0)
+    dl = sac.logs()
+    for dk, rk in (('Q/q1_loss', 'Q/q1_loss'), ('sac_Q/q2_loss', 'sac_Q/q2_loss'), ('policy_loss', 'pi_loss')):
+        assert abs(dl[dk] - lg[rk]) <= 1e-3 * (1 + abs(lg[rk])), (dk, dl[dk], lg[rk])
+    dev = {k: v.cpu().numpy().astype(np.float64) for k, v in sac.state_dict().items()}
+    ref = {'params': np.append(flat(st.params), st.log_alpha), 'target': flat(st.target),
+           'adam_m': np.concatenate([flat(st.opt_pi.m), flat(st.opt_q1.m), flat(st.opt_q2.m), flat(st.opt_a.m)]),
+           'adam_v': np.concatenate([flat(st.opt_pi.v), flat(st.opt_q1.v), flat(st.opt_q2.v), flat(st.opt_a.v)])}
+    for k in ref:
+        err = np.abs(dev[k] - ref[k]) / (1 + np.abs(ref[k]))
+        assert np.quantile(err, 0.99) <= 1e-4 and err.max() <= 1e-2, (k, np.quantile(err, 0.99), err.max())
+    # the raw device buffers: everything outside the [H1, H2] corner of each tensor is exactly zero
+    pad = np.ones(sac._n_dev, bool)
+    pad[sac._pad] = False
+    for w, extra in ((0, 1), (1, 0), (2, 1), (3, 1), (4, 1)):
+        raw = sac._copy(w, sac._n_dev + extra).cpu().numpy()[:sac._n_dev]
+        assert np.all(raw[pad] == 0), (w, np.abs(raw[pad]).max())
