@@ -18,6 +18,7 @@
 // pre-step parameters), beside the batch loss tail (logs, the alpha update, the step counter).
 #include <vector>
 #include <cstring>
+#include <cstdlib>
 
 #define MOPO_GEMM_KERNELS 0   // the grouped-GEMM kernels are bnn_train.hip's; this file uses the helpers only
 #include "sac_wgrad.h"
@@ -74,6 +75,8 @@ struct Sac {
   float *opart[8];                // [ncq][n][OPW] output-layer partials of the 8 instances (sac_rows.h)
   float *dapart[2];               // [ncq][n][OPW] action-gradient partials of Q1 / Q2 at (s, pi(s))
   uint64_t* stamps = nullptr;     // MOPO_SAC_STAMPS builds: [slot][block][8]
+  unsigned* sync = nullptr;       // fused F2 + B1 launch: [nrb][2] row-block counters, then the timeout word
+  bool fuse = true;               // F2 and B1 as one launch (sac_f2b1_kernel)
   float *dhead, *dh2p, *dh1p;
   // graph
   bool use_graph = true;
@@ -164,6 +167,14 @@ static int launch_gather(Sac* h, int par, const mopo_pool_desc* env, const mopo_
 // One SAC step on batch bt[par], reading parameters Pb[par] and writing the updated ones to
 // Pb[1 - par].  With `prefetch`, B1 also gathers the next step's batch into bt[1 - par] (a separate
 // gather launch, or a forked graph branch, costs more than it hides).
+#ifndef MOPO_SAC_FUSE
+#define MOPO_SAC_FUSE 1   // default of the fused F2 + B1 launch; the environment variable MOPO_SAC_FUSE overrides it
+#endif
+static bool sac_fuse_default() {
+  const char* e = std::getenv("MOPO_SAC_FUSE");
+  return e ? std::atoi(e) != 0 : MOPO_SAC_FUSE != 0;
+}
+
 static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
                          const float* eps_in_s, const float* eps_in_n, hipStream_t s, bool prefetch) {
   const SacDims& d = h->d;
@@ -209,13 +220,15 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     f.hd.iter = h->iter; f.hd.seed = seed; f.hd.eps_out[0] = h->eps_s; f.hd.eps_out[1] = h->eps_n;
     f.hd.gen_eps = (eps_in_s ? 0 : 1) | (eps_in_n ? 0 : 2);   // the heads whose noise is not injected
     f.st = Stamps{h->stamps, 0};
+    if (h->fuse) { f.sync_reset = h->sync; f.n_sync = 2 * nrb; }   // this step's F2 -> B1 counters
     hipLaunchKernelGGL(sac_fwd_kernel<false>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
     MOPO_HIP(hipGetLastError());
   }
   // ---- F2: the policy head from F1's partials -> Q1/Q2(s, pi(s)) (main), Qt1/Qt2(s', pi(s')) (target);
   //      the main critics' blocks also emit their action-gradient partials (dq = 1)
+  FwdArgsR f2{};
   {
-    FwdArgsR f{};
+    FwdArgsR& f = f2;
     f.ninst = 4; f.n = n; f.H = H; f.A = A; f.ncq = ncq; f.nrb = nrb;
     for (int i = 0; i < 4; ++i) {
       const int qi = i & 1;
@@ -236,8 +249,11 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     hd.head_out[0] = h->out[0]; hd.head_out[1] = h->out[1]; hd.logp[0] = h->logp_s; hd.logp[1] = h->logp_n;
     hd.seed = seed; hd.iter = h->iter;
     f.st = Stamps{h->stamps, 1};
-    hipLaunchKernelGGL(sac_fwd_kernel<true>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
-    MOPO_HIP(hipGetLastError());
+    f.sync = h->sync;
+    if (!h->fuse) {
+      hipLaunchKernelGGL(sac_fwd_kernel<true>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
+      MOPO_HIP(hipGetLastError());
+    }
   }
   // ---- B1: per-row TD targets and dq -> Q1/Q2(s,a) dh1; the policy's row-local backward chain; the
   //      step control; the gather of the next step's batch (with `prefetch`)
@@ -257,7 +273,9 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     pr.dapart[0] = h->dapart[0]; pr.dapart[1] = h->dapart[1];
     pr.qpart[0] = h->opart[4]; pr.qpart[1] = h->opart[5];
     pr.b3[0] = Wq(0, 5); pr.b3[1] = Wq(1, 5);
-    pr.head_s = h->out[0]; pr.eps_s = h->eps_s; pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
+    // the policy noise of pi(s): F1's draws, or the injected array itself (F2's copy of it is not handed over)
+    pr.head_s = h->out[0]; pr.eps_s = eps_in_s ? eps_in_s : h->eps_s;
+    pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
     pr.h2p = h->h2[0]; pr.h1p = h->h1[0]; pr.W2p = P + o.pW2;
     pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p; pr.prior = h->prior;
     d.gather = prefetch ? 1 : 0;
@@ -265,9 +283,15 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       d.ga = gather_args(h, 1 - par, env, mod, seed, nullptr);
       d.ga.iter_add = 1;                       // the next step's batch (the counter advances in B2)
     }
-    d.st = Stamps{h->stamps, 2};
+    d.st = Stamps{h->stamps, h->fuse ? 1 : 2};
+    d.sync = h->sync;
     if (ncq1 * nrb < 2 && prefetch) return fail("sac: B1 needs at least one gather block");
-    hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq1, nrb, 4), dim3(B1_WAVES * 64), 0, s, d);
+    if (h->fuse) {
+      static_assert(B1_COLS == RB_COLS && B1_WAVES == 4, "the fused F2 + B1 launch shares the F2 grid");
+      hipLaunchKernelGGL(sac_f2b1_kernel, dim3(ncq, nrb, 8), dim3(256), 0, s, f2, d);
+    } else {
+      hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq1, nrb, 4), dim3(B1_WAVES * 64), 0, s, d);
+    }
     MOPO_HIP(hipGetLastError());
   }
   // ---- B2: every weight gradient with its fused TF1 Adam (+ Polyak for the critics), beside the batch
@@ -302,6 +326,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     g.ad.slot0 = 0;
     g.L = L; g.A = A; g.ncq = ncq; g.tent = h->tent; g.logs = h->logs; g.iter = h->iter;
     g.prior = h->prior; g.eps_s = h->eps_s;
+    g.sync_tmo = h->fuse ? h->sync + 2 * nrb : nullptr;
     g.st = Stamps{h->stamps, 3};
     if (tot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
     h->nslots = tot;
@@ -341,7 +366,8 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   std::vector<std::pair<void**, size_t>> reg;
   auto f = [&](float** p, size_t cnt) { reg.push_back({(void**)p, cnt * 4}); };
   f(&h->Pb[1], tot); f(&h->norm_part, 2 * (size_t)h->nslots_cap);
-  const size_t npart = (size_t)ceil_div(H, RB_COLS) * n * OPW;
+  const int64_t ns = (n + 15) / 16 * 16;   // per-row records padded to whole row blocks (sac_rows.h rows_ns)
+  const size_t npart = (size_t)ceil_div(H, RB_COLS) * ns * OPW;
   for (int i = 0; i < 8; ++i) f(&h->opart[i], npart);
   for (int i = 0; i < 2; ++i) f(&h->dapart[i], npart);
 #if MOPO_SAC_STAMPS
@@ -357,7 +383,9 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
     reg.push_back({(void**)&t.idx, (size_t)n * 8});
   }
   for (int i = 0; i < 8; ++i) { f(&h->h1[i], n * H); f(&h->h2[i], n * H); f(&h->out[i], n * 2 * A); }
-  f(&h->logp_s, n); f(&h->logp_n, n); f(&h->eps_s, n * A); f(&h->eps_n, n * A);
+  f(&h->logp_s, 2 * ns); f(&h->logp_n, 2 * ns); f(&h->eps_s, n * A); f(&h->eps_n, n * A);
+  reg.push_back({(void**)&h->sync, (size_t)(2 * (ns / 16) + 4) * 4});
+  h->fuse = sac_fuse_default();
   for (int i = 0; i < 4; ++i) { f(&h->dq[i], n); f(&h->dh1[i], n * H); }
   f(&h->dhead, n * 2 * A); f(&h->dh2p, n * H); f(&h->dh1p, n * H);
   size_t total = 0;

@@ -91,6 +91,49 @@ constexpr int DPW = 8;               // ... of the action-gradient partials (A <
 constexpr int MAX_NCQ = 4;           // column blocks of 64 (H <= 256)
 constexpr int DH2_TILES = 4;         // dh2p column tiles per wave (H <= 256 over >= 4 waves)
 
+// Row-block-exclusive layouts of everything F2 hands to B1 (so the fused F2 + B1 launch, sac_f2b1_kernel, can
+// hand it over in-launch): every 128-B line holds ONE 16-row block's values, so no workgroup ever caches a line
+// of a row block whose producers have not finished.  Per-row records are strided by ns = n rounded up to 16.
+static __device__ __forceinline__ int rows_ns(int n) { return (n + 15) & ~15; }
+// a critic's output-layer partial of (column block cq, row r): [nrb][ncq][16]
+static __device__ __forceinline__ int qp_idx(int cq, int r, int ncq) { return ((r >> 4) * ncq + cq) * 16 + (r & 15); }
+// a head's log-prob of row r: [nrb][32] (the second half of each 128-B line unused)
+static __device__ __forceinline__ int lp_idx(int r) { return (r >> 4) * 32 + (r & 15); }
+// a store the fused launch hands over in-launch: write-through (sc1), drained before the row block's counter add
+template <bool SC1>
+static __device__ __forceinline__ void hstore(float* p, float v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+// ---- in-launch hand-off of the fused F2 + B1 launch (cdna_hip_programming.md Guideline 16, R1 form): the
+// producer's payload stores are write-through, every wave drains them, the workgroup barrier, then ONE lane's
+// agent-scope add to its row block's counter; the consumer polls that word (one lane, relaxed), then ONE agent
+// acquire, the drain and the workgroup barrier before the plain loads of the handed-off rows.  A consumer only
+// ever waits on producers with lower workgroup ids (all of them are dispatched first), and every spin is bounded:
+// on a give-up it sets the sticky timeout word, which the loss tail turns into NaN logs.
+constexpr unsigned SAC_SPIN_LIMIT = 1u << 19;
+static __device__ __forceinline__ void handoff_signal(unsigned* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+static __device__ __forceinline__ void handoff_wait(unsigned* cnt, unsigned target, unsigned* tmo) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > SAC_SPIN_LIMIT) {
+        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
 struct PolicyRows {
   int n, O, A, H, ncq;
   const float* dapart[2];            // Q1 / Q2 at (s, pi(s)): [ncq][n][DPW] partials of dh1 W1[O:]^T (dq = 1)
@@ -113,8 +156,12 @@ struct PolicyRows {
 // block pays one memory latency, then computes.
 // S: >= 16 (H + 4) floats of LDS; hs: >= 3 * 128 floats.  Blocks of 4 or 8 waves (64 or 128 dh1p
 // columns).  H % 16 == 0, H <= 256 (one dh2p column per thread), A <= 8.
+// FUSED (sac_f2b1_kernel): the operands of earlier launches are issued first, then the block waits for its
+// row block's F2 producers (*cnt >= target) and loads what they handed over.
+template <bool FUSED = false>
 static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs,
-                                                         const Stamps& st) {
+                                                         const Stamps& st, unsigned* cnt = nullptr,
+                                                         unsigned target = 0, unsigned* tmo = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int H = c.H, A = c.A, HS = H + 4, n = c.n;
   const int pcols = 16 * (int)(blockDim.x >> 6);   // dh1p columns of the block: one 16-wide tile per wave
@@ -125,25 +172,31 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   //      the dh1p tile and the h1p mask, the critics' partials
   const int hr = tid >> 3, hj = tid & 7, hrow = r0 + hr;
   const bool hon = tid < 128 && hj < A && hrow < n;
-  const auto dh = rsrc(c.head_s, (int64_t)n * 2 * A), de = rsrc(c.eps_s, (int64_t)n * A);
-  const float mu = bload(dh, hon ? hrow * 2 * A + hj : -1);
-  const float raw = bload(dh, hon ? hrow * 2 * A + A + hj : -1);
-  const float ep = bload(de, hon ? hrow * A + hj : -1);
-  const float la = *c.log_alpha;
+  const int ns = rows_ns(n);
+  float mu, raw, ep;
   float qv[2][MAX_NCQ];                // Q1 / Q2(s, pi) partials of this thread's row: the chain's first link
   float dap[2][MAX_NCQ];
+  auto handed = [&]() {                // what F2 wrote: head, critic partials, action-gradient partials
+    const auto dh = rsrc(c.head_s, (int64_t)n * 2 * A), de = rsrc(c.eps_s, (int64_t)n * A);
+    mu = bload(dh, hon ? hrow * 2 * A + hj : -1);
+    raw = bload(dh, hon ? hrow * 2 * A + A + hj : -1);
+    ep = bload(de, hon ? hrow * A + hj : -1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const auto dq = rsrc(c.qpart[i], (int64_t)c.ncq * ns);
+      const auto dp = rsrc(c.dapart[i], (int64_t)c.ncq * ns * DPW);
+#pragma unroll
+      for (int q = 0; q < MAX_NCQ; ++q) {
+        qv[i][q] = bload(dq, (hon && q < c.ncq) ? qp_idx(q, hrow, c.ncq) : -1);
+        dap[i][q] = bload(dp, (hon && q < c.ncq) ? (q * ns + hrow) * DPW + hj : -1);
+      }
+    }
+  };
+  if constexpr (!FUSED) handed();
+  const float la = *c.log_alpha;
   float b3v[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const auto dq = rsrc(c.qpart[i], (int64_t)c.ncq * n);
-    const auto dp = rsrc(c.dapart[i], (int64_t)c.ncq * n * DPW);
-#pragma unroll
-    for (int q = 0; q < MAX_NCQ; ++q) {
-      qv[i][q] = bload(dq, (hon && q < c.ncq) ? q * n + hrow : -1);
-      dap[i][q] = bload(dp, (hon && q < c.ncq) ? (q * n + hrow) * DPW + hj : -1);
-    }
-    b3v[i] = *c.b3[i];
-  }
+  for (int i = 0; i < 2; ++i) b3v[i] = *c.b3[i];
   // dh2p tiles of this wave: 16 columns each, tiles w, w + nw, ... (at most DH2_TILES)
   const int nw = (int)(blockDim.x >> 6), nt2 = (H + 15) >> 4;
   const auto dwm = rsrc(c.Wm, (int64_t)H * A), dwl = rsrc(c.Wl, (int64_t)H * A), dh2 = rsrc(c.h2p, (int64_t)n * H);
@@ -173,6 +226,10 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   float m1[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
+  if constexpr (FUSED) {
+    handoff_wait(cnt, target, tmo);
+    handed();
+  }
   stamp(st, 1);
   // ---- squashed-Gaussian head backward (mopo.py:282-308 differentiated; pi_loss mopo.py:371-377)
   float* dmu_s = hs + 128;
@@ -296,6 +353,8 @@ struct FwdArgsR {
   FwdInst in[4];
   FwdHead hd;
   Stamps st;
+  unsigned* sync;                    // fused F2 + B1: [nrb][2] counters (policy / target instances) + timeout
+  unsigned* sync_reset; int n_sync;  // F1: block (0, 0, 0) zeroes the step's counters
 };
 
 // the head of row r, action j (8 lanes per row; every lane of the 8 calls both halves): the loads (issued
@@ -320,11 +379,12 @@ static __device__ __forceinline__ HeadIn rows_head_load(const FwdHead& h, int nx
                                                         int j, bool ok) {
   HeadIn o;
   const bool on = ok && j < A;
-  const auto dp = rsrc(h.opart[nxt], (int64_t)ncq * n * OPW);
+  const int ns = rows_ns(n);
+  const auto dp = rsrc(h.opart[nxt], (int64_t)ncq * ns * OPW);
 #pragma unroll
   for (int c = 0; c < MAX_NCQ; ++c) {     // unconditional loads (out-of-range ones return 0)
-    o.pm[c] = bload(dp, (on && c < ncq) ? (c * n + r) * OPW + j : -1);
-    o.pl[c] = bload(dp, (on && c < ncq) ? (c * n + r) * OPW + A + j : -1);
+    o.pm[c] = bload(dp, (on && c < ncq) ? (c * ns + r) * OPW + j : -1);
+    o.pl[c] = bload(dp, (on && c < ncq) ? (c * ns + r) * OPW + A + j : -1);
   }
   o.bm = bload(rsrc(h.bm, A), on ? j : -1);
   o.bl = bload(rsrc(h.bl, A), on ? j : -1);
@@ -333,6 +393,7 @@ static __device__ __forceinline__ HeadIn rows_head_load(const FwdHead& h, int nx
   return o;
 }
 
+template <bool SC1>
 static __device__ __forceinline__ float rows_head(const FwdHead& h, const HeadIn& in, int nxt, int A, int r, int j,
                                                   bool ok, bool store) {
   const bool on = ok && j < A;
@@ -353,15 +414,15 @@ static __device__ __forceinline__ float rows_head(const FwdHead& h, const HeadIn
         - 2.f * (0.6931471805599453f - u - softplusf(-2.f * u));    // squash correction (:292)
     act = tanhf(u);
     if (store) {
-      if (h.eps_in[nxt]) h.eps_out[nxt][r * A + j] = z;
-      h.head_out[nxt][r * 2 * A + j] = mu;
-      h.head_out[nxt][r * 2 * A + A + j] = raw;
+      if (h.eps_in[nxt]) h.eps_out[nxt][r * A + j] = z;     // (B1 reads the injected noise itself)
+      hstore<SC1>(&h.head_out[nxt][r * 2 * A + j], mu);
+      hstore<SC1>(&h.head_out[nxt][r * 2 * A + A + j], raw);
     }
   }
   v += __shfl_xor(v, 1);
   v += __shfl_xor(v, 2);
   v += __shfl_xor(v, 4);
-  if (store && ok && j == 0) h.logp[nxt][r] = v;
+  if (store && ok && j == 0) hstore<SC1>(&h.logp[nxt][lp_idx(r)], v);
   return act;
 }
 
@@ -404,10 +465,11 @@ static __device__ __forceinline__ void rows_contract(const float* As, const f32x
 }
 
 // wave 0: partial output dots of the block's tile, Out[r][j] = sum_{c < COLS} T[r][c] WT[j][c] (COLS / 4
-// MFMAs; row stride COLS + 4); rows r < n and j < nout are stored to part[row][ldp]
-template <int COLS>
+// MFMAs; row stride COLS + 4); rows r < n and j < nout are stored: a critic's (nout == 1) at qp_idx, the
+// policy's to opart[cq][row][OPW] (row stride rows_ns(n))
+template <int COLS, bool SC1>
 static __device__ __forceinline__ void rows_partial_out(const float* T, const float* WT, int li, int lk, int i0, int n,
-                                                        int nout, int ldp, float* part) {
+                                                        int nout, int cq, int ncq, float* opart) {
   constexpr int LD = COLS + 4;
   f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
@@ -421,7 +483,7 @@ static __device__ __forceinline__ void rows_partial_out(const float* T, const fl
     const int orow = i0 + 4 * lk + rr;
     if (li < nout && orow < n) {
       const float v = acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr];
-      part[(int64_t)orow * ldp + li] = v;
+      hstore<SC1>(opart + (nout == 1 ? qp_idx(cq, orow, ncq) : ((int64_t)cq * rows_ns(n) + orow) * OPW + li), v);
     }
   }
 }
@@ -456,21 +518,31 @@ static __device__ __forceinline__ void step7_loads(const FwdInst& p, int w, int 
   }
 }
 
-// Grid (column block, row block, instance): linear block id cq + ncq (rb + nrb ii).  H <= GKC, H % 16 == 0.
-template <bool HEAD>
-static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a) {
-  __shared__ __attribute__((aligned(16))) float As[RB_LDS_A];
-  __shared__ __attribute__((aligned(16))) float Ts[RB_LDS_T];
-  __shared__ __attribute__((aligned(16))) float Wo[RB_LDS_T];
-  __shared__ float act_s[16][8];
-  __shared__ float da_s[4][16][9];
+// LDS of one forward row-block workgroup (F1 / F2)
+struct FwdLds {
+  float As[RB_LDS_A];
+  float Ts[RB_LDS_T];
+  float Wo[RB_LDS_T];
+  float act_s[16][8];
+  float da_s[4][16][9];
+};
+
+// One forward row-block workgroup: column block cq, row block rb, instance ii (grid indices, SGPRs: the
+// instance's fields then come from the kernel arguments by scalar loads -- a divided linear index made them
+// VGPRs, and every buffer descriptor built from them needed a waterfall loop).  H <= GKC, H % 16 == 0.
+// FUSED (F2 inside sac_f2b1_kernel): every store B1 reads is write-through, and the block ends by signalling
+// its row block's counter.
+template <bool HEAD, bool FUSED>
+static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int rb, int ii, FwdLds& L) {
+  float* As = L.As;
+  float* Ts = L.Ts;
+  float* Wo = L.Wo;
+  auto& act_s = L.act_s;
+  auto& da_s = L.da_s;
   stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // grid (ncq, nrb, ninst): the indices are SGPRs, so the instance's fields come from the kernel
-  // arguments by scalar loads (a divided linear index made them VGPRs: every buffer descriptor built
-  // from them then needed a waterfall loop)
-  const int ii = blockIdx.z, rb = blockIdx.y, cq = blockIdx.x;
   const FwdInst p = pick4(a.in, ii);
+  if (!HEAD && a.sync_reset && cq == 0 && rb == 0 && ii == 0 && tid < a.n_sync) a.sync_reset[tid] = 0u;
   const int n = a.n, H = a.H, A = a.A;
   const int i0 = rb * 16, c0 = cq * RB_COLS, jw = c0 + w * 16;
   // ---- 0. F2: the head's operands first (the head is the first link of this launch's chain)
@@ -542,7 +614,7 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
   if (HEAD) {
     if (tid < 128) {
       const bool store = cq == 0 && (ii == 0 || ii == 2);  // Q1(s,pi) / Qt1(s',pi') blocks publish the head
-      act_s[hr][hj] = rows_head(a.hd, hin, p.head, A, hrow, hj, hrow < n, store);
+      act_s[hr][hj] = rows_head<FUSED>(a.hd, hin, p.head, A, hrow, hj, hrow < n, store);
     }
     lds_barrier();
 #pragma unroll
@@ -605,10 +677,8 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
   }
   lds_barrier();
   // ---- 6. partial output dots of the block's 64 columns (wave 0, MFMA)
-  if (w == 0) {                     // a critic's records are 1 float (dense rows: the loss reads stay coalesced)
-    const int ldp = p.nout == 1 ? 1 : OPW;
-    rows_partial_out<RB_COLS>(Ts, Wo, li, lk, i0, n, p.nout, ldp, p.opart + (int64_t)cq * n * ldp);
-  }
+  if (w == 0)                       // a critic's records are 1 float, row-block-major (qp_idx)
+    rows_partial_out<RB_COLS, FUSED>(Ts, Wo, li, lk, i0, n, p.nout, cq, a.ncq, p.opart);
   // ---- 7. F2, Q1 / Q2 at (s, pi(s)): the critic's backward share of the block (dq = 1): wave w forms
   //         dh1 rows k in [64 w, 64 w + 64) of D(k, r) = sum_c W2[k][c0 + c] G(r, c), G = W3[c0 + c]
   //         (h2 > 0) (K = the block's 64 columns), masked by h1 > 0, then its partial of the action
@@ -652,11 +722,19 @@ static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a
       if (tid < 128) {                                       // waves' partials in wave order
         const int rr = tid >> 3, aa = tid & 7, orow = i0 + rr;
         const float v = da_s[0][rr][aa] + da_s[1][rr][aa] + da_s[2][rr][aa] + da_s[3][rr][aa];
-        if (aa < A && orow < n) p.dapart[((int64_t)cq * n + orow) * DPW + aa] = v;
+        if (aa < A && orow < n) hstore<FUSED>(&p.dapart[((int64_t)cq * rows_ns(n) + orow) * DPW + aa], v);
       }
     }
   }
+  if constexpr (FUSED) handoff_signal(a.sync + 2 * rb + (ii >= 2 ? 1 : 0));
   stamp(a.st, 4);
+}
+
+// Grid (column block, row block, instance): linear block id cq + ncq (rb + nrb ii).
+template <bool HEAD>
+static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a) {
+  __shared__ __attribute__((aligned(16))) FwdLds L;
+  fwd_block<HEAD, false>(a, blockIdx.x, blockIdx.y, blockIdx.z, L);
 }
 
 // ---- B1 -----------------------------------------------------------------------------------------
@@ -679,17 +757,18 @@ struct RowIn { float pv[6][MAX_NCQ]; float b3[6]; float la, rew, term, logp_n; }
 
 static __device__ __forceinline__ RowIn row_losses_load(const LossRows& L, int n, int ncq, int r, bool on) {
   RowIn o;
+  const int ns = rows_ns(n);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    const auto dp = rsrc(L.qpart[i], (int64_t)ncq * n);
+    const auto dp = rsrc(L.qpart[i], (int64_t)ncq * ns);
 #pragma unroll
-    for (int c = 0; c < MAX_NCQ; ++c) o.pv[i][c] = bload(dp, (on && c < ncq) ? c * n + r : -1);
+    for (int c = 0; c < MAX_NCQ; ++c) o.pv[i][c] = bload(dp, (on && c < ncq) ? qp_idx(c, r, ncq) : -1);
     o.b3[i] = *L.b3[i];
   }
   o.la = *L.log_alpha;
   o.rew = bload(rsrc(L.rew, n), on ? r : -1);
   o.term = bload(rsrc(L.term, n), on ? r : -1);
-  o.logp_n = bload(rsrc(L.logp_n, n), on ? r : -1);
+  o.logp_n = bload(rsrc(L.logp_n, 2 * ns), on ? lp_idx(r) : -1);
   return o;
 }
 
@@ -738,6 +817,7 @@ struct Dh1Args {
   int gather;                        // 1: the other z = 0 blocks gather the next step's batch (ga)
   GatherArgs ga;
   Stamps st;
+  unsigned* sync;                    // fused F2 + B1: the F2 counters ([nrb][2]) and the timeout word [2 nrb]
 };
 
 // Block 0: the step's scalar control -- TF1 Adam's step size from the beta powers (every Adam of the step
@@ -756,41 +836,54 @@ static __device__ __forceinline__ void step_control(const Dh1Args& a) {
   a.beta_pow[3] = ((ts % every) + every) % every == 0 ? 1.f : 0.f;
 }
 
-// Grid (column block, row block, 4): z = 0: block (0, 0) the step control, the other blocks the gather of
-// the next step's batch; z = 1, 2: Q1 / Q2(s, a) dh1 tiles; z = 3: the policy-row blocks.
-// B1 runs 8-wave workgroups (16 rows x 128 columns), one per CU.
-static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const Dh1Args a) {
-  __shared__ __attribute__((aligned(16))) float As[RB_LDS_A];
-  __shared__ __attribute__((aligned(16))) float Ts[16 * B1_TLD];
-  __shared__ float dqs[16];
+// LDS of one B1 workgroup
+struct Dh1Lds {
+  float As[RB_LDS_A];
+  float Ts[16 * B1_TLD];
+  float dqs[16];
+};
+
+// One B1 workgroup (grid indices x = column block, y = row block, z): z = 0: block (0, 0) the step control,
+// the other blocks the gather of the next step's batch; z = 1, 2: Q1 / Q2(s, a) dh1 tiles; z = 3: the
+// policy-row blocks.  FUSED (inside sac_f2b1_kernel): the z = 1..3 blocks issue the operands of earlier
+// launches, then wait for their row block's F2 producers before loading what F2 wrote.
+template <bool FUSED>
+static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y, int z, Dh1Lds& S) {
+  float* As = S.As;
+  float* Ts = S.Ts;
+  float* dqs = S.dqs;
   stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (blockIdx.z == 0) {
-    const int zb = blockIdx.x + gridDim.x * blockIdx.y;
+  const unsigned tgt = 2u * (unsigned)a.ncq;   // F2 producers of one counter: 2 instances x ncq column blocks
+  if (z == 0) {
+    const int zb = x + a.ncq1 * y;
     if (zb == 0) {
       step_control(a);
     } else if (a.gather) {
       const GatherArgs& g = a.ga;
-      const int C = 2 * g.O + g.A + 2, tot = g.n * C, stride = (gridDim.x * gridDim.y - 1) * blockDim.x;
+      const int C = 2 * g.O + g.A + 2, tot = g.n * C, stride = (a.ncq1 * a.nrb - 1) * (int)blockDim.x;
       for (int e = (zb - 1) * blockDim.x + tid; e < tot; e += stride) gather_elem(g, e / C, e % C);
     }
     stamp(a.st, 4);
     return;
   }
-  if (blockIdx.z == 3) {              // the policy-row blocks: the action-gradient partials came from F2
-    policy_rows_block(a.pr, blockIdx.y * a.ncq1 + blockIdx.x, As, Ts, a.st);
+  if (z == 3) {                       // the policy-row blocks: the action-gradient partials came from F2
+    if constexpr (FUSED)
+      policy_rows_block<true>(a.pr, y * a.ncq1 + x, As, Ts, a.st, a.sync + 2 * y, tgt, a.sync + 2 * a.nrb);
+    else
+      policy_rows_block<false>(a.pr, y * a.ncq1 + x, As, Ts, a.st);
     stamp(a.st, 4);
     return;
   }
-  const int rb = blockIdx.y, cq = blockIdx.x;
-  const Dh1Inst p = blockIdx.z == 1 ? a.in[0] : a.in[1];
+  const int rb = y, cq = x;
+  const Dh1Inst p = z == 1 ? a.in[0] : a.in[1];
   const int n = a.n, H = a.H;
   const int i0 = rb * 16, c0 = cq * B1_COLS, jw = c0 + w * 16;
   const int li = lane & 15, lk = lane >> 4;
   // ---- 0. the dq of the block's 16 rows first (the partials of F1 / F2; one lane per row): the A slab
-  //         below waits on it
+  //         below waits on it (fused: after the wait below)
   RowIn rin{};
-  if (tid < 16) rin = row_losses_load(a.L, n, a.ncq, i0 + tid, i0 + tid < n);
+  if (!FUSED && tid < 16) rin = row_losses_load(a.L, n, a.ncq, i0 + tid, i0 + tid < n);
   // ---- 1. operands in the order the chain consumes them: the A slab's h2 rows and W3, the h1 mask of this
   //         lane's outputs, then this wave's W2^T operand straight into MFMA registers (B(m, c) = W2[c][m]:
   //         lane (li, lk) holds W2[jw + li][64 lk + 4 s .. + 3])
@@ -818,6 +911,10 @@ static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const 
     const int m = 64 * lk + 4 * i, c = jw + li;
     bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                           dw2, ((m < H && c < H) ? c * H + m : -4) * 4, 0, 0));
+  }
+  if constexpr (FUSED) {              // the targets' partials and logp(s') come from this launch's F2 blocks
+    handoff_wait(a.sync + 2 * rb + 1, tgt, a.sync + 2 * a.nrb);
+    if (tid < 16) rin = row_losses_load(a.L, n, a.ncq, i0 + tid, i0 + tid < n);
   }
   // ---- 2. dq of the block's 16 rows (one lane per row)
   if (tid < 16) {
@@ -857,6 +954,29 @@ static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const 
     if (orow < n && col < H) p.dh1[(int64_t)orow * H + col] = v;
   }
   stamp(a.st, 4);
+}
+
+// B1 as its own launch: grid (ncq1, nrb, 4), B1_WAVES-wave workgroups
+static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const Dh1Args a) {
+  __shared__ __attribute__((aligned(16))) Dh1Lds S;
+  dh1_block<false>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
+}
+
+// F2 and B1 as ONE launch, grid (ncq, nrb, 8): z < 4 the F2 blocks (instance z), z >= 4 the B1 blocks (B1's
+// z - 4).  Blocks are dispatched in linear-id order (z-major), so every F2 block is resident or done before a
+// B1 block starts, and a B1 block only waits on F2 blocks: no wait can block a producer.  What it buys: B1's
+// operands from earlier launches (weights, F1's activations) arrive while F2 runs, and the F2 -> B1 seam is a
+// per-row-block hand-off instead of a grid-wide boundary.  Requires ncq1 == ncq (B1_COLS == RB_COLS).
+union F2B1Lds {
+  FwdLds f;
+  Dh1Lds b;
+};
+static __global__ __launch_bounds__(256, 2) void sac_f2b1_kernel(const FwdArgsR f, const Dh1Args b) {
+  __shared__ __attribute__((aligned(16))) F2B1Lds S;
+  if (blockIdx.z < 4)
+    fwd_block<true, true>(f, blockIdx.x, blockIdx.y, blockIdx.z, S.f);
+  else
+    dh1_block<true>(b, blockIdx.x, blockIdx.y, blockIdx.z - 4, S.b);
 }
 
 }  // namespace mopo

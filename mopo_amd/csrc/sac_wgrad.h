@@ -51,6 +51,7 @@ struct WgradArgs {
   int prior;                         // action_prior 'normal': the policy loss logs - log N(a; 0, I)
   const float* eps_s;                // [n][A] the step's policy noise of pi(s) (for the action)
   Stamps st;
+  const unsigned* sync_tmo;          // the fused F2 + B1 launch's sticky timeout word, or NULL
 };
 
 // Block 0: per-row loss terms of all n rows (thread t: rows t, t + 1024, ...), block sums in a fixed order
@@ -67,13 +68,13 @@ static __device__ __forceinline__ void wgrad_loss_tail(const WgradArgs& a, float
     lr_t = *ad.lr_t;
   }
   float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const auto dls = rsrc(a.L.head_s, (int64_t)n * 2 * A), dlp = rsrc(a.L.logp_s, n);
+  const auto dls = rsrc(a.L.head_s, (int64_t)n * 2 * A), dlp = rsrc(a.L.logp_s, 2 * rows_ns(n));
   for (int r0 = 0; r0 < n; r0 += blockDim.x) {
     const int r = r0 + tid;
     const bool on = r < n;
     // every load of the row first (one memory latency), then the terms
     const RowIn in = row_losses_load(a.L, n, a.ncq, r, on);
-    const float lps = bload(dlp, on ? r : -1);
+    const float lps = bload(dlp, on ? lp_idx(r) : -1);
     float lsv[8], muv[8], epv[8];
     const auto dep = rsrc(a.eps_s, (int64_t)n * A);
 #pragma unroll
@@ -125,6 +126,12 @@ static __device__ __forceinline__ void wgrad_loss_tail(const WgradArgs& a, float
   const float m1 = red[2] / fn, m2 = red[3] / fn, mlp = red[4] / fn, ment = red[5] / fn;
   const float pil = red[6] / fn;                                      // mopo.py:371-377
   const float ga = -(mlp + a.tent);                                   // d/dlog_alpha of -mean(la*(logp+H))
+  if (a.sync_tmo && *a.sync_tmo) {    // a fused launch gave up waiting (sac_rows.h handoff_wait): poison the logs
+    const float nan = __builtin_nanf("");
+    for (int i = 0; i < LOG_N; ++i) a.logs[i] = nan;
+    *a.iter += 1;
+    return;
+  }
   const_cast<float*>(ad.G)[ad.total] = ga;
   float* logs = a.logs;
   logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;

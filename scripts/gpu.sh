@@ -9,6 +9,7 @@
 #   ab          headline A/B over abv/<v>.so for v in $AB (scripts/ab.sh)
 #   sac_ab      SAC parity on each abv/<v>.so of $AB, then the step-time A/B (scripts/ab_sac.sh)
 #   train_ab    BNN.train parity, then the train leg under each env setting of $VARS
+#   env_ab      bench (SAC + headline) alternating the env settings in $VARS (comma-joined per variant)
 #   stamps      SAC phase stamps from abv/sac_stamps.so (scripts/sac_stamps.py)
 # usage: bash scripts/gpu.sh tests bench ;  AB="new old" bash scripts/gpu.sh sac_ab
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -59,6 +60,16 @@ for step in "$@"; do
         done
         cat gpurun_out/ab_train.txt
       fi ;;
+    env_ab)
+      : > gpurun_out/env_ab.txt; rc=0
+      for i in 1 2 3; do
+        for v in ${VARS}; do
+          env ${v//,/ } timeout -k 10 150 python bench.py --no-cpu-baseline --no-c3 --no-alt-dtypes --train-epochs 0 --steps 5 \
+            --warmup 2 ${BENCH_ARGS} > gpurun_out/env_ab_cur.json 2> gpurun_out/env_ab_cur.err || { rc=1; tail -5 gpurun_out/env_ab_cur.err; break 2; }
+          python -c "import json; d=json.load(open('gpurun_out/env_ab_cur.json')); print('$v', 'sac', round(d['sac']['us_per_step'], 2), 'us/step', 'rollout', round(d['value']/1e6, 2), 'M/s ens', round(d['kernel_ms_avg']['ensemble_fwd'], 4))" >> gpurun_out/env_ab.txt
+        done
+      done
+      cat gpurun_out/env_ab.txt ;;
     stamps)
       keep; cp abv/sac_stamps.so mopo_amd/libmopo_hip.so
       timeout -k 10 120 python scripts/sac_stamps.py > gpurun_out/sac_stamps.txt 2>&1; rc=$?

@@ -363,3 +363,38 @@ def test_sac_nonsquare_hidden_steps_vs_oracle():
     for w, extra in ((0, 1), (1, 0), (2, 1), (3, 1), (4, 1)):
         raw = sac._copy(w, sac._n_dev + extra).cpu().numpy()[:sac._n_dev]
         assert np.all(raw[pad] == 0), (w, np.abs(raw[pad]).max())
+
+
+@pytest.mark.parametrize('o,a,h,n', [(17, 6, 256, 256), (11, 3, 64, 100)])
+def test_sac_fused_f2b1_bit_identical_to_separate_launches(o, a, h, n, monkeypatch):
+    """The fused F2 + B1 launch (sac_rows.h sac_f2b1_kernel: an in-launch row-block hand-off instead of a
+    kernel boundary) computes exactly the separate launches' arithmetic, so 300 graph-replayed steps must
+    end bit-identical to MOPO_SAC_FUSE=0 -- any stale read of a handed-off line (L1 / L2 non-coherence,
+    sac_rows.h handoff_wait) would show as a difference -- and the logs must stay finite (a consumer that
+    gave up waiting poisons them)."""
+    import torch
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.sac import SAC
+    rs = np.random.RandomState(21)
+    pl = []
+    for rows in (400, 2000):
+        s = {'observations': rs.normal(size=(rows, o)).astype(np.float32),
+             'actions': rs.uniform(-1, 1, (rows, a)).astype(np.float32),
+             'next_observations': rs.normal(size=(rows, o)).astype(np.float32),
+             'rewards': rs.normal(size=(rows, 1)).astype(np.float32),
+             'terminals': rs.uniform(size=(rows, 1)) < 0.1}
+        p = SimpleReplayPool(obs_dim=o, act_dim=a, max_size=rows)
+        p.add_samples(s)
+        pl.append(p)
+    fl = flat(osac.init_params(o, a, h, seed=3)).astype(np.float32)
+    out = {}
+    for fuse in ('0', '1'):
+        monkeypatch.setenv('MOPO_SAC_FUSE', fuse)
+        sac = SAC(o, a, h, batch_size=n, real_ratio=0.05, target_entropy=-3, params=fl)
+        sac._do_training(0, pl[0], pl[1], n_steps=300, seed=19)
+        torch.cuda.synchronize()
+        lg = sac.logs()
+        assert all(np.isfinite(v) for v in lg.values()), (fuse, lg)
+        out[fuse] = {k: v.cpu().numpy() for k, v in sac.state_dict().items()}
+    for k in out['0']:
+        np.testing.assert_array_equal(out['1'][k], out['0'][k], err_msg=k)
