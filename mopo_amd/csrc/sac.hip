@@ -76,6 +76,7 @@ struct Sac {
   float *dapart[2];               // [ncq][n][OPW] action-gradient partials of Q1 / Q2 at (s, pi(s))
   uint64_t* stamps = nullptr;     // MOPO_SAC_STAMPS builds: [slot][block][8]
   unsigned* sync = nullptr;       // fused F2 + B1 launch: [nrb][2] row-block counters, then the timeout word
+                                  //   (each on its own 128-B line: sac_rows.h SYNC_STRIDE)
   bool fuse = true;               // F2 and B1 as one launch (sac_f2b1_kernel)
   float *dhead, *dh2p, *dh1p;
   // graph
@@ -326,7 +327,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     g.ad.slot0 = 0;
     g.L = L; g.A = A; g.ncq = ncq; g.tent = h->tent; g.logs = h->logs; g.iter = h->iter;
     g.prior = h->prior; g.eps_s = h->eps_s;
-    g.sync_tmo = h->fuse ? h->sync + 2 * nrb : nullptr;
+    g.sync_tmo = h->fuse ? h->sync + 2 * nrb * SYNC_STRIDE : nullptr;
     g.st = Stamps{h->stamps, 3};
     if (tot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
     h->nslots = tot;
@@ -384,7 +385,7 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   }
   for (int i = 0; i < 8; ++i) { f(&h->h1[i], n * H); f(&h->h2[i], n * H); f(&h->out[i], n * 2 * A); }
   f(&h->logp_s, 2 * ns); f(&h->logp_n, 2 * ns); f(&h->eps_s, n * A); f(&h->eps_n, n * A);
-  reg.push_back({(void**)&h->sync, (size_t)(2 * (ns / 16) + 4) * 4});
+  reg.push_back({(void**)&h->sync, (size_t)(2 * (ns / 16) + 1) * SYNC_STRIDE * 4});
   h->fuse = sac_fuse_default();
   for (int i = 0; i < 4; ++i) { f(&h->dq[i], n); f(&h->dh1[i], n * H); }
   f(&h->dhead, n * 2 * A); f(&h->dh2p, n * H); f(&h->dh1p, n * H);

@@ -113,6 +113,10 @@ static __device__ __forceinline__ void hstore(float* p, float v) {
 // ever waits on producers with lower workgroup ids (all of them are dispatched first), and every spin is bounded:
 // on a give-up it sets the sticky timeout word, which the loss tail turns into NaN logs.
 constexpr unsigned SAC_SPIN_LIMIT = 1u << 19;
+constexpr int SYNC_STRIDE = 32;      // one counter per 128-B line: counter c at sync[c * SYNC_STRIDE]
+#ifndef MOPO_SAC_FUSE_ACQ
+#define MOPO_SAC_FUSE_ACQ 1          // the consumer's agent acquire after the poll (A/B knob)
+#endif
 static __device__ __forceinline__ void handoff_signal(unsigned* cnt) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -128,8 +132,10 @@ static __device__ __forceinline__ void handoff_wait(unsigned* cnt, unsigned targ
         break;
       }
     }
+#if MOPO_SAC_FUSE_ACQ
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   }
   __syncthreads();
 }
@@ -542,7 +548,7 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const FwdInst p = pick4(a.in, ii);
-  if (!HEAD && a.sync_reset && cq == 0 && rb == 0 && ii == 0 && tid < a.n_sync) a.sync_reset[tid] = 0u;
+  if (!HEAD && a.sync_reset && cq == 0 && rb == 0 && ii == 0 && tid < a.n_sync) a.sync_reset[tid * SYNC_STRIDE] = 0u;
   const int n = a.n, H = a.H, A = a.A;
   const int i0 = rb * 16, c0 = cq * RB_COLS, jw = c0 + w * 16;
   // ---- 0. F2: the head's operands first (the head is the first link of this launch's chain)
@@ -726,7 +732,7 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
       }
     }
   }
-  if constexpr (FUSED) handoff_signal(a.sync + 2 * rb + (ii >= 2 ? 1 : 0));
+  if constexpr (FUSED) handoff_signal(a.sync + (2 * rb + (ii >= 2 ? 1 : 0)) * SYNC_STRIDE);
   stamp(a.st, 4);
 }
 
@@ -869,7 +875,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
   }
   if (z == 3) {                       // the policy-row blocks: the action-gradient partials came from F2
     if constexpr (FUSED)
-      policy_rows_block<true>(a.pr, y * a.ncq1 + x, As, Ts, a.st, a.sync + 2 * y, tgt, a.sync + 2 * a.nrb);
+      policy_rows_block<true>(a.pr, y * a.ncq1 + x, As, Ts, a.st, a.sync + 2 * y * SYNC_STRIDE, tgt, a.sync + 2 * a.nrb * SYNC_STRIDE);
     else
       policy_rows_block<false>(a.pr, y * a.ncq1 + x, As, Ts, a.st);
     stamp(a.st, 4);
@@ -913,7 +919,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
                                           dw2, ((m < H && c < H) ? c * H + m : -4) * 4, 0, 0));
   }
   if constexpr (FUSED) {              // the targets' partials and logp(s') come from this launch's F2 blocks
-    handoff_wait(a.sync + 2 * rb + 1, tgt, a.sync + 2 * a.nrb);
+    handoff_wait(a.sync + (2 * rb + 1) * SYNC_STRIDE, tgt, a.sync + 2 * a.nrb * SYNC_STRIDE);
     if (tid < 16) rin = row_losses_load(a.L, n, a.ncq, i0 + tid, i0 + tid < n);
   }
   // ---- 2. dq of the block's 16 rows (one lane per row)

@@ -39,9 +39,10 @@ for step in "$@"; do
     sac_ab)
       keep; rc=0
       for v in $AB; do
-        cp abv/$v.so mopo_amd/libmopo_hip.so
-        timeout -k 10 300 $PYT tests/test_gpu_sac.py tests/test_gpu_ref.py -q -x -k "sac or SAC" > gpurun_out/sac_tests_$v.log 2>&1
-        rc=$?; echo "== $v parity rc=$rc: $(tail -1 gpurun_out/sac_tests_$v.log)"
+        so=${v%%:*}; envs=""; [ "$so" != "$v" ] && envs=${v#*:}
+        cp abv/$so.so mopo_amd/libmopo_hip.so
+        env $envs timeout -k 10 300 $PYT tests/test_gpu_sac.py tests/test_gpu_ref.py -q -x -k "sac or SAC" > gpurun_out/sac_tests_$so.log 2>&1
+        rc=$?; echo "== $v parity rc=$rc: $(tail -1 gpurun_out/sac_tests_$so.log)"
         [ $rc -ne 0 ] && break
       done
       [ $rc -eq 0 ] && { AB="$AB_EXTRA $AB" bash scripts/ab_sac.sh; rc=$?; }
