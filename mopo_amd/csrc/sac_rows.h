@@ -233,7 +233,9 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
 #pragma unroll
   for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
   if constexpr (FUSED) {
+    stamp(st, 5);
     handoff_wait(cnt, target, tmo);
+    stamp(st, 6);
     handed();
   }
   stamp(st, 1);
@@ -919,7 +921,9 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
                                           dw2, ((m < H && c < H) ? c * H + m : -4) * 4, 0, 0));
   }
   if constexpr (FUSED) {              // the targets' partials and logp(s') come from this launch's F2 blocks
+    stamp(a.st, 5);
     handoff_wait(a.sync + (2 * rb + 1) * SYNC_STRIDE, tgt, a.sync + 2 * a.nrb * SYNC_STRIDE);
+    stamp(a.st, 6);
     if (tid < 16) rin = row_losses_load(a.L, n, a.ncq, i0 + tid, i0 + tid < n);
   }
   // ---- 2. dq of the block's 16 rows (one lane per row)

@@ -72,9 +72,12 @@ for step in "$@"; do
       done
       cat gpurun_out/env_ab.txt ;;
     stamps)
-      keep; cp abv/sac_stamps.so mopo_amd/libmopo_hip.so
-      timeout -k 10 120 python scripts/sac_stamps.py > gpurun_out/sac_stamps.txt 2>&1; rc=$?
-      restore; cat gpurun_out/sac_stamps.txt ;;
+      keep; cp abv/sac_stamps.so mopo_amd/libmopo_hip.so; : > gpurun_out/sac_timeline.txt; rc=0
+      for v in ${VARS:-MOPO_SAC_FUSE=1}; do
+        echo "== $v" >> gpurun_out/sac_timeline.txt
+        env ${v//,/ } timeout -k 10 120 python scripts/sac_timeline.py >> gpurun_out/sac_timeline.txt 2>&1 || { rc=1; break; }
+      done
+      restore; cat gpurun_out/sac_timeline.txt ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
   echo "== step $step rc=$rc"
