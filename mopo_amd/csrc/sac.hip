@@ -77,7 +77,7 @@ struct Sac {
   uint64_t* stamps = nullptr;     // MOPO_SAC_STAMPS builds: [slot][block][8]
   unsigned* sync = nullptr;       // fused F2 + B1 launch: [nrb][2] row-block counters, then the timeout word
                                   //   (each on its own 128-B line: sac_rows.h SYNC_STRIDE)
-  bool fuse = true;               // F2 and B1 as one launch (sac_f2b1_kernel)
+  int fuse = 2;                   // 0: F1, F2, B1 separate; 1: F2 + B1 one launch; 2: F1 + F2 + B1 one launch
   float *dhead, *dh2p, *dh1p;
   // graph
   bool use_graph = true;
@@ -169,11 +169,13 @@ static int launch_gather(Sac* h, int par, const mopo_pool_desc* env, const mopo_
 // Pb[1 - par].  With `prefetch`, B1 also gathers the next step's batch into bt[1 - par] (a separate
 // gather launch, or a forked graph branch, costs more than it hides).
 #ifndef MOPO_SAC_FUSE
-#define MOPO_SAC_FUSE 1   // default of the fused F2 + B1 launch; the environment variable MOPO_SAC_FUSE overrides it
+#define MOPO_SAC_FUSE 2   // 0: F1, F2, B1 as three launches; 1: F2 + B1 fused; 2: F1 + F2 + B1 fused (the
+                          // environment variable MOPO_SAC_FUSE overrides it at mopo_sac_create)
 #endif
-static bool sac_fuse_default() {
+static int sac_fuse_default() {
   const char* e = std::getenv("MOPO_SAC_FUSE");
-  return e ? std::atoi(e) != 0 : MOPO_SAC_FUSE != 0;
+  const int v = e ? std::atoi(e) : MOPO_SAC_FUSE;
+  return v < 0 ? 0 : v > 2 ? 2 : v;
 }
 
 static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
@@ -201,8 +203,9 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   L.logp_s = h->logp_s; L.logp_n = h->logp_n; L.head_s = h->out[0]; L.rew = bt.rew; L.term = bt.term;
   L.log_alpha = P + o.total; L.gamma = h->gamma; L.rscale = h->rscale;
   // ---- F1: pi(s), pi(s'), Q1(s,a), Q2(s,a) hidden layers + partial output layers
+  FwdArgsR f1{};
   {
-    FwdArgsR f{};
+    FwdArgsR& f = f1;
     f.ninst = 4; f.n = n; f.H = H; f.A = A; f.ncq = ncq; f.nrb = nrb;
     for (int i = 0; i < 2; ++i) {
       FwdInst& q = f.in[i];
@@ -221,9 +224,12 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     f.hd.iter = h->iter; f.hd.seed = seed; f.hd.eps_out[0] = h->eps_s; f.hd.eps_out[1] = h->eps_n;
     f.hd.gen_eps = (eps_in_s ? 0 : 1) | (eps_in_n ? 0 : 2);   // the heads whose noise is not injected
     f.st = Stamps{h->stamps, 0};
-    if (h->fuse) { f.sync_reset = h->sync; f.n_sync = 2 * nrb; }   // this step's F2 -> B1 counters
-    hipLaunchKernelGGL(sac_fwd_kernel<false>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
-    MOPO_HIP(hipGetLastError());
+    if (h->fuse == 1) { f.sync_reset = h->sync; f.n_sync = SYNC_N * nrb; }   // this step's F2 -> B1 counters
+    f.sync = h->sync;
+    if (h->fuse < 2) {
+      hipLaunchKernelGGL(sac_fwd_kernel<false>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
+      MOPO_HIP(hipGetLastError());
+    }
   }
   // ---- F2: the policy head from F1's partials -> Q1/Q2(s, pi(s)) (main), Qt1/Qt2(s', pi(s')) (target);
   //      the main critics' blocks also emit their action-gradient partials (dq = 1)
@@ -251,7 +257,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     hd.seed = seed; hd.iter = h->iter;
     f.st = Stamps{h->stamps, 1};
     f.sync = h->sync;
-    if (!h->fuse) {
+    if (h->fuse == 0) {
       hipLaunchKernelGGL(sac_fwd_kernel<true>, dim3(ncq, nrb, 4), dim3(256), 0, s, f);
       MOPO_HIP(hipGetLastError());
     }
@@ -275,7 +281,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     pr.qpart[0] = h->opart[4]; pr.qpart[1] = h->opart[5];
     pr.b3[0] = Wq(0, 5); pr.b3[1] = Wq(1, 5);
     // the policy noise of pi(s): F1's draws, or the injected array itself (F2's copy of it is not handed over)
-    pr.head_s = h->out[0]; pr.eps_s = eps_in_s ? eps_in_s : h->eps_s;
+    pr.head_s = h->out[0]; pr.eps_s = eps_in_s ? eps_in_s : h->eps_s; pr.lde = eps_in_s ? A : EPW;
     pr.log_alpha = P + o.total; pr.Wm = P + o.pWm; pr.Wl = P + o.pWl;
     pr.h2p = h->h2[0]; pr.h1p = h->h1[0]; pr.W2p = P + o.pW2;
     pr.dhead = h->dhead; pr.dh2p = h->dh2p; pr.dh1p = h->dh1p; pr.prior = h->prior;
@@ -284,11 +290,14 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       d.ga = gather_args(h, 1 - par, env, mod, seed, nullptr);
       d.ga.iter_add = 1;                       // the next step's batch (the counter advances in B2)
     }
-    d.st = Stamps{h->stamps, h->fuse ? 1 : 2};
+    d.st = Stamps{h->stamps, h->fuse == 2 ? 0 : h->fuse ? 1 : 2};
     d.sync = h->sync;
     if (ncq1 * nrb < 2 && prefetch) return fail("sac: B1 needs at least one gather block");
-    if (h->fuse) {
-      static_assert(B1_COLS == RB_COLS && B1_WAVES == 4, "the fused F2 + B1 launch shares the F2 grid");
+    static_assert(B1_COLS == RB_COLS && B1_WAVES == 4, "the fused launches share the F1 / F2 grid");
+    if (h->fuse == 2) {
+      f2.st = Stamps{h->stamps, 0};
+      hipLaunchKernelGGL(sac_f12b1_kernel, dim3(ncq, nrb, 12), dim3(256), 0, s, f1, f2, d);
+    } else if (h->fuse == 1) {
       hipLaunchKernelGGL(sac_f2b1_kernel, dim3(ncq, nrb, 8), dim3(256), 0, s, f2, d);
     } else {
       hipLaunchKernelGGL(sac_dh1_kernel, dim3(ncq1, nrb, 4), dim3(B1_WAVES * 64), 0, s, d);
@@ -327,7 +336,8 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     g.ad.slot0 = 0;
     g.L = L; g.A = A; g.ncq = ncq; g.tent = h->tent; g.logs = h->logs; g.iter = h->iter;
     g.prior = h->prior; g.eps_s = h->eps_s;
-    g.sync_tmo = h->fuse ? h->sync + 2 * nrb * SYNC_STRIDE : nullptr;
+    g.sync_tmo = h->fuse ? h->sync + SYNC_N * nrb * SYNC_STRIDE : nullptr;
+    if (h->fuse == 2) { g.sync_reset = h->sync; g.n_sync = SYNC_N * nrb; }
     g.st = Stamps{h->stamps, 3};
     if (tot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
     h->nslots = tot;
@@ -384,8 +394,8 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
     reg.push_back({(void**)&t.idx, (size_t)n * 8});
   }
   for (int i = 0; i < 8; ++i) { f(&h->h1[i], n * H); f(&h->h2[i], n * H); f(&h->out[i], n * 2 * A); }
-  f(&h->logp_s, 2 * ns); f(&h->logp_n, 2 * ns); f(&h->eps_s, n * A); f(&h->eps_n, n * A);
-  reg.push_back({(void**)&h->sync, (size_t)(2 * (ns / 16) + 1) * SYNC_STRIDE * 4});
+  f(&h->logp_s, 2 * ns); f(&h->logp_n, 2 * ns); f(&h->eps_s, ns * EPW); f(&h->eps_n, ns * EPW);
+  reg.push_back({(void**)&h->sync, (size_t)(SYNC_N * (ns / 16) + 1) * SYNC_STRIDE * 4});
   h->fuse = sac_fuse_default();
   for (int i = 0; i < 4; ++i) { f(&h->dq[i], n); f(&h->dh1[i], n * H); }
   f(&h->dhead, n * 2 * A); f(&h->dh2p, n * H); f(&h->dh1p, n * H);

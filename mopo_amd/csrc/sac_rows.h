@@ -88,6 +88,7 @@ static __device__ __forceinline__ void gather_elem(const GatherArgs& g, int r, i
 // gradients of the next launch read with dh1p.
 constexpr int OPW = 16;              // floats per (column block, row) record of the policy's output partials
 constexpr int DPW = 8;               // ... of the action-gradient partials (A <= 8); a critic's is 1 float
+constexpr int EPW = 8;               // row stride of the step's policy-noise records eps_out (A <= 8)
 constexpr int MAX_NCQ = 4;           // column blocks of 64 (H <= 256)
 constexpr int DH2_TILES = 4;         // dh2p column tiles per wave (H <= 256 over >= 4 waves)
 
@@ -114,6 +115,11 @@ static __device__ __forceinline__ void hstore(float* p, float v) {
 // on a give-up it sets the sticky timeout word, which the loss tail turns into NaN logs.
 constexpr unsigned SAC_SPIN_LIMIT = 1u << 19;
 constexpr int SYNC_STRIDE = 32;      // one counter per 128-B line: counter c at sync[c * SYNC_STRIDE]
+// the counters of one row block rb: sync[(SYNC_N rb + class) SYNC_STRIDE]; the timeout word after the last
+enum { SYNC_PI_S = 0, SYNC_PI_N = 1, SYNC_Q_SA = 2, SYNC_F2_MAIN = 3, SYNC_F2_TGT = 4, SYNC_N = 5 };
+static __device__ __forceinline__ unsigned* sync_at(unsigned* sync, int rb, int c) {
+  return sync + (SYNC_N * rb + c) * SYNC_STRIDE;
+}
 #ifndef MOPO_SAC_FUSE_ACQ
 #define MOPO_SAC_FUSE_ACQ 1          // the consumer's agent acquire after the poll (A/B knob)
 #endif
@@ -146,7 +152,7 @@ struct PolicyRows {
   // Q1 / Q2(s, pi) = b3 + the critics' forward partials [ncq][n]: the min-Q selection
   const float* qpart[2]; const float* b3[2];
   const float* head_s;               // [n][2A] mean | raw log_std
-  const float* eps_s;                // [n][A]
+  const float* eps_s; int lde;       // [n][lde]: F1's draws (EPW) or the injected noise (A)
   const float* log_alpha;
   const float* Wm; const float* Wl;  // [H][A]
   const float* h2p; const float* h1p;// [n][H]
@@ -162,12 +168,13 @@ struct PolicyRows {
 // block pays one memory latency, then computes.
 // S: >= 16 (H + 4) floats of LDS; hs: >= 3 * 128 floats.  Blocks of 4 or 8 waves (64 or 128 dh1p
 // columns).  H % 16 == 0, H <= 256 (one dh2p column per thread), A <= 8.
-// FUSED (sac_f2b1_kernel): the operands of earlier launches are issued first, then the block waits for its
-// row block's F2 producers (*cnt >= target) and loads what they handed over.
-template <bool FUSED = false>
+// FZ >= 1 (fused launches): the operands of earlier launches are issued first, then the block waits for its
+// row block's F2 producers (sync class SYNC_F2_MAIN >= 2 ncq) and loads what they handed over; FZ = 2 (F1 +
+// F2 + B1): the pi(s) activations (h1p, h2p) are loaded after the row block's pi(s) blocks of F1 are done.
+template <int FZ = 0>
 static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs,
-                                                         const Stamps& st, unsigned* cnt = nullptr,
-                                                         unsigned target = 0, unsigned* tmo = nullptr) {
+                                                         const Stamps& st, unsigned* sync = nullptr,
+                                                         int nrb = 0) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int H = c.H, A = c.A, HS = H + 4, n = c.n;
   const int pcols = 16 * (int)(blockDim.x >> 6);   // dh1p columns of the block: one 16-wide tile per wave
@@ -183,10 +190,10 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   float qv[2][MAX_NCQ];                // Q1 / Q2(s, pi) partials of this thread's row: the chain's first link
   float dap[2][MAX_NCQ];
   auto handed = [&]() {                // what F2 wrote: head, critic partials, action-gradient partials
-    const auto dh = rsrc(c.head_s, (int64_t)n * 2 * A), de = rsrc(c.eps_s, (int64_t)n * A);
+    const auto dh = rsrc(c.head_s, (int64_t)n * 2 * A), de = rsrc(c.eps_s, (int64_t)n * c.lde);
     mu = bload(dh, hon ? hrow * 2 * A + hj : -1);
     raw = bload(dh, hon ? hrow * 2 * A + A + hj : -1);
-    ep = bload(de, hon ? hrow * A + hj : -1);
+    ep = bload(de, hon ? hrow * c.lde + hj : -1);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const auto dq = rsrc(c.qpart[i], (int64_t)c.ncq * ns);
@@ -198,7 +205,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
       }
     }
   };
-  if constexpr (!FUSED) handed();
+  if constexpr (FZ == 0) handed();
   const float la = *c.log_alpha;
   float b3v[2];
 #pragma unroll
@@ -215,9 +222,18 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
     for (int s2 = 0; s2 < 4; ++s2) {
       const int k = 4 * (s2 & 1) + lk;
       wb[q][s2] = bload(s2 < 2 ? dwm : dwl, (on && k < A) ? c2 * A + k : -1);
-      h2v[q][s2] = bload(dh2, on ? (r0 + 4 * lk + s2) * H + c2 : -1);     // rows >= n: past the extent
     }
   }
+  auto f1_loads = [&]() {             // F1's pi(s) activations at this thread's dh2p columns
+#pragma unroll
+    for (int q = 0; q < DH2_TILES; ++q) {
+      const int c2 = (w + q * nw) * 16 + li;
+      const bool on = w + q * nw < nt2 && c2 < H;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) h2v[q][s2] = bload(dh2, on ? (r0 + 4 * lk + s2) * H + c2 : -1);  // rows >= n: 0
+    }
+  };
+  if constexpr (FZ < 2) f1_loads();
   const int j0 = cq * pcols + w * 16, col = j0 + li;
   const bool tile_on = j0 < H;
   const auto dw2 = rsrc(c.W2p, (int64_t)H * H);
@@ -230,11 +246,20 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   }
   const auto dm1 = rsrc(c.h1p, (int64_t)n * H);
   float m1[4];
+  auto m1_loads = [&]() {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
-  if constexpr (FUSED) {
+    for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
+  };
+  if constexpr (FZ < 2) m1_loads();
+  if constexpr (FZ >= 1) {
+    unsigned* tmo = sync + SYNC_N * nrb * SYNC_STRIDE;
     stamp(st, 5);
-    handoff_wait(cnt, target, tmo);
+    if constexpr (FZ == 2) {
+      handoff_wait(sync_at(sync, rb, SYNC_PI_S), (unsigned)c.ncq, tmo);
+      f1_loads();
+      m1_loads();
+    }
+    handoff_wait(sync_at(sync, rb, SYNC_F2_MAIN), 2u * (unsigned)c.ncq, tmo);
     stamp(st, 6);
     handed();
   }
@@ -396,8 +421,9 @@ static __device__ __forceinline__ HeadIn rows_head_load(const FwdHead& h, int nx
   }
   o.bm = bload(rsrc(h.bm, A), on ? j : -1);
   o.bl = bload(rsrc(h.bl, A), on ? j : -1);
-  const float* ein = h.eps_in[nxt] ? h.eps_in[nxt] : h.eps_out[nxt];   // injected, or F1's draws
-  o.z = bload(rsrc(ein, (int64_t)n * A), on ? r * A + j : -1);
+  const float* ein = h.eps_in[nxt] ? h.eps_in[nxt] : h.eps_out[nxt];   // injected ([n][A]), or F1's draws ([n][EPW])
+  const int lde = h.eps_in[nxt] ? A : EPW;
+  o.z = bload(rsrc(ein, (int64_t)n * lde), on ? r * lde + j : -1);
   return o;
 }
 
@@ -422,7 +448,7 @@ static __device__ __forceinline__ float rows_head(const FwdHead& h, const HeadIn
         - 2.f * (0.6931471805599453f - u - softplusf(-2.f * u));    // squash correction (:292)
     act = tanhf(u);
     if (store) {
-      if (h.eps_in[nxt]) h.eps_out[nxt][r * A + j] = z;     // (B1 reads the injected noise itself)
+      if (h.eps_in[nxt]) h.eps_out[nxt][r * EPW + j] = z;   // (B1 reads the injected noise itself)
       hstore<SC1>(&h.head_out[nxt][r * 2 * A + j], mu);
       hstore<SC1>(&h.head_out[nxt][r * 2 * A + A + j], raw);
     }
@@ -538,10 +564,13 @@ struct FwdLds {
 // One forward row-block workgroup: column block cq, row block rb, instance ii (grid indices, SGPRs: the
 // instance's fields then come from the kernel arguments by scalar loads -- a divided linear index made them
 // VGPRs, and every buffer descriptor built from them needed a waterfall loop).  H <= GKC, H % 16 == 0.
-// FUSED (F2 inside sac_f2b1_kernel): every store B1 reads is write-through, and the block ends by signalling
-// its row block's counter.
-template <bool HEAD, bool FUSED>
+// FZ, the fusion level: 0 a launch of its own; 1 F2 inside sac_f2b1_kernel (F2 + B1); 2 F1 or F2 inside
+// sac_f12b1_kernel (F1 + F2 + B1).  A fused block's stores that a later phase of the launch reads are
+// write-through, and the block ends by signalling its row block's counter; a fused F2 block (FZ = 2) issues
+// its weight operands, then waits for its row block's pi blocks of F1 before loading the head's partials.
+template <bool HEAD, int FZ>
 static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int rb, int ii, FwdLds& L) {
+  constexpr bool SC = HEAD ? FZ >= 1 : FZ == 2;   // this block's stores are handed over in-launch
   float* As = L.As;
   float* Ts = L.Ts;
   float* Wo = L.Wo;
@@ -556,7 +585,7 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   // ---- 0. F2: the head's operands first (the head is the first link of this launch's chain)
   const int hr = tid >> 3, hj = tid & 7, hrow = i0 + hr;
   HeadIn hin{};
-  if (HEAD && tid < 128) hin = rows_head_load(a.hd, p.head, n, A, a.ncq, hrow, hj, hrow < n);
+  if (HEAD && FZ < 2 && tid < 128) hin = rows_head_load(a.hd, p.head, n, A, a.ncq, hrow, hj, hrow < n);
   // ---- 1. every global operand, issued up front in the order the chain consumes them: layer 1 (its
   //         MFMAs then run while the layer-2 operand is still arriving -- loads return in order, so
   //         layer-1 operands queued behind it waited for all of it), this wave's W2 operand straight into
@@ -617,12 +646,19 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   // ---- F1, pi(s) / pi(s') blocks of column block 0: this step's policy noise of their 16 rows (while the
   //      operands arrive), which F2's head loads
   if (!HEAD && ii < 2 && cq == 0 && ((a.hd.gen_eps >> ii) & 1) && tid < 128 && hj < A && hrow < n)
-    a.hd.eps_out[ii][hrow * A + hj] = head_noise(a.hd.seed, *a.hd.iter, hrow, ii, hj);
+    hstore<SC>(&a.hd.eps_out[ii][hrow * EPW + hj], head_noise(a.hd.seed, *a.hd.iter, hrow, ii, hj));
+  // ---- F2 inside the F1 + F2 + B1 launch: the head's partials once the row block's pi blocks are done
+  if constexpr (HEAD && FZ == 2) {
+    stamp(a.st, 5);
+    handoff_wait(sync_at(a.sync, rb, p.head == 0 ? SYNC_PI_S : SYNC_PI_N), (unsigned)a.ncq, a.sync + SYNC_N * a.nrb * SYNC_STRIDE);
+    stamp(a.st, 6);
+    if (tid < 128) hin = rows_head_load(a.hd, p.head, n, A, a.ncq, hrow, hj, hrow < n);
+  }
   // ---- 2. F2: the policy head of the block's 16 rows (its action feeds layer 1)
   if (HEAD) {
     if (tid < 128) {
       const bool store = cq == 0 && (ii == 0 || ii == 2);  // Q1(s,pi) / Qt1(s',pi') blocks publish the head
-      act_s[hr][hj] = rows_head<FUSED>(a.hd, hin, p.head, A, hrow, hj, hrow < n, store);
+      act_s[hr][hj] = rows_head<SC>(a.hd, hin, p.head, A, hrow, hj, hrow < n, store);
     }
     lds_barrier();
 #pragma unroll
@@ -664,7 +700,7 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   if (cq == 0 && p.h1 && tid < H) {  // the first-layer slab for the backward pass (coalesced in k)
 #pragma unroll 4
     for (int rr = 0; rr < 16; ++rr)
-      if (i0 + rr < n) p.h1[(int64_t)(i0 + rr) * H + tid] = As[rr * RB_LD + tid];
+      if (i0 + rr < n) hstore<SC>(&p.h1[(int64_t)(i0 + rr) * H + tid], As[rr * RB_LD + tid]);
   }
   // ---- 4. layer 2: the wave's 16 x 16 tile over the whole K
   f32x4 acc[4];
@@ -680,13 +716,13 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   for (int rr = 0; rr < 4; ++rr) {
     const int orow = i0 + 4 * lk + rr;
     const float v = (col < H && orow < n) ? fmaxf(acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr] + b2v, 0.f) : 0.f;
-    if (p.h2 && orow < n && col < H) p.h2[(int64_t)orow * H + col] = v;
+    if (p.h2 && orow < n && col < H) hstore<SC>(&p.h2[(int64_t)orow * H + col], v);
     Ts[(4 * lk + rr) * RB_TLD + w * 16 + li] = v;
   }
   lds_barrier();
   // ---- 6. partial output dots of the block's 64 columns (wave 0, MFMA)
   if (w == 0)                       // a critic's records are 1 float, row-block-major (qp_idx)
-    rows_partial_out<RB_COLS, FUSED>(Ts, Wo, li, lk, i0, n, p.nout, cq, a.ncq, p.opart);
+    rows_partial_out<RB_COLS, SC>(Ts, Wo, li, lk, i0, n, p.nout, cq, a.ncq, p.opart);
   // ---- 7. F2, Q1 / Q2 at (s, pi(s)): the critic's backward share of the block (dq = 1): wave w forms
   //         dh1 rows k in [64 w, 64 w + 64) of D(k, r) = sum_c W2[k][c0 + c] G(r, c), G = W3[c0 + c]
   //         (h2 > 0) (K = the block's 64 columns), masked by h1 > 0, then its partial of the action
@@ -730,11 +766,12 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
       if (tid < 128) {                                       // waves' partials in wave order
         const int rr = tid >> 3, aa = tid & 7, orow = i0 + rr;
         const float v = da_s[0][rr][aa] + da_s[1][rr][aa] + da_s[2][rr][aa] + da_s[3][rr][aa];
-        if (aa < A && orow < n) hstore<FUSED>(&p.dapart[((int64_t)cq * rows_ns(n) + orow) * DPW + aa], v);
+        if (aa < A && orow < n) hstore<SC>(&p.dapart[((int64_t)cq * rows_ns(n) + orow) * DPW + aa], v);
       }
     }
   }
-  if constexpr (FUSED) handoff_signal(a.sync + (2 * rb + (ii >= 2 ? 1 : 0)) * SYNC_STRIDE);
+  if constexpr (SC)
+    handoff_signal(sync_at(a.sync, rb, HEAD ? (ii >= 2 ? SYNC_F2_TGT : SYNC_F2_MAIN) : (ii < 2 ? ii : SYNC_Q_SA)));
   stamp(a.st, 4);
 }
 
@@ -742,7 +779,7 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
 template <bool HEAD>
 static __global__ __launch_bounds__(256, 2) void sac_fwd_kernel(const FwdArgsR a) {
   __shared__ __attribute__((aligned(16))) FwdLds L;
-  fwd_block<HEAD, false>(a, blockIdx.x, blockIdx.y, blockIdx.z, L);
+  fwd_block<HEAD, 0>(a, blockIdx.x, blockIdx.y, blockIdx.z, L);
 }
 
 // ---- B1 -----------------------------------------------------------------------------------------
@@ -853,16 +890,16 @@ struct Dh1Lds {
 
 // One B1 workgroup (grid indices x = column block, y = row block, z): z = 0: block (0, 0) the step control,
 // the other blocks the gather of the next step's batch; z = 1, 2: Q1 / Q2(s, a) dh1 tiles; z = 3: the
-// policy-row blocks.  FUSED (inside sac_f2b1_kernel): the z = 1..3 blocks issue the operands of earlier
-// launches, then wait for their row block's F2 producers before loading what F2 wrote.
-template <bool FUSED>
+// policy-row blocks.  FZ >= 1 (inside a fused launch): the z = 1..3 blocks issue the operands of earlier
+// launches, then wait for their row block's F2 producers before loading what F2 wrote; FZ = 2 (F1 + F2 + B1)
+// also waits for the row block's F1 blocks before loading F1's activations (h1, h2).
+template <int FZ>
 static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y, int z, Dh1Lds& S) {
   float* As = S.As;
   float* Ts = S.Ts;
   float* dqs = S.dqs;
   stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const unsigned tgt = 2u * (unsigned)a.ncq;   // F2 producers of one counter: 2 instances x ncq column blocks
   if (z == 0) {
     const int zb = x + a.ncq1 * y;
     if (zb == 0) {
@@ -876,10 +913,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
     return;
   }
   if (z == 3) {                       // the policy-row blocks: the action-gradient partials came from F2
-    if constexpr (FUSED)
-      policy_rows_block<true>(a.pr, y * a.ncq1 + x, As, Ts, a.st, a.sync + 2 * y * SYNC_STRIDE, tgt, a.sync + 2 * a.nrb * SYNC_STRIDE);
-    else
-      policy_rows_block<false>(a.pr, y * a.ncq1 + x, As, Ts, a.st);
+    policy_rows_block<FZ>(a.pr, y * a.ncq1 + x, As, Ts, a.st, a.sync, a.nrb);
     stamp(a.st, 4);
     return;
   }
@@ -891,7 +925,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
   // ---- 0. the dq of the block's 16 rows first (the partials of F1 / F2; one lane per row): the A slab
   //         below waits on it (fused: after the wait below)
   RowIn rin{};
-  if (!FUSED && tid < 16) rin = row_losses_load(a.L, n, a.ncq, i0 + tid, i0 + tid < n);
+  if (FZ == 0 && tid < 16) rin = row_losses_load(a.L, n, a.ncq, i0 + tid, i0 + tid < n);
   // ---- 1. operands in the order the chain consumes them: the A slab's h2 rows and W3, the h1 mask of this
   //         lane's outputs, then this wave's W2^T operand straight into MFMA registers (B(m, c) = W2[c][m]:
   //         lane (li, lk) holds W2[jw + li][64 lk + 4 s .. + 3])
@@ -900,18 +934,19 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
   const int am = 4 * (tid & 63), ar = 4 * (w & 3);
   const auto dh2 = rsrc(p.h2, (int64_t)n * H);
   f32x4 h2v[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    h2v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           dh2, ((slab && am < H && i0 + ar + q < n) ? (i0 + ar + q) * H + am : -4) * 4, 0, 0));
-  const f32x4 w3v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  rsrc(p.w3, H), ((slab && am < H) ? am : -4) * 4, 0, 0));
   float m1[4];
-  {
+  auto f1_loads = [&]() {             // F1's Q(s, a) activations: the slab's h2 rows, this lane's h1 mask
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      h2v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             dh2, ((slab && am < H && i0 + ar + q < n) ? (i0 + ar + q) * H + am : -4) * 4, 0, 0));
     const auto dm1 = rsrc(p.h1, (int64_t)n * H);
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) m1[rr] = bload(dm1, (jw + li < H && i0 + 4 * lk + rr < n) ? (i0 + 4 * lk + rr) * H + jw + li : -1);
-  }
+  };
+  if constexpr (FZ < 2) f1_loads();
+  const f32x4 w3v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  rsrc(p.w3, H), ((slab && am < H) ? am : -4) * 4, 0, 0));
   const auto dw2 = rsrc(p.w2, (int64_t)H * H);
   f32x4 bp[16];
 #pragma unroll
@@ -920,9 +955,14 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
     bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                           dw2, ((m < H && c < H) ? c * H + m : -4) * 4, 0, 0));
   }
-  if constexpr (FUSED) {              // the targets' partials and logp(s') come from this launch's F2 blocks
+  if constexpr (FZ >= 1) {            // the targets' partials and logp(s') come from this launch's F2 blocks
+    unsigned* tmo = a.sync + SYNC_N * a.nrb * SYNC_STRIDE;
     stamp(a.st, 5);
-    handoff_wait(a.sync + (2 * rb + 1) * SYNC_STRIDE, tgt, a.sync + 2 * a.nrb * SYNC_STRIDE);
+    if constexpr (FZ == 2) {          // ... and the Q(s, a) activations from its F1 blocks
+      handoff_wait(sync_at(a.sync, rb, SYNC_Q_SA), 2u * (unsigned)a.ncq, tmo);
+      f1_loads();
+    }
+    handoff_wait(sync_at(a.sync, rb, SYNC_F2_TGT), 2u * (unsigned)a.ncq, tmo);
     stamp(a.st, 6);
     if (tid < 16) rin = row_losses_load(a.L, n, a.ncq, i0 + tid, i0 + tid < n);
   }
@@ -969,7 +1009,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
 // B1 as its own launch: grid (ncq1, nrb, 4), B1_WAVES-wave workgroups
 static __global__ __launch_bounds__(B1_WAVES * 64, 1) void sac_dh1_kernel(const Dh1Args a) {
   __shared__ __attribute__((aligned(16))) Dh1Lds S;
-  dh1_block<false>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
+  dh1_block<0>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
 }
 
 // F2 and B1 as ONE launch, grid (ncq, nrb, 8): z < 4 the F2 blocks (instance z), z >= 4 the B1 blocks (B1's
@@ -984,9 +1024,24 @@ union F2B1Lds {
 static __global__ __launch_bounds__(256, 2) void sac_f2b1_kernel(const FwdArgsR f, const Dh1Args b) {
   __shared__ __attribute__((aligned(16))) F2B1Lds S;
   if (blockIdx.z < 4)
-    fwd_block<true, true>(f, blockIdx.x, blockIdx.y, blockIdx.z, S.f);
+    fwd_block<true, 1>(f, blockIdx.x, blockIdx.y, blockIdx.z, S.f);
   else
-    dh1_block<true>(b, blockIdx.x, blockIdx.y, blockIdx.z - 4, S.b);
+    dh1_block<1>(b, blockIdx.x, blockIdx.y, blockIdx.z - 4, S.b);
+}
+
+// F1, F2 and B1 as ONE launch, grid (ncq, nrb, 12): z < 4 F1 (instance z), 4 <= z < 8 F2 (instance z - 4),
+// z >= 8 B1 (B1's z - 8).  Dispatch in linear-id order again means a block only ever waits on producers with
+// lower ids: F2 on its row block's pi blocks of F1, B1 on its row block's F1 and F2 blocks.  Besides B1's, the
+// F2 blocks' weight operands now arrive while F1 runs.  The counters are zeroed by the previous step's
+// weight-gradient launch (sac_wgrad.h) and at creation.
+static __global__ __launch_bounds__(256, 2) void sac_f12b1_kernel(const FwdArgsR f1, const FwdArgsR f2, const Dh1Args b) {
+  __shared__ __attribute__((aligned(16))) F2B1Lds S;
+  if (blockIdx.z < 4)
+    fwd_block<false, 2>(f1, blockIdx.x, blockIdx.y, blockIdx.z, S.f);
+  else if (blockIdx.z < 8)
+    fwd_block<true, 2>(f2, blockIdx.x, blockIdx.y, blockIdx.z - 4, S.f);
+  else
+    dh1_block<2>(b, blockIdx.x, blockIdx.y, blockIdx.z - 8, S.b);
 }
 
 }  // namespace mopo

@@ -49,9 +49,10 @@ struct WgradArgs {
   float* logs;
   int64_t* iter;
   int prior;                         // action_prior 'normal': the policy loss logs - log N(a; 0, I)
-  const float* eps_s;                // [n][A] the step's policy noise of pi(s) (for the action)
+  const float* eps_s;                // [n][EPW] the step's policy noise of pi(s) (for the action)
   Stamps st;
-  const unsigned* sync_tmo;          // the fused F2 + B1 launch's sticky timeout word, or NULL
+  const unsigned* sync_tmo;          // a fused launch's sticky timeout word, or NULL
+  unsigned* sync_reset; int n_sync;  // F1 + F2 + B1 fused: the loss tail zeroes the next step's counters
 };
 
 // Block 0: per-row loss terms of all n rows (thread t: rows t, t + 1024, ...), block sums in a fixed order
@@ -61,6 +62,7 @@ static __device__ __forceinline__ void wgrad_loss_tail(const WgradArgs& a, float
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   const int n = a.n, A = a.A;
   const AdamCtx& ad = a.ad;
+  if (a.sync_reset && tid < a.n_sync) a.sync_reset[tid * SYNC_STRIDE] = 0u;   // read by the next launch only
   AdamIn al{0.f, 0.f, 0.f, 0.f};
   float lr_t = 0.f;
   if (tid == 0) {
@@ -76,12 +78,12 @@ static __device__ __forceinline__ void wgrad_loss_tail(const WgradArgs& a, float
     const RowIn in = row_losses_load(a.L, n, a.ncq, r, on);
     const float lps = bload(dlp, on ? lp_idx(r) : -1);
     float lsv[8], muv[8], epv[8];
-    const auto dep = rsrc(a.eps_s, (int64_t)n * A);
+    const auto dep = rsrc(a.eps_s, (int64_t)n * EPW);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       lsv[j] = bload(dls, (on && j < A) ? r * 2 * A + A + j : -1);
       muv[j] = bload(dls, (a.prior && on && j < A) ? r * 2 * A + j : -1);
-      epv[j] = bload(dep, (a.prior && on && j < A) ? r * A + j : -1);
+      epv[j] = bload(dep, (a.prior && on && j < A) ? r * EPW + j : -1);
     }
     if (!on) continue;
     const RowQ o = row_losses(a.L, in);

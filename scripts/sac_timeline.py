@@ -33,9 +33,12 @@ def main():
     st = buf.reshape(4, 1024, 8).astype(np.int64)
     t0 = st[0, :256, 0].min()
     us = lambda x: (x - t0) * 0.01
-    fused = (st[1, 256:512, 0] > 0).any()
+    fused = (st[1, 256:512, 0] > 0).any() or (st[0, 256:768, 0] > 0).any()
     groups = [('F1', st[0, :256])]
-    if fused:
+    if (st[0, 256:768, 0] > 0).any():     # F1 + F2 + B1 in one launch: all in slot 0
+        groups = [('F1 (fused)', st[0, :256]), ('F2 (fused)', st[0, 256:512]), ('B1 step/gather (fused)', st[0, 512:576]),
+                  ('B1 critic dh1 (fused)', st[0, 576:704]), ('B1 policy rows (fused)', st[0, 704:768])]
+    elif fused:
         groups += [('F2 (fused)', st[1, :256]), ('B1 step/gather (fused)', st[1, 256:320]),
                    ('B1 critic dh1 (fused)', st[1, 320:448]), ('B1 policy rows (fused)', st[1, 448:512])]
     else:
@@ -43,7 +46,7 @@ def main():
                    ('B1 policy rows', st[2, 192:256])]
     nb = int((st[3, :, 0] > 0).sum())
     groups += [('B2 loss tail', st[3, :1]), ('B2 tiles', st[3, 1:nb])]
-    print('SAC step timeline (%s), us after the first F1 start' % ('fused F2 + B1' if fused else 'separate launches'))
+    print('SAC step timeline (%s), us after the first F1 start' % (os.environ.get('MOPO_SAC_FUSE', 'default fusion')))
     for name, g in groups:
         g = g[g[:, 0] > 0]
         if not len(g):

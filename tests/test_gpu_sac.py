@@ -366,10 +366,10 @@ def test_sac_nonsquare_hidden_steps_vs_oracle():
 
 
 @pytest.mark.parametrize('o,a,h,n', [(17, 6, 256, 256), (11, 3, 64, 100)])
-def test_sac_fused_f2b1_bit_identical_to_separate_launches(o, a, h, n, monkeypatch):
-    """The fused F2 + B1 launch (sac_rows.h sac_f2b1_kernel: an in-launch row-block hand-off instead of a
-    kernel boundary) computes exactly the separate launches' arithmetic, so 300 graph-replayed steps must
-    end bit-identical to MOPO_SAC_FUSE=0 -- any stale read of a handed-off line (L1 / L2 non-coherence,
+def test_sac_fused_launches_bit_identical_to_separate_launches(o, a, h, n, monkeypatch):
+    """The fused launches (sac_rows.h sac_f2b1_kernel: F2 + B1, sac_f12b1_kernel: F1 + F2 + B1, with
+    in-launch row-block hand-offs instead of kernel boundaries) compute exactly the separate launches'
+    arithmetic, so 300 graph-replayed steps must end bit-identical to MOPO_SAC_FUSE=0 -- any stale read of a handed-off line (L1 / L2 non-coherence,
     sac_rows.h handoff_wait) would show as a difference -- and the logs must stay finite (a consumer that
     gave up waiting poisons them)."""
     import torch
@@ -388,7 +388,7 @@ def test_sac_fused_f2b1_bit_identical_to_separate_launches(o, a, h, n, monkeypat
         pl.append(p)
     fl = flat(osac.init_params(o, a, h, seed=3)).astype(np.float32)
     out = {}
-    for fuse in ('0', '1'):
+    for fuse in ('0', '1', '2'):
         monkeypatch.setenv('MOPO_SAC_FUSE', fuse)
         sac = SAC(o, a, h, batch_size=n, real_ratio=0.05, target_entropy=-3, params=fl)
         sac._do_training(0, pl[0], pl[1], n_steps=300, seed=19)
@@ -396,5 +396,6 @@ def test_sac_fused_f2b1_bit_identical_to_separate_launches(o, a, h, n, monkeypat
         lg = sac.logs()
         assert all(np.isfinite(v) for v in lg.values()), (fuse, lg)
         out[fuse] = {k: v.cpu().numpy() for k, v in sac.state_dict().items()}
-    for k in out['0']:
-        np.testing.assert_array_equal(out['1'][k], out['0'][k], err_msg=k)
+    for f in ('1', '2'):
+        for k in out['0']:
+            np.testing.assert_array_equal(out[f][k], out['0'][k], err_msg='MOPO_SAC_FUSE=%s %s' % (f, k))
