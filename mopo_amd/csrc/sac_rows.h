@@ -115,6 +115,12 @@ static __device__ __forceinline__ void hstore(float* p, float v) {
 // on a give-up it sets the sticky timeout word, which the loss tail turns into NaN logs.
 constexpr unsigned SAC_SPIN_LIMIT = 1u << 19;
 constexpr int SYNC_STRIDE = 32;      // one counter per 128-B line: counter c at sync[c * SYNC_STRIDE]
+#ifndef MOPO_SAC_B1_LATE
+// 1: in the F1 + F2 + B1 launch a B1 block waits for its row block's F1 blocks before issuing ANY operand
+// (its loads then do not compete with F1's); 0: it prefetches the weights first
+#define MOPO_SAC_B1_LATE 1
+#endif
+constexpr bool B1_LATE = MOPO_SAC_B1_LATE != 0;
 // the counters of one row block rb: sync[(SYNC_N rb + class) SYNC_STRIDE]; the timeout word after the last
 enum { SYNC_PI_S = 0, SYNC_PI_N = 1, SYNC_Q_SA = 2, SYNC_F2_MAIN = 3, SYNC_F2_TGT = 4, SYNC_N = 5 };
 static __device__ __forceinline__ unsigned* sync_at(unsigned* sync, int rb, int c) {
@@ -206,6 +212,8 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
     }
   };
   if constexpr (FZ == 0) handed();
+  if constexpr (FZ == 2 && B1_LATE)   // F1's pi(s) blocks of this row block first, then every operand
+    handoff_wait(sync_at(sync, rb, SYNC_PI_S), (unsigned)c.ncq, sync + SYNC_N * nrb * SYNC_STRIDE);
   const float la = *c.log_alpha;
   float b3v[2];
 #pragma unroll
@@ -233,7 +241,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
       for (int s2 = 0; s2 < 4; ++s2) h2v[q][s2] = bload(dh2, on ? (r0 + 4 * lk + s2) * H + c2 : -1);  // rows >= n: 0
     }
   };
-  if constexpr (FZ < 2) f1_loads();
+  if constexpr (FZ < 2 || B1_LATE) f1_loads();
   const int j0 = cq * pcols + w * 16, col = j0 + li;
   const bool tile_on = j0 < H;
   const auto dw2 = rsrc(c.W2p, (int64_t)H * H);
@@ -250,11 +258,11 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
 #pragma unroll
     for (int i = 0; i < 4; ++i) m1[i] = bload(dm1, col < H ? (r0 + 4 * lk + i) * H + col : -1);
   };
-  if constexpr (FZ < 2) m1_loads();
+  if constexpr (FZ < 2 || B1_LATE) m1_loads();
   if constexpr (FZ >= 1) {
     unsigned* tmo = sync + SYNC_N * nrb * SYNC_STRIDE;
     stamp(st, 5);
-    if constexpr (FZ == 2) {
+    if constexpr (FZ == 2 && !B1_LATE) {
       handoff_wait(sync_at(sync, rb, SYNC_PI_S), (unsigned)c.ncq, tmo);
       f1_loads();
       m1_loads();
@@ -922,6 +930,8 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
   const int n = a.n, H = a.H;
   const int i0 = rb * 16, c0 = cq * B1_COLS, jw = c0 + w * 16;
   const int li = lane & 15, lk = lane >> 4;
+  if constexpr (FZ == 2 && B1_LATE)   // F1's Q(s, a) blocks of this row block first, then every operand
+    handoff_wait(sync_at(a.sync, rb, SYNC_Q_SA), 2u * (unsigned)a.ncq, a.sync + SYNC_N * a.nrb * SYNC_STRIDE);
   // ---- 0. the dq of the block's 16 rows first (the partials of F1 / F2; one lane per row): the A slab
   //         below waits on it (fused: after the wait below)
   RowIn rin{};
@@ -944,7 +954,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) m1[rr] = bload(dm1, (jw + li < H && i0 + 4 * lk + rr < n) ? (i0 + 4 * lk + rr) * H + jw + li : -1);
   };
-  if constexpr (FZ < 2) f1_loads();
+  if constexpr (FZ < 2 || B1_LATE) f1_loads();
   const f32x4 w3v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                   rsrc(p.w3, H), ((slab && am < H) ? am : -4) * 4, 0, 0));
   const auto dw2 = rsrc(p.w2, (int64_t)H * H);
@@ -958,7 +968,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
   if constexpr (FZ >= 1) {            // the targets' partials and logp(s') come from this launch's F2 blocks
     unsigned* tmo = a.sync + SYNC_N * a.nrb * SYNC_STRIDE;
     stamp(a.st, 5);
-    if constexpr (FZ == 2) {          // ... and the Q(s, a) activations from its F1 blocks
+    if constexpr (FZ == 2 && !B1_LATE) {   // ... and the Q(s, a) activations from its F1 blocks
       handoff_wait(sync_at(a.sync, rb, SYNC_Q_SA), 2u * (unsigned)a.ncq, tmo);
       f1_loads();
     }
