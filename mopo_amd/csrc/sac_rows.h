@@ -117,8 +117,9 @@ constexpr unsigned SAC_SPIN_LIMIT = 1u << 19;
 constexpr int SYNC_STRIDE = 32;      // one counter per 128-B line: counter c at sync[c * SYNC_STRIDE]
 #ifndef MOPO_SAC_B1_LATE
 // 1: in the F1 + F2 + B1 launch a B1 block waits for its row block's F1 blocks before issuing ANY operand
-// (its loads then do not compete with F1's); 0: it prefetches the weights first
-#define MOPO_SAC_B1_LATE 1
+// (its loads then do not compete with F1's); 0: it prefetches the weights first -- measured 37.9-38.0 vs
+// 39.6-39.9 us/step for 1 (profiles/r05_sac_ab_fused.txt): the prefetch matters more than F1's slowdown
+#define MOPO_SAC_B1_LATE 0
 #endif
 constexpr bool B1_LATE = MOPO_SAC_B1_LATE != 0;
 // the counters of one row block rb: sync[(SYNC_N rb + class) SYNC_STRIDE]; the timeout word after the last
