@@ -77,7 +77,8 @@ struct Sac {
   uint64_t* stamps = nullptr;     // MOPO_SAC_STAMPS builds: [slot][block][8]
   unsigned* sync = nullptr;       // fused F2 + B1 launch: [nrb][2] row-block counters, then the timeout word
                                   //   (each on its own 128-B line: sac_rows.h SYNC_STRIDE)
-  int fuse = 2;                   // 0: F1, F2, B1 separate; 1: F2 + B1 one launch; 2: F1 + F2 + B1 one launch
+  int fuse = 2;                   // 0: F1, F2, B1 separate; 1: F2 + B1 one launch; 2: F1 + F2 + B1 one launch;
+                                  // 3: the whole step (+ the weight gradients and the loss tail) one launch
   float *dhead, *dh2p, *dh1p;
   // graph
   bool use_graph = true;
@@ -169,13 +170,14 @@ static int launch_gather(Sac* h, int par, const mopo_pool_desc* env, const mopo_
 // Pb[1 - par].  With `prefetch`, B1 also gathers the next step's batch into bt[1 - par] (a separate
 // gather launch, or a forked graph branch, costs more than it hides).
 #ifndef MOPO_SAC_FUSE
-#define MOPO_SAC_FUSE 2   // 0: F1, F2, B1 as three launches; 1: F2 + B1 fused; 2: F1 + F2 + B1 fused (the
-                          // environment variable MOPO_SAC_FUSE overrides it at mopo_sac_create)
+#define MOPO_SAC_FUSE 2   // 0: F1, F2, B1 as three launches; 1: F2 + B1 fused; 2: F1 + F2 + B1 fused; 3: the
+                          // whole step as one launch (the environment variable MOPO_SAC_FUSE overrides it at
+                          // mopo_sac_create; 3 needs batch <= 256, else 2)
 #endif
 static int sac_fuse_default() {
   const char* e = std::getenv("MOPO_SAC_FUSE");
   const int v = e ? std::atoi(e) : MOPO_SAC_FUSE;
-  return v < 0 ? 0 : v > 2 ? 2 : v;
+  return v < 0 ? 0 : v > 3 ? 3 : v;
 }
 
 static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
@@ -264,8 +266,9 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
   }
   // ---- B1: per-row TD targets and dq -> Q1/Q2(s,a) dh1; the policy's row-local backward chain; the
   //      step control; the gather of the next step's batch (with `prefetch`)
+  Dh1Args b1a{};
   {
-    Dh1Args d{};
+    Dh1Args& d = b1a;
     const int ncq1 = ceil_div(H, B1_COLS);
     d.n = n; d.H = H; d.A = A; d.ncq = ncq; d.ncq1 = ncq1; d.nrb = nrb;
     for (int i = 0; i < 2; ++i) {
@@ -290,12 +293,14 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
       d.ga = gather_args(h, 1 - par, env, mod, seed, nullptr);
       d.ga.iter_add = 1;                       // the next step's batch (the counter advances in B2)
     }
-    d.st = Stamps{h->stamps, h->fuse == 2 ? 0 : h->fuse ? 1 : 2};
+    d.st = Stamps{h->stamps, h->fuse >= 2 ? 0 : h->fuse ? 1 : 2};
     d.sync = h->sync;
     if (ncq1 * nrb < 2 && prefetch) return fail("sac: B1 needs at least one gather block");
     static_assert(B1_COLS == RB_COLS && B1_WAVES == 4, "the fused launches share the F1 / F2 grid");
-    if (h->fuse == 2) {
-      f2.st = Stamps{h->stamps, 0};
+    f2.st = Stamps{h->stamps, h->fuse >= 2 ? 0 : 1};
+    if (h->fuse == 3) {
+      // the single-launch step: launched below, with the weight-gradient blocks
+    } else if (h->fuse == 2) {
       hipLaunchKernelGGL(sac_f12b1_kernel, dim3(ncq, nrb, 12), dim3(256), 0, s, f1, f2, d);
     } else if (h->fuse == 1) {
       hipLaunchKernelGGL(sac_f2b1_kernel, dim3(ncq, nrb, 8), dim3(256), 0, s, f2, d);
@@ -323,6 +328,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     ps.push_back(wprob(H, A, h->h2[0], H, h->dhead + A, 2 * A, G + o.pWl, A, G + o.pbl));
     ps.push_back(wprob(O, H, bt.sa, W, h->dh1p, H, G + o.pW1, H, G + o.pb1));
     if ((int)ps.size() > WG_MAXP) return fail("sac: too many weight-gradient problems");
+    for (size_t i = 0; i < ps.size(); ++i) ps[i].cls = i < 6 ? 0 : 1;   // critics' (B1 critic blocks) / the policy's
     int tot = 0;
     for (size_t i = 0; i < ps.size(); ++i) {
       g.p[i] = ps[i];
@@ -336,12 +342,17 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     g.ad.slot0 = 0;
     g.L = L; g.A = A; g.ncq = ncq; g.tent = h->tent; g.logs = h->logs; g.iter = h->iter;
     g.prior = h->prior; g.eps_s = h->eps_s;
-    g.sync_tmo = h->fuse ? h->sync + SYNC_N * nrb * SYNC_STRIDE : nullptr;
+    g.sync_tmo = h->fuse ? h->sync + (SYNC_N * nrb + SYNC_TMO) * SYNC_STRIDE : nullptr;
     if (h->fuse == 2) { g.sync_reset = h->sync; g.n_sync = SYNC_N * nrb; }
-    g.st = Stamps{h->stamps, 3};
+    g.st = Stamps{h->stamps, h->fuse == 3 ? 0 : 3};
     if (tot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
     h->nslots = tot;
-    hipLaunchKernelGGL(sac_wgrad_kernel, dim3(1 + tot), dim3(1024), 0, s, g);
+    if (h->fuse == 3) {
+      const int zb2 = ceil_div(1 + tot, ncq * nrb);
+      hipLaunchKernelGGL(sac_step_kernel, dim3(ncq, nrb, 12 + zb2), dim3(256), 0, s, f1, f2, b1a, g);
+    } else {
+      hipLaunchKernelGGL(sac_wgrad_kernel, dim3(1 + tot), dim3(1024), 0, s, g);
+    }
     MOPO_HIP(hipGetLastError());
   }
   return 0;
@@ -395,8 +406,9 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   }
   for (int i = 0; i < 8; ++i) { f(&h->h1[i], n * H); f(&h->h2[i], n * H); f(&h->out[i], n * 2 * A); }
   f(&h->logp_s, 2 * ns); f(&h->logp_n, 2 * ns); f(&h->eps_s, ns * EPW); f(&h->eps_n, ns * EPW);
-  reg.push_back({(void**)&h->sync, (size_t)(SYNC_N * (ns / 16) + 1) * SYNC_STRIDE * 4});
+  reg.push_back({(void**)&h->sync, (size_t)(SYNC_N * (ns / 16) + SYNC_GLOBAL) * SYNC_STRIDE * 4});
   h->fuse = sac_fuse_default();
+  if (h->fuse == 3 && batch > WG_KC) h->fuse = 2;   // the single-launch tiles stage one K chunk
   for (int i = 0; i < 4; ++i) { f(&h->dq[i], n); f(&h->dh1[i], n * H); }
   f(&h->dhead, n * 2 * A); f(&h->dh2p, n * H); f(&h->dh1p, n * H);
   size_t total = 0;

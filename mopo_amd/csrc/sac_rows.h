@@ -123,7 +123,12 @@ constexpr int SYNC_STRIDE = 32;      // one counter per 128-B line: counter c at
 #endif
 constexpr bool B1_LATE = MOPO_SAC_B1_LATE != 0;
 // the counters of one row block rb: sync[(SYNC_N rb + class) SYNC_STRIDE]; the timeout word after the last
-enum { SYNC_PI_S = 0, SYNC_PI_N = 1, SYNC_Q_SA = 2, SYNC_F2_MAIN = 3, SYNC_F2_TGT = 4, SYNC_N = 5 };
+// F1 blocks: pi(s), pi(s'), Q(s, a); F2: main / target critics; B1: step control + gather, critic dh1, policy rows
+enum { SYNC_PI_S = 0, SYNC_PI_N = 1, SYNC_Q_SA = 2, SYNC_F2_MAIN = 3, SYNC_F2_TGT = 4, SYNC_B1_CTL = 5, SYNC_B1_Q = 6,
+       SYNC_B1_PI = 7, SYNC_N = 8 };
+// global words after the per-row-block counters (x SYNC_STRIDE): the sticky timeout word, then the single-launch
+// step's count of finished weight-gradient tiles
+enum { SYNC_TMO = 0, SYNC_B2_DONE = 1, SYNC_GLOBAL = 2 };
 static __device__ __forceinline__ unsigned* sync_at(unsigned* sync, int rb, int c) {
   return sync + (SYNC_N * rb + c) * SYNC_STRIDE;
 }
@@ -135,6 +140,32 @@ static __device__ __forceinline__ void handoff_signal(unsigned* cnt) {
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// the same wait over ONE class of every row block (lane r of wave 0 polls row block r's counter, nrb <= 64)
+static __device__ __forceinline__ void handoff_wait_rows(unsigned* sync, int nrb, int cls, unsigned target,
+                                                         unsigned* tmo) {
+  if (threadIdx.x < 64) {
+    const int r = threadIdx.x;
+    unsigned spins = 0;
+    while (true) {
+      const unsigned v = r < nrb ? __hip_atomic_load(sync + (SYNC_N * r + cls) * SYNC_STRIDE, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) : target;
+      if (__all(v >= target)) break;
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > SAC_SPIN_LIMIT) {
+        if (r == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+#if MOPO_SAC_FUSE_ACQ
+    if (r == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#endif
+  }
+  __syncthreads();
+}
+
 static __device__ __forceinline__ void handoff_wait(unsigned* cnt, unsigned target, unsigned* tmo) {
   if (threadIdx.x == 0) {
     unsigned spins = 0;
@@ -213,7 +244,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
     }
   };
   if constexpr (FZ == 0) handed();
-  if constexpr (FZ == 2 && B1_LATE)   // F1's pi(s) blocks of this row block first, then every operand
+  if constexpr (FZ >= 2 && B1_LATE)   // F1's pi(s) blocks of this row block first, then every operand
     handoff_wait(sync_at(sync, rb, SYNC_PI_S), (unsigned)c.ncq, sync + SYNC_N * nrb * SYNC_STRIDE);
   const float la = *c.log_alpha;
   float b3v[2];
@@ -263,7 +294,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   if constexpr (FZ >= 1) {
     unsigned* tmo = sync + SYNC_N * nrb * SYNC_STRIDE;
     stamp(st, 5);
-    if constexpr (FZ == 2 && !B1_LATE) {
+    if constexpr (FZ >= 2 && !B1_LATE) {
       handoff_wait(sync_at(sync, rb, SYNC_PI_S), (unsigned)c.ncq, tmo);
       f1_loads();
       m1_loads();
@@ -308,8 +339,8 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
       dls = -g + dstd * sd;
       if (!(raw >= -20.f && raw <= 2.f)) dls = 0.f;                 // clip_by_value grad
       if (cq == 0) {
-        c.dhead[(int64_t)hrow * 2 * A + hj] = dmu;
-        c.dhead[(int64_t)hrow * 2 * A + A + hj] = dls;
+        hstore<FZ == 3>(&c.dhead[(int64_t)hrow * 2 * A + hj], dmu);
+        hstore<FZ == 3>(&c.dhead[(int64_t)hrow * 2 * A + A + hj], dls);
       }
     }
     dmu_s[tid] = dmu;
@@ -336,7 +367,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
           const int row = 4 * lk + i;
           const float v = h2v[q][i] > 0.f ? d[i] : 0.f;
           S[row * HS + c2] = v;
-          if (cq == 0 && r0 + row < n) c.dh2p[(int64_t)(r0 + row) * H + c2] = v;
+          if (cq == 0 && r0 + row < n) hstore<FZ == 3>(&c.dh2p[(int64_t)(r0 + row) * H + c2], v);
         }
       }
     }
@@ -358,7 +389,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
     const int row = r0 + 4 * lk + i;                                // D: col li, row 4 lk + i
     if (row < n && col < H) {
       const float v = acc[0][i] + acc[1][i] + acc[2][i] + acc[3][i];
-      c.dh1p[(int64_t)row * H + col] = m1[i] > 0.f ? v : 0.f;
+      hstore<FZ == 3>(&c.dh1p[(int64_t)row * H + col], m1[i] > 0.f ? v : 0.f);
     }
   }
 }
@@ -457,7 +488,7 @@ static __device__ __forceinline__ float rows_head(const FwdHead& h, const HeadIn
         - 2.f * (0.6931471805599453f - u - softplusf(-2.f * u));    // squash correction (:292)
     act = tanhf(u);
     if (store) {
-      if (h.eps_in[nxt]) h.eps_out[nxt][r * EPW + j] = z;   // (B1 reads the injected noise itself)
+      if (h.eps_in[nxt]) hstore<SC1>(&h.eps_out[nxt][r * EPW + j], z);   // (B1 reads the injected noise itself)
       hstore<SC1>(&h.head_out[nxt][r * 2 * A + j], mu);
       hstore<SC1>(&h.head_out[nxt][r * 2 * A + A + j], raw);
     }
@@ -579,7 +610,7 @@ struct FwdLds {
 // its weight operands, then waits for its row block's pi blocks of F1 before loading the head's partials.
 template <bool HEAD, int FZ>
 static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int rb, int ii, FwdLds& L) {
-  constexpr bool SC = HEAD ? FZ >= 1 : FZ == 2;   // this block's stores are handed over in-launch
+  constexpr bool SC = HEAD ? FZ >= 1 : FZ >= 2;   // this block's stores are handed over in-launch
   float* As = L.As;
   float* Ts = L.Ts;
   float* Wo = L.Wo;
@@ -657,7 +688,7 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   if (!HEAD && ii < 2 && cq == 0 && ((a.hd.gen_eps >> ii) & 1) && tid < 128 && hj < A && hrow < n)
     hstore<SC>(&a.hd.eps_out[ii][hrow * EPW + hj], head_noise(a.hd.seed, *a.hd.iter, hrow, ii, hj));
   // ---- F2 inside the F1 + F2 + B1 launch: the head's partials once the row block's pi blocks are done
-  if constexpr (HEAD && FZ == 2) {
+  if constexpr (HEAD && FZ >= 2) {
     stamp(a.st, 5);
     handoff_wait(sync_at(a.sync, rb, p.head == 0 ? SYNC_PI_S : SYNC_PI_N), (unsigned)a.ncq, a.sync + SYNC_N * a.nrb * SYNC_STRIDE);
     stamp(a.st, 6);
@@ -871,23 +902,24 @@ struct Dh1Args {
   int gather;                        // 1: the other z = 0 blocks gather the next step's batch (ga)
   GatherArgs ga;
   Stamps st;
-  unsigned* sync;                    // fused F2 + B1: the F2 counters ([nrb][2]) and the timeout word [2 nrb]
+  unsigned* sync;                    // fused launches: the row-block counters (sync_at) and the global words
 };
 
 // Block 0: the step's scalar control -- TF1 Adam's step size from the beta powers (every Adam of the step
 // shares it: identical step counts), the beta powers of the next step, and whether this step's timestep
 // moves the targets (mopo.py:780-799, 843-845: n_train_repeat steps share one timestep).  The step counter
 // itself advances in the loss tail of the next launch (sac_wgrad.h), after every reader of this step's.
+template <bool SC>
 static __device__ __forceinline__ void step_control(const Dh1Args& a) {
   if (threadIdx.x != 0) return;
   const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
   const int64_t it = *a.iter, base = a.tctl[0];
   const int64_t rep = a.tctl[1] > 0 ? a.tctl[1] : 1, every = a.tctl[2] > 0 ? a.tctl[2] : 1;
-  a.beta_pow[2] = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);             // TF1 Adam step size
+  hstore<SC>(&a.beta_pow[2], a.lr * sqrtf(1.f - b2p) / (1.f - b1p));   // TF1 Adam step size
   a.beta_pow[0] = b1p * 0.9f;
   a.beta_pow[1] = b2p * 0.999f;
   const int64_t ts = (it - base) / rep;
-  a.beta_pow[3] = ((ts % every) + every) % every == 0 ? 1.f : 0.f;
+  hstore<SC>(&a.beta_pow[3], ((ts % every) + every) % every == 0 ? 1.f : 0.f);
 }
 
 // LDS of one B1 workgroup
@@ -903,7 +935,7 @@ struct Dh1Lds {
 // launches, then wait for their row block's F2 producers before loading what F2 wrote; FZ = 2 (F1 + F2 + B1)
 // also waits for the row block's F1 blocks before loading F1's activations (h1, h2).
 template <int FZ>
-static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y, int z, Dh1Lds& S) {
+static __device__ __forceinline__ void dh1_block(const Dh1Args a, int x, int y, int z, Dh1Lds& S) {
   float* As = S.As;
   float* Ts = S.Ts;
   float* dqs = S.dqs;
@@ -912,17 +944,19 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
   if (z == 0) {
     const int zb = x + a.ncq1 * y;
     if (zb == 0) {
-      step_control(a);
+      step_control<FZ == 3>(a);
     } else if (a.gather) {
       const GatherArgs& g = a.ga;
       const int C = 2 * g.O + g.A + 2, tot = g.n * C, stride = (a.ncq1 * a.nrb - 1) * (int)blockDim.x;
       for (int e = (zb - 1) * blockDim.x + tid; e < tot; e += stride) gather_elem(g, e / C, e % C);
     }
+    if constexpr (FZ == 3) handoff_signal(sync_at(a.sync, y, SYNC_B1_CTL));   // read iter / wrote lr_t
     stamp(a.st, 4);
     return;
   }
   if (z == 3) {                       // the policy-row blocks: the action-gradient partials came from F2
     policy_rows_block<FZ>(a.pr, y * a.ncq1 + x, As, Ts, a.st, a.sync, a.nrb);
+    if constexpr (FZ == 3) handoff_signal(sync_at(a.sync, y, SYNC_B1_PI));
     stamp(a.st, 4);
     return;
   }
@@ -931,7 +965,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
   const int n = a.n, H = a.H;
   const int i0 = rb * 16, c0 = cq * B1_COLS, jw = c0 + w * 16;
   const int li = lane & 15, lk = lane >> 4;
-  if constexpr (FZ == 2 && B1_LATE)   // F1's Q(s, a) blocks of this row block first, then every operand
+  if constexpr (FZ >= 2 && B1_LATE)   // F1's Q(s, a) blocks of this row block first, then every operand
     handoff_wait(sync_at(a.sync, rb, SYNC_Q_SA), 2u * (unsigned)a.ncq, a.sync + SYNC_N * a.nrb * SYNC_STRIDE);
   // ---- 0. the dq of the block's 16 rows first (the partials of F1 / F2; one lane per row): the A slab
   //         below waits on it (fused: after the wait below)
@@ -969,7 +1003,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
   if constexpr (FZ >= 1) {            // the targets' partials and logp(s') come from this launch's F2 blocks
     unsigned* tmo = a.sync + SYNC_N * a.nrb * SYNC_STRIDE;
     stamp(a.st, 5);
-    if constexpr (FZ == 2 && !B1_LATE) {   // ... and the Q(s, a) activations from its F1 blocks
+    if constexpr (FZ >= 2 && !B1_LATE) {   // ... and the Q(s, a) activations from its F1 blocks
       handoff_wait(sync_at(a.sync, rb, SYNC_Q_SA), 2u * (unsigned)a.ncq, tmo);
       f1_loads();
     }
@@ -983,7 +1017,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
     if (i0 + tid < n) {
       const RowQ rq = row_losses(a.L, rin);
       dq = ((p.kind == 0 ? rq.q[0] : rq.q[1]) - rq.y) * (1.f / (float)n);
-      if (cq == 0) p.dq[i0 + tid] = dq;
+      if (cq == 0) hstore<FZ == 3>(&p.dq[i0 + tid], dq);
     }
     dqs[tid] = dq;
   }
@@ -1012,8 +1046,9 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args& a, int x, int y,
   for (int rr = 0; rr < 4; ++rr) {
     const int orow = i0 + 4 * lk + rr;
     const float v = (col < H && orow < n && m1[rr] > 0.f) ? acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr] : 0.f;
-    if (orow < n && col < H) p.dh1[(int64_t)orow * H + col] = v;
+    if (orow < n && col < H) hstore<FZ == 3>(&p.dh1[(int64_t)orow * H + col], v);
   }
+  if constexpr (FZ == 3) handoff_signal(sync_at(a.sync, rb, SYNC_B1_Q));
   stamp(a.st, 4);
 }
 

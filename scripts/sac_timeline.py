@@ -44,8 +44,11 @@ def main():
     else:
         groups += [('F2', st[1, :256]), ('B1 step/gather', st[2, :64]), ('B1 critic dh1', st[2, 64:192]),
                    ('B1 policy rows', st[2, 192:256])]
-    nb = int((st[3, :, 0] > 0).sum())
-    groups += [('B2 loss tail', st[3, :1]), ('B2 tiles', st[3, 1:nb])]
+    if os.environ.get('MOPO_SAC_FUSE') == '3':   # the whole step in slot 0: B2 blocks from 768 on
+        groups += [('B2 loss tail (fused)', st[0, 768:769]), ('B2 tiles (fused)', st[0, 769:1024])]
+    else:
+        nb = int((st[3, :, 0] > 0).sum())
+        groups += [('B2 loss tail', st[3, :1]), ('B2 tiles', st[3, 1:nb])]
     print('SAC step timeline (%s), us after the first F1 start' % (os.environ.get('MOPO_SAC_FUSE', 'default fusion')))
     for name, g in groups:
         g = g[g[:, 0] > 0]

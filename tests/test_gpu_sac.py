@@ -388,7 +388,7 @@ def test_sac_fused_launches_bit_identical_to_separate_launches(o, a, h, n, monke
         pl.append(p)
     fl = flat(osac.init_params(o, a, h, seed=3)).astype(np.float32)
     out = {}
-    for fuse in ('0', '1', '2'):
+    for fuse in ('0', '1', '2', '3'):
         monkeypatch.setenv('MOPO_SAC_FUSE', fuse)
         sac = SAC(o, a, h, batch_size=n, real_ratio=0.05, target_entropy=-3, params=fl)
         sac._do_training(0, pl[0], pl[1], n_steps=300, seed=19)
@@ -396,6 +396,6 @@ def test_sac_fused_launches_bit_identical_to_separate_launches(o, a, h, n, monke
         lg = sac.logs()
         assert all(np.isfinite(v) for v in lg.values()), (fuse, lg)
         out[fuse] = {k: v.cpu().numpy() for k, v in sac.state_dict().items()}
-    for f in ('1', '2'):
+    for f in ('1', '2', '3'):
         for k in out['0']:
             np.testing.assert_array_equal(out[f][k], out['0'][k], err_msg='MOPO_SAC_FUSE=%s %s' % (f, k))
