@@ -166,6 +166,41 @@ static __device__ __forceinline__ void handoff_wait_rows(unsigned* sync, int nrb
   __syncthreads();
 }
 
+// wave 0 polls two classes of every row block (lane r: row block r; nrb <= 64) and, when ctl_target > 0, the
+// step-control counter of row block 0, with a long sleep between polls (for blocks that expect to wait long);
+// ONE acquire when all are done (acq = false: none -- the caller reads nothing the producers wrote)
+static __device__ __forceinline__ void handoff_wait_all(unsigned* sync, int nrb, int c1, unsigned t1, int c2,
+                                                        unsigned t2, unsigned ctl_target, unsigned* tmo, bool acq) {
+  if (threadIdx.x < 64) {
+    const int r = threadIdx.x;
+    unsigned spins = 0;
+    while (true) {
+      bool ok = true;
+      if (r < nrb) {
+        ok = __hip_atomic_load(sync + (SYNC_N * r + c1) * SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= t1 &&
+             (t2 == 0u || __hip_atomic_load(sync + (SYNC_N * r + c2) * SYNC_STRIDE, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT) >= t2);
+        if (r == 0 && ctl_target)
+          ok = ok && __hip_atomic_load(sync + SYNC_B1_CTL * SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                         ctl_target;
+      }
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(8);
+      if (++spins > SAC_SPIN_LIMIT) {
+        if (r == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+#if MOPO_SAC_FUSE_ACQ
+    if (r == 0 && acq) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#endif
+  }
+  __syncthreads();
+}
+
 static __device__ __forceinline__ void handoff_wait(unsigned* cnt, unsigned target, unsigned* tmo) {
   if (threadIdx.x == 0) {
     unsigned spins = 0;

@@ -285,6 +285,7 @@ struct Wg4Lds {
 static __device__ __forceinline__ void wgrad_tile4(const WgradArgs g, int bid, Wg4Lds& L, unsigned* sync, int nrb,
                                                    int ncq) {
   unsigned* tmo = sync + (SYNC_N * nrb + SYNC_TMO) * SYNC_STRIDE;
+  stamp(g.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int pi = 0;
   while (pi + 1 < g.np && bid >= g.prefix[pi + 1]) ++pi;
@@ -311,10 +312,34 @@ static __device__ __forceinline__ void wgrad_tile4(const WgradArgs g, int bid, W
   const int64_t c_idx = p.colsum ? (int64_t)(p.colsum - ad.G) + min(gj, p.N - 1) : 0;
   AdamIn c_in{0.f, 0.f, 0.f, 0.f};
   if (c_on) c_in = adam_load(ad, c_idx);
-  // ---- the A panel once F1 is done for every row block (element e = tid + 256 q: row e % 32, k e / 32)
-  handoff_wait_rows(sync, nrb, SYNC_PI_S, (unsigned)ncq, tmo);
-  handoff_wait_rows(sync, nrb, SYNC_Q_SA, 2u * (unsigned)ncq, tmo);
+  // ---- B1 done for every row block (so F1 and F2 too: B1's blocks waited on them) and the step control
+  //      (lr_t, the target flag): ONE acquire, then the A panel (element e = tid + 256 q: row e % 32, k e / 32)
+  stamp(g.st, 5);
+  handoff_wait_all(sync, nrb, p.cls ? SYNC_B1_PI : SYNC_B1_Q, p.cls ? (unsigned)ncq : 2u * (unsigned)ncq,
+                   p.cls ? SYNC_B1_Q : SYNC_B1_PI, 0u, (unsigned)ncq, tmo, true);
+  stamp(g.st, 6);
   const auto dA = rsrc(p.A, (int64_t)(n - 1) * p.lda + p.M);
+  const float lr_t = *ad.lr_t;
+  const bool r1 = p.bu != nullptr;
+  const auto dB = rsrc(r1 ? p.bm : p.B, (int64_t)(n - 1) * (r1 ? p.bldm : p.ldb) + p.N);
+  const auto dU = rsrc(p.bu, r1 ? n : 0);
+  const float bv = r1 ? bload(rsrc(p.bv, p.N), gj) : 0.f;
+  // B of K quarters kq0, kq0 + 1 straight into registers (a rank-1 masked B: the mask operand and dq, both
+  // loaded unconditionally so no load waits on another)
+  float vb[2][4][4], vu[2][4][4];
+  auto load_b = [&](int kq0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = 64 * (kq0 + h) + 16 * lk + 4 * s2 + u;
+          vb[h][s2][u] = bload(dB, k * (r1 ? p.bldm : p.ldb) + gj);
+          vu[h][s2][u] = r1 ? bload(dU, k) : 0.f;
+        }
+  };
+  load_b(0);
   {
     float va[32];
 #pragma unroll
@@ -328,28 +353,19 @@ static __device__ __forceinline__ void wgrad_tile4(const WgradArgs g, int bid, W
       L.As[(e & 31) * WG_KP + (e >> 5)] = va[q];
     }
   }
-  // ---- B1's gradients (and the step control's lr_t / target flag)
-  handoff_wait_rows(sync, nrb, p.cls ? SYNC_B1_PI : SYNC_B1_Q, p.cls ? (unsigned)ncq : 2u * (unsigned)ncq, tmo);
-  handoff_wait(sync_at(sync, 0, SYNC_B1_CTL), (unsigned)ncq, tmo);
-  const float lr_t = *ad.lr_t;
-  const bool r1 = p.bu != nullptr;
-  const auto dB = rsrc(r1 ? p.bm : p.B, (int64_t)(n - 1) * (r1 ? p.bldm : p.ldb) + p.N);
-  const auto dU = rsrc(p.bu, r1 ? n : 0);
-  const float bv = r1 ? bload(rsrc(p.bv, p.N), gj) : 0.f;
+  lds_barrier();
   f32x4 acc0[4], acc1[4];
 #pragma unroll
   for (int kq = 0; kq < 4; ++kq) {
+    if (kq == 2) load_b(2);
+    const int h = kq & 1;
     acc0[kq] = zero4();
     acc1[kq] = zero4();
     float b[4][4];
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = 64 * kq + 16 * lk + 4 * s2 + u;
-        const float vb = bload(dB, k * (r1 ? p.bldm : p.ldb) + gj);
-        b[s2][u] = r1 ? (vb > 0.f ? bload(dU, k) * bv : 0.f) : vb;
-      }
+      for (int u = 0; u < 4; ++u) b[s2][u] = r1 ? (vb[h][s2][u] > 0.f ? vu[h][s2][u] * bv : 0.f) : vb[h][s2][u];
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
       const f32x4 a4 = ld4(L.As + (16 * qi + li) * WG_KP + 64 * kq + 16 * lk + 4 * s2);
@@ -406,6 +422,7 @@ static __device__ __forceinline__ void wgrad_tile4(const WgradArgs g, int bid, W
     }
   }
   handoff_signal(sync + (SYNC_N * nrb + SYNC_B2_DONE) * SYNC_STRIDE);
+  stamp(g.st, 4);
 }
 
 // The loss tail of the single-launch step with 256 threads, exactly sac_wgrad_kernel's 1024-thread sums: thread
@@ -415,14 +432,16 @@ static __device__ __forceinline__ void wgrad_tile4(const WgradArgs g, int bid, W
 static __device__ __forceinline__ void wgrad_loss_tail4(const WgradArgs a, float* sh, unsigned* sync, int nrb,
                                                         int ncq, int ntiles) {
   unsigned* tmo = sync + (SYNC_N * nrb + SYNC_TMO) * SYNC_STRIDE;
+  stamp(a.st, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n = a.n, A = a.A;
   const AdamCtx& ad = a.ad;
   AdamIn al{0.f, 0.f, 0.f, 0.f};
   if (tid == 0) al = adam_load(ad, ad.total);                       // log_alpha = the last parameter
-  handoff_wait_rows(sync, nrb, SYNC_B1_CTL, (unsigned)ncq, tmo);   // every reader of the step counter is done
-  handoff_wait_rows(sync, nrb, SYNC_B1_Q, 2u * (unsigned)ncq, tmo);
-  handoff_wait_rows(sync, nrb, SYNC_B1_PI, (unsigned)ncq, tmo);
+  // B1 done (critic and policy blocks; F1 and F2 before them), then every step-control / gather block (the
+  // readers of the step counter): ONE acquire
+  handoff_wait_all(sync, nrb, SYNC_B1_Q, 2u * (unsigned)ncq, SYNC_B1_PI, (unsigned)ncq, 0u, tmo, false);
+  handoff_wait_all(sync, nrb, SYNC_B1_CTL, (unsigned)ncq, SYNC_B1_CTL, 0u, 0u, tmo, true);
   const float lr_t = *ad.lr_t;
   float red[4][7];
 #pragma unroll
@@ -497,8 +516,20 @@ static __device__ __forceinline__ void wgrad_loss_tail4(const WgradArgs a, float
     logs[LOG_ALPHA] = expf(al.p); logs[LOG_ENTROPY] = ment; logs[LOG_LOGP] = mlp; logs[LOG_PI_LOSS] = pil;
     adam_apply(ad, ad.total, ga, al, lr_t);
   }
-  // every tile is done with the counters: zero them for the next step, then advance the step counter
-  handoff_wait(sync + (SYNC_N * nrb + SYNC_B2_DONE) * SYNC_STRIDE, (unsigned)ntiles, tmo);
+  // every tile is done with the counters: zero them for the next step, then advance the step counter (nothing
+  // the tiles wrote is read here: no acquire)
+  if (tid == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(sync + (SYNC_N * nrb + SYNC_B2_DONE) * SYNC_STRIDE, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT) < (unsigned)ntiles) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++spins > SAC_SPIN_LIMIT) {
+        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
   if (*tmo && tid == 0) {            // a wait gave up (sac_rows.h handoff_wait): poison the logs
     const float nan = __builtin_nanf("");
     for (int i = 0; i < LOG_N; ++i) a.logs[i] = nan;
@@ -508,6 +539,7 @@ static __device__ __forceinline__ void wgrad_loss_tail4(const WgradArgs a, float
     sync[(SYNC_N * nrb + SYNC_B2_DONE) * SYNC_STRIDE] = 0u;
     *a.iter += 1;
   }
+  stamp(a.st, 4);
 }
 
 // The whole SAC step as ONE launch, grid (ncq, nrb, 12 + zb2): z < 4 F1, 4 <= z < 8 F2, 8 <= z < 12 B1, then
@@ -517,7 +549,10 @@ union StepLds {
   F2B1Lds a;
   Wg4Lds b;
 };
-static __global__ __launch_bounds__(256, 2) void sac_step_kernel(const FwdArgsR f1, const FwdArgsR f2, const Dh1Args d,
+#ifndef MOPO_SAC_STEP_MINB
+#define MOPO_SAC_STEP_MINB 2   // workgroups per CU the single-launch step's registers are capped for
+#endif
+static __global__ __launch_bounds__(256, MOPO_SAC_STEP_MINB) void sac_step_kernel(const FwdArgsR f1, const FwdArgsR f2, const Dh1Args d,
                                                                  const WgradArgs g) {
   __shared__ __attribute__((aligned(16))) StepLds S;
   const int z = blockIdx.z;
