@@ -464,11 +464,14 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
 #ifndef BNN_F16_XCD
 #define BNN_F16_XCD 1
 #endif
+#ifndef BNN_F16_MINB_WIDE
+#define BNN_F16_MINB_WIDE 1  // H = 400 (NB2 = 26): workgroups per CU the f16s kernel's registers are capped for
+#endif
 #ifndef BNN_F16_MINB
 #define BNN_F16_MINB 2  // 4-wave workgroups per CU: 2 (170 VGPRs, no scratch) measured 0.5 % faster than 3 (28 B/lane spill)
 #endif
 template <int NB2, int NBO, int MODE, int WAVES, int PS = 1, int NBU = NB2>
-__global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES) void bnn_fwd_f16s_kernel(
+__global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? BNN_F16_MINB_WIDE : BNN_F16_MINB * 4 / WAVES) void bnn_fwd_f16s_kernel(
     const BnnDev w, const FwdArgs a) {
   constexpr int P = 2, KG = NB2 / 2;
   constexpr bool KH = NBU < NB2;  // the hidden layers' last k-group is half padding: 16-deep MFMAs there
@@ -580,6 +583,127 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? 1 : BNN_F16_MINB * 4 / WAVES
   f32x4 hd[NBO];
   layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, PS, true, NBO, KH>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd, lds,
                                                                   wv, lane, s_in);
+  const float f = inv_row * w.wscale[4 * E + e] * kNegLn2;  // the head's input is y' = -log2(e) y
+#pragma unroll
+  for (int nb = 0; nb < NBO; ++nb) hd[nb] *= f;
+  head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
+                           (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
+}
+
+// ---- f16x3 forward at H = 400 in column halves (bnn_fwd_f16h_kernel): bnn_fwd_f16s_kernel's arithmetic, product
+// for product, with every layer's output blocks computed in two passes over the layer's input (blocks [0, NHA)
+// then [NHA, NB2), each pass streaming its half of every weight slice), so only one half's accumulators are
+// live beside the other's results: 2 workgroups per CU (256 registers) instead of 1 (376).  The input row's
+// split is the same split_f16_pair under the same row scale (made inside the layer as for the hidden layers).
+#ifndef BNN_F16_HALF
+#define BNN_F16_HALF 1  // 1: H = 400 f16x3 runs bnn_fwd_f16h_kernel; 0: bnn_fwd_f16s_kernel
+#endif
+#ifndef BNN_F16H_MINB
+#define BNN_F16H_MINB 2
+#endif
+template <int NB2, int NBO, int MODE, int WAVES, int NBU>
+__global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd_f16h_kernel(const BnnDev w,
+                                                                                          const FwdArgs a) {
+  constexpr int P = 2, KG = NB2 / 2;
+  constexpr bool KH = NBU < NB2;  // the hidden layers' last k-group is half padding: 16-deep MFMAs there
+  constexpr int NHA = NB2 / 2, NHB = NB2 - NHA, NHBU = NBU - NHA;
+  constexpr int NBMAX = NHB > NBO ? NHB : NBO;
+  constexpr int SLOT = Stage<NBMAX, WAVES>::SLOTS * 256;
+  constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + BIAS_LDS];  // one array (see layer_lds)
+  float* lds_bias = lds + 2 * SLOT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4;
+  const int m = lane & 15;
+  const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
+  const int groups = ceil_div(a.ntiles, WAVES);
+  const int C = ceil_div(groups, 8);  // XCD-aware order as bnn_fwd_f16s_kernel
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int e = j / C, grp = xcd * C + j % C;
+  if (grp >= groups) return;
+  const int64_t row = (int64_t)(grp * WAVES + wv) * 16 + m;
+  if ((int64_t)grp * WAVES * 16 >= count) return;
+  const int IN = w.IN, O = w.O, E = w.E;
+  const bool ok = row < count;
+  auto row_max = [&](float mx) {
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    return fmaxf(mx, __shfl_xor(mx, 32));
+  };
+  float x1[1][8];
+  if (a.xs) {
+    const f32x4 lo = ok ? ld4(a.xs + row * XS_STRIDE + 4 * g) : zero4();
+    const f32x4 hi = ok ? ld4(a.xs + row * XS_STRIDE + 16 + 4 * g) : zero4();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      x1[0][t] = lo[t];
+      x1[0][4 + t] = hi[t];
+    }
+  } else {
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int k = slot_feat(bf16_kperm(g, jj), IN);
+      float v = 0.f;
+      if (ok && k >= 0) {
+        float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
+                          : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
+        v = (raw - w.mu[k]) / w.sigma[k];
+      }
+      x1[0][jj] = v;
+    }
+  }
+  float mx = 0.f;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) mx = fmaxf(mx, fabsf(x1[0][jj]));
+  float s_in, inv_row;
+  row_scale(row_max(mx), s_in, inv_row);
+  const int64_t bs = w.BS;
+  f32x4 accA[NHA], accB[NHB];
+  float hf[KG][8];
+  // the two passes of a layer (the bias, all NB2 * 16 values, rides with pass A's first slice)
+  auto layer2 = [&](const float* wl, const auto& in, auto kgc, const float* bias) {
+    constexpr int KGL = decltype(kgc)::value;
+    constexpr bool KHL = KGL > 1 && KH;
+    layer_lds_split_f32<KGL, NHA, WAVES, SLOT, P, 1, true, NHA, KHL, NB2, NB2 * 4>(wl, in, accA, lds, wv, lane, s_in,
+                                                                                  bias, lds_bias);
+    layer_lds_split_f32<KGL, NHB, WAVES, SLOT, P, 1, true, NHBU, KHL, NB2>(wl + NHA * 256, in, accB, lds, wv, lane,
+                                                                           s_in);
+  };
+  // block bi of the layer's output -> values (bi & 1) * 4 + t of k-group bi / 2 of the next input
+  auto to_input = [&](const float* b, float f) {
+    float mxv = 0.f;
+#pragma unroll
+    for (int bi = 0; bi < NHA; ++bi) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(b + bi * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float y = swish_log2(fmaf(accA[bi][t], f, bb[t]));
+        hf[bi / 2][(bi & 1) * 4 + t] = y;
+        mxv = fmaxf(mxv, fabsf(y));
+      }
+    }
+#pragma unroll
+    for (int bi = NHA; bi < NB2; ++bi) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(b + bi * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        // an odd hidden-block count leaves the last block all padding: zero, not computed
+        const float y = bi < NBU ? swish_log2(fmaf(accB[bi - NHA][t], f, bb[t])) : 0.f;
+        hf[bi / 2][(bi & 1) * 4 + t] = y;
+        mxv = fmaxf(mxv, fabsf(y));
+      }
+    }
+    row_scale(row_max(mxv), s_in, inv_row);
+  };
+  constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.6931471805599453f;
+  layer2(w.w0b + (int64_t)e * P * NB2 * 256, x1, std::integral_constant<int, 1>{}, w.b0 + e * bs);
+  to_input(lds_bias, inv_row * w.wscale[e] * kNegLog2e);  // layer 0's input is x itself
+  for (int l = 0; l < 3; ++l) {
+    layer2(w.whb + ((int64_t)l * E + e) * KG * P * NB2 * 256, hf, std::integral_constant<int, KG>{},
+           w.bh + ((int64_t)l * E + e) * bs);
+    to_input(lds_bias, inv_row * w.wscale[(1 + l) * E + e]);
+  }
+  f32x4 hd[NBO];
+  layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, 1, true, NBO, KH>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd, lds,
+                                                                 wv, lane, s_in);
   const float f = inv_row * w.wscale[4 * E + e] * kNegLn2;  // the head's input is y' = -log2(e) y
 #pragma unroll
   for (int nb = 0; nb < NBO; ++nb) hd[nb] *= f;
@@ -1114,6 +1238,16 @@ static int launch_f16s(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   if constexpr (BNN_F16_RING && NB2 <= 16) {
     if (ring_shape<NB2>(h)) return launch_ring<NB2, NBO, 2, BNN_RING_DEPTH_F16>(h, mode, a, s);
     return fail("bnn f16x3: unsupported hidden size");
+  }
+  if constexpr (BNN_F16_HALF && NB2 == 26) {   // H = 400: the column-half kernel (two workgroups per CU)
+    if (h->dev.NBH == NB2 - 1) {
+      if (mode == FWD_PREDICT)
+        hipLaunchKernelGGL((bnn_fwd_f16h_kernel<NB2, NBO, FWD_PREDICT, WV, NB2 - 1>), grid, block, 0, s, h->dev, a);
+      else
+        hipLaunchKernelGGL((bnn_fwd_f16h_kernel<NB2, NBO, FWD_ROLLOUT, WV, NB2 - 1>), grid, block, 0, s, h->dev, a);
+      MOPO_HIP(hipGetLastError());
+      return 0;
+    }
   }
   if constexpr (NB2 <= 16) {
     if (h->dev.NBH == NB2 - 1) {

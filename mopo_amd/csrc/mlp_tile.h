@@ -400,20 +400,24 @@ __device__ __forceinline__ void row_scale(float mx, float& s, float& inv) {
 // layer_lds_split with f32 activations held (8 VGPRs per k-group instead of 4 * P): each k-group's P
 // bf16 parts are split when its first slice is consumed, so only one k-group's parts are live.
 // F16: the 2 fp16 parts of in * s (split_f16_scaled; s = the row scale) on the f16 MFMA.
-template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false, int NBU = NB, bool KH = false>
+// NBS > NB (PS = 1): the layer's slices hold NBS output blocks, of which this call computes the NB starting at
+// wf (a column subset: the H = 400 f16x3 kernel's column halves); BQ: bias quads staged with the first slice
+template <int KG, int NB, int WAVES, int SLOT, int P, int PS = P, bool F16 = false, int NBU = NB, bool KH = false,
+          int NBS = NB, int BQ = NB * 4>
 __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf, const float (&in)[KG][8],
                                                     f32x4 (&acc)[NB], float* lds, int w, int lane, float sc = 1.f,
                                                     const float* __restrict__ bias = nullptr,
                                                     float* lds_bias = nullptr) {
   static_assert(P % PS == 0, "parts per slice must divide the parts");
-  constexpr int SPK = P / PS, S = KG * SPK, NF = PS * NB;
+  static_assert(NBS == NB || PS == 1, "a column subset needs one part per slice");
+  constexpr int SPK = P / PS, S = KG * SPK, NF = PS * NB, SSTR = PS * NBS;   // SSTR: slice stride (fragments)
   static_assert(Stage<NF, WAVES>::SLOTS * 256 <= SLOT, "slice larger than its buffer");
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) acc[nb] = zero4();
   bf16x8 cur[P];
   __syncthreads();
   stage_slice<NF, WAVES>(wf, lds, w, lane);
-  if (bias) stage_bias<NB * 4, WAVES>(bias, lds_bias, w, lane);  // published by the first barrier below
+  if (bias) stage_bias<BQ, WAVES>(bias, lds_bias, w, lane);  // published by the first barrier below
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int kg = s / SPK;
@@ -441,7 +445,7 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
       }
     }
     __syncthreads();
-    if (s + 1 < S) stage_slice<NF, WAVES>(wf + (s + 1) * NF * 256, lds + ((s + 1) & 1) * SLOT, w, lane);
+    if (s + 1 < S) stage_slice<NF, WAVES>(wf + (s + 1) * SSTR * 256, lds + ((s + 1) & 1) * SLOT, w, lane);
     __builtin_amdgcn_sched_barrier(0);
     const float* b = lds + (s & 1) * SLOT;
 #if MOPO_SPLIT_PF <= 1
