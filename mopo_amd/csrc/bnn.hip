@@ -601,6 +601,9 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? BNN_F16_MINB_WIDE : BNN_F16_
 #ifndef BNN_F16H_MINB
 #define BNN_F16H_MINB 2
 #endif
+#ifndef BNN_F16H_XCDMEM
+#define BNN_F16H_XCDMEM 1  // E % 8 == 0: each XCD owns E / 8 members (their weights fetched into one L2)
+#endif
 template <int NB2, int NBO, int MODE, int WAVES, int NBU>
 __global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd_f16h_kernel(const BnnDev w,
                                                                                           const FwdArgs a) {
@@ -616,45 +619,25 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd
   const int m = lane & 15;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
-  const int C = ceil_div(groups, 8);  // XCD-aware order as bnn_fwd_f16s_kernel
+  const int IN = w.IN, O = w.O, E = w.E;
+  // XCD-owned members (E % 8 == 0, launch_f16s): XCD x runs members x, x + 8, ... over EVERY row group,
+  // member-major, so each member's weights are fetched into ONE XCD's L2 (the row groups stream past them).
+  // Otherwise the XCD-aware order of bnn_fwd_f16s_kernel: XCD x takes row groups [x C, (x + 1) C) of every
+  // member.  (A workgroup looping over its XCD's members with the rows in registers spilled 145-197 VGPRs.)
+  const bool own = a.xcd_members != 0;
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-  const int e = j / C, grp = xcd * C + j % C;
-  if (grp >= groups) return;
+  const int C = ceil_div(groups, 8);
+  const int e = own ? xcd + 8 * (j / groups) : j / C;
+  const int grp = own ? j % groups : xcd * C + j % C;
+  if (grp >= groups || e >= E) return;
   const int64_t row = (int64_t)(grp * WAVES + wv) * 16 + m;
   if ((int64_t)grp * WAVES * 16 >= count) return;
-  const int IN = w.IN, O = w.O, E = w.E;
   const bool ok = row < count;
   auto row_max = [&](float mx) {
     mx = fmaxf(mx, __shfl_xor(mx, 16));
     return fmaxf(mx, __shfl_xor(mx, 32));
   };
-  float x1[1][8];
-  if (a.xs) {
-    const f32x4 lo = ok ? ld4(a.xs + row * XS_STRIDE + 4 * g) : zero4();
-    const f32x4 hi = ok ? ld4(a.xs + row * XS_STRIDE + 16 + 4 * g) : zero4();
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      x1[0][t] = lo[t];
-      x1[0][4 + t] = hi[t];
-    }
-  } else {
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int k = slot_feat(bf16_kperm(g, jj), IN);
-      float v = 0.f;
-      if (ok && k >= 0) {
-        float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
-                          : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
-        v = (raw - w.mu[k]) / w.sigma[k];
-      }
-      x1[0][jj] = v;
-    }
-  }
-  float mx = 0.f;
-#pragma unroll
-  for (int jj = 0; jj < 8; ++jj) mx = fmaxf(mx, fabsf(x1[0][jj]));
   float s_in, inv_row;
-  row_scale(row_max(mx), s_in, inv_row);
   const int64_t bs = w.BS;
   f32x4 accA[NHA], accB[NHB];
   float hf[KG][8];
@@ -694,6 +677,32 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd
     row_scale(row_max(mxv), s_in, inv_row);
   };
   constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.6931471805599453f;
+  float x1[1][8];
+  if (a.xs) {
+    const f32x4 lo = ok ? ld4(a.xs + row * XS_STRIDE + 4 * g) : zero4();
+    const f32x4 hi = ok ? ld4(a.xs + row * XS_STRIDE + 16 + 4 * g) : zero4();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      x1[0][t] = lo[t];
+      x1[0][4 + t] = hi[t];
+    }
+  } else {
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int k = slot_feat(bf16_kperm(g, jj), IN);
+      float v = 0.f;
+      if (ok && k >= 0) {
+        float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
+                          : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
+        v = (raw - w.mu[k]) / w.sigma[k];
+      }
+      x1[0][jj] = v;
+    }
+  }
+  float mx = 0.f;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) mx = fmaxf(mx, fabsf(x1[0][jj]));
+  row_scale(row_max(mx), s_in, inv_row);
   layer2(w.w0b + (int64_t)e * P * NB2 * 256, x1, std::integral_constant<int, 1>{}, w.b0 + e * bs);
   to_input(lds_bias, inv_row * w.wscale[e] * kNegLog2e);  // layer 0's input is x itself
   for (int l = 0; l < 3; ++l) {
@@ -702,8 +711,8 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd
     to_input(lds_bias, inv_row * w.wscale[(1 + l) * E + e]);
   }
   f32x4 hd[NBO];
-  layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, 1, true, NBO, KH>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd, lds,
-                                                                 wv, lane, s_in);
+  layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, 1, true, NBO, KH>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd,
+                                                                 lds, wv, lane, s_in);
   const float f = inv_row * w.wscale[4 * E + e] * kNegLn2;  // the head's input is y' = -log2(e) y
 #pragma unroll
   for (int nb = 0; nb < NBO; ++nb) hd[nb] *= f;
@@ -1241,6 +1250,8 @@ static int launch_f16s(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   }
   if constexpr (BNN_F16_HALF && NB2 == 26) {   // H = 400: the column-half kernel (two workgroups per CU)
     if (h->dev.NBH == NB2 - 1) {
+      a.xcd_members = (BNN_F16H_XCDMEM && h->E % 8 == 0) ? 1 : 0;
+      if (a.xcd_members) grid = dim3(8 * ceil_div(a.ntiles, WV) * (h->E / 8));   // (XCD, member, row group)
       if (mode == FWD_PREDICT)
         hipLaunchKernelGGL((bnn_fwd_f16h_kernel<NB2, NBO, FWD_PREDICT, WV, NB2 - 1>), grid, block, 0, s, h->dev, a);
       else

@@ -65,6 +65,7 @@ struct FwdArgs {
   // rollout's actor): replaces the per-member f64 obs / act loads and scaler transform
   const float* xs;
   int ntiles;             // tiles per member in the grid
+  int xcd_members;        // H = 400 f16x3 kernel: 1 = every XCD owns E / 8 members (set by launch_f16s)
   // predict outputs
   float* mean;            // [E][B][D]
   float* var;

@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD
 mkdir -p gpurun_out
 export TMPDIR=/tmp MOPO_ROLLOUT_SPLIT=1
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --sac-steps 16 --no-c3 --no-alt-dtypes --train-epochs 0 --prof-steps 1"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --sac-steps 16 --no-c3 --no-alt-dtypes --train-epochs 0 --prof-steps 1 ${BENCH_ARGS}"
 for v in ${AB:-new old}; do
   cp abv/$v.so mopo_amd/libmopo_hip.so
   for C in FETCH_SIZE WRITE_SIZE; do
