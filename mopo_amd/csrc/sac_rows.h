@@ -597,6 +597,9 @@ static __device__ __forceinline__ void rows_partial_out(const float* T, const fl
   }
 }
 
+#ifndef MOPO_SAC_S7_PRE
+#define MOPO_SAC_S7_PRE 0   // fused F2 (FZ >= 2): the step-7 operands before the wait on F1 (A/B knob)
+#endif
 #ifndef MOPO_SAC_S7_EARLY
 // 1: issue step 7's operand loads right after the layer-2 MFMAs instead of in step 7 -- measured 45.4 vs
 // 43.6 us/step (same-box A/B): they delay the epilogue's own loads and stores more than they hide
@@ -722,7 +725,13 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   //      operands arrive), which F2's head loads
   if (!HEAD && ii < 2 && cq == 0 && ((a.hd.gen_eps >> ii) & 1) && tid < 128 && hj < A && hrow < n)
     hstore<SC>(&a.hd.eps_out[ii][hrow * EPW + hj], head_noise(a.hd.seed, *a.hd.iter, hrow, ii, hj));
-  // ---- F2 inside the F1 + F2 + B1 launch: the head's partials once the row block's pi blocks are done
+  // ---- F2 inside the F1 + F2 + B1 launch: the head's partials once the row block's pi blocks are done (with
+  //      MOPO_SAC_S7_PRE the main critics' step-7 operands are issued before the wait too: the block idles there)
+  f32x4 wa2[4][4], wb1[4];
+  constexpr bool S7PRE = HEAD && FZ >= 2 && MOPO_SAC_S7_PRE;
+  if constexpr (S7PRE) {
+    if (p.dapart) step7_loads(p, w, li, lk, c0, H, A, wa2, wb1);
+  }
   if constexpr (HEAD && FZ >= 2) {
     stamp(a.st, 5);
     handoff_wait(sync_at(a.sync, rb, p.head == 0 ? SYNC_PI_S : SYNC_PI_N), (unsigned)a.ncq, a.sync + SYNC_N * a.nrb * SYNC_STRIDE);
@@ -780,7 +789,6 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   // ---- 4. layer 2: the wave's 16 x 16 tile over the whole K
   f32x4 acc[4];
   rows_contract(As, bp, li, lk, acc);
-  f32x4 wa2[4][4], wb1[4];
 #if MOPO_SAC_S7_EARLY
   if (HEAD && p.dapart) step7_loads(p, w, li, lk, c0, H, A, wa2, wb1);
 #endif
@@ -806,7 +814,7 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   {
     if (HEAD && p.dapart) {
 #if !MOPO_SAC_S7_EARLY
-      step7_loads(p, w, li, lk, c0, H, A, wa2, wb1);
+      if constexpr (!S7PRE) step7_loads(p, w, li, lk, c0, H, A, wa2, wb1);
 #endif
       const int kw = 64 * w;
       // G(r = li, c = 16 s + 4 lk + u) from the block's h2 tile and W3 (Wo row 0)
