@@ -761,6 +761,9 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
     MOPO_TRF(2, 13, 3) MOPO_TRF(1, 13, 2) MOPO_TRF(1, 2, 2) MOPO_TRF(2, 2, 3) MOPO_TRF(2, 16, 3) MOPO_TRF(1, 16, 2)
     return fail("bnn train: no row-block instantiation for these widths (use_rows)");
 #undef MOPO_TRF
+    // on this path h->G holds only the max/min log-var gradients (train_rows.h loss tail); the W/b
+    // gradients stay in the tile workgroups' registers and go straight into Adam, never through G
+    // (ad.G is then only the base the Adam state offsets are taken against)
     if (train_wg2()) {
       TrainWg2 g{};
       g.M = M;

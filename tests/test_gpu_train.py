@@ -223,3 +223,21 @@ def test_train_loop_joint_head_matches_oracle():
     rm, rv = obnn.forward(obnn.from_mat_list(got, smv=False), X[:20])
     np.testing.assert_allclose(mean, rm, rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(var, rv, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize('wg2,nt', [(1, 512), (1, 1024), (0, 512)])
+def test_wgrad_launch_variants_match_oracle(wg2, nt):
+    """The weight-gradient launch knobs (MOPO_TRAIN_WG2: the persistent XCD-local tile launch or the
+    grouped-GEMM launch; MOPO_TRAIN_WG2_NT: 512- or 1024-thread tile workgroups) are read once per
+    process, so each setting runs the epoch and train-loop parity tests above in a fresh process."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MOPO_TRAIN_WG2=str(wg2), MOPO_TRAIN_WG2_NT=str(nt))
+    r = subprocess.run([sys.executable, '-m', 'pytest', '-p', 'no:cacheprovider', '-q', '-x', '-m', 'gpu',
+                        os.path.join(root, 'tests', 'test_gpu_train.py'),
+                        '-k', 'epoch_matches_oracle_steps or train_loop_matches_oracle'],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert ' passed' in r.stdout and 'skipped' not in r.stdout.splitlines()[-1], r.stdout[-500:]
