@@ -384,11 +384,24 @@ class BNN:
         losses_d = torch.empty(E, dtype=torch.float32, device=dev)
         break_train, grad_updates, epoch = False, 0, 0
         self._max_epochs_since_update = max_epochs_since_update
+        # the shuffle uniforms are drawn on the host while the epoch's steps run and reach the device by one
+        # DMA from a pinned buffer queued behind them (a pageable copy was staged in chunks by the host and
+        # left the GPU idle ~5 ms per epoch); the event keeps the next draw from overwriting a pending copy
+        keys_h = torch.empty(E * n, dtype=torch.float64, pin_memory=True)
+        keys_hn = keys_h.numpy().reshape(E, n)
+        keys = torch.empty(E * n, dtype=torch.float64, device=dev)
+        copied = None
         t0 = time.time()
         for epoch in (range(max_epochs) if max_epochs is not None else itertools.count()):
             L.check(L.lib().mopo_bnn_train_epoch(t, L.ptr(x), L.ptr(y), L.ptr(idxs), n, int(batch_size), None))
             grad_updates += int(np.ceil(n / batch_size))
-            keys = torch.from_numpy(np.random.uniform(size=[E, n])).to(dev)      # shuffle_rows :385-387
+            u = np.random.uniform(size=[E, n])                                      # shuffle_rows :385-387
+            if copied is not None:
+                copied.synchronize()
+            keys_hn[...] = u
+            keys.copy_(keys_h, non_blocking=True)
+            copied = torch.cuda.Event()
+            copied.record()
             L.check(L.lib().mopo_bnn_train_shuffle(t, L.ptr(idxs), L.ptr(keys), n, None))
             if not hide_progress and holdout_ratio >= 1e-12 and num_holdout > 0:
                 L.check(L.lib().mopo_bnn_train_eval_mse(t, L.ptr(hold_x), L.ptr(hold_y), None, num_holdout,
