@@ -140,6 +140,84 @@ static __device__ __forceinline__ void rows_gemm(const float* As, const float* W
   }
 }
 
+// rows_gemm with the layer's first TR_PF k-groups of B loaded ahead (rows_pre), by the fused kernel across
+// the previous layer's epilogue and barrier: the weights do not depend on the activations, so a layer
+// no longer starts on an exposed L2 round trip
+struct RowsW {
+  __amdgpu_buffer_rsrc_t d;
+  int K, N, ldw;
+};
+template <bool KT>
+static __device__ __forceinline__ RowsW rows_w(const float* Wv, int Kv, int Nv, int ldwv) {
+  const float* W = uniform_ptr(Wv);
+  RowsW r;
+  r.K = __builtin_amdgcn_readfirstlane(Kv);
+  r.N = __builtin_amdgcn_readfirstlane(Nv);
+  r.ldw = __builtin_amdgcn_readfirstlane(ldwv);
+  r.d = rsrc(W, KT ? (int64_t)(r.N - 1) * r.ldw + r.K : (int64_t)(r.K - 1) * r.ldw + r.N);
+  return r;
+}
+template <bool KT, int TW>
+static __device__ __forceinline__ void rows_ld(const RowsW& W, int grp, int c, int lane, float (&bv)[4][TW]) {
+  const int lk = lane >> 4, k0 = 16 * grp + 4 * lk;
+  const int K = W.K, N = W.N, ldw = W.ldw;
+  if constexpr (KT) {
+#pragma unroll
+    for (int q = 0; q < TW; ++q) {
+      const f32x4 v = bload4(W.d, ((c + q < N) & (k0 < K)) ? (c + q) * ldw + k0 : -1);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) bv[u][q] = v[u];
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = ((c < N) & (k0 + u < K)) ? (k0 + u) * ldw + c : -1;
+      if constexpr (TW == 4) {
+        const f32x4 v = bload4(W.d, idx);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[u][q] = v[q];
+      } else if constexpr (TW == 2) {
+        const f32x2 v = bload2(W.d, idx);
+        bv[u][0] = v[0];
+        bv[u][1] = v[1];
+      } else {
+        bv[u][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(W.d, idx * 4, 0, 0));
+      }
+    }
+  }
+}
+template <bool KT, int G, int TW>
+static __device__ __forceinline__ void rows_pre(const RowsW& W, int c, int lane, float (&pre)[TR_PF][4][TW]) {
+  if (__builtin_amdgcn_readfirstlane(c - 4 * (lane & 15)) >= W.N) return;   // rows_gemm's no-column exit
+#pragma unroll
+  for (int grp = 0; grp < TR_PF && grp < G; ++grp) rows_ld<KT, TW>(W, grp, c, lane, pre[grp]);
+}
+template <bool KT, int G, int TW>
+static __device__ __forceinline__ void rows_gemm_pre(const float* As, const RowsW& W, int c, int lane,
+                                                     const float (&pre)[TR_PF][4][TW], f32x4 (&acc)[TW]) {
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < TW; ++q) acc[q] = zero4();
+  if (__builtin_amdgcn_readfirstlane(c - 4 * li) >= W.N) return;
+  float bq[G + TR_PF][4][TW];
+#pragma unroll
+  for (int grp = 0; grp < TR_PF && grp < G; ++grp)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < TW; ++q) bq[grp][u][q] = pre[grp][u][q];
+#pragma unroll
+  for (int grp = 0; grp < G; ++grp) {
+    if (grp + TR_PF < G) rows_ld<KT, TW>(W, grp + TR_PF, c, lane, bq[grp + TR_PF]);
+    __builtin_amdgcn_sched_barrier(0);
+    const f32x4 a4 = ld4(As + li * TR_LD + 16 * grp + 4 * lk);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < TW; ++q) acc[q] = mfma4(a4[u], bq[grp][u][q], acc[q]);
+  }
+}
+
 // a lane's TW consecutive floats at p (16-B / 8-B aligned)
 template <int TW>
 static __device__ __forceinline__ void st_tw(float* p, const float (&v)[TW]) {
@@ -392,6 +470,9 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_bwd_rows_kernel
 // backward's input buffer, and the batch-level tail moves to the weight-gradient launch (bnn_train.hip
 // train_wgrad_kernel), which only needs this step's lr_t -- block 0 writes it here (the tail advances
 // the beta powers after every reader of them in this step).
+#ifndef TR_XPF
+#define TR_XPF 1   // the next layer's first weight k-groups issued before this layer's epilogue (rows_pre)
+#endif
 template <int G0, int GH, int GD>
 static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(const TrainRows a) {
   __shared__ __attribute__((aligned(16))) float buf[2][16 * TR_LD];
@@ -405,6 +486,17 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
   }
   if (!tr_block(blockIdx.x, a.nrb, a.E, e, rb)) return;
   const int M = a.M, IN = a.IN, H = a.H, D = a.D, i0 = rb * 16;
+  const int c0 = 64 * (w & 3) + 4 * li + TR_TW * (w >> 2);   // this lane's first column
+  auto wfwd = [&](int l) {
+    const int K = l == 0 ? IN : H, N = l == TR_NHID ? 2 * D : H;
+    return rows_w<false>(a.P + a.W[l] + (int64_t)e * K * N, K, N, N);
+  };
+  auto wbwd = [&](int l) {   // layer l: [H -> Nl], read transposed
+    const int Nl = l == TR_NHID ? 2 * D : H;
+    return rows_w<true>(a.P + a.W[l] + (int64_t)e * H * Nl, Nl, H, Nl);
+  };
+  float pre[TR_PF][4][TR_TW];
+  if (TR_XPF) rows_pre<false, G0, TR_TW>(wfwd(0), c0, lane, pre);   // in flight during the gather
   {  // gather (train_fwd_rows_kernel)
     const int W = IN + D, KP = ((IN + 15) >> 4) << 4;
     const int64_t base = a.bstep ? (int64_t)(*a.bstep) * a.batch : 0;
@@ -425,7 +517,6 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
     }
     lds_barrier();
   }
-  const int c0 = 64 * (w & 3) + 4 * li + TR_TW * (w >> 2);   // this lane's first column
   const int lk = lane >> 4;
   auto fwd = [&](auto gtag, int l) {
     constexpr int G = decltype(gtag)::value;
@@ -434,7 +525,13 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
     float bias[TR_TW] = {};
     if (c0 < N) ld_tw<TR_TW>(a.P + a.b[l] + (int64_t)e * N + c0, bias);
     f32x4 acc[TR_TW];
-    rows_gemm<false, G, TR_TW>(buf[l & 1], Wl, K, N, N, c0, lane, acc);
+    if (TR_XPF) {
+      rows_gemm_pre<false, G, TR_TW>(buf[l & 1], wfwd(l), c0, lane, pre, acc);
+      if (l < TR_NHID) rows_pre<false, GH, TR_TW>(wfwd(l + 1), c0, lane, pre);
+      else rows_pre<true, GD, TR_TW>(wbwd(TR_NHID), c0, lane, pre);   // the backward's first layer
+    } else {
+      rows_gemm<false, G, TR_TW>(buf[l & 1], Wl, K, N, N, c0, lane, acc);
+    }
     float* out = buf[(l + 1) & 1];
     if (__builtin_amdgcn_readfirstlane(c0 - 4 * li) < N) {
 #pragma unroll
@@ -521,7 +618,12 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
       if (c0 < Kl) ld_tw<TR_TW>(zb[l - 1] + (4 * lk + i) * TR_LD + c0, zm[i]);
     }
     f32x4 acc[TR_TW];
-    rows_gemm<true, G, TR_TW>(buf[(TR_NHID - l) & 1], Wl, Nl, Kl, Nl, c0, lane, acc);
+    if (TR_XPF) {
+      rows_gemm_pre<true, G, TR_TW>(buf[(TR_NHID - l) & 1], wbwd(l), c0, lane, pre, acc);
+      if (l > 1) rows_pre<true, GH, TR_TW>(wbwd(l - 1), c0, lane, pre);
+    } else {
+      rows_gemm<true, G, TR_TW>(buf[(TR_NHID - l) & 1], Wl, Nl, Kl, Nl, c0, lane, acc);
+    }
     float* out = buf[(TR_NHID - l + 1) & 1];
     if (__builtin_amdgcn_readfirstlane(c0 - 4 * li) < Kl) {
 #pragma unroll

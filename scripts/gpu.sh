@@ -9,6 +9,7 @@
 #   ab          headline A/B over abv/<v>.so for v in $AB (scripts/ab.sh)
 #   sac_ab      SAC parity on each abv/<v>.so of $AB, then the step-time A/B (scripts/ab_sac.sh)
 #   train_ab    BNN.train parity, then the train leg under each env setting of $VARS
+#   train_so_ab BNN.train parity on each abv/<v>.so of $AB, then the train leg alternating them
 #   env_ab      bench (SAC + headline) alternating the env settings in $VARS (comma-joined per variant)
 #   stamps      SAC phase stamps from abv/sac_stamps.so (scripts/sac_stamps.py)
 # usage: bash scripts/gpu.sh tests bench ;  AB="new old" bash scripts/gpu.sh sac_ab
@@ -61,6 +62,27 @@ for step in "$@"; do
         done
         cat gpurun_out/ab_train.txt
       fi ;;
+    train_so_ab)
+      # BNN.train parity on each abv/<v>.so of $AB, then the train leg alternating the builds
+      keep; rc=0; : > gpurun_out/ab_train.txt
+      for v in $AB; do
+        cp abv/$v.so mopo_amd/libmopo_hip.so
+        timeout -k 10 300 $PYT tests/test_gpu_train.py -q -x -k "not variants" > gpurun_out/train_tests_$v.log 2>&1
+        rc=$?; echo "== $v parity rc=$rc: $(tail -1 gpurun_out/train_tests_$v.log)"
+        [ $rc -ne 0 ] && break
+      done
+      if [ $rc -eq 0 ]; then
+        for i in 1 2 3; do
+          for v in $AB; do
+            cp abv/$v.so mopo_amd/libmopo_hip.so
+            timeout -k 10 200 python bench.py --no-cpu-baseline --no-c3 --no-alt-dtypes --sac-steps 16 --steps 3 --warmup 1 \
+              --train-epochs ${TRAIN_EPOCHS:-3} > gpurun_out/abt_cur.json 2> gpurun_out/abt_cur.err || { rc=1; tail -5 gpurun_out/abt_cur.err; break 2; }
+            python -c "import json; d=json.load(open('gpurun_out/abt_cur.json')); t=d['model_train']; print('$v', round(t['value']), 'steps/s', round(t['ms_per_epoch'], 2), 'ms/epoch')" >> gpurun_out/ab_train.txt
+          done
+        done
+        cat gpurun_out/ab_train.txt
+      fi
+      restore ;;
     env_ab)
       : > gpurun_out/env_ab.txt; rc=0
       for i in 1 2 3; do
