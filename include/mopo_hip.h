@@ -196,6 +196,8 @@ int mopo_bnn_train_logs(mopo_bnn_train_t h, float* h_logs, int n);
  * followed by the 8 list lengths into out (8 per + 8 ints; out may be NULL) and returns per (< 0: error).
  * No reference counterpart: a layout detail of bnn.py:425-432's minibatch op on this device. */
 int mopo_bnn_train_tile_lists(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap);
+/* The same for the single-launch step (MOPO_TRAIN_STEP1): each list ordered by layer, the heads first. */
+int mopo_bnn_train_tile_lists_step(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap);
 
 /* ---- fused model rollout (MOPO._rollout_model) ----------------------------------------- */
 typedef struct mopo_rollout_s* mopo_rollout_t;

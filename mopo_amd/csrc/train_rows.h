@@ -359,7 +359,9 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_fwd_rows_kernel
 constexpr int TR_TAIL_CH = 8;     // chunks per output column, at most
 constexpr int TR_TAIL_SH = 512;   // floats of sh the tail may use (3 per (chunk, column))
 // TR: TrainRows or TrainTail (the fields used here)
-template <class TR>
+// KEEP_POW: leave the beta powers and the minibatch counter to the caller (train_step_kernel advances them
+// once every workgroup of its launch has read them)
+template <class TR, bool KEEP_POW = false>
 static __device__ __forceinline__ void train_loss_tail(const TR& a, float* sh) {
   const int D = a.D, n = a.E * a.nrb;
   const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];  // every thread reads them before thread 0 advances them
@@ -402,10 +404,12 @@ static __device__ __forceinline__ void train_loss_tail(const TR& a, float* sh) {
     float loss = 0.f;
     for (int dd = 0; dd < D; ++dd) loss += sh[dd];
     a.logs[0] = loss;                                               // data term of the train loss
-    a.beta_pow[2] = lr_t;
-    a.beta_pow[0] = b1p * 0.9f;
-    a.beta_pow[1] = b2p * 0.999f;
-    if (a.bstep_inc) *a.bstep_inc += 1;
+    if (!KEEP_POW) {
+      a.beta_pow[2] = lr_t;
+      a.beta_pow[0] = b1p * 0.9f;
+      a.beta_pow[1] = b2p * 0.999f;
+      if (a.bstep_inc) *a.bstep_inc += 1;
+    }
   }
 }
 
@@ -473,18 +477,44 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_bwd_rows_kernel
 #ifndef TR_XPF
 #define TR_XPF 1   // the next layer's first weight k-groups issued before this layer's epilogue (rows_pre)
 #endif
-template <int G0, int GH, int GD>
-static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(const TrainRows a) {
-  __shared__ __attribute__((aligned(16))) float buf[2][16 * TR_LD];
-  __shared__ __attribute__((aligned(16))) float zb[TR_NHID][16 * TR_LD];
-  __shared__ float red[3][64][17];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15;
-  int e, rb;
-  if (blockIdx.x == 0 && tid == 0) {
-    const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
-    a.beta_pow[2] = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);          // this step's TF1 Adam step size
+// The fused rows body, shared by train_rows_kernel and the single-launch step (bnn_train.hip
+// train_step_kernel, SIG = true).  SIG: the rows another workgroup of the launch reads (X, the swish
+// outputs, the heads' and the hidden layers' output gradients, the loss partials) are stored write-through
+// (sc1) and each stage ends in a hand-off (cdna_hip_programming.md Guideline 16): every wave drains its
+// stores, the workgroup barrier, then one agent-scope add to ready[(e (NHID + 1) + l) TS_STRIDE], the count
+// of row blocks of member e whose layer-l weight-gradient operands are complete (l = NHID after the output
+// gradient, l - 1 after the backward of layer l).
+constexpr int TS_STRIDE = 32;   // one counter per 128-B line
+constexpr int TR_LDS_FLOATS = (2 + TR_NHID) * 16 * TR_LD + 3 * 64 * 17;
+template <bool SC>
+static __device__ __forceinline__ void st_h(float* p, float v) {
+  if constexpr (SC) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool SC, int TW>
+static __device__ __forceinline__ void st_tw_h(float* p, const float (&v)[TW]) {
+  if constexpr (SC) {
+#pragma unroll
+    for (int q = 0; q < TW; ++q) __hip_atomic_store(p + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    st_tw<TW>(p, v);
   }
-  if (!tr_block(blockIdx.x, a.nrb, a.E, e, rb)) return;
+}
+static __device__ __forceinline__ void rows_signal(unsigned* c) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int G0, int GH, int GD, bool SIG>
+static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float* lds, unsigned* ready, int e, int rb) {
+  float (*buf)[16 * TR_LD] = reinterpret_cast<float (*)[16 * TR_LD]>(lds);
+  float (*zb)[16 * TR_LD] = reinterpret_cast<float (*)[16 * TR_LD]>(lds + 2 * 16 * TR_LD);
+  float (*red)[64][17] = reinterpret_cast<float (*)[64][17]>(lds + (2 + TR_NHID) * 16 * TR_LD);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15;
+  auto signal = [&](int l) {
+    if constexpr (SIG) rows_signal(ready + (e * (TR_NHID + 1) + l) * TS_STRIDE);
+  };
   const int M = a.M, IN = a.IN, H = a.H, D = a.D, i0 = rb * 16;
   const int c0 = 64 * (w & 3) + 4 * li + TR_TW * (w >> 2);   // this lane's first column
   auto wfwd = [&](int l) {
@@ -509,7 +539,7 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
       const int64_t er = (int64_t)e * M + row;
       if (c < IN) {
         const float x = (a.inputs[src * IN + c] - a.mu[c]) / a.sigma[c];   // utils.py:96
-        a.X[er * IN + c] = x;
+        st_h<SIG>(&a.X[er * IN + c], x);
         buf[0][r * TR_LD + c] = x;
       } else {
         a.T[er * D + (c - IN)] = a.targets[src * D + (c - IN)];
@@ -545,7 +575,7 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
           st_tw<TR_TW>(zb[l] + r * TR_LD + c0, v);             // pre-activation, for swish' below
 #pragma unroll
           for (int q = 0; q < TR_TW; ++q) v[q] = swish_fast(v[q]);
-          if (ok) st_tw<TR_TW>(a.Hh[l] + ((int64_t)e * M + row) * H + c0, v);
+          if (ok) st_tw_h<SIG, TR_TW>(a.Hh[l] + ((int64_t)e * M + row) * H + c0, v);
         } else if (ok) {
           st_tw<TR_TW>(a.OUT + ((int64_t)e * M + row) * 2 * D + c0, v);
         }
@@ -581,8 +611,8 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
       const float dlv1 = dlv * sb;
       g_mean = 2.f * err * inv * s;
       g_lv = dlv1 * sa;
-      a.dOUT[er * 2 * D + d] = g_mean;
-      a.dOUT[er * 2 * D + D + d] = g_lv;
+      st_h<SIG>(&a.dOUT[er * 2 * D + d], g_mean);
+      st_h<SIG>(&a.dOUT[er * 2 * D + D + d], g_lv);
       c_mn = dlv * (1.f - sb);
       c_mx = dlv1 * (1.f - sa);
       c_loss = (err * err * inv + lv) * s;
@@ -601,8 +631,9 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
     for (int k = 0; k < 3; ++k)
       for (int r = 0; r < 16; ++r) t3[k] += red[k][tid][r];
     float* pp = a.lpart + (((int64_t)e * a.nrb + rb) * D + tid) * 4;
-    pp[0] = t3[0]; pp[1] = t3[1]; pp[2] = t3[2];
+    st_h<SIG>(pp, t3[0]); st_h<SIG>(pp + 1, t3[1]); st_h<SIG>(pp + 2, t3[2]);
   }
+  signal(TR_NHID);   // the heads' weight-gradient operands (Hh[NHID - 1], dOUT) and the loss partials
   // ---- the activation-gradient chain (train_bwd_rows_kernel), swish'(Z) from LDS; dY of layer l sits in
   //      buf[(TR_NHID - l) & 1] as in that kernel (dy = buf[TR_NHID & 1] = buf[0] for 4 hidden layers)
   static_assert((TR_NHID & 1) == 0, "the backward's first input buffer is buf[0]");
@@ -633,14 +664,27 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
         float v[TR_TW];
 #pragma unroll
         for (int q = 0; q < TR_TW; ++q) v[q] = ok ? acc[q][i] * dswish_fast(zm[i][q]) : 0.f;
-        if (ok) st_tw<TR_TW>(a.dZ[l - 1] + ((int64_t)e * M + row) * H + c0, v);
+        if (ok) st_tw_h<SIG, TR_TW>(a.dZ[l - 1] + ((int64_t)e * M + row) * H + c0, v);
         st_tw<TR_TW>(out + r * TR_LD + c0, v);
       }
     }
-    lds_barrier();
+    if constexpr (SIG) signal(l - 1);   // layer l - 1's operands (Hh[l - 2] or X, dZ[l - 1]); a full barrier
+    else lds_barrier();
   };
   bwd(std::integral_constant<int, GD>{}, TR_NHID);
   for (int l = TR_NHID - 1; l >= 1; --l) bwd(std::integral_constant<int, GH>{}, l);
+}
+
+template <int G0, int GH, int GD>
+static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(const TrainRows a) {
+  __shared__ __attribute__((aligned(16))) float lds[TR_LDS_FLOATS];
+  int e, rb;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
+    a.beta_pow[2] = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);          // this step's TF1 Adam step size
+  }
+  if (!tr_block(blockIdx.x, a.nrb, a.E, e, rb)) return;
+  train_rows_body<G0, GH, GD, false>(a, lds, nullptr, e, rb);
 }
 
 }  // namespace mopo

@@ -78,17 +78,20 @@ def test_error_reporting():
     assert b'num_networks' in L.mopo_last_error()
 
 
+@pytest.mark.parametrize('step', [False, True])
 @pytest.mark.parametrize('E,O,A,H', [(7, 17, 6, 200), (7, 11, 3, 200), (5, 17, 6, 256), (16, 17, 6, 32), (1, 3, 1, 8)])
-def test_train_weight_gradient_tile_lists(E, O, A, H):
+def test_train_weight_gradient_tile_lists(E, O, A, H, step):
     """The training step's weight-gradient tiles (bnn_train.hip make_wlist, host only): every (layer,
     member, tile row, tile column) of the 5 layers exactly once over the 8 XCD lists, the lists within one
-    tile of an even share, and -- except the overflow past that share -- member e's tiles on list e mod 8."""
+    tile of an even share, and -- except the overflow past that share -- member e's tiles on list e mod 8.
+    step: the single-launch step's lists (order 2), whose entries are also ordered by layer, heads first."""
     from mopo_amd import _lib
     L = _lib.lib()
-    per = L.mopo_bnn_train_tile_lists(E, O, A, H, None, 0)
+    fn = L.mopo_bnn_train_tile_lists_step if step else L.mopo_bnn_train_tile_lists
+    per = fn(E, O, A, H, None, 0)
     assert per > 0
     out = np.empty(8 * per + 8, np.int32)
-    assert L.mopo_bnn_train_tile_lists(E, O, A, H, out.ctypes.data, out.size) == per
+    assert fn(E, O, A, H, out.ctypes.data, out.size) == per
     cnt = out[8 * per:]
     IN, D = O + A, O + 1
     dims = [(IN, H), (H, H), (H, H), (H, H), (H, 2 * D)]
@@ -98,6 +101,8 @@ def test_train_weight_gradient_tile_lists(E, O, A, H):
     for x in range(8):
         lst = out[x * per:x * per + cnt[x]]
         assert np.all(out[x * per + cnt[x]:(x + 1) * per] == -1)
+        if step:
+            assert np.all(np.diff(lst & 7) <= 0)
         for v in lst:
             t = (v & 7, (v >> 3) & 15, (v >> 7) & 31, (v >> 12) & 31)
             got.append(t)
@@ -109,4 +114,4 @@ def test_train_weight_gradient_tile_lists(E, O, A, H):
     # tiles kept at home: all of them when the members fill the XCDs evenly, at least the even share otherwise
     assert home >= min(len(want), sum(min(per_member * len(range(x, E, 8)), target) for x in range(8)))
     with pytest.raises(Exception):
-        _lib.check(L.mopo_bnn_train_tile_lists(E, O, A, H, out.ctypes.data, 3))
+        _lib.check(fn(E, O, A, H, out.ctypes.data, 3))

@@ -225,16 +225,19 @@ def test_train_loop_joint_head_matches_oracle():
     np.testing.assert_allclose(var, rv, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize('wg2,nt', [(1, 512), (1, 1024), (0, 512)])
-def test_wgrad_launch_variants_match_oracle(wg2, nt):
+@pytest.mark.parametrize('knobs', ['MOPO_TRAIN_WG2=1,MOPO_TRAIN_WG2_NT=512', 'MOPO_TRAIN_WG2=1,MOPO_TRAIN_WG2_NT=1024',
+                                   'MOPO_TRAIN_WG2=0', 'MOPO_TRAIN_STEP1=1', 'MOPO_TRAIN_STEP1=1,MOPO_TRAIN_STEP_NWX=3'])
+def test_wgrad_launch_variants_match_oracle(knobs):
     """The weight-gradient launch knobs (MOPO_TRAIN_WG2: the persistent XCD-local tile launch or the
-    grouped-GEMM launch; MOPO_TRAIN_WG2_NT: 512- or 1024-thread tile workgroups) are read once per
-    process, so each setting runs the epoch and train-loop parity tests above in a fresh process."""
+    grouped-GEMM launch; MOPO_TRAIN_WG2_NT: 512- or 1024-thread tile workgroups; MOPO_TRAIN_STEP1: the
+    whole step as one launch with in-launch hand-offs, MOPO_TRAIN_STEP_NWX its tile workgroups per XCD)
+    are read once per process, so each setting runs the epoch and train-loop parity tests above in a
+    fresh process."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MOPO_TRAIN_WG2=str(wg2), MOPO_TRAIN_WG2_NT=str(nt))
+    env = dict(os.environ, **dict(kv.split('=') for kv in knobs.split(',')))
     r = subprocess.run([sys.executable, '-m', 'pytest', '-p', 'no:cacheprovider', '-q', '-x', '-m', 'gpu',
                         os.path.join(root, 'tests', 'test_gpu_train.py'),
                         '-k', 'epoch_matches_oracle_steps or train_loop_matches_oracle'],
