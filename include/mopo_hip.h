@@ -198,6 +198,9 @@ int mopo_bnn_train_logs(mopo_bnn_train_t h, float* h_logs, int n);
 int mopo_bnn_train_tile_lists(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap);
 /* The same for the single-launch step (MOPO_TRAIN_STEP1): each list ordered by layer, the heads first. */
 int mopo_bnn_train_tile_lists_step(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap);
+/* Diagnostic builds only (MOPO_TRAIN_STAMPS=1; otherwise returns -1): the single-launch step's
+ * per-workgroup phase stamps of the last step, [block][8] (bnn_train.hip mopo_bnn_train_debug_stamps). */
+int mopo_bnn_train_debug_stamps(uint64_t* h_out, int64_t n);
 
 /* ---- fused model rollout (MOPO._rollout_model) ----------------------------------------- */
 typedef struct mopo_rollout_s* mopo_rollout_t;

@@ -80,6 +80,7 @@ SIGNATURES = {
     'mopo_bnn_train_logs': (c_int, [c_void_p, c_void_p, c_int]),
     'mopo_bnn_train_tile_lists': (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_i64]),
     'mopo_bnn_train_tile_lists_step': (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_i64]),
+    'mopo_bnn_train_debug_stamps': (c_int, [c_void_p, c_i64]),
     'mopo_rollout_create': (c_int, [C.POINTER(c_void_p), c_void_p, c_i64, c_int]),
     'mopo_rollout_destroy': (c_int, [c_void_p]),
     'mopo_rollout_run': (c_int, [c_void_p, C.POINTER(RolloutArgs), C.POINTER(PoolDesc), c_void_p]),

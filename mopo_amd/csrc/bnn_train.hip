@@ -652,17 +652,18 @@ static __global__ __launch_bounds__(NT, NT / 128) void train_wgrad2_kernel(const
 
 // ---- the whole minibatch step as ONE launch (MOPO_TRAIN_STEP1) ------------------------------------------
 // Workgroups [0, nrw): the row blocks (train_rows_body<SIG = true>: member e's blocks on XCD e mod 8, each
-// stage ending in a hand-off on ready[e][l]); [nrw, nrw + 8 nwx): weight-gradient tile workgroups, nwx per
-// XCD, taking the entries of their XCD's list (tiles in readiness order: layer NHID first) from a per-XCD
-// work counter, each tile waiting until all nrb row blocks of its (member, layer) have signalled -- so the
-// heads' and the top hidden layers' tiles run on the CUs the 7 x 16 row blocks leave idle while the row
-// blocks are still in their backward chain; the last workgroup: the batch-level tail (loss partials, the
-// log-var bounds' Adam), which then waits for every other workgroup of the launch before it advances the
-// beta powers and the minibatch counter (every workgroup derives this step's lr_t from them at its start)
-// and zeroes the launch's counters for the next launch.  Waits are only ever on lower workgroup ids
-// (dispatched first), every spin is bounded (a give-up sets the timeout word; the tail then writes NaN to
-// the loss log).  Handed-off rows are stored write-through by the producers and read by the tiles with sc1
-// loads (Guideline 16's R1 form): correct wherever the dispatcher puts a workgroup.
+// stage handed off on ready[e][l]); workgroup nrw: the batch-level tail (the loss partials once every
+// member's row blocks are past their output gradient, the log-var bounds' Adam), which then waits for every
+// other workgroup of the launch before it advances the beta powers and the minibatch counter (every
+// workgroup derives this step's lr_t from them at its start) and zeroes the launch's counters; the rest:
+// weight-gradient tile workgroups, nwx per XCD, taking the entries of their XCD's list (tiles in readiness
+// order: layer NHID first) from a per-XCD work counter, each tile waiting until all nrb row blocks of its
+// (member, layer) have signalled -- so the heads' and the top hidden layers' tiles run on the CUs the 7 x 16
+// row blocks leave idle while the row blocks are still in their backward chain.  The tiles wait only on row
+// blocks (lower ids, dispatched first, never waiting themselves) and nothing waits on the tail, so the
+// launch drains whatever the placement; every spin is bounded (a give-up sets the timeout word; the tail then
+// writes NaN to the loss log).  Handed-off rows are stored write-through by the producers and read by the
+// tiles with sc1 loads (cdna_hip_programming.md Guideline 16, R1 form).
 struct TrainStep {
   TrainRows r;
   TrainWg2 g;
@@ -727,21 +728,29 @@ static __device__ __forceinline__ void ts_tiles(const TrainStep& s, float* As, f
   const float b1p = s.r.beta_pow[0], b2p = s.r.beta_pow[1];
   const float lr_t = s.r.lr * sqrtf(1.f - b2p) / (1.f - b1p);     // train_rows_kernel's block 0 expression
   const int qd = w & 3, qi = qd >> 1, qj = qd & 1, kq = w >> 2, li = lane & 15, lk = lane >> 4;
-  if (tid == 0) slot[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the list entries this workgroup runs come from the XCD's work counter, two ahead: the entry after the
+  // next one is requested at the top of each tile and read at the top of the following one
+  if (tid == 0) {
+    slot[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    slot[1] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
-  int i = slot[0];
+  const int i = slot[0];
+  int inx = __builtin_amdgcn_readfirstlane(slot[1]);
   __syncthreads();
   if (i >= cnt) return;
+  unsigned pend = 0;
+  if (tid == 0) pend = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   Wg2Tile cur = wg2_tile(g, __builtin_amdgcn_readfirstlane(lst[i]));
+  AdamIn a_in[C::NE], c_in;
+  wg2_adam_in<NT>(ad, cur, tid, a_in, c_in);          // not produced in this launch: ahead of the wait
   ts_wait(ready(cur), (unsigned)nrb, tmo);
+  tstamp(1);
+  int ntile = 1;
   f32x4 va[C::NQ], vb[C::NQ];
   wg2_issue_sc1<NT>(cur, M, 0, tid, va, vb);
-  AdamIn a_in[C::NE], c_in;
-  wg2_adam_in<NT>(ad, cur, tid, a_in, c_in);
   while (true) {
-    unsigned nxt = 0;
-    if (tid == 0) nxt = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int inx = cnt;
+    int after = cnt;
     bool pref = false;
     Wg2Tile nx = cur;
     AdamIn a_nx[C::NE], c_nx{0.f, 0.f, 0.f, 0.f};
@@ -762,18 +771,21 @@ static __device__ __forceinline__ void ts_tiles(const TrainStep& s, float* As, f
             Bs[(r0 + u) * TW2_KP + k0 + (NT / 8) * q] = vb[q][u];
           }
       }
-      if (kc == 0 && tid == 0) slot[0] = (int)nxt;
+      if (kc == 0 && tid == 0) slot[0] = (int)pend;   // requested a whole tile ago
       lds_barrier();
-      if (kc == 0) inx = __builtin_amdgcn_readfirstlane(slot[0]);
+      if (kc == 0) {
+        after = __builtin_amdgcn_readfirstlane(slot[0]);
+        if (tid == 0) pend = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if (kc + TW2_KC < M) {
         wg2_issue_sc1<NT>(cur, M, kc + TW2_KC, tt, va, vb);
       } else if (inx < cnt) {
         nx = wg2_tile(g, __builtin_amdgcn_readfirstlane(lst[inx]));
-        // prefetch the next tile only when its operands are already complete (else after this epilogue)
+        wg2_adam_in<NT>(ad, nx, tt, a_nx, c_nx);
+        // the next tile's operand rows only when they are already complete (else after this epilogue)
         if (__builtin_amdgcn_readfirstlane(ts_load(ready(nx))) >= (unsigned)nrb) {
           pref = true;
           wg2_issue_sc1<NT>(nx, M, 0, tt, va, vb);
-          wg2_adam_in<NT>(ad, nx, tt, a_nx, c_nx);
         }
       }
 #pragma unroll
@@ -818,16 +830,19 @@ static __device__ __forceinline__ void ts_tiles(const TrainStep& s, float* As, f
       if (cur.cs && tid % C::CT == 0 && cj < cur.N) adam_apply(ad, cur.b0 + cj, cs, c_in, lr_t);
     }
     if (inx >= cnt) break;
+    ++ntile;
     if (!pref) {
       ts_wait(ready(nx), (unsigned)nrb, tmo);
       wg2_issue_sc1<NT>(nx, M, 0, tid, va, vb);
-      wg2_adam_in<NT>(ad, nx, tid, a_nx, c_nx);
     }
     lds_barrier();                                   // the partials are read before the next panels land
     cur = nx;
+    inx = after;
     for (int h = 0; h < C::NE; ++h) a_in[h] = a_nx[h];
     c_in = c_nx;
   }
+  tstamp(2);
+  tstamp(3, ntile);
 }
 
 template <int G0, int GH, int GD>
@@ -837,7 +852,8 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_step_kernel(con
                                                                                            : 2 * TW2_T * TW2_KP + 64];
   const int b = blockIdx.x, E = s.r.E;
   unsigned* glob = s.sync + E * (NHID + 1) * TS_STRIDE;
-  if (b == (int)gridDim.x - 1) {   // the batch-level tail
+  tstamp(0);
+  if (b == s.nrw) {   // the batch-level tail, right after the row blocks: its loss sums run beside the tiles
     if (threadIdx.x < 64) {        // every member's row blocks are past their output gradient
       const int e = threadIdx.x;
       unsigned spins = 0;
@@ -854,7 +870,9 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_step_kernel(con
       }
     }
     __syncthreads();
+    tstamp(1);
     train_loss_tail<TrainTail, true>(s.g.t, lds);
+    tstamp(2);
     if (threadIdx.x == 0) {   // every other workgroup has read the beta powers and the counters
       const unsigned others = gridDim.x - 1;
       unsigned spins = 0;
@@ -876,13 +894,14 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_step_kernel(con
       for (int c = 0; c < 8; ++c) glob[(TS_WORK + c) * TS_STRIDE] = 0u;
       glob[TS_DONE * TS_STRIDE] = 0u;
     }
+    tstamp(3);
     return;
   }
   if (b < s.nrw) {
     int e, rb;
     if (tr_block(b, s.r.nrb, E, e, rb)) train_rows_body<G0, GH, GD, true>(s.r, lds, s.sync, e, rb);
   } else {
-    ts_tiles<512>(s, lds, lds + TW2_T * TW2_KP, reinterpret_cast<int*>(lds + 2 * TW2_T * TW2_KP), (b - s.nrw) & 7);
+    ts_tiles<512>(s, lds, lds + TW2_T * TW2_KP, reinterpret_cast<int*>(lds + 2 * TW2_T * TW2_KP), b & 7);
   }
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_fetch_add(glob + TS_DONE * TS_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1273,6 +1292,21 @@ static int tile_lists(int E, int obs_dim, int act_dim, int hidden, int order, in
     std::copy(host.begin(), host.end(), out);
   }
   return per;
+}
+
+// Diagnostic builds only (MOPO_TRAIN_STAMPS=1; otherwise -1): the single-launch step's per-workgroup stamps
+// of the last step ([block][8]: rows 0 start, 1..5 the hand-offs l = NHID .. 0; tiles 0 start, 1 first
+// wait done, 2 end, 3 tiles done; the tail 0 start, 1 rows ready, 2 loss tail done, 3 end), 100 MHz clock
+extern "C" int mopo_bnn_train_debug_stamps(uint64_t* h_out, int64_t n) {
+#if MOPO_TRAIN_STAMPS
+  MOPO_REQUIRE(h_out && n >= 0 && n <= 2048 * 8, "mopo_bnn_train_debug_stamps: bad output");
+  MOPO_HIP(hipDeviceSynchronize());
+  MOPO_HIP(hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_train_stamps), n * 8));
+  return 0;
+#else
+  (void)h_out; (void)n;
+  return fail("mopo_bnn_train_debug_stamps: library built without MOPO_TRAIN_STAMPS");
+#endif
 }
 
 extern "C" int mopo_bnn_train_destroy(mopo_bnn_train_t hh) {

@@ -363,26 +363,31 @@ typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 struct F16Pair {
   uint32_t hi, lo;
 };
-__device__ __forceinline__ F16Pair split_f16_pair(float a, float b, float s) {
-  const float as = a * s, bs = b * s;
-  uint32_t h;
-  asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h) : "v"(as), "v"(bs));
-  const float ah = (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
-  const float bh = (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16));
-  uint32_t l;
-  asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(l) : "v"(as - ah), "v"(bs - bh));
-  return {h, l};
-}
-
-// the same split of two values already multiplied by their row scale
+// The remainders v - f32(hi) come from ONE v_fma_mix_f32 each (the fp16 half read in place, times -1,
+// plus v; a full 32-bit result): exact, as the subtraction is (hi = RN16(v) is within half an fp16 ulp of
+// v), so the parts are bit-identical to the convert + subtract form, one VALU op per value fewer
+// (MOPO_F16_MIXSUB=0: that form)
+#ifndef MOPO_F16_MIXSUB
+#define MOPO_F16_MIXSUB 1
+#endif
 __device__ __forceinline__ F16Pair split_f16_pair_prescaled(float as, float bs) {
   uint32_t h;
   asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h) : "v"(as), "v"(bs));
-  const float ah = (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
-  const float bh = (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16));
+  float la, lb;
+  if (MOPO_F16_MIXSUB) {
+    asm volatile("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(la) : "v"(h), "v"(as));
+    asm volatile("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(lb) : "v"(h), "v"(bs));
+  } else {
+    la = as - (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
+    lb = bs - (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16));
+  }
   uint32_t l;
-  asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(l) : "v"(as - ah), "v"(bs - bh));
+  asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(l) : "v"(la), "v"(lb));
   return {h, l};
+}
+
+__device__ __forceinline__ F16Pair split_f16_pair(float a, float b, float s) {
+  return split_f16_pair_prescaled(a * s, b * s);
 }
 
 // power-of-two scale s with max |v| * s in [2^14, 2^15) (mx >= 0; zero / tiny rows clamp, inf / NaN

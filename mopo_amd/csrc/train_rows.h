@@ -484,6 +484,22 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_bwd_rows_kernel
 // stores, the workgroup barrier, then one agent-scope add to ready[(e (NHID + 1) + l) TS_STRIDE], the count
 // of row blocks of member e whose layer-l weight-gradient operands are complete (l = NHID after the output
 // gradient, l - 1 after the backward of layer l).
+#ifndef MOPO_TRAIN_STAMPS
+#define MOPO_TRAIN_STAMPS 0   // diagnostic builds: per-workgroup phase stamps of train_step_kernel
+#endif
+#if MOPO_TRAIN_STAMPS
+__device__ uint64_t g_train_stamps[2048 * 8];
+#endif
+// stamp i of this workgroup (wave 0; its lanes all store the same value); v: a value instead of the clock
+static __device__ __forceinline__ void tstamp(int i, int64_t v = -1) {
+#if MOPO_TRAIN_STAMPS
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0 && blockIdx.x < 2048)
+    __hip_atomic_store(&g_train_stamps[blockIdx.x * 8 + i], v < 0 ? __builtin_amdgcn_s_memrealtime() : (uint64_t)v,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  (void)i; (void)v;
+#endif
+}
 constexpr int TS_STRIDE = 32;   // one counter per 128-B line
 constexpr int TR_LDS_FLOATS = (2 + TR_NHID) * 16 * TR_LD + 3 * 64 * 17;
 template <bool SC>
@@ -513,7 +529,10 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
   float (*red)[64][17] = reinterpret_cast<float (*)[64][17]>(lds + (2 + TR_NHID) * 16 * TR_LD);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15;
   auto signal = [&](int l) {
-    if constexpr (SIG) rows_signal(ready + (e * (TR_NHID + 1) + l) * TS_STRIDE);
+    if constexpr (SIG) {
+      rows_signal(ready + (e * (TR_NHID + 1) + l) * TS_STRIDE);
+      tstamp(1 + TR_NHID - l);
+    }
   };
   const int M = a.M, IN = a.IN, H = a.H, D = a.D, i0 = rb * 16;
   const int c0 = 64 * (w & 3) + 4 * li + TR_TW * (w >> 2);   // this lane's first column
@@ -633,7 +652,10 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     float* pp = a.lpart + (((int64_t)e * a.nrb + rb) * D + tid) * 4;
     st_h<SIG>(pp, t3[0]); st_h<SIG>(pp + 1, t3[1]); st_h<SIG>(pp + 2, t3[2]);
   }
-  signal(TR_NHID);   // the heads' weight-gradient operands (Hh[NHID - 1], dOUT) and the loss partials
+  // the hand-offs are signalled one stage late, right after the next layer's MFMAs: by then the stage's
+  // write-through stores have long completed, so the drain in front of the signal costs nothing (signalled
+  // at once it stalled every wave on its stores, ~1 us per stage); the last one goes out at the end
+  int pending = TR_NHID;   // the heads' weight-gradient operands (Hh[NHID - 1], dOUT) and the loss partials
   // ---- the activation-gradient chain (train_bwd_rows_kernel), swish'(Z) from LDS; dY of layer l sits in
   //      buf[(TR_NHID - l) & 1] as in that kernel (dy = buf[TR_NHID & 1] = buf[0] for 4 hidden layers)
   static_assert((TR_NHID & 1) == 0, "the backward's first input buffer is buf[0]");
@@ -651,9 +673,11 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     f32x4 acc[TR_TW];
     if (TR_XPF) {
       rows_gemm_pre<true, G, TR_TW>(buf[(TR_NHID - l) & 1], wbwd(l), c0, lane, pre, acc);
+      if constexpr (SIG) signal(pending);
       if (l > 1) rows_pre<true, GH, TR_TW>(wbwd(l - 1), c0, lane, pre);
     } else {
       rows_gemm<true, G, TR_TW>(buf[(TR_NHID - l) & 1], Wl, Nl, Kl, Nl, c0, lane, acc);
+      if constexpr (SIG) signal(pending);
     }
     float* out = buf[(TR_NHID - l + 1) & 1];
     if (__builtin_amdgcn_readfirstlane(c0 - 4 * li) < Kl) {
@@ -668,11 +692,13 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
         st_tw<TR_TW>(out + r * TR_LD + c0, v);
       }
     }
-    if constexpr (SIG) signal(l - 1);   // layer l - 1's operands (Hh[l - 2] or X, dZ[l - 1]); a full barrier
-    else lds_barrier();
+    pending = l - 1;   // layer l - 1's operands (Hh[l - 2] or X, dZ[l - 1])
+    lds_barrier();
   };
   bwd(std::integral_constant<int, GD>{}, TR_NHID);
   for (int l = TR_NHID - 1; l >= 1; --l) bwd(std::integral_constant<int, GH>{}, l);
+  if constexpr (SIG) signal(pending);
+  (void)pending;
 }
 
 template <int G0, int GH, int GD>

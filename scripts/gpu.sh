@@ -12,6 +12,7 @@
 #   train_so_ab BNN.train parity on each abv/<v>.so of $AB, then the train leg alternating them
 #   env_ab      bench (SAC + headline) alternating the env settings in $VARS (comma-joined per variant)
 #   stamps      SAC phase stamps from abv/sac_stamps.so (scripts/sac_stamps.py)
+#   train_stamps  single-launch BNN.train step stamps from abv/train_stamps.so (scripts/train_timeline.py)
 # usage: bash scripts/gpu.sh tests bench ;  AB="new old" bash scripts/gpu.sh sac_ab
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
@@ -100,6 +101,13 @@ for step in "$@"; do
         env ${v//,/ } timeout -k 10 120 python scripts/sac_timeline.py >> gpurun_out/sac_timeline.txt 2>&1 || { rc=1; break; }
       done
       restore; cat gpurun_out/sac_timeline.txt ;;
+    train_stamps)
+      keep; cp abv/train_stamps.so mopo_amd/libmopo_hip.so; : > gpurun_out/train_timeline.txt; rc=0
+      for v in ${VARS:-MOPO_TRAIN_STEP1=1}; do
+        echo "== $v" >> gpurun_out/train_timeline.txt
+        env ${v//,/ } timeout -k 10 120 python scripts/train_timeline.py >> gpurun_out/train_timeline.txt 2>&1 || { rc=1; break; }
+      done
+      restore; cat gpurun_out/train_timeline.txt ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
   echo "== step $step rc=$rc"
