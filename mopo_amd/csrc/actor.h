@@ -32,6 +32,9 @@ struct ActorArgs {
   // 0: f32 MFMA on the fragment-major f32 packing; 4 (DT_F16X3): the f16x3 split (mlp_tile.h) on the
   // f16 packing (pack_actor with f16 = 1)
   int dtype;
+  // 1: no other launch runs beside this one (an unsplit rollout): the f16x3 ring actor (actor_f16q_kernel,
+  // 203 VGPRs), faster alone, slower beside the other row part's ensemble launch
+  int alone;
 };
 
 int launch_actor(const ActorArgs& a, hipStream_t s);

@@ -567,10 +567,11 @@ __global__ __launch_bounds__(ACT_WAVES * 64, R == 1 ? 2 : 1) void actor_f16r_ker
 // (2 slices: the fp16 parts), layer 2 (2 KG slices) and the whole head (its 2 KG fragments as one
 // slice) -- slice j + 2 copied while slice j is consumed, behind counted vmcnt + raw barriers.  The
 // hidden biases ride into LDS once, ahead of the first slices; the head's output rows reuse a ring slot.
+// Same-box A/B (round 4): actor 0.062 -> 0.054 ms alone, but the split rollout 1.6 % slower (203 VGPRs
+// beside the concurrent ensemble launch of the other row part), so it runs only where the actor runs
+// alone (ActorArgs::alone: unsplit rollouts -- one-step C3, compacting walker / hopper rollouts)
 #ifndef ACT_F16_RING
-#define ACT_F16_RING 0  // same-box A/B: actor 0.062 -> 0.054 ms alone, but the rollout 1.6 % slower (203 VGPRs
-                        // beside the concurrent ensemble launch of the other row part), so it stays off (and
-                        // is compiled only in ACT_F16_RING = 1 A/B builds)
+#define ACT_F16_RING 1
 #endif
 #if ACT_F16_RING
 template <int NBP>
@@ -745,7 +746,7 @@ int launch_actor(const ActorArgs& a, hipStream_t s) {
 #endif
   if (a.dtype == DT_F16X3) {
 #if ACT_F16_RING
-    if (a.Hp == 256) hipLaunchKernelGGL(actor_f16q_kernel<16>, grid, block, 0, s, a);
+    if (a.alone && a.Hp == 256) hipLaunchKernelGGL(actor_f16q_kernel<16>, grid, block, 0, s, a);
     else
 #endif
     if (a.Hp == 256) hipLaunchKernelGGL(actor_f16_kernel<16>, grid, block, 0, s, a);

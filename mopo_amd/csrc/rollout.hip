@@ -365,6 +365,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     aa.sel_in = a->d_model_inds ? a->d_model_inds + (int64_t)i * B + off : nullptr;
     aa.rand_act = a->rollout_random;
     aa.dtype = a->actor_dtype;
+    aa.alone = !split;
     aa.act_uni = a->d_act_uniform ? a->d_act_uniform + ((int64_t)i * B + off) * A : nullptr;
     aa.elites = a->d_elites; aa.n_elites = a->n_elites;
     aa.xs = h->xs + off * XS_STRIDE; aa.xs_mu = bnn->dev.mu; aa.xs_sigma = bnn->dev.sigma; aa.xs_in = bnn->dev.IN;
