@@ -11,7 +11,7 @@ flt = sys.argv[2] if len(sys.argv) > 2 else ''
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(d, 'pmc*', '*counter_collection.csv'))):
     for r in csv.DictReader(open(f)):
-        n = r['Kernel_Name'].split('(')[0].replace('void ', '')
+        n = r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0].replace('void ', '')
         if flt in n:
             agg[n][r['Counter_Name']].append(float(r['Counter_Value']))
 for n, cs in agg.items():

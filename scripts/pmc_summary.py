@@ -21,7 +21,7 @@ def load(d):
         if not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
-            n = r['Kernel_Name'].split('(')[0].replace('void ', '')
+            n = r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0].replace('void ', '')
             agg[n][r['Counter_Name']].append(float(r['Counter_Value']))
             agg[n]['_grid'].append(float(r['Grid_Size']))
     return agg
