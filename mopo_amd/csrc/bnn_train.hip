@@ -457,7 +457,16 @@ static __global__ __launch_bounds__(256, 2) void train_wgrad_kernel(const TrainW
 // j, j + nwx, ...) and load the next tile's panels and Adam inputs into registers while the current tile's
 // MFMAs and epilogue run, so a workgroup has two tiles in flight instead of one memory latency per tile.
 // The last block runs the batch-level tail (train_loss_tail).
-constexpr int TW2_T = 32, TW2_KC = 256, TW2_KP = TW2_KC + 4;
+#ifndef TRAIN_WG2_KC
+// K rows staged per chunk (LDS: 2 x 32 x (KC + 4) floats per workgroup).  128 (33 KB, 76 VGPRs) lets three
+// 512-thread workgroups share a CU instead of two at 256 (66.5 KB, 95 VGPRs): same box, 13.61-13.69k vs
+// 13.41-13.45k grad-steps/s (profiles/r05_train_ab_wg2_chunk.txt; four per CU at a 64-VGPR cap spill: 13.4k)
+#define TRAIN_WG2_KC 128
+#endif
+#ifndef TRAIN_WG2_MINW
+#define TRAIN_WG2_MINW 0   // > 0: waves per SIMD the tile kernel's registers are capped for (0: NT / 128)
+#endif
+constexpr int TW2_T = 32, TW2_KC = TRAIN_WG2_KC, TW2_KP = TW2_KC + 4;
 struct TrainWg2 {
   int M;                               // minibatch rows per member (the contraction length)
   int nwx, per_x;                      // tile workgroups per XCD; list stride per XCD
@@ -544,7 +553,7 @@ static __device__ __forceinline__ void wg2_adam_in(const AdamCtx& ad, const Wg2T
 }
 
 template <int NT>
-static __global__ __launch_bounds__(NT, NT / 128) void train_wgrad2_kernel(const TrainWg2 g) {
+static __global__ __launch_bounds__(NT, TRAIN_WG2_MINW > 0 ? TRAIN_WG2_MINW : NT / 128) void train_wgrad2_kernel(const TrainWg2 g) {
   using C = Wg2<NT>;
   __shared__ __attribute__((aligned(16))) float As[TW2_T * TW2_KP];   // [i][k]; later the K-part partials
   __shared__ __attribute__((aligned(16))) float Bs[TW2_T * TW2_KP];   // [j][k]
@@ -1018,7 +1027,8 @@ int train_wg2_nt() {
 int train_wg2_nwx() {
   static const int v = [] {
     const char* e = std::getenv("MOPO_TRAIN_WG2_NWX");
-    return e ? std::max(1, std::atoi(e)) : 64;   // two workgroups per CU (LDS: 2 x 66.5 KB)
+    // the resident workgroups: three 512-thread ones per CU (TRAIN_WG2_KC), one 1024-thread one
+    return e ? std::max(1, std::atoi(e)) : (train_wg2_nt() == 1024 ? 32 : 96);
   }();
   return v;
 }

@@ -65,18 +65,21 @@ for step in "$@"; do
       fi ;;
     train_so_ab)
       # BNN.train parity on each abv/<v>.so of $AB, then the train leg alternating the builds
+      # AB entries: <so> or <so>:ENV=VAL[,ENV=VAL]
       keep; rc=0; : > gpurun_out/ab_train.txt
       for v in $AB; do
-        cp abv/$v.so mopo_amd/libmopo_hip.so
-        timeout -k 10 300 $PYT tests/test_gpu_train.py -q -x -k "not variants" > gpurun_out/train_tests_$v.log 2>&1
-        rc=$?; echo "== $v parity rc=$rc: $(tail -1 gpurun_out/train_tests_$v.log)"
+        so=${v%%:*}; envs=""; [ "$so" != "$v" ] && envs=${v#*:}
+        cp abv/$so.so mopo_amd/libmopo_hip.so
+        env ${envs//,/ } timeout -k 10 300 $PYT tests/test_gpu_train.py -q -x -k "not variants" > gpurun_out/train_tests_$so.log 2>&1
+        rc=$?; echo "== $v parity rc=$rc: $(tail -1 gpurun_out/train_tests_$so.log)"
         [ $rc -ne 0 ] && break
       done
       if [ $rc -eq 0 ]; then
         for i in 1 2 3; do
           for v in $AB; do
-            cp abv/$v.so mopo_amd/libmopo_hip.so
-            timeout -k 10 200 python bench.py --no-cpu-baseline --no-c3 --no-alt-dtypes --sac-steps 16 --steps 3 --warmup 1 \
+            so=${v%%:*}; envs=""; [ "$so" != "$v" ] && envs=${v#*:}
+            cp abv/$so.so mopo_amd/libmopo_hip.so
+            env ${envs//,/ } timeout -k 10 200 python bench.py --no-cpu-baseline --no-c3 --no-alt-dtypes --sac-steps 16 --steps 3 --warmup 1 \
               --train-epochs ${TRAIN_EPOCHS:-3} > gpurun_out/abt_cur.json 2> gpurun_out/abt_cur.err || { rc=1; tail -5 gpurun_out/abt_cur.err; break 2; }
             python -c "import json; d=json.load(open('gpurun_out/abt_cur.json')); t=d['model_train']; print('$v', round(t['value']), 'steps/s', round(t['ms_per_epoch'], 2), 'ms/epoch')" >> gpurun_out/ab_train.txt
           done
