@@ -606,8 +606,11 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     }
     lds_barrier();
   };
+  if constexpr (!SIG) tstamp(1);
   fwd(std::integral_constant<int, G0>{}, 0);
+  if constexpr (!SIG) tstamp(2);
   for (int l = 1; l <= TR_NHID; ++l) fwd(std::integral_constant<int, GH>{}, l);
+  if constexpr (!SIG) tstamp(3);
   // ---- output gradient and the block's partial sums (train_fwd_rows_kernel); dY of the heads also into
   //      buf[0] (the backward's input; zero-padded to a multiple of 16 columns)
   const float* o = buf[(TR_NHID + 1) & 1];
@@ -655,6 +658,7 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
   // the hand-offs are signalled one stage late, right after the next layer's MFMAs: by then the stage's
   // write-through stores have long completed, so the drain in front of the signal costs nothing (signalled
   // at once it stalled every wave on its stores, ~1 us per stage); the last one goes out at the end
+  if constexpr (!SIG) tstamp(4);
   int pending = TR_NHID;   // the heads' weight-gradient operands (Hh[NHID - 1], dOUT) and the loss partials
   // ---- the activation-gradient chain (train_bwd_rows_kernel), swish'(Z) from LDS; dY of layer l sits in
   //      buf[(TR_NHID - l) & 1] as in that kernel (dy = buf[TR_NHID & 1] = buf[0] for 4 hidden layers)
@@ -696,7 +700,12 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     lds_barrier();
   };
   bwd(std::integral_constant<int, GD>{}, TR_NHID);
-  for (int l = TR_NHID - 1; l >= 1; --l) bwd(std::integral_constant<int, GH>{}, l);
+  if constexpr (!SIG) tstamp(5);
+  for (int l = TR_NHID - 1; l >= 1; --l) {
+    bwd(std::integral_constant<int, GH>{}, l);
+    if (!SIG && l == 2) tstamp(6);
+  }
+  if constexpr (!SIG) tstamp(7);
   if constexpr (SIG) signal(pending);
   (void)pending;
 }
@@ -710,6 +719,7 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
     a.beta_pow[2] = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);          // this step's TF1 Adam step size
   }
   if (!tr_block(blockIdx.x, a.nrb, a.E, e, rb)) return;
+  tstamp(0);
   train_rows_body<G0, GH, GD, false>(a, lds, nullptr, e, rb);
 }
 

@@ -40,6 +40,11 @@ def main():
             v = np.array([us(st[b, c]) for b in idx if st[b, c] > 0])
             if len(v):
                 print('%-8s %-22s p50 %7.2f  min %7.2f  max %7.2f  (n=%d)' % (name, lab, np.median(v), v.min(), v.max(), len(v)))
+    if os.environ.get('MOPO_TRAIN_STEP1', '0') == '0':   # the rows launch of the two-launch step alone
+        print('rows launch (two-launch step), %d row blocks, us' % len(rows))
+        show('rows', rows, range(8), ['start', 'gather done', 'layer 0', 'hidden + heads', 'loss + dY',
+                                      'bwd l4', 'bwd l3, l2', 'bwd l1 (end)'])
+        return
     print('single-launch train step, %d workgroups (%d row blocks, %d tile workgroups, 1 tail), us' % (nblk, len(rows), len(tiles)))
     show('rows', rows, range(6), ['start', 'fwd+loss (l=4 ready)', 'bwd l4 (l=3 ready)', 'bwd l3 (l=2 ready)',
                                   'bwd l2 (l=1 ready)', 'bwd l1 (l=0 ready)'])
