@@ -143,6 +143,9 @@ static __device__ __forceinline__ void rows_gemm(const float* As, const float* W
 // rows_gemm with the layer's first TR_PF k-groups of B loaded ahead (rows_pre), by the fused kernel across
 // the previous layer's epilogue and barrier: the weights do not depend on the activations, so a layer
 // no longer starts on an exposed L2 round trip
+#ifndef TR_LDOFF
+#define TR_LDOFF 1   // rows_ld: plain offsets, bounds by the buffer range (0: per-load masks, measured slower)
+#endif
 struct RowsW {
   __amdgpu_buffer_rsrc_t d;
   int K, N, ldw;
@@ -161,6 +164,44 @@ template <bool KT, int TW>
 static __device__ __forceinline__ void rows_ld(const RowsW& W, int grp, int c, int lane, float (&bv)[4][TW]) {
   const int lk = lane >> 4, k0 = 16 * grp + 4 * lk;
   const int K = W.K, N = W.N, ldw = W.ldw;
+#if defined(TR_KNOB_NOB)   // timing-only builds: no weight loads
+  for (int u = 0; u < 4; ++u)
+    for (int q = 0; q < TW; ++q) bv[u][q] = 0.001f * (k0 + u + q);
+  return;
+#endif
+#if TR_LDOFF
+  // no per-load bounds arithmetic: rows past the operand (k >= K, or c >= N for KT) fall past the buffer
+  // descriptor's range and read 0; the columns c >= N of a row read the next row's (finite) values, which
+  // only reach output columns the epilogue zeroes / never stores, or meet the zero padding of A
+  (void)K; (void)N;
+  if constexpr (KT) {
+#pragma unroll
+    for (int q = 0; q < TW; ++q) {
+      const f32x4 v = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(W.d, ((c + q) * ldw + 4 * lk) * 4 + 64 * grp, 0, 0));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) bv[u][q] = v[u];
+    }
+  } else {
+    const int vb = (4 * lk * ldw + c) * 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int off = vb + (16 * grp + u) * ldw * 4;
+      if constexpr (TW == 4) {
+        const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(W.d, off, 0, 0));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[u][q] = v[q];
+      } else if constexpr (TW == 2) {
+        const f32x2 v = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(W.d, off, 0, 0));
+        bv[u][0] = v[0];
+        bv[u][1] = v[1];
+      } else {
+        bv[u][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(W.d, off, 0, 0));
+      }
+    }
+  }
+  return;
+#endif
   if constexpr (KT) {
 #pragma unroll
     for (int q = 0; q < TW; ++q) {
@@ -214,7 +255,13 @@ static __device__ __forceinline__ void rows_gemm_pre(const float* As, const Rows
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int q = 0; q < TW; ++q) acc[q] = mfma4(a4[u], bq[grp][u][q], acc[q]);
+      for (int q = 0; q < TW; ++q) {
+#if defined(TR_KNOB_NOMFMA)   // timing-only builds: no MFMAs
+        acc[q][u] = fmaf(a4[u], bq[grp][u][q], acc[q][u]);
+#else
+        acc[q] = mfma4(a4[u], bq[grp][u][q], acc[q]);
+#endif
+      }
   }
 }
 

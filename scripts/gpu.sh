@@ -105,10 +105,14 @@ for step in "$@"; do
       done
       restore; cat gpurun_out/sac_timeline.txt ;;
     train_stamps)
-      keep; cp abv/train_stamps.so mopo_amd/libmopo_hip.so; : > gpurun_out/train_timeline.txt; rc=0
-      for v in ${VARS:-MOPO_TRAIN_STEP1=1}; do
-        echo "== $v" >> gpurun_out/train_timeline.txt
-        env ${v//,/ } timeout -k 10 120 python scripts/train_timeline.py >> gpurun_out/train_timeline.txt 2>&1 || { rc=1; break; }
+      # each stamps build of $SOS (default abv/train_stamps.so) under each env setting of $VARS
+      keep; : > gpurun_out/train_timeline.txt; rc=0
+      for so in ${SOS:-train_stamps}; do
+        cp abv/$so.so mopo_amd/libmopo_hip.so
+        for v in ${VARS:-MOPO_TRAIN_STEP1=1}; do
+          echo "== $so $v" >> gpurun_out/train_timeline.txt
+          env ${v//,/ } timeout -k 10 120 python scripts/train_timeline.py >> gpurun_out/train_timeline.txt 2>&1 || { rc=1; break 2; }
+        done
       done
       restore; cat gpurun_out/train_timeline.txt ;;
     *) echo "unknown step $step"; rc=2 ;;
