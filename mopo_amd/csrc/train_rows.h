@@ -82,6 +82,10 @@ constexpr int TR_WAVES = TR_WAVES_CFG, TR_TW = 16 / TR_WAVES;
 #endif
 // k-groups of B loaded ahead of their MFMAs (4 / 7: 11.52k -> 11.41k / 11.10k grad-steps/s, same-box A/B)
 constexpr int TR_PF = TR_PF_CFG;
+#ifndef TR_PF_B_CFG
+#define TR_PF_B_CFG TR_PF_CFG   // the fused rows kernel's backward (transposed weight reads)
+#endif
+constexpr int TR_PF_B = TR_PF_B_CFG, TR_PFM = TR_PF > TR_PF_B ? TR_PF : TR_PF_B;
 template <bool KT, int G, int TW>
 static __device__ __forceinline__ void rows_gemm(const float* As, const float* Wv, int Kv, int Nv, int ldwv, int c,
                                                  int lane, f32x4 (&acc)[TW]) {
@@ -173,7 +177,7 @@ static __device__ __forceinline__ void rows_ld(const RowsW& W, int grp, int c, i
   // no per-load bounds arithmetic: rows past the operand (k >= K, or c >= N for KT) fall past the buffer
   // descriptor's range and read 0; the columns c >= N of a row read the next row's (finite) values, which
   // only reach output columns the epilogue zeroes / never stores, or meet the zero padding of A
-  (void)K; (void)N;
+  (void)K;
   if constexpr (KT) {
 #pragma unroll
     for (int q = 0; q < TW; ++q) {
@@ -183,7 +187,9 @@ static __device__ __forceinline__ void rows_ld(const RowsW& W, int grp, int c, i
       for (int u = 0; u < 4; ++u) bv[u][q] = v[u];
     }
   } else {
-    const int vb = (4 * lk * ldw + c) * 4;
+    // a lane whose columns are all past N (the padding of the last column block) reads nothing: its base
+    // offset is pushed past the range (no L2 traffic for the 56 padding columns of a 200-wide layer)
+    const int vb = c < N ? (4 * lk * ldw + c) * 4 : (1 << 30);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int off = vb + (16 * grp + u) * ldw * 4;
@@ -228,28 +234,30 @@ static __device__ __forceinline__ void rows_ld(const RowsW& W, int grp, int c, i
   }
 }
 template <bool KT, int G, int TW>
-static __device__ __forceinline__ void rows_pre(const RowsW& W, int c, int lane, float (&pre)[TR_PF][4][TW]) {
+static __device__ __forceinline__ void rows_pre(const RowsW& W, int c, int lane, float (&pre)[TR_PFM][4][TW]) {
+  constexpr int PF = KT ? TR_PF_B : TR_PF;
   if (__builtin_amdgcn_readfirstlane(c - 4 * (lane & 15)) >= W.N) return;   // rows_gemm's no-column exit
 #pragma unroll
-  for (int grp = 0; grp < TR_PF && grp < G; ++grp) rows_ld<KT, TW>(W, grp, c, lane, pre[grp]);
+  for (int grp = 0; grp < PF && grp < G; ++grp) rows_ld<KT, TW>(W, grp, c, lane, pre[grp]);
 }
 template <bool KT, int G, int TW>
 static __device__ __forceinline__ void rows_gemm_pre(const float* As, const RowsW& W, int c, int lane,
-                                                     const float (&pre)[TR_PF][4][TW], f32x4 (&acc)[TW]) {
+                                                     const float (&pre)[TR_PFM][4][TW], f32x4 (&acc)[TW]) {
+  constexpr int PF = KT ? TR_PF_B : TR_PF;
   const int li = lane & 15, lk = lane >> 4;
 #pragma unroll
   for (int q = 0; q < TW; ++q) acc[q] = zero4();
   if (__builtin_amdgcn_readfirstlane(c - 4 * li) >= W.N) return;
-  float bq[G + TR_PF][4][TW];
+  float bq[G + PF][4][TW];
 #pragma unroll
-  for (int grp = 0; grp < TR_PF && grp < G; ++grp)
+  for (int grp = 0; grp < PF && grp < G; ++grp)
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int q = 0; q < TW; ++q) bq[grp][u][q] = pre[grp][u][q];
 #pragma unroll
   for (int grp = 0; grp < G; ++grp) {
-    if (grp + TR_PF < G) rows_ld<KT, TW>(W, grp + TR_PF, c, lane, bq[grp + TR_PF]);
+    if (grp + PF < G) rows_ld<KT, TW>(W, grp + PF, c, lane, bq[grp + PF]);
     __builtin_amdgcn_sched_barrier(0);
     const f32x4 a4 = ld4(As + li * TR_LD + 16 * grp + 4 * lk);
 #pragma unroll
@@ -591,7 +599,7 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     const int Nl = l == TR_NHID ? 2 * D : H;
     return rows_w<true>(a.P + a.W[l] + (int64_t)e * H * Nl, Nl, H, Nl);
   };
-  float pre[TR_PF][4][TR_TW];
+  float pre[TR_PFM][4][TR_TW];
   if (TR_XPF) rows_pre<false, G0, TR_TW>(wfwd(0), c0, lane, pre);   // in flight during the gather
   {  // gather (train_fwd_rows_kernel)
     const int W = IN + D, KP = ((IN + 15) >> 4) << 4;
