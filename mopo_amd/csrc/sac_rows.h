@@ -114,6 +114,13 @@ static __device__ __forceinline__ void hstore(float* p, float v) {
 // ever waits on producers with lower workgroup ids (all of them are dispatched first), and every spin is bounded:
 // on a give-up it sets the sticky timeout word, which the loss tail turns into NaN logs.
 constexpr unsigned SAC_SPIN_LIMIT = 1u << 19;
+#ifndef MOPO_SAC_LDOFF
+#define MOPO_SAC_LDOFF 1   // the forward blocks' W1 / W2 operand loads at plain offsets (bounds by the range)
+#endif
+#ifndef MOPO_SAC_LDOFF2
+#define MOPO_SAC_LDOFF2 0  // the same for step 7's, B1's critic and policy-row W2 loads (H a multiple of 64):
+                           // 37.3-37.9 vs 37.0-37.2 us/step with the forward blocks' alone (same box), so off
+#endif
 constexpr int SYNC_STRIDE = 32;      // one counter per 128-B line: counter c at sync[c * SYNC_STRIDE]
 #ifndef MOPO_SAC_B1_LATE
 // 1: in the F1 + F2 + B1 launch a B1 block waits for its row block's F1 blocks before issuing ANY operand
@@ -314,10 +321,18 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
   const auto dw2 = rsrc(c.W2p, (int64_t)H * H);
   const int boff = (tile_on ? col : 0) * H;
   f32x4 bq[16];                       // B(k, j) = W2p[j][k]: lane (li, lk) contracts k = 64 lk + 4 t + u
+  if (MOPO_SAC_LDOFF2 && (H & 63) == 0) {
+    // k < H exactly when 64 lk < H: one base per lane, plain offsets
+    const int vb = 64 * lk < H ? (boff + 64 * lk) * 4 : (1 << 30);
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    const int k = 64 * lk + 4 * t;
-    bq[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dw2, (k < H ? boff + k : -4) * 4, 0, 0));
+    for (int t = 0; t < 16; ++t)
+      bq[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dw2, vb + 16 * t, 0, 0));
+  } else {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int k = 64 * lk + 4 * t;
+      bq[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dw2, (k < H ? boff + k : -4) * 4, 0, 0));
+    }
   }
   const auto dm1 = rsrc(c.h1p, (int64_t)n * H);
   float m1[4];
@@ -613,14 +628,25 @@ static __device__ __forceinline__ void step7_loads(const FwdInst& p, int w, int 
                                                    f32x4 (&wa2)[4][4], f32x4 (&wb1)[4]) {
   const int kw = 64 * w;
   const auto dw2 = rsrc(p.w2, (int64_t)H * H);
+  if (MOPO_SAC_LDOFF2 && (H & 63) == 0) {
+    // whole 64-column blocks: every c < H, and rows k >= H fall past the range (H H): plain offsets
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      const int vb = ((kw + 16 * t + li) * H + c0 + 4 * lk) * 4;
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) {
-      const int k = kw + 16 * t + li, c = c0 + 16 * s2 + 4 * lk;
-      wa2[t][s2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 dw2, ((k < H && c < H) ? k * H + c : -4) * 4, 0, 0));
+      for (int s2 = 0; s2 < 4; ++s2)
+        wa2[t][s2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dw2, vb + 64 * s2, 0, 0));
     }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int k = kw + 16 * t + li, c = c0 + 16 * s2 + 4 * lk;
+        wa2[t][s2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   dw2, ((k < H && c < H) ? k * H + c : -4) * 4, 0, 0));
+      }
+  }
   const auto dwa = rsrc(p.w1a, p.w1a ? (int64_t)A * H : 0);
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -687,11 +713,19 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       const int k = w * 64 + kt * 16 + r;
+#if MOPO_SAC_LDOFF
+      // W1 rows j >= k1 fall past the descriptor's range (k1 H) and read 0; a lane past H reads nothing
+      const int vb = k < H ? (q4 * H + k) * 4 : (1 << 30);
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        wa[kt][s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dw, vb + 16 * s * H, 0, 0));
+#else
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         const int j = 4 * s + q4;
         wa[kt][s] = bload(dw, (j < k1 && k < H) ? j * H + k : -1);
       }
+#endif
       bv[kt] = bload(db, k < H ? k : -1);
     }
   }
@@ -699,6 +733,15 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   {
     const auto dbw = rsrc(p.w2, (int64_t)H * H);
     const bool con = jw + li < H;
+#if MOPO_SAC_LDOFF
+    // plain offsets (one add per load): rows k >= H fall past the range (H H) and read 0
+    const int vb = con ? (64 * lk * H + jw + li) * 4 : (1 << 30);
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        bp[s2][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dbw, vb + (4 * s2 + u) * H * 4, 0, 0));
+#else
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2)
 #pragma unroll
@@ -706,6 +749,7 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
         const int k = 64 * lk + 4 * s2 + u;
         bp[s2][u] = bload(dbw, (con && k < H) ? k * H + jw + li : -1);
       }
+#endif
   }
   float wov[4];
   {
@@ -1037,11 +1081,19 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args a, int x, int y, 
                                                   rsrc(p.w3, H), ((slab && am < H) ? am : -4) * 4, 0, 0));
   const auto dw2 = rsrc(p.w2, (int64_t)H * H);
   f32x4 bp[16];
+  if (MOPO_SAC_LDOFF2 && (H & 63) == 0) {
+    // m < H exactly when 64 lk < H; c >= H: past the range
+    const int vb = (64 * lk < H && jw + li < H) ? ((jw + li) * H + 64 * lk) * 4 : (1 << 30);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int m = 64 * lk + 4 * i, c = jw + li;
-    bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                          dw2, ((m < H && c < H) ? c * H + m : -4) * 4, 0, 0));
+    for (int i = 0; i < 16; ++i)
+      bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dw2, vb + 16 * i, 0, 0));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = 64 * lk + 4 * i, c = jw + li;
+      bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            dw2, ((m < H && c < H) ? c * H + m : -4) * 4, 0, 0));
+    }
   }
   if constexpr (FZ >= 1) {            // the targets' partials and logp(s') come from this launch's F2 blocks
     unsigned* tmo = a.sync + SYNC_N * a.nrb * SYNC_STRIDE;
