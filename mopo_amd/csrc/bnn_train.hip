@@ -1020,7 +1020,8 @@ int build_wlist(Train* h) {
 int train_wg2_nt() {
   static const int v = [] {
     const char* e = std::getenv("MOPO_TRAIN_WG2_NT");
-    return e && std::atoi(e) == 1024 ? 1024 : 512;
+    const int n = e ? std::atoi(e) : 512;
+    return n == 1024 ? 1024 : n == 256 ? 256 : 512;
   }();
   return v;
 }
@@ -1028,7 +1029,7 @@ int train_wg2_nwx() {
   static const int v = [] {
     const char* e = std::getenv("MOPO_TRAIN_WG2_NWX");
     // the resident workgroups: three 512-thread ones per CU (TRAIN_WG2_KC), one 1024-thread one
-    return e ? std::max(1, std::atoi(e)) : (train_wg2_nt() == 1024 ? 32 : 96);
+    return e ? std::max(1, std::atoi(e)) : (train_wg2_nt() == 1024 ? 32 : train_wg2_nt() == 256 ? 192 : 96);
   }();
   return v;
 }
@@ -1142,6 +1143,7 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
       t.E = E; t.nrb = a.nrb; t.D = D; t.lpart = h->lpart; t.mx = L.mx; t.mn = L.mn;
       t.logs = h->logs; t.beta_pow = h->beta_pow; t.bstep_inc = a.bstep_inc; t.lr = h->lr; t.G = h->G; t.ad = ad;
       if (train_wg2_nt() == 1024) hipLaunchKernelGGL(train_wgrad2_kernel<1024>, dim3(8 * g.nwx + 1), dim3(1024), 0, s, g);
+      else if (train_wg2_nt() == 256) hipLaunchKernelGGL(train_wgrad2_kernel<256>, dim3(8 * g.nwx + 1), dim3(256), 0, s, g);
       else hipLaunchKernelGGL(train_wgrad2_kernel<512>, dim3(8 * g.nwx + 1), dim3(512), 0, s, g);
       MOPO_HIP(hipGetLastError());
       return 0;
