@@ -75,7 +75,11 @@ def parse():
     p.add_argument('--sac-steps', type=int, default=1000)
     p.add_argument('--cpu-sac-steps', type=int, default=1000)
     p.add_argument('--no-c3', action='store_true', help='skip the secondary C3 (bf16 walker2d) line')
-    p.add_argument('--train-epochs', type=int, default=2, help='timed BNN.train epochs (0: skip)')
+    p.add_argument('--train-epochs', type=int, default=6,
+                   help='timed BNN.train epochs in one train() call (0: skip); 6 is the fewest a from-scratch MOPO '
+                        'model-training call runs (mopo.py:528 passes max_epochs=None, bnn.py:326 stops only after '
+                        'more than max_epochs_since_update=5 epochs without improvement); the per-call draws, '
+                        'holdout evaluation and repack are inside the timed region')
     p.add_argument('--cpu-train-steps', type=int, default=10)
     p.add_argument('--ensemble-dtype', default=DEFAULT_ENSEMBLE_DTYPE, choices=list(DTYPES),
                    help='headline ensemble-forward arithmetic (mopo_amd.bnn.DTYPES); the default is the one '
