@@ -282,6 +282,15 @@ static int split_parts() {  // MOPO_ROLLOUT_SPLIT=<parts> (0 or 1: one stream); 
   return v;
 }
 
+// MOPO_ROLLOUT_PRIO=1 (A/B): parts 1.. of the split on the greatest-priority stream
+static int split_prio() {
+  static const int v = [] {
+    const char* e = std::getenv("MOPO_ROLLOUT_PRIO");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 // MOPO_ROLLOUT_PART0=<permille> (A/B): part 0's share of the rows in a 2-part split (default 500)
 static int split_part0_permille() {
   static const int v = [] {
@@ -420,7 +429,13 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
   if (split) {
     for (int k = 1; k < nsplit; ++k)
       if (!h->sp[k]) {
-        MOPO_HIP(hipStreamCreateWithFlags(&h->sp[k], hipStreamNonBlocking));
+        if (split_prio()) {   // A/B: the later part's chain on the greatest-priority stream
+          int least = 0, greatest = 0;
+          MOPO_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+          MOPO_HIP(hipStreamCreateWithPriority(&h->sp[k], hipStreamNonBlocking, greatest));
+        } else {
+          MOPO_HIP(hipStreamCreateWithFlags(&h->sp[k], hipStreamNonBlocking));
+        }
         MOPO_HIP(hipEventCreateWithFlags(&h->ev_fork[k], hipEventDisableTiming));
         MOPO_HIP(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
       }
