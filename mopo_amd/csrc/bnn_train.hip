@@ -72,6 +72,7 @@ struct Train {
   float* logs = nullptr;       // [4]: last train loss (data term), ...
   float *mu = nullptr, *sigma = nullptr;
   float *X = nullptr, *T = nullptr, *Z[NHID] = {}, *Hh[NHID] = {}, *OUT = nullptr, *dOUT = nullptr, *dZ[NHID] = {};
+  float *X2 = nullptr, *T2 = nullptr;   // the staged gather's second row buffers (odd steps of a graph)
   std::vector<int> snap;       // members with a snapshot
   int32_t* wlist = nullptr;    // weight-gradient tiles per XCD (train_wgrad2_kernel): [8][wl_per_x], counts [8]
   int32_t* wcnt = nullptr;
@@ -1055,8 +1056,19 @@ int train_step_nwx() {
 #define MOPO_TRAIN_FUSED 1  // forward + backward rows in one launch, the loss tail in the weight-gradient launch
 #endif
 
+// MOPO_TRAIN_STAGE (default 1): graph-captured full minibatches read rows the previous step gathered
+// (train_rows.h TrainRows::staged); needs 16 (IN + D) <= 1024 (two items per row-block thread)
+bool train_stage(const Train* h) {
+  static const int v = [] {
+    const char* e = std::getenv("MOPO_TRAIN_STAGE");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v != 0 && MOPO_TRAIN_FUSED && 16 * (h->L.IN + h->L.D) <= 2 * TR_WAVES * 64;
+}
+
+
 int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t* idx, int64_t stride, bool use_bstep,
-              int batch, int M, hipStream_t s) {
+              int batch, int M, hipStream_t s, bool staged = false) {
   const Layout& L = h->L;
   const int E = L.E, H = L.H, IN = L.IN, D = L.D, D2 = 2 * D;
   const float* P = h->Pb[par];
@@ -1070,6 +1082,11 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
   for (int l = 0; l <= NHID; ++l) { a.W[l] = L.W[l]; a.b[l] = L.b[l]; }
   a.mx = L.mx; a.mn = L.mn;
   a.X = h->X; a.T = h->T; a.OUT = h->OUT; a.dOUT = h->dOUT;
+  if (staged) {   // step parity par reads X / T[par], gathers the next step into the other pair
+    a.staged = 1;
+    a.X = par ? h->X2 : h->X; a.T = par ? h->T2 : h->T;
+    a.Xn = par ? h->X : h->X2; a.Tn = par ? h->T : h->T2;
+  }
   for (int l = 0; l < NHID; ++l) { a.Z[l] = h->Z[l]; a.Hh[l] = h->Hh[l]; a.dZ[l] = h->dZ[l]; }
   a.lpart = h->lpart; a.logs = h->logs; a.beta_pow = h->beta_pow; a.bstep_inc = use_bstep ? h->bstep : nullptr;
   a.lr = h->lr; a.G = h->G; a.ad = ad;
@@ -1089,7 +1106,7 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
     for (int l = 0; l <= NHID; ++l) {
       g.K[l] = l == 0 ? IN : H;
       g.N[l] = l == NHID ? D2 : H;
-      g.A[l] = l == 0 ? h->X : h->Hh[l - 1];
+      g.A[l] = l == 0 ? a.X : h->Hh[l - 1];
       g.B[l] = l == NHID ? h->dOUT : h->dZ[l];
       g.W[l] = L.W[l];
       g.b[l] = L.b[l];
@@ -1132,7 +1149,7 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
       for (int l = 0; l <= NHID; ++l) {
         g.K[l] = l == 0 ? IN : H;
         g.N[l] = l == NHID ? D2 : H;
-        g.A[l] = l == 0 ? h->X : h->Hh[l - 1];
+        g.A[l] = l == 0 ? a.X : h->Hh[l - 1];
         g.B[l] = l == NHID ? h->dOUT : h->dZ[l];
         g.W[l] = L.W[l];
         g.b[l] = L.b[l];
@@ -1155,7 +1172,7 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
     for (int l = NHID, i = 0; l >= 0; --l, ++i) {   // dW_l = X_in^T dY (+ db = colsum dY), decay + Adam; batch = member
       const int K = l == 0 ? IN : H, N = l == NHID ? D2 : H;
       const float* dY = l == NHID ? h->dOUT : h->dZ[l];
-      const float* Xin = l == 0 ? h->X : h->Hh[l - 1];
+      const float* Xin = l == 0 ? a.X : h->Hh[l - 1];   // a.X: the staged pair
       GemmProb w = mk(K, N, M, Xin, K, 1, dY, N, 0, h->G + L.W[l], N);
       w.colsum = h->G + L.b[l];
       w.adam = 1;
@@ -1221,7 +1238,7 @@ int capture(Train* h, int which, const float* in, const float* tg, const int32_t
   int rc = 0;
   for (int i = 0; i < steps && !rc; ++i) {
     if (use_rows(h)) {
-      rc = step_rows(h, i & 1, in, tg, idx, n_idx, true, batch, batch, gs);
+      rc = step_rows(h, i & 1, in, tg, idx, n_idx, true, batch, batch, gs, train_stage(h) && !train_step1());
     } else {
       rc = launch_gather(h, in, tg, idx, n_idx, true, batch, batch, gs);
       if (!rc) rc = step_impl(h, i & 1, batch, true, gs);
@@ -1265,7 +1282,7 @@ extern "C" int mopo_bnn_train_create(mopo_bnn_train_t* out, int E, int obs_dim, 
   reg.push_back({(void**)&h->bstep, 4});
   reg.push_back({(void**)&h->tsync, (size_t)(E * (NHID + 1) + TS_GLOBAL) * TS_STRIDE * 4});   // zeroed below
   reg.push_back({(void**)&h->ticket, 4});
-  f(&h->X, E * mM * L.IN); f(&h->T, E * mM * L.D); f(&h->OUT, E * mM * 2 * L.D); f(&h->dOUT, E * mM * 2 * L.D);
+  f(&h->X, E * mM * L.IN); f(&h->T, E * mM * L.D); f(&h->X2, E * max_batch * L.IN); f(&h->T2, E * max_batch * L.D); f(&h->OUT, E * mM * 2 * L.D); f(&h->dOUT, E * mM * 2 * L.D);
   for (int l = 0; l < NHID; ++l) { f(&h->Z[l], E * mM * L.H); f(&h->Hh[l], E * mM * L.H); f(&h->dZ[l], E * mM * L.H); }
   size_t bytes = 0;
   for (auto& r : reg) bytes += (r.second + 255) & ~(size_t)255;
@@ -1454,6 +1471,9 @@ extern "C" int mopo_bnn_train_epoch(mopo_bnn_train_t hh, const float* d_in, cons
         return -1;
       h->gkey[0] = d_in; h->gkey[1] = d_tg; h->gkey[2] = d_idxs; h->gkey_n = n_idx; h->gkey_b = batch;
     }
+    // staged steps: the epoch's first minibatch is gathered here, every later one by the step before it
+    if (use_rows(h) && train_stage(h) && !train_step1() && launch_gather(h, d_in, d_tg, d_idxs, n_idx, true, batch, batch, gs))
+      return -1;
     int64_t i = 0;
     for (; i + TRAIN_GRAPH_STEPS <= nfull; i += TRAIN_GRAPH_STEPS) MOPO_HIP(hipGraphLaunch(h->gexec[0], gs));
     for (; i + 2 <= nfull; i += 2) MOPO_HIP(hipGraphLaunch(h->gexec[1], gs));

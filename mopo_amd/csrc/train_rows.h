@@ -37,6 +37,10 @@ struct TrainRows {
   const float* P;                    // this step's parameters (training layout, bnn_train.hip)
   int64_t W[TR_NHID + 1], b[TR_NHID + 1], mx, mn;
   float* X; float* T; float* Z[TR_NHID]; float* Hh[TR_NHID]; float* OUT; float* dOUT; float* dZ[TR_NHID];
+  // staged (graph-captured full minibatches): this step's rows are already gathered in X / T (by the
+  // previous step, or the epoch's first gather), and the block gathers the NEXT step's rows into Xn / Tn,
+  // its loads issued at the start and stored at the end (the gather's dependent chain off the step's path)
+  int staged; float* Xn; float* Tn;
   float* lpart;                      // [E][nrb][D][4]: d loss / d maxlv, d loss / d minlv, loss (per row block)
   // the batch-level tail (train_bwd_rows_kernel's block (0, 0))
   float* logs; float* beta_pow; int* bstep_inc; float lr; float* G; AdamCtx ad;
@@ -601,11 +605,45 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
   };
   float pre[TR_PFM][4][TR_TW];
   if (TR_XPF) rows_pre<false, G0, TR_TW>(wfwd(0), c0, lane, pre);   // in flight during the gather
-  {  // gather (train_fwd_rows_kernel)
+  // the next step's rows (staged): two items per thread at most (host: 16 (IN + D) <= 2 TR_WAVES 64)
+  constexpr int NPF = 2;
+  float pf_v[NPF];
+  int pf_src[NPF];
+  bool staged = !SIG && a.staged;
+  if (staged) {   // the indices now; the rows they name after layer 0; the stores at the end
+    const int W = IN + D;
+    const int64_t nb = (int64_t)(*a.bstep + 1) * a.batch;
+    const auto drows = rsrc(reinterpret_cast<const float*>(a.rows), (int64_t)a.E * a.stride);
+#pragma unroll
+    for (int q = 0; q < NPF; ++q) {
+      const int i = tid + q * TR_WAVES * 64, row = i0 + (i / W);
+      // past the index array: row 0 (the last full step prefetches for a minibatch that does not come)
+      pf_src[q] = i < 16 * W ? __builtin_bit_cast(int, __builtin_amdgcn_raw_buffer_load_b32(
+                                   drows, (int)((e * a.stride + nb + row) * 4), 0, 0)) : 0;
+    }
+  }
+  auto prefetch_rows = [&]() {
+    if (!staged) return;
+    const int W = IN + D;
+#pragma unroll
+    for (int q = 0; q < NPF; ++q) {
+      const int i = tid + q * TR_WAVES * 64, c = i % W;
+      const int64_t src = pf_src[q];
+      pf_v[q] = i >= 16 * W ? 0.f : c < IN ? (a.inputs[src * IN + c] - a.mu[c]) / a.sigma[c]   // utils.py:96
+                                           : a.targets[src * D + (c - IN)];
+    }
+  };
+  {  // gather (train_fwd_rows_kernel); staged: this step's rows from X
     const int W = IN + D, KP = ((IN + 15) >> 4) << 4;
     const int64_t base = a.bstep ? (int64_t)(*a.bstep) * a.batch : 0;
     for (int i = tid; i < 16 * KP; i += TR_WAVES * 64) buf[0][(i / KP) * TR_LD + i % KP] = 0.f;
     lds_barrier();
+    if (staged) {
+      for (int i = tid; i < 16 * IN; i += TR_WAVES * 64) {
+        const int r = i / IN, c = i % IN;
+        buf[0][r * TR_LD + c] = a.X[((int64_t)e * M + i0 + r) * IN + c];
+      }
+    } else
     for (int i = tid; i < 16 * W; i += TR_WAVES * 64) {
       const int r = i / W, c = i % W, row = i0 + r;
       if (row >= M) continue;
@@ -663,6 +701,7 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
   };
   if constexpr (!SIG) tstamp(1);
   fwd(std::integral_constant<int, G0>{}, 0);
+  prefetch_rows();
   if constexpr (!SIG) tstamp(2);
   for (int l = 1; l <= TR_NHID; ++l) fwd(std::integral_constant<int, GH>{}, l);
   if constexpr (!SIG) tstamp(3);
@@ -762,6 +801,18 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
   }
   if constexpr (!SIG) tstamp(7);
   if constexpr (SIG) signal(pending);
+  if (staged) {   // the next step's rows, loaded at the start
+    const int W = IN + D;
+#pragma unroll
+    for (int q = 0; q < NPF; ++q) {
+      const int i = tid + q * TR_WAVES * 64, r = i / W, c = i % W;
+      const int64_t er = (int64_t)e * M + i0 + r;
+      if (i < 16 * W) {
+        if (c < IN) a.Xn[er * IN + c] = pf_v[q];
+        else a.Tn[er * D + (c - IN)] = pf_v[q];
+      }
+    }
+  }
   (void)pending;
 }
 

@@ -226,12 +226,13 @@ def test_train_loop_joint_head_matches_oracle():
 
 
 @pytest.mark.parametrize('knobs', ['MOPO_TRAIN_WG2=1,MOPO_TRAIN_WG2_NT=512', 'MOPO_TRAIN_WG2=1,MOPO_TRAIN_WG2_NT=1024',
-                                   'MOPO_TRAIN_WG2=1,MOPO_TRAIN_WG2_NT=256',
+                                   'MOPO_TRAIN_WG2=1,MOPO_TRAIN_WG2_NT=256', 'MOPO_TRAIN_STAGE=0',
                                    'MOPO_TRAIN_WG2=0', 'MOPO_TRAIN_STEP1=1', 'MOPO_TRAIN_STEP1=1,MOPO_TRAIN_STEP_NWX=3'])
 def test_wgrad_launch_variants_match_oracle(knobs):
     """The weight-gradient launch knobs (MOPO_TRAIN_WG2: the persistent XCD-local tile launch or the
     grouped-GEMM launch; MOPO_TRAIN_WG2_NT: 256-, 512- or 1024-thread tile workgroups; MOPO_TRAIN_STEP1: the
-    whole step as one launch with in-launch hand-offs, MOPO_TRAIN_STEP_NWX its tile workgroups per XCD)
+    whole step as one launch with in-launch hand-offs, MOPO_TRAIN_STEP_NWX its tile workgroups per XCD;
+    MOPO_TRAIN_STAGE=0: every row block gathers its own minibatch rows)
     are read once per process, so each setting runs the epoch and train-loop parity tests above in a
     fresh process."""
     import os
