@@ -186,6 +186,10 @@ int mopo_bnn_train_eval_mse(mopo_bnn_train_t h, const float* d_inputs, const flo
 /* shuffle_rows (bnn.py:385-387): d_idxs[e] <- d_idxs[e][argsort(d_keys[e])], keys f64 [E, n]
  * (the np.random.uniform draws). */
 int mopo_bnn_train_shuffle(mopo_bnn_train_t h, int32_t* d_idxs, const double* d_keys, int64_t n, void* stream);
+/* The same shuffle with the order (the key sort) computed on order_stream, which may run beside the
+ * epoch's steps; only the apply to d_idxs is queued on stream, behind the order. */
+int mopo_bnn_train_shuffle_async(mopo_bnn_train_t h, int32_t* d_idxs, const double* d_keys, int64_t n,
+                                 void* order_stream, void* stream);
 /* _save_state(member) / _set_state (bnn.py:264-285). */
 int mopo_bnn_train_snapshot(mopo_bnn_train_t h, int member, void* stream);
 int mopo_bnn_train_restore(mopo_bnn_train_t h, void* stream);
@@ -316,6 +320,8 @@ int mopo_mt_get_state(mopo_mt_t h, uint32_t* key624, int* pos, int* has_gauss, d
 int mopo_mt_normal(mopo_mt_t h, double* h_out, int64_t n);                  /* legacy_gauss */
 int mopo_mt_randint(mopo_mt_t h, int64_t* h_out, int64_t n, int64_t low, int64_t high); /* randint(low, high, n) */
 int mopo_mt_random_sample(mopo_mt_t h, double* h_out, int64_t n);
+/* randint(low, high, n) written as int32 (BNN.train's bootstrap indices, bnn.py:402) */
+int mopo_mt_randint_i32(mopo_mt_t h, int32_t* h_out, int64_t n, int64_t low, int64_t high);
 
 #ifdef __cplusplus
 }

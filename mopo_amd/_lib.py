@@ -75,6 +75,7 @@ SIGNATURES = {
     'mopo_bnn_train_epoch': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p]),
     'mopo_bnn_train_eval_mse': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     'mopo_bnn_train_shuffle': (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
+    'mopo_bnn_train_shuffle_async': (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_void_p, c_void_p]),
     'mopo_bnn_train_snapshot': (c_int, [c_void_p, c_int, c_void_p]),
     'mopo_bnn_train_restore': (c_int, [c_void_p, c_void_p]),
     'mopo_bnn_train_logs': (c_int, [c_void_p, c_void_p, c_int]),
@@ -107,6 +108,7 @@ SIGNATURES = {
     'mopo_mt_normal': (c_int, [c_void_p, c_void_p, c_i64]),
     'mopo_mt_randint': (c_int, [c_void_p, c_void_p, c_i64, c_i64, c_i64]),
     'mopo_mt_random_sample': (c_int, [c_void_p, c_void_p, c_i64]),
+    'mopo_mt_randint_i32': (c_int, [c_void_p, c_void_p, c_i64, c_i64, c_i64]),
 }
 
 _lib = None

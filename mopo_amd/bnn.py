@@ -379,7 +379,22 @@ class BNN:
         t = self._trainer(batch_size, max(max_logging, 1))
         self._train_params(t, self._mats)
         L.check(L.lib().mopo_bnn_train_fit_scaler(t, L.ptr(x), n, None))          # bnn.py:399-400
-        idxs = torch.from_numpy(np.random.randint(n, size=[E, n]).astype(np.int32)).to(dev)  # :402
+        # np.random's draws come from the native MT19937 replica (the global stream is moved in and out,
+        # so it advances exactly as the reference's), written straight into pinned buffers kept across
+        # calls: numpy's randint + a pageable copy held the first epoch's launch back ~8 ms per call
+        mt = self._host_rng()
+        if getattr(self, '_pinned_free', None) is not None:
+            self._pinned_free.synchronize()              # the previous call's copies out of the buffers
+        idxs_h = self._pinned('idxs', E * n, torch.int32)
+        numpy_draws = os.environ.get('MOPO_TRAIN_NUMPY_DRAWS') == '1'               # A/B knob
+        if numpy_draws:
+            idxs_h.numpy()[:] = np.random.randint(n, size=E * n)
+        else:
+            mt.sync_from_numpy()
+            mt.randint(0, n, [E, n], out=idxs_h.numpy())                            # bnn.py:402
+            mt.sync_to_numpy()
+        idxs = torch.empty(E * n, dtype=torch.int32, device=dev)
+        idxs.copy_(idxs_h, non_blocking=True)
         self._start_train()
         losses_d = torch.empty(E, dtype=torch.float32, device=dev)
         break_train, grad_updates, epoch = False, 0, 0
@@ -387,22 +402,38 @@ class BNN:
         # the shuffle uniforms are drawn on the host while the epoch's steps run and reach the device by one
         # DMA from a pinned buffer queued behind them (a pageable copy was staged in chunks by the host and
         # left the GPU idle ~5 ms per epoch); the event keeps the next draw from overwriting a pending copy
-        keys_h = torch.empty(E * n, dtype=torch.float64, pin_memory=True)
-        keys_hn = keys_h.numpy().reshape(E, n)
+        keys_h = self._pinned('keys', E * n, torch.float64)
+        keys_hn = keys_h.numpy()
         keys = torch.empty(E * n, dtype=torch.float64, device=dev)
-        copied = None
+        copied = torch.cuda.Event()
+        copied.record()
+        # the keys' copy and sort run on a side stream beside the epoch's steps (which leave CUs idle);
+        # only the apply to idxs waits for the epoch (mopo_bnn_train_shuffle_async)
+        side = None if os.environ.get('MOPO_TRAIN_SHUFFLE_SIDE') == '0' else self._side_stream()
+        if side is not None:
+            keys.record_stream(side)
         t0 = time.time()
         for epoch in (range(max_epochs) if max_epochs is not None else itertools.count()):
             L.check(L.lib().mopo_bnn_train_epoch(t, L.ptr(x), L.ptr(y), L.ptr(idxs), n, int(batch_size), None))
             grad_updates += int(np.ceil(n / batch_size))
-            u = np.random.uniform(size=[E, n])                                      # shuffle_rows :385-387
-            if copied is not None:
-                copied.synchronize()
-            keys_hn[...] = u
-            keys.copy_(keys_h, non_blocking=True)
+            copied.synchronize()
+            if numpy_draws:
+                keys_hn[:] = np.random.uniform(size=E * n)
+            else:
+                mt.sync_from_numpy()
+                mt.random_sample([E, n], out=keys_hn)                               # shuffle_rows :385-387
+                mt.sync_to_numpy()
             copied = torch.cuda.Event()
-            copied.record()
-            L.check(L.lib().mopo_bnn_train_shuffle(t, L.ptr(idxs), L.ptr(keys), n, None))
+            if side is None:
+                keys.copy_(keys_h, non_blocking=True)
+                copied.record()
+                L.check(L.lib().mopo_bnn_train_shuffle(t, L.ptr(idxs), L.ptr(keys), n, None))
+            else:
+                with torch.cuda.stream(side):
+                    keys.copy_(keys_h, non_blocking=True)
+                    copied.record(side)
+                L.check(L.lib().mopo_bnn_train_shuffle_async(t, L.ptr(idxs), L.ptr(keys), n,
+                                                             L.stream_ptr(side), None))
             if not hide_progress and holdout_ratio >= 1e-12 and num_holdout > 0:
                 L.check(L.lib().mopo_bnn_train_eval_mse(t, L.ptr(hold_x), L.ptr(hold_y), None, num_holdout,
                                                         L.ptr(losses_d), None))
@@ -412,6 +443,7 @@ class BNN:
                 break
             if max_t and time.time() - t0 > max_t:
                 break
+        self._pinned_free = copied
         L.check(L.lib().mopo_bnn_train_restore(t, None))                           # _set_state :491
         if num_holdout > 0:
             L.check(L.lib().mopo_bnn_train_eval_mse(t, L.ptr(hold_x), L.ptr(hold_y), None, num_holdout,
@@ -424,6 +456,29 @@ class BNN:
         self._train_epochs, self._train_grad_updates = epoch + 1, grad_updates
         val_loss = np.sort(holdout_losses)[:self.num_elites].mean()
         return OrderedDict({'val_loss': val_loss})
+
+    def _host_rng(self):
+        mt = getattr(self, '_mt', None)
+        if mt is None:
+            from .rng import LegacyRandomState
+            mt = self._mt = LegacyRandomState(0)
+        return mt
+
+    def _side_stream(self):
+        import torch
+        st = getattr(self, '_side', None)
+        if st is None:
+            st = self._side = torch.cuda.Stream()
+        return st
+
+    def _pinned(self, name, n, dtype):
+        """A pinned host buffer of n elements kept across train() calls (pinning costs ~ms per MB)."""
+        import torch
+        bufs = self.__dict__.setdefault('_pinned_bufs', {})
+        b = bufs.get(name)
+        if b is None or b.numel() < n or b.dtype != dtype:
+            b = bufs[name] = torch.empty(n, dtype=dtype, pin_memory=True)
+        return b[:n]
 
     def _start_train(self):                                                         # bnn.py:324-327
         self._snapshots = {i: (None, 1e10) for i in range(self.num_nets)}

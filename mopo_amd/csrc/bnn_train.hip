@@ -84,6 +84,7 @@ struct Train {
   // graphs (full-batch steps), keyed by the epoch's data pointers
   hipStream_t gs = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  hipEvent_t ev_order = nullptr, ev_applied = nullptr;   // shuffle: order ready / order consumed
   hipGraphExec_t gexec[3] = {nullptr, nullptr, nullptr};
   hipGraph_t graph[3] = {nullptr, nullptr, nullptr};
   const void* gkey[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -1344,6 +1345,8 @@ extern "C" int mopo_bnn_train_destroy(mopo_bnn_train_t hh) {
   drop_graphs(h);
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   if (h->ev_out) (void)hipEventDestroy(h->ev_out);
+  if (h->ev_order) (void)hipEventDestroy(h->ev_order);
+  if (h->ev_applied) (void)hipEventDestroy(h->ev_applied);
   if (h->gs) (void)hipStreamDestroy(h->gs);
   if (h->sort_keys) (void)hipFree(h->sort_keys);  // one allocation (keys | values | offsets | temp)
   if (h->wlist) (void)hipFree(h->wlist);
@@ -1506,21 +1509,31 @@ extern "C" int mopo_bnn_train_eval_mse(mopo_bnn_train_t hh, const float* d_in, c
 
 extern "C" int mopo_bnn_train_shuffle(mopo_bnn_train_t hh, int32_t* d_idxs, const double* d_keys, int64_t n,
                                       void* stream) {
+  return mopo_bnn_train_shuffle_async(hh, d_idxs, d_keys, n, stream, stream);
+}
+
+extern "C" int mopo_bnn_train_shuffle_async(mopo_bnn_train_t hh, int32_t* d_idxs, const double* d_keys, int64_t n,
+                                            void* order_stream, void* stream) {
   Train* h = reinterpret_cast<Train*>(hh);
   MOPO_REQUIRE(h && d_idxs && d_keys && n >= 1, "mopo_bnn_train_shuffle: bad argument");
   MOPO_REQUIRE(n * h->L.E < (1ll << 31), "mopo_bnn_train_shuffle: index set too large");
-  hipStream_t s = (hipStream_t)stream;
+  hipStream_t s = (hipStream_t)stream, os = (hipStream_t)order_stream;
   const int E = h->L.E;
   const int64_t tot = n * E;
   int seg_bits = 0;
   while ((1 << seg_bits) < E) ++seg_bits;
   const int end_bit = 53 + seg_bits;
+  if (!h->ev_order) {
+    MOPO_HIP(hipEventCreateWithFlags(&h->ev_order, hipEventDisableTiming));
+    MOPO_HIP(hipEventCreateWithFlags(&h->ev_applied, hipEventDisableTiming));
+  }
   if (h->sort_cap < tot) {
+    MOPO_HIP(hipStreamSynchronize(s));           // the buffers below may still be read by an earlier apply
     if (h->sort_keys) (void)hipFree(h->sort_keys);
     h->sort_tmp = nullptr; h->sort_keys = nullptr;
     size_t tb = 0;
     MOPO_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                                (const int32_t*)nullptr, (int32_t*)nullptr, (int)tot, 0, end_bit, s));
+                                                (const int32_t*)nullptr, (int32_t*)nullptr, (int)tot, 0, end_bit, os));
     // one allocation: keys in | keys out | values in | values out | temp storage
     const size_t kb = (size_t)tot * 8, vb = (size_t)tot * 4;
     char* m = nullptr;
@@ -1531,21 +1544,30 @@ extern "C" int mopo_bnn_train_shuffle(mopo_bnn_train_t hh, int32_t* d_idxs, cons
     h->sort_tmp = (void*)(((uintptr_t)(m + 2 * kb + 2 * vb) + 255) & ~(uintptr_t)255);
     h->sort_tmp_bytes = tb;
     h->sort_cap = tot;
+  } else if (os != s) {
+    // the order is computed on the caller's order stream, which can run beside the epoch's steps; it
+    // must not overwrite the order buffers before the previous shuffle's apply has read them
+    MOPO_HIP(hipStreamWaitEvent(os, h->ev_applied, 0));
   }
   uint64_t* kin = reinterpret_cast<uint64_t*>(h->sort_keys);
   uint64_t* kout = kin + h->sort_cap;
-  hipLaunchKernelGGL(sort_keys_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, d_keys, n, E, kin,
+  hipLaunchKernelGGL(sort_keys_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, os, d_keys, n, E, kin,
                      h->sort_vals_in);
   MOPO_HIP(hipGetLastError());
   size_t tb = h->sort_tmp_bytes;
   // one radix sort of (member, 53-bit integer of the uniform) == np.argsort within each member row
   MOPO_HIP(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp, tb, kin, kout, h->sort_vals_in, h->sort_vals, (int)tot, 0,
-                                              end_bit, s));
+                                              end_bit, os));
+  if (os != s) {
+    MOPO_HIP(hipEventRecord(h->ev_order, os));
+    MOPO_HIP(hipStreamWaitEvent(s, h->ev_order, 0));
+  }
   int32_t* tmp_idx = h->sort_vals_in;  // reuse: copy of the current indices
   MOPO_HIP(hipMemcpyAsync(tmp_idx, d_idxs, tot * 4, hipMemcpyDeviceToDevice, s));
   hipLaunchKernelGGL(apply_order_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, h->sort_vals, tmp_idx,
                      n, E, d_idxs);
   MOPO_HIP(hipGetLastError());
+  MOPO_HIP(hipEventRecord(h->ev_applied, s));
   return 0;
 }
 

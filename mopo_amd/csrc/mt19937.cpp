@@ -8,6 +8,7 @@
 // doubles from two 32-bit draws, polar gauss, masked bounded ints) is reproduced here and
 // checked against numpy itself in tests/test_rng.py.  State can be exchanged with
 // np.random.get_state()/set_state() so the device rollout can consume the caller's stream.
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -53,14 +54,65 @@ struct MT {
     key[N - 1] = key[M - 1] ^ (y >> 1) ^ (-(y & 1u) & MATRIX_A);
     pos = 0;
   }
-  uint32_t next32() {
-    if (pos == N) reload();
-    uint32_t y = key[pos++];
+  static uint32_t temper(uint32_t y) {
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
     y ^= (y >> 18);
     return y;
+  }
+  uint32_t next32() {
+    if (pos == N) reload();
+    return temper(key[pos++]);
+  }
+  // The rest of the current block tempered into t (reloading first when it is used up); returns its
+  // length.  The caller advances pos by what it consumes, so the stream position stays exact.
+  int block(uint32_t* t) {
+    if (pos == N) reload();
+    const int cnt = N - pos;
+    for (int j = 0; j < cnt; ++j) t[j] = temper(key[pos + j]);
+    return cnt;
+  }
+  // n values of randint(low, low + rng + 1): the same masked rejection as bounded(), a block of tempered
+  // draws at a time with a branch-free accept (a rejected value is overwritten by the next draw)
+  template <typename T>
+  void bounded_fill(T* out, int64_t n, int64_t low, uint32_t rng) {
+    if (rng == 0 || rng == 0xffffffffu) {
+      for (int64_t i = 0; i < n; ++i) out[i] = (T)(low + (int64_t)bounded(rng));
+      return;
+    }
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t t[N];
+    int64_t k = 0;
+    while (k < n) {
+      const int cnt = block(t);
+      int j = 0;
+      for (; j < cnt && k < n; ++j) {
+        const uint32_t v = t[j] & mask;
+        out[k] = (T)(low + (int64_t)v);
+        k += (v <= rng);
+      }
+      pos += j;
+    }
+  }
+  // n doubles of random_sample: two tempered draws each (a pair may straddle a reload)
+  void random_fill(double* out, int64_t n) {
+    uint32_t t[N];
+    int64_t i = 0;
+    while (i < n) {
+      if ((N - pos) < 2 || pos == N) {
+        out[i++] = next_double();
+        continue;
+      }
+      const int cnt = block(t) & ~1;
+      int j = 0;
+      for (; j < cnt && i < n; j += 2, ++i) {
+        const int32_t a = (int32_t)(t[j] >> 5), b = (int32_t)(t[j + 1] >> 6);
+        out[i] = (a * 67108864.0 + b) / 9007199254740992.0;
+      }
+      pos += j;
+    }
   }
   double next_double() {
     int32_t a = (int32_t)(next32() >> 5), b = (int32_t)(next32() >> 6);
@@ -147,8 +199,7 @@ extern "C" int mopo_mt_normal(mopo_mt_t h, double* out, int64_t n) {
 
 extern "C" int mopo_mt_random_sample(mopo_mt_t h, double* out, int64_t n) {
   if (!h || (!out && n)) return mopo::fail("mopo_mt_random_sample: NULL argument");
-  MT* m = reinterpret_cast<MT*>(h);
-  for (int64_t i = 0; i < n; ++i) out[i] = m->next_double();
+  reinterpret_cast<MT*>(h)->random_fill(out, n);
   return 0;
 }
 
@@ -157,7 +208,14 @@ extern "C" int mopo_mt_randint(mopo_mt_t h, int64_t* out, int64_t n, int64_t low
   if (high <= low) return mopo::fail("mopo_mt_randint: low >= high");
   const uint64_t rng = (uint64_t)(high - 1 - low);
   if (rng > 0xffffffffull) return mopo::fail("mopo_mt_randint: range >= 2^32 not supported");
-  MT* m = reinterpret_cast<MT*>(h);
-  for (int64_t i = 0; i < n; ++i) out[i] = low + (int64_t)m->bounded((uint32_t)rng);
+  reinterpret_cast<MT*>(h)->bounded_fill(out, n, low, (uint32_t)rng);
+  return 0;
+}
+
+extern "C" int mopo_mt_randint_i32(mopo_mt_t h, int32_t* out, int64_t n, int64_t low, int64_t high) {
+  if (!h || (!out && n)) return mopo::fail("mopo_mt_randint_i32: NULL argument");
+  if (high <= low) return mopo::fail("mopo_mt_randint_i32: low >= high");
+  if (low < INT32_MIN || high - 1 > INT32_MAX) return mopo::fail("mopo_mt_randint_i32: values outside int32");
+  reinterpret_cast<MT*>(h)->bounded_fill(out, n, low, (uint32_t)(high - 1 - low));
   return 0;
 }

@@ -33,15 +33,22 @@ class LegacyRandomState:
         L.check(L.lib().mopo_mt_normal(self._h, out.ctypes.data, n))
         return out.reshape(size)
 
-    def random_sample(self, size):
+    def random_sample(self, size, out=None):
+        """``out``: an optional C-contiguous float64 array (e.g. a pinned host tensor's numpy view) the
+        draws are written into."""
         n = int(np.prod(size))
-        out = np.empty(n, np.float64)
+        out = np.empty(n, np.float64) if out is None else _check_out(out, n, np.float64)
         L.check(L.lib().mopo_mt_random_sample(self._h, out.ctypes.data, n))
         return out.reshape(size)
 
-    def randint(self, low, high, size):
+    def randint(self, low, high, size, out=None):
+        """np.random.randint(low, high, size); ``out`` may be int64 or int32 (the same draws)."""
         n = int(np.prod(size))
-        out = np.empty(n, np.int64)
+        if out is not None and out.dtype == np.int32:
+            out = _check_out(out, n, np.int32)
+            L.check(L.lib().mopo_mt_randint_i32(self._h, out.ctypes.data, n, int(low), int(high)))
+            return out.reshape(size)
+        out = np.empty(n, np.int64) if out is None else _check_out(out, n, np.int64)
         L.check(L.lib().mopo_mt_randint(self._h, out.ctypes.data, n, int(low), int(high)))
         return out.reshape(size)
 
@@ -64,3 +71,9 @@ class LegacyRandomState:
 
     def sync_to_numpy(self):
         np.random.set_state(self.get_state())
+
+
+def _check_out(out, n, dtype):
+    if out.dtype != dtype or out.size != n or not out.flags['C_CONTIGUOUS'] or not out.flags['WRITEABLE']:
+        raise ValueError('out must be a writeable C-contiguous %s array of %d elements' % (np.dtype(dtype).name, n))
+    return out

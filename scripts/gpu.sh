@@ -57,7 +57,7 @@ for step in "$@"; do
         for i in 1 2; do
           for v in ${VARS:-"MOPO_TRAIN_WG2=1 MOPO_TRAIN_WG2=0"}; do
             env ${v//,/ } timeout -k 10 200 python bench.py --no-cpu-baseline --no-c3 --no-alt-dtypes --sac-steps 16 --steps 3 \
-              --warmup 1 --train-epochs 3 > gpurun_out/abt_cur.json 2> gpurun_out/abt_cur.err || { rc=1; tail -5 gpurun_out/abt_cur.err; break 2; }
+              --warmup 1 --train-epochs ${TRAIN_EPOCHS:-3} > gpurun_out/abt_cur.json 2> gpurun_out/abt_cur.err || { rc=1; tail -5 gpurun_out/abt_cur.err; break 2; }
             python -c "import json; d=json.load(open('gpurun_out/abt_cur.json')); t=d['model_train']; print('$v', round(t['value']), 'steps/s', round(t['ms_per_epoch'], 2), 'ms/epoch')" >> gpurun_out/ab_train.txt
           done
         done

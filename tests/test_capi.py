@@ -54,6 +54,33 @@ def test_mt19937_randint_choice_bit_exact(high):
     np.testing.assert_array_equal(r.random_sample(99), np.random.random_sample(99))
 
 
+@pytest.mark.parametrize('skip', [0, 1, 623])
+def test_mt19937_block_draws_bit_exact_and_leave_numpy_state(skip):
+    """The block-wise randint / random_sample (BNN.train's bootstrap indices and shuffle keys,
+    bnn.py:385-387, 402) at that call's size, starting at any stream position (a random_sample pair
+    straddling a reload included): same values and the same generator state afterwards as numpy."""
+    from mopo_amd.rng import LegacyRandomState
+    r = LegacyRandomState(0)
+    n = 5003
+    for draw in ('randint32', 'randint64', 'uniform'):
+        np.random.seed(7)
+        np.random.randint(0, 2 ** 32 - 1, size=skip, dtype=np.uint64)  # one 32-bit draw each
+        r.sync_from_numpy()
+        if draw == 'uniform':
+            exp = np.random.uniform(size=[7, n])
+            got = r.random_sample([7, n], out=np.empty(7 * n))
+        else:
+            exp = np.random.randint(n, size=[7, n])
+            dt = np.int32 if draw == 'randint32' else np.int64
+            got = r.randint(0, n, [7, n], out=np.empty(7 * n, dt))
+        np.testing.assert_array_equal(got, exp)
+        st_np, st_r = np.random.get_state(), r.get_state()
+        np.testing.assert_array_equal(st_np[1], st_r[1])
+        assert st_np[2:] == st_r[2:]
+    with pytest.raises(ValueError):
+        r.randint(0, 5, [4], out=np.empty(3, np.int32))
+
+
 def test_mt19937_state_exchange_with_numpy():
     from mopo_amd.rng import LegacyRandomState
     np.random.seed(5)

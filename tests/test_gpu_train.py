@@ -126,7 +126,10 @@ def test_eval_mse_matches_oracle():
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5)
 
 
-def test_shuffle_rows_is_numpy_argsort_order():
+@pytest.mark.parametrize('side', [False, True])
+def test_shuffle_rows_is_numpy_argsort_order(side):
+    """side: the order computed on a second stream (mopo_bnn_train_shuffle_async), three shuffles in a
+    row so each order waits for the previous apply."""
     import torch
     from mopo_amd import _lib as L
     m = model()
@@ -134,10 +137,18 @@ def test_shuffle_rows_is_numpy_argsort_order():
     rs = np.random.RandomState(5)
     n = 1000
     idxs = rs.randint(n, size=[E, n]).astype(np.int32)
-    keys = rs.uniform(size=[E, n])
     d_idx = torch.from_numpy(idxs.copy()).cuda()
-    L.check(L.lib().mopo_bnn_train_shuffle(t, L.ptr(d_idx), L.ptr(torch.from_numpy(keys).cuda()), n, None))
-    ref = idxs[np.arange(E)[:, None], np.argsort(keys, axis=-1)]                  # bnn.py:385-387
+    ref = idxs
+    st = torch.cuda.Stream()
+    for _ in range(3 if side else 1):
+        keys = rs.uniform(size=[E, n])
+        d_keys = torch.from_numpy(keys).cuda()
+        torch.cuda.synchronize()
+        if side:
+            L.check(L.lib().mopo_bnn_train_shuffle_async(t, L.ptr(d_idx), L.ptr(d_keys), n, L.stream_ptr(st), None))
+        else:
+            L.check(L.lib().mopo_bnn_train_shuffle(t, L.ptr(d_idx), L.ptr(d_keys), n, None))
+        ref = ref[np.arange(E)[:, None], np.argsort(keys, axis=-1)]               # bnn.py:385-387
     np.testing.assert_array_equal(d_idx.cpu().numpy(), ref)
 
 
@@ -227,7 +238,8 @@ def test_train_loop_joint_head_matches_oracle():
 
 @pytest.mark.parametrize('knobs', ['MOPO_TRAIN_WG2=1,MOPO_TRAIN_WG2_NT=512', 'MOPO_TRAIN_WG2=1,MOPO_TRAIN_WG2_NT=1024',
                                    'MOPO_TRAIN_WG2=1,MOPO_TRAIN_WG2_NT=256', 'MOPO_TRAIN_STAGE=0',
-                                   'MOPO_TRAIN_WG2=0', 'MOPO_TRAIN_STEP1=1', 'MOPO_TRAIN_STEP1=1,MOPO_TRAIN_STEP_NWX=3'])
+                                   'MOPO_TRAIN_WG2=0', 'MOPO_TRAIN_STEP1=1', 'MOPO_TRAIN_STEP1=1,MOPO_TRAIN_STEP_NWX=3',
+                                   'MOPO_TRAIN_SHUFFLE_SIDE=0,MOPO_TRAIN_NUMPY_DRAWS=1'])
 def test_wgrad_launch_variants_match_oracle(knobs):
     """The weight-gradient launch knobs (MOPO_TRAIN_WG2: the persistent XCD-local tile launch or the
     grouped-GEMM launch; MOPO_TRAIN_WG2_NT: 256-, 512- or 1024-thread tile workgroups; MOPO_TRAIN_STEP1: the
