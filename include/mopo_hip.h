@@ -192,6 +192,8 @@ int mopo_bnn_train_shuffle_async(mopo_bnn_train_t h, int32_t* d_idxs, const doub
                                  void* order_stream, void* stream);
 /* _save_state(member) / _set_state (bnn.py:264-285). */
 int mopo_bnn_train_snapshot(mopo_bnn_train_t h, int member, void* stream);
+/* _save_state for several members in one launch (the members whose holdout loss improved this epoch). */
+int mopo_bnn_train_snapshot_members(mopo_bnn_train_t h, const int* h_members, int n, void* stream);
 int mopo_bnn_train_restore(mopo_bnn_train_t h, void* stream);
 /* h_logs[0] = data term of the last minibatch's training loss. */
 int mopo_bnn_train_logs(mopo_bnn_train_t h, float* h_logs, int n);

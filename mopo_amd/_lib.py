@@ -77,6 +77,7 @@ SIGNATURES = {
     'mopo_bnn_train_shuffle': (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
     'mopo_bnn_train_shuffle_async': (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_void_p, c_void_p]),
     'mopo_bnn_train_snapshot': (c_int, [c_void_p, c_int, c_void_p]),
+    'mopo_bnn_train_snapshot_members': (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     'mopo_bnn_train_restore': (c_int, [c_void_p, c_void_p]),
     'mopo_bnn_train_logs': (c_int, [c_void_p, c_void_p, c_int]),
     'mopo_bnn_train_tile_lists': (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_i64]),

@@ -485,14 +485,16 @@ class BNN:
         self._epochs_since_update = 0
 
     def _save_best(self, t, epoch, holdout_losses):                                  # bnn.py:301-322
-        updated = False
+        updated = []
         for i in range(len(holdout_losses)):
             current = holdout_losses[i]
             _, best = self._snapshots[i]
             if (best - current) / best > 0.01:
                 self._snapshots[i] = (epoch, current)
-                L.check(L.lib().mopo_bnn_train_snapshot(t, i, None))
-                updated = True
+                updated.append(i)
+        if updated:                                                                 # one launch
+            arr = (C.c_int * len(updated))(*updated)
+            L.check(L.lib().mopo_bnn_train_snapshot_members(t, arr, len(updated), None))
         self._epochs_since_update = 0 if updated else self._epochs_since_update + 1
         return self._epochs_since_update > self._max_epochs_since_update
 

@@ -220,9 +220,10 @@ __global__ __launch_bounds__(LOSS_TPB) void train_loss_kernel(const LossArgs a) 
 }
 
 // ---- mse loss per member (inc_var_loss=False): mean over rows and dims of (mean - y)^2 --------
-__global__ __launch_bounds__(256) void train_mse_kernel(const float* __restrict__ OUT, const float* __restrict__ T,
-                                                        int M, int D, float* __restrict__ losses) {
-  __shared__ float sh[4];
+constexpr int MSE_TPB = 1024;
+__global__ __launch_bounds__(MSE_TPB) void train_mse_kernel(const float* __restrict__ OUT, const float* __restrict__ T,
+                                                            int M, int D, float* __restrict__ losses) {
+  __shared__ float sh[MSE_TPB / 64];
   const int e = blockIdx.x;
   float acc = 0.f;
   for (int i = threadIdx.x; i < M * D; i += blockDim.x) {
@@ -234,7 +235,11 @@ __global__ __launch_bounds__(256) void train_mse_kernel(const float* __restrict_
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) losses[e] = (sh[0] + sh[1] + sh[2] + sh[3]) / ((float)M * (float)D);
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < MSE_TPB / 64; ++w) t += sh[w];
+    losses[e] = t / ((float)M * (float)D);
+  }
 }
 
 // ---- scaler fit (utils.py:69-86): mean / std over rows, f64 accumulation, std < 1e-12 -> 1 ----
@@ -282,11 +287,25 @@ __global__ void format_kernel(const mopo_pool_desc p, int O, int A, const int64_
 }
 
 // ---- per-member variable copy (snapshots): dir 0: P -> S, 1: S -> P for member e ------------
+constexpr int MAX_MEMBERS_SET = 64;
 struct MemberSpan { int64_t off[2 * (NHID + 1)]; int64_t len[2 * (NHID + 1)]; };
 
 __global__ void member_copy_kernel(float* __restrict__ P, float* __restrict__ S, const MemberSpan sp, int e,
                                    int dir) {
   const int k = blockIdx.y;
+  const int64_t len = sp.len[k], off = sp.off[k] + (int64_t)e * len;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x) {
+    if (dir == 0) S[off + i] = P[off + i];
+    else P[off + i] = S[off + i];
+  }
+}
+
+// the same copy for a set of members in one launch (blockIdx.z = position in the set)
+struct MemberSet { int n; int e[MAX_MEMBERS_SET]; };
+
+__global__ void members_copy_kernel(float* __restrict__ P, float* __restrict__ S, const MemberSpan sp,
+                                    const MemberSet ms, int dir) {
+  const int k = blockIdx.y, e = ms.e[blockIdx.z];
   const int64_t len = sp.len[k], off = sp.off[k] + (int64_t)e * len;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x) {
     if (dir == 0) S[off + i] = P[off + i];
@@ -337,7 +356,7 @@ int launch_gather(Train* h, const float* in, const float* tg, const int32_t* row
 }
 
 // forward of the 4 swish layers + heads on X (M rows per member) with parameters P
-int forward(Train* h, const float* P, int M, hipStream_t s) {
+int forward(Train* h, const float* P, int M, hipStream_t s, int tile = 0) {
   const Layout& L = h->L;
   const int E = L.E, H = L.H, IN = L.IN, D2 = 2 * L.D;
   for (int l = 0; l <= NHID; ++l) {
@@ -351,9 +370,18 @@ int forward(Train* h, const float* P, int M, hipStream_t s) {
       if (l < NHID) { p.act = ACT_SWISH; p.Z = h->Z[l] + (int64_t)e * M * N; }
       g.push_back(p);
     }
-    if (launch_group(g, s)) return -1;
+    if (launch_group(g, s, nullptr, nullptr, nullptr, tile)) return -1;
   }
   return 0;
+}
+
+// the holdout evaluation's GEMM tiles (MOPO_EVAL_TILE, default 32: ~1000 rows per member)
+int eval_tile() {
+  static const int v = [] {
+    const char* e = std::getenv("MOPO_EVAL_TILE");
+    return e ? std::atoi(e) : 32;
+  }();
+  return v;
 }
 
 // one minibatch Adam step on the gathered X/T (M rows per member): P = Pb[par] -> Pb[1 - par]
@@ -1501,8 +1529,10 @@ extern "C" int mopo_bnn_train_eval_mse(mopo_bnn_train_t hh, const float* d_in, c
   MOPO_REQUIRE(h && d_in && d_tg && d_losses, "mopo_bnn_train_eval_mse: NULL argument");
   MOPO_REQUIRE(n >= 1 && n <= h->maxM, "mopo_bnn_train_eval_mse: n must be in [1, max(max_batch, max_eval)]");
   hipStream_t s = (hipStream_t)stream;
-  if (launch_gather(h, d_in, d_tg, d_rows, n, false, 0, n, s) || forward(h, h->Pb[0], n, s)) return -1;
-  hipLaunchKernelGGL(train_mse_kernel, dim3(h->L.E), dim3(256), 0, s, h->OUT, h->T, n, h->L.D, d_losses);
+  if (launch_gather(h, d_in, d_tg, d_rows, n, false, 0, n, s) ||
+      forward(h, h->Pb[0], n, s, n >= 32 ? eval_tile() : 0))
+    return -1;
+  hipLaunchKernelGGL(train_mse_kernel, dim3(h->L.E), dim3(MSE_TPB), 0, s, h->OUT, h->T, n, h->L.D, d_losses);
   MOPO_HIP(hipGetLastError());
   return 0;
 }
@@ -1581,14 +1611,38 @@ extern "C" int mopo_bnn_train_snapshot(mopo_bnn_train_t hh, int member, void* st
   return 0;
 }
 
+static int copy_members(Train* h, const std::vector<int>& members, int dir, hipStream_t s) {
+  for (size_t i0 = 0; i0 < members.size(); i0 += MAX_MEMBERS_SET) {
+    MemberSet ms{};
+    ms.n = (int)std::min(members.size() - i0, (size_t)MAX_MEMBERS_SET);
+    for (int i = 0; i < ms.n; ++i) ms.e[i] = members[i0 + i];
+    hipLaunchKernelGGL(members_copy_kernel, dim3(64, 2 * (NHID + 1), ms.n), dim3(256), 0, s, h->Pb[0], h->S,
+                       member_span(h->L), ms, dir);
+    MOPO_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+extern "C" int mopo_bnn_train_snapshot_members(mopo_bnn_train_t hh, const int* h_members, int n, void* stream) {
+  Train* h = reinterpret_cast<Train*>(hh);
+  MOPO_REQUIRE(h && (h_members || n == 0) && n >= 0, "mopo_bnn_train_snapshot_members: bad argument");
+  std::vector<int> ms;
+  for (int i = 0; i < n; ++i) {
+    const int e = h_members[i];
+    MOPO_REQUIRE(e >= 0 && e < h->L.E, "mopo_bnn_train_snapshot_members: bad member");
+    if (std::find(ms.begin(), ms.end(), e) == ms.end()) ms.push_back(e);
+  }
+  if (ms.empty()) return 0;
+  if (copy_members(h, ms, 0, (hipStream_t)stream)) return -1;
+  for (int e : ms)
+    if (std::find(h->snap.begin(), h->snap.end(), e) == h->snap.end()) h->snap.push_back(e);
+  return 0;
+}
+
 extern "C" int mopo_bnn_train_restore(mopo_bnn_train_t hh, void* stream) {
   Train* h = reinterpret_cast<Train*>(hh);
   MOPO_REQUIRE(h, "mopo_bnn_train_restore: NULL handle");
-  for (int e : h->snap) {
-    hipLaunchKernelGGL(member_copy_kernel, dim3(64, 2 * (NHID + 1)), dim3(256), 0, (hipStream_t)stream, h->Pb[0], h->S,
-                       member_span(h->L), e, 1);
-    MOPO_HIP(hipGetLastError());
-  }
+  if (!h->snap.empty() && copy_members(h, h->snap, 1, (hipStream_t)stream)) return -1;
   h->snap.clear();
   return 0;
 }
