@@ -228,6 +228,86 @@ __global__ __launch_bounds__(256) void rollout_post_kernel(const PostArgs a) {
   }
 }
 
+// The same post-processing for the common case (sampled steps, max-aleatoric penalty: neither pen_dist
+// nor det) with one thread per (row, dim): POSTF_ROWS rows of D lanes each, packed back to back (the
+// 32-lane groups above leave 14 of 32 lanes idle at D = 18).  Each row's pool position is computed once
+// (its 64-bit modulo by one lane); values and draws are the ones rollout_post_kernel makes.
+constexpr int POSTF_ROWS = 16, POSTF_MAXD = 64;   // PB % POSTF_ROWS == 0: a block's rows share one chunk
+__global__ __launch_bounds__(1024) void rollout_post_flat_kernel(const PostArgs a) {
+  __shared__ double srow[POSTF_ROWS][POSTF_MAXD];
+  __shared__ int64_t spos[POSTF_ROWS];
+  __shared__ int kept[POSTF_ROWS];
+  const int tid = threadIdx.x;
+  const int O = a.O, D = O + 1;
+  const int64_t r0 = (int64_t)blockIdx.x * POSTF_ROWS;
+  const int64_t count = *a.cnt;
+  if (tid < POSTF_ROWS) {
+    const int64_t row = r0 + tid;
+    spos[tid] = a.stage_base >= 0 ? a.stage_base + row : (a.pool.d_state[0] + a.pool_off + row) % a.pool.max_size;
+  }
+  const int rl = tid / D, sub = tid - rl * D;
+  const int64_t row = r0 + rl;
+  const bool on = rl < POSTF_ROWS && row < count;
+  double s = 0.0;
+  if (on) {
+    float m = a.mean_sel[row * D + sub];
+    if (sub >= 1) m = (float)((double)m + a.obs[row * O + sub - 1]);    // fake_env.py:66
+    double e;
+    if (a.eps) {
+      e = a.eps[row * D + sub];
+    } else {  // Philox normal `sub` of the row's stream (perf mode of fake_env.py:72)
+      const int64_t u = a.uid[row];
+      u32x4 c{(uint32_t)u, (uint32_t)((uint64_t)u >> 32) ^ ((uint32_t)(sub >> 2) << 20), a.step, RNG_OBS_NOISE};
+      u32x4 r = philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+      float z0, z1;
+      if (sub & 2) box_muller(r.z, r.w, z0, z1);
+      else box_muller(r.x, r.y, z0, z1);
+      e = (double)((sub & 1) ? z1 : z0);
+    }
+    s = (double)m + e * (double)a.std_sel[row * D + sub];              // fake_env.py:72
+    srow[rl][sub] = s;
+  }
+  __syncthreads();
+  if (on && sub >= 1) {                                                // next_obs = samples[:, 1:] (:90)
+    a.obs_next[row * O + sub - 1] = s;
+    a.pool.d_next_obs[spos[rl] * O + sub - 1] = (float)s;
+  }
+  if (tid < POSTF_ROWS) {
+    const int64_t rr = r0 + tid;
+    bool keep = false;
+    if (rr < count) {
+      const bool term = term_fn(a.term_kind, &srow[tid][1], O);        // fake_env.py:91
+      const double s0 = srow[tid][0];
+      const float pen = __uint_as_float(a.pen[rr]);
+      const double pr = a.coeff != 0.f ? s0 - (double)a.coeff * (double)pen : s0;   // fake_env.py:115
+      const int64_t pos = spos[tid];
+      a.pool.d_rew[pos] = (float)pr;
+      a.pool.d_term[pos] = term ? 1 : 0;
+      keep = !term;
+      if (a.keep) a.keep[rr] = keep ? 1 : 0;
+    }
+    kept[tid] = keep ? 1 : 0;
+  }
+  if (a.blockcnt) {
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+#pragma unroll
+      for (int i = 0; i < POSTF_ROWS; ++i) t += kept[i];
+      if (t) atomicAdd(a.blockcnt + r0 / PB, t);
+    }
+  }
+}
+
+// MOPO_POST_FLAT=0 (A/B): the 32-lane-per-row post kernel for every step
+static int post_flat() {
+  static const int v = [] {
+    const char* e = std::getenv("MOPO_POST_FLAT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
 __global__ __launch_bounds__(PB) void rollout_compact_kernel(int O, const int* blockcnt, const uint8_t* keepf,
                                                              const int* cnt, const double* obs_src,
                                                              double* obs_dst, const int64_t* uid_src,
@@ -437,7 +517,11 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
       KTimer t(h, KC_POST, ss);
       // with compaction the post kernel adds each block's kept rows into its PB-row chunk count
       if (compact) MOPO_HIP(hipMemsetAsync(h->blockcnt, 0, (size_t)nblk * sizeof(int), ss));
-      hipLaunchKernelGGL(rollout_post_kernel, dim3(ceil_div((int)n, POST_RPB)), dim3(256), 0, ss, pa);
+      if (post_flat() && !pen_dist && !det && D <= POSTF_MAXD)
+        hipLaunchKernelGGL(rollout_post_flat_kernel, dim3(ceil_div((int)n, POSTF_ROWS)),
+                           dim3((POSTF_ROWS * D + 63) / 64 * 64), 0, ss, pa);
+      else
+        hipLaunchKernelGGL(rollout_post_kernel, dim3(ceil_div((int)n, POST_RPB)), dim3(256), 0, ss, pa);
     }
     MOPO_HIP(hipGetLastError());
     return 0;

@@ -10,7 +10,7 @@ for i in 1 2 3; do
     cp abv/$so.so mopo_amd/libmopo_hip.so
     env $envs timeout -k 10 120 python bench.py --no-cpu-baseline --no-c3 --sac-steps 16 --train-epochs 0 --steps 20 ${BENCH_ARGS} \
       > gpurun_out/ab_cur.json 2> gpurun_out/ab_cur.err || { echo "bench $v failed"; tail -5 gpurun_out/ab_cur.err; exit 1; }
-    python -c "import json,sys; d=json.load(open('gpurun_out/ab_cur.json')); print('$v', round(d['value']/1e6,2), 'M/s', 'ens', round(d['kernel_ms_avg']['ensemble_fwd'],4), 'actor', round(d['kernel_ms_avg']['actor'],4), 'start', round(d['kernel_ms_avg'].get('start',0),4))" >> gpurun_out/ab.txt
+    python -c "import json,sys; d=json.load(open('gpurun_out/ab_cur.json')); print('$v', round(d['value']/1e6,2), 'M/s', 'ens', round(d['kernel_ms_avg']['ensemble_fwd'],4), 'actor', round(d['kernel_ms_avg']['actor'],4), 'start', round(d['kernel_ms_avg'].get('start',0),4), 'post', round(d['kernel_ms_avg'].get('fakeenv_post',0),4))" >> gpurun_out/ab.txt
   done
 done
 cat gpurun_out/ab.txt
