@@ -16,15 +16,20 @@ namespace mopo {
 // (biases zero-padded to whole 16-blocks so the kernel stages them into LDS with global_load_lds)
 // f16 (f16x3): W1 [1][2][NB] | W2 [NB/2][2][NB] | head [NB/2][2][1] fragments of 64 lanes x 8 fp16
 // (256 floats each, the ensemble's bf16 fragment layout with its k permutation), then the same biases,
-// then 3 inverse weight scales and 3 max-|W| words (actor_wmax_kernel)
+// then 3 inverse weight scales (+5 spare floats) and actor_wmax_kernel's WMAX_BLOCKS x 3 partial max-|W|
+constexpr int WMAX_BLOCKS = 64;   // actor_wmax_kernel's grid (<= 64: one wave reduces the partials)
+
 __host__ __device__ int64_t actor_packed_floats(int O, int Hp, int f16) {
   const int KG0 = (O + 15) / 16, NB = (Hp + 15) / 16;
-  if (f16) return (int64_t)(2 * NB + NB * NB + NB) * 256 + 2LL * NB * 16 + 16 + 8;
+  if (f16) return (int64_t)(2 * NB + NB * NB + NB) * 256 + 2LL * NB * 16 + 16 + 8 + 3 * WMAX_BLOCKS;
   return (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256 + (int64_t)NB * 256 + 2LL * NB * 16 + 16;
 }
 
-// max |W| of the three weight matrices (W1, W2, [Wmu | Wls]) as ordered uint bits -> wmax[3]
-__global__ void actor_wmax_kernel(const float* __restrict__ P, int O, int A, int Hp, uint32_t* __restrict__ wmax) {
+// max |W| of the three weight matrices (W1, W2, [Wmu | Wls]): block b's maxima -> wpart[3 b + q] (plain
+// stores: no zeroing launch before it, no atomics; pack_actor_f16_kernel reduces the WMAX_BLOCKS partials)
+__global__ __launch_bounds__(256) void actor_wmax_kernel(const float* __restrict__ P, int O, int A, int Hp,
+                                                         float* __restrict__ wpart) {
+  __shared__ float sm[4][3];
   const float* W1 = P;
   const float* W2 = W1 + O * Hp + Hp;
   const float* Wm = W2 + Hp * Hp + Hp;
@@ -42,21 +47,35 @@ __global__ void actor_wmax_kernel(const float* __restrict__ P, int O, int A, int
   for (int q = 0; q < 3; ++q) {
     float v = m[q];
     for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    if ((threadIdx.x & 63) == 0 && v > 0.f) atomicMax(wmax + q, __float_as_uint(v));
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6][q] = v;
   }
+  __syncthreads();
+  if (threadIdx.x < 3)
+    wpart[3 * blockIdx.x + threadIdx.x] =
+        fmaxf(fmaxf(sm[0][threadIdx.x], sm[1][threadIdx.x]), fmaxf(sm[2][threadIdx.x], sm[3][threadIdx.x]));
 }
 
 // f16x3 packing: fp16 parts of W * 2^k (k per matrix from wmax: max |W| 2^k in [2^14, 2^15)), the
 // biases as in the f32 packing, and the 3 inverse scales
 __global__ void pack_actor_f16_kernel(const float* __restrict__ P, int O, int A, int Hp, float* __restrict__ dst,
-                                      const uint32_t* __restrict__ wmax) {
+                                      const float* __restrict__ wpart) {
   const int NB = ceil_div(Hp, 16), KG = NB / 2;
   const float* W1 = P;
   const float* W2 = W1 + O * Hp + Hp;
   const float* Wm = W2 + Hp * Hp + Hp;
   const float* Wl = Wm + Hp * A + A;
+  __shared__ float smax[3];
+  if (threadIdx.x < 64) {   // the max over actor_wmax_kernel's per-block partials (exact in any order)
+    float v[3];
+    for (int q = 0; q < 3; ++q) v[q] = threadIdx.x < WMAX_BLOCKS ? wpart[3 * threadIdx.x + q] : 0.f;
+    for (int q = 0; q < 3; ++q)
+      for (int o = 32; o >= 1; o >>= 1) v[q] = fmaxf(v[q], __shfl_xor(v[q], o));
+    if (threadIdx.x == 0)
+      for (int q = 0; q < 3; ++q) smax[q] = v[q];
+  }
+  __syncthreads();
   float sc[3], inv[3];
-  for (int q = 0; q < 3; ++q) row_scale(__uint_as_float(wmax[q]), sc[q], inv[q]);
+  for (int q = 0; q < 3; ++q) row_scale(smax[q], sc[q], inv[q]);
   const int64_t f1 = 2LL * NB, f2 = (int64_t)KG * 2 * NB, fh = (int64_t)KG * 2;
   const int64_t nfrag = (f1 + f2 + fh) * 512;  // fp16 elements
   short* d16 = reinterpret_cast<short*>(dst);
@@ -148,13 +167,12 @@ int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s, 
     MOPO_REQUIRE(Hp % 32 == 0, "actor f16x3: hidden width must be a multiple of 32");
     MOPO_REQUIRE(O <= 32 && 2 * A <= 16, "actor f16x3: obs_dim <= 32, act_dim <= 8");
     const int NB = Hp / 16;
-    uint32_t* wmax = reinterpret_cast<uint32_t*>(dst + (2LL * NB + NB * NB + NB) * 256 + 2LL * NB * 16 + 16 + 3);
-    MOPO_HIP(hipMemsetAsync(wmax, 0, 3 * sizeof(uint32_t), s));
-    hipLaunchKernelGGL(actor_wmax_kernel, dim3(64), dim3(256), 0, s, P, O, A, Hp, wmax);
+    float* wpart = dst + (2LL * NB + NB * NB + NB) * 256 + 2LL * NB * 16 + 16 + 8;
+    hipLaunchKernelGGL(actor_wmax_kernel, dim3(WMAX_BLOCKS), dim3(256), 0, s, P, O, A, Hp, wpart);
     MOPO_HIP(hipGetLastError());
     const int64_t tot = (2LL * NB + NB * NB + NB) * 512 + 2LL * NB * 16 + 16 + 3;
     hipLaunchKernelGGL(pack_actor_f16_kernel, dim3((int)std::min<int64_t>((tot + 255) / 256, 1024)), dim3(256), 0, s,
-                       P, O, A, Hp, dst, (const uint32_t*)wmax);
+                       P, O, A, Hp, dst, (const float*)wpart);
     MOPO_HIP(hipGetLastError());
     return 0;
   }
