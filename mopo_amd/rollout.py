@@ -10,6 +10,7 @@ transitions land in a device ``SimpleReplayPool`` in the reference's order.  Two
   compared to the reference for identical inputs.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -127,8 +128,15 @@ class ModelRollout:
         import torch
         dev = env_obs.device
         B = int(batch_size)
-        steps = torch.zeros(max(horizon, 1), dtype=torch.int64, device=dev)
-        el = torch.as_tensor(np.asarray(elites, np.int32)).to(dev)
+        # every steps[i], i < horizon, is stored by the rollout's advance kernels when B > 0 (no fill launch);
+        # the elites' device copy is kept while they stay the same (no H2D copy per rollout)
+        legacy = os.environ.get('MOPO_ROLLOUT_FILL') == '1'                       # A/B knob: the old launches
+        alloc = torch.empty if (B > 0 and int(horizon) > 0 and not legacy) else torch.zeros
+        steps = alloc(max(horizon, 1), dtype=torch.int64, device=dev)
+        ekey = (tuple(int(e) for e in np.asarray(elites).ravel()), str(dev))
+        if getattr(self, '_elites', (None, None))[0] != ekey or legacy:
+            self._elites = (ekey, torch.as_tensor(np.asarray(elites, np.int32)).to(dev))
+        el = self._elites[1]
         keep = [steps, el]
 
         def dptr(x, dt):
