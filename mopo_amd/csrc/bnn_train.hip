@@ -496,7 +496,17 @@ static __global__ __launch_bounds__(256, 2) void train_wgrad_kernel(const TrainW
 #ifndef TRAIN_WG2_MINW
 #define TRAIN_WG2_MINW 0   // > 0: waves per SIMD the tile kernel's registers are capped for (0: NT / 128)
 #endif
-constexpr int TW2_T = 32, TW2_KC = TRAIN_WG2_KC, TW2_KP = TW2_KC + 4;
+// LDS panels [row][k] of the weight-gradient tiles: k XOR-swizzled by row group ((row >> 2) & 7, in units of
+// 4 floats: a b128 read of 4 consecutive k stays contiguous) at a 140-float row stride, so the transposing
+// b32 stores (8 rows x 8 k per 32-lane group) hit 32 distinct banks instead of 8 and the b128 MFMA reads
+// conflict less (modelled with MI355X_MICROARCH's LDS lane groups: 128 + 320 vs 512 + 256 LDS cycles per chunk)
+#ifndef TW2_SWZ
+#define TW2_SWZ 1
+#endif
+constexpr int TW2_T = 32, TW2_KC = TRAIN_WG2_KC, TW2_KP = TW2_KC + (TW2_SWZ ? 12 : 4);
+static __device__ __forceinline__ int tw2_at(int row, int k) {
+  return row * TW2_KP + (TW2_SWZ ? (k ^ (((row >> 2) & 7) << 2)) : k);
+}
 struct TrainWg2 {
   int M;                               // minibatch rows per member (the contraction length)
   int nwx, per_x;                      // tile workgroups per XCD; list stride per XCD
@@ -583,7 +593,9 @@ static __device__ __forceinline__ void wg2_adam_in(const AdamCtx& ad, const Wg2T
 }
 
 template <int NT>
-static __global__ __launch_bounds__(NT, TRAIN_WG2_MINW > 0 ? TRAIN_WG2_MINW : NT / 128) void train_wgrad2_kernel(const TrainWg2 g) {
+// 512 threads: registers capped for 6 waves per SIMD, i.e. three workgroups per CU (the swizzled indexing
+// otherwise takes 82 VGPRs: two)
+static __global__ __launch_bounds__(NT, TRAIN_WG2_MINW > 0 ? TRAIN_WG2_MINW : (NT == 512 ? 6 : NT / 128)) void train_wgrad2_kernel(const TrainWg2 g) {
   using C = Wg2<NT>;
   __shared__ __attribute__((aligned(16))) float As[TW2_T * TW2_KP];   // [i][k]; later the K-part partials
   __shared__ __attribute__((aligned(16))) float Bs[TW2_T * TW2_KP];   // [j][k]
@@ -626,8 +638,8 @@ static __global__ __launch_bounds__(NT, TRAIN_WG2_MINW > 0 ? TRAIN_WG2_MINW : NT
         for (int q = 0; q < C::NQ; ++q)
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            As[(r0 + u) * TW2_KP + k0 + (NT / 8) * q] = va[q][u];
-            Bs[(r0 + u) * TW2_KP + k0 + (NT / 8) * q] = vb[q][u];
+            As[tw2_at(r0 + u, k0 + (NT / 8) * q)] = va[q][u];
+            Bs[tw2_at(r0 + u, k0 + (NT / 8) * q)] = vb[q][u];
           }
       }
       lds_barrier();
@@ -641,17 +653,17 @@ static __global__ __launch_bounds__(NT, TRAIN_WG2_MINW > 0 ? TRAIN_WG2_MINW : NT
 #pragma unroll
       for (int s = 0; s < C::KW / 16; ++s) {         // k = KW kq + (KW / 4) lk + 4 s + u
         const int k = C::KW * kq + (C::KW / 4) * lk + 4 * s;
-        const f32x4 a4 = ld4(As + (16 * qi + li) * TW2_KP + k), b4 = ld4(Bs + (16 * qj + li) * TW2_KP + k);
+        const f32x4 a4 = ld4(As + tw2_at(16 * qi + li, k)), b4 = ld4(Bs + tw2_at(16 * qj + li, k));
         acc0 = mfma4(a4[0], b4[0], acc0);
         acc1 = mfma4(a4[1], b4[1], acc1);
         acc0 = mfma4(a4[2], b4[2], acc0);
         acc1 = mfma4(a4[3], b4[3], acc1);
       }
       if (cur.cs) {                                  // column tid / CT, k = CK (tid % CT) .. + CK - 1
-        const float* bp = Bs + (tid / C::CT) * TW2_KP + C::CK * (tid % C::CT);
+        const int crow = tid / C::CT, ck0 = C::CK * (tid % C::CT);
 #pragma unroll
         for (int v = 0; v < C::CK; v += 4) {
-          const f32x4 x0 = ld4(bp + v);
+          const f32x4 x0 = ld4(Bs + tw2_at(crow, ck0 + v));
           cs += (x0[0] + x0[1]) + (x0[2] + x0[3]);
         }
       }
@@ -806,8 +818,8 @@ static __device__ __forceinline__ void ts_tiles(const TrainStep& s, float* As, f
         for (int q = 0; q < C::NQ; ++q)
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            As[(r0 + u) * TW2_KP + k0 + (NT / 8) * q] = va[q][u];
-            Bs[(r0 + u) * TW2_KP + k0 + (NT / 8) * q] = vb[q][u];
+            As[tw2_at(r0 + u, k0 + (NT / 8) * q)] = va[q][u];
+            Bs[tw2_at(r0 + u, k0 + (NT / 8) * q)] = vb[q][u];
           }
       }
       if (kc == 0 && tid == 0) slot[0] = (int)pend;   // requested a whole tile ago
@@ -830,17 +842,17 @@ static __device__ __forceinline__ void ts_tiles(const TrainStep& s, float* As, f
 #pragma unroll
       for (int s2 = 0; s2 < C::KW / 16; ++s2) {
         const int k = C::KW * kq + (C::KW / 4) * lk + 4 * s2;
-        const f32x4 a4 = ld4(As + (16 * qi + li) * TW2_KP + k), b4 = ld4(Bs + (16 * qj + li) * TW2_KP + k);
+        const f32x4 a4 = ld4(As + tw2_at(16 * qi + li, k)), b4 = ld4(Bs + tw2_at(16 * qj + li, k));
         acc0 = mfma4(a4[0], b4[0], acc0);
         acc1 = mfma4(a4[1], b4[1], acc1);
         acc0 = mfma4(a4[2], b4[2], acc0);
         acc1 = mfma4(a4[3], b4[3], acc1);
       }
       if (cur.cs) {
-        const float* bp = Bs + (tid / C::CT) * TW2_KP + C::CK * (tid % C::CT);
+        const int crow = tid / C::CT, ck0 = C::CK * (tid % C::CT);
 #pragma unroll
         for (int v = 0; v < C::CK; v += 4) {
-          const f32x4 x0 = ld4(bp + v);
+          const f32x4 x0 = ld4(Bs + tw2_at(crow, ck0 + v));
           cs += (x0[0] + x0[1]) + (x0[2] + x0[3]);
         }
       }
