@@ -27,7 +27,10 @@
 namespace mopo {
 
 constexpr int TR_NHID = 4;
-constexpr int TR_LD = 260;   // LDS row stride (floats) of a 16-row activation block: K <= 256 (+4: b128 reads conflict-free)
+#ifndef TR_LD_CFG
+#define TR_LD_CFG 260
+#endif
+constexpr int TR_LD = TR_LD_CFG;   // LDS row stride (floats) of a 16-row activation block: K <= 256 (+4: b128 reads conflict-free)
 
 struct TrainRows {
   int E, M, IN, H, D, nrb;
