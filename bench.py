@@ -35,8 +35,9 @@ MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) 
 # ensemble dtype -> (bf16 parts per operand, bf16 products per f32 product); fp32 runs f32 MFMA
 SPLIT = {'bf16': (1, 1), 'bf16x3': (2, 3), 'bf16x6': (3, 6), 'f16x3': (2, 3)}
 DTYPE_DESC = {'fp32': 'fp32 (f32 MFMA 16x16x4)',
-              'bf16x6': 'f32 (f32 operands split into 3 bf16 parts, 6 bf16 MFMA products, f32 accumulate: '
-                        'f32-accurate, held to the fp32 parity tolerances)',
+              'bf16x6': 'f32 (exact f32 operands: each split into 3 round-to-nearest bf16 parts with x0+x1+x2 == x '
+                        'for 2^-100 <= |x| < 2^127; 6 bf16 MFMA products, the 3 dropped ones <= 2^-23 |x w| in total; '
+                        'f32 accumulate; held to the fp32 parity tolerances)',
               'bf16x3': 'f32 operands as 2 bf16 parts (3 bf16 MFMA products, ~17 significand bits, f32 accumulate)',
               'bf16': 'bf16 (f32 accumulate)',
               'f16x3': 'f32 (f32 operands as 2 fp16 parts under power-of-two scales, 3 f16 MFMA products, f32 '
@@ -84,6 +85,9 @@ def parse():
     p.add_argument('--ensemble-dtype', default=DEFAULT_ENSEMBLE_DTYPE, choices=list(DTYPES),
                    help='headline ensemble-forward arithmetic (mopo_amd.bnn.DTYPES); the default is the one '
                         'MOPO.train runs (mopo_amd.bnn.DEFAULT_ENSEMBLE_DTYPE)')
+    p.add_argument('--actor-dtype', default=None, choices=['fp32', 'f16x3'],
+                   help="the rollout policy's arithmetic (default: mopo_amd.rollout.default_actor_dtype of the "
+                        'ensemble dtype)')
     p.add_argument('--no-alt-dtypes', action='store_true',
                    help='skip the extra headline-workload lines with the other ensemble dtypes')
     p.add_argument('--prof-steps', type=int, default=20, help='untimed rollouts timed per kernel with HIP events')
@@ -178,7 +182,8 @@ def rollout_step(args, ro, pool, pi, env, staging, epoch, rank, world):
     spec = CONFIGS[args.config]
     tk, pen = static_fns[spec['domain']].term_kind, spec['penalty']
     if world == 1:
-        return ro.run(env, pi, pool, args.batch, args.horizon, tk, pen, [0, 1, 2, 3, 4], seed=88, epoch=epoch)
+        return ro.run(env, pi, pool, args.batch, args.horizon, tk, pen, [0, 1, 2, 3, 4], seed=88, epoch=epoch,
+                      actor_dtype=getattr(args, 'actor_dtype', None))
     # RCCL all-gather of each step's staged transitions (overlapping the next step) into every rank's pool
     return staging.run(env, pi, pool, tk, pen, [0, 1, 2, 3, 4], seed=88, epoch=epoch)
 
@@ -302,7 +307,10 @@ def roofline_of(dtype, rows, ms, flop_row=FLOP_BNN_ROW):
     parts, prods = SPLIT[dtype]
     if dtype == 'f16x3':
         kern = ('bnn_fwd_ring_kernel<P=2> (ensemble forward on a 3-slot LDS ring, f16 MFMA 16x16x32, 3 products per f32 '
-                'product; bnn_fwd_f16s_kernel at H > 256)')
+                'product; bnn_fwd_f16h_kernel at H > 256)')
+    elif dtype == 'bf16x6':
+        kern = ('bnn_fwd_ring_kernel<P=3> (ensemble forward on a 3-slot LDS ring, exact 3-part bf16 split, bf16 MFMA '
+                '16x16x32, 6 products per f32 product)')
     else:
         kern = 'bnn_fwd_bf16_kernel<P=%d> (ensemble forward, bf16 MFMA 16x16x32, %d products per f32 product)' % (
             parts, prods)
@@ -526,10 +534,9 @@ def sac_leg(args, pool, env, dev, world):
 
 
 def cpu_baseline_sac(args):
-    """Oracle SAC steps (numpy restatement of mopo.py:204-466, 834-853) on the host: ``cpu_sac_steps``
-    (1000) consecutive steps at batch 256 on one SAC state, timed as 5 consecutive runs of a fifth each
-    after a warm-up run (a bounded sample: BASELINE.md section 3 asks for 5 runs of 1000 steps, about 40 s
-    here); the median run's rate."""
+    """Oracle SAC steps (numpy restatement of mopo.py:204-466, 834-853) on the host, as BASELINE.md section 3
+    times them: runs of ``cpu_sac_steps`` (1000) consecutive steps at batch 256 on one SAC state, the median
+    of 5 timed runs after a warm-up run."""
     from oracle import sac as osac
     rs = np.random.RandomState(0)
     st = osac.SACState(osac.init_params(O, A, HP, seed=2, dtype=np.float32))
@@ -539,7 +546,7 @@ def cpu_baseline_sac(args):
     batch = {'observations': rs.normal(size=(n, O)).astype(np.float32), 'actions': rs.uniform(-1, 1, (n, A)).astype(np.float32),
              'next_observations': rs.normal(size=(n, O)).astype(np.float32), 'rewards': rs.normal(size=(n, 1)).astype(np.float32),
              'terminals': np.zeros((n, 1), bool)}
-    per = max(args.cpu_sac_steps // CPU_RUNS, 1)
+    per = max(args.cpu_sac_steps, 1)
 
     def run():
         t0 = time.perf_counter()
@@ -548,10 +555,9 @@ def cpu_baseline_sac(args):
         return per, time.perf_counter() - t0
     med, runs, units, secs = median_runs(run)
     return {'value': med, 'unit': 'grad-steps/s', 'cores': blas_threads(), 'kind': 'port', 'runs': runs, 'median': med,
-            'steps_consecutive': units, 'steps_per_run': per,
-            'sample': 'oracle numpy SAC step (fp32 arrays), batch 256: %d consecutive steps on one SAC state, timed as '
-                      '%d runs of %d (%.2f s) after a warm-up run of %d; BASELINE.md section 3 times 5 runs of 1000'
-                      % (units, CPU_RUNS, per, secs, per)}
+            'steps_per_run': per,
+            'sample': 'oracle numpy SAC step (fp32 arrays), batch 256: %d timed runs of %d consecutive steps (%.2f s) '
+                      'after a warm-up run of %d' % (CPU_RUNS, per, secs, per)}
 
 
 def main():
@@ -633,9 +639,81 @@ def main():
         out['cpu_baseline_sac'] = cpu_baseline_sac(args)
         if args.train_epochs > 0:
             out['cpu_baseline_train'] = cpu_baseline_train(args)
-    print(json.dumps(out))
+    write_detail(args, out)
+    print(json.dumps(compact_line(out)))
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+LINE_LIMIT = 7000   # the driver keeps the last ~8 KB of stdout: the one bench line must fit in it whole
+
+
+def _r(x, n=4):
+    return None if x is None else float('%.*g' % (n, x))
+
+
+def compact_line(out):
+    """The one stdout line: the contract keys, the headline roofline, the CPU baseline, SAC, BNN.train and
+    the credited-precision (fp32 / exact-operand) legs, each reduced to its figures.  Every leg in full
+    (kernel tables, per-run CPU rates, sample descriptions) goes to the detail file (write_detail)."""
+    keys = ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step', 'higher_is_better', 'scaling',
+            'vs_baseline', 'dtype', 'data', 'config', 'product_default_dtype')
+    line = {k: out[k] for k in keys if k in out}
+    r = out['roofline']
+    line['roofline'] = {'bound': r['bound'], 'achieved': _r(r['achieved']), 'peak': r['peak'], 'unit': r['unit'],
+                        'frac': _r(r['frac']), 'traffic': r.get('traffic'),
+                        'algorithmic_bytes': r.get('algorithmic_bytes_per_launch'),
+                        'kernel': r['kernel'].split(' (')[0], 'avg_launch_ms': _r(r['avg_launch_ms'], 5),
+                        'flop_per_launch': r.get('flop_per_launch')}
+    line['kernel_ms_avg'] = {k: _r(v) for k, v in out['kernel_ms_avg'].items()}
+    s = out['sac']
+    line['sac'] = {'per_gpu': _r(s['per_gpu'], 5), 'us_per_step': _r(s['us_per_step'], 4),
+                   'frac': _r(s['roofline']['frac']), 'floor_us': _r(s['roofline']['floor_us']),
+                   'traffic': s['roofline'].get('traffic'), 'bytes_algorithmic': s['roofline']['bytes_per_step'],
+                   'steps_timed': s['steps_timed']}
+    if 'model_train' in out:
+        t = out['model_train']
+        line['model_train'] = {'value': _r(t['value'], 5), 'unit': t['unit'], 'ms_per_epoch': _r(t['ms_per_epoch']),
+                               'tflops': _r(t['tflops_achieved'])}
+    legs = {}
+    for k, v in out.get('headline_other_dtypes', {}).items():
+        legs['C2_' + k] = {'value': _r(v['value']), 'frac': _r(v['roofline']['frac']),
+                           'ms': _r(v['roofline']['avg_launch_ms'])}
+    for k, v in out.get('extra_configs', {}).items():
+        rr = v.get('roofline')
+        legs[k] = {'value': _r(v['value']), 'frac': _r(rr['frac']) if rr else None,
+                   'ms': _r(rr['avg_launch_ms']) if rr else None}
+    if legs:
+        line['legs'] = legs
+    if 'C2_fp32' in legs:
+        line['fp32_leg'] = legs['C2_fp32']
+    for k in ('cpu_baseline', 'cpu_baseline_1core', 'cpu_baseline_sac', 'cpu_baseline_train'):
+        c = out.get(k)
+        if not c:
+            continue
+        d = {'value': _r(c['value'], 5), 'unit': c['unit'], 'cores': c['cores'], 'kind': c['kind'],
+             'median': _r(c['median'], 5), 'runs': [_r(x) for x in c['runs']]}
+        if k == 'cpu_baseline':
+            d['sample'] = c['sample']
+            d['configs'] = {n: _r(v['value']) for n, v in c.get('configs', {}).items()}
+        line[k] = d
+    line['detail'] = 'every leg in full: gpurun_out/bench_detail.json (copied to profiles/r06_bench_full.json)'
+    s = json.dumps(line)
+    if len(s) > LINE_LIMIT:   # never let the headline fall out of the driver's tail
+        for k in ('kernel_ms_avg', 'legs', 'cpu_baseline_1core'):
+            line.pop(k, None)
+    return line
+
+
+def write_detail(args, out):
+    """The full result (every leg, kernel tables, CPU-baseline runs) as one JSON file beside the bench line."""
+    path = os.environ.get('MOPO_BENCH_DETAIL', os.path.join(ROOT, 'gpurun_out', 'bench_detail.json'))
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, 'w') as f:
+            json.dump(out, f, indent=1)
+    except OSError as e:   # a read-only tree must not cost the bench line
+        print('bench detail not written: %s' % e, file=sys.stderr)
 
 
 def workload_key(args):

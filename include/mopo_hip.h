@@ -202,9 +202,7 @@ int mopo_bnn_train_logs(mopo_bnn_train_t h, float* h_logs, int n);
  * followed by the 8 list lengths into out (8 per + 8 ints; out may be NULL) and returns per (< 0: error).
  * No reference counterpart: a layout detail of bnn.py:425-432's minibatch op on this device. */
 int mopo_bnn_train_tile_lists(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap);
-/* The same for the single-launch step (MOPO_TRAIN_STEP1): each list ordered by layer, the heads first. */
-int mopo_bnn_train_tile_lists_step(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap);
-/* Diagnostic builds only (MOPO_TRAIN_STAMPS=1; otherwise returns -1): the single-launch step's
+/* Diagnostic builds only (MOPO_TRAIN_STAMPS=1; otherwise returns -1): the rows launch's
  * per-workgroup phase stamps of the last step, [block][8] (bnn_train.hip mopo_bnn_train_debug_stamps). */
 int mopo_bnn_train_debug_stamps(uint64_t* h_out, int64_t n);
 
@@ -293,6 +291,13 @@ int mopo_sac_step(mopo_sac_t h, const mopo_pool_desc* env_pool, const mopo_pool_
                   int n_steps, uint64_t seed, const int64_t* d_idx, const float* d_eps_s,
                   const float* d_eps_n, void* stream);
 int mopo_sac_set_graph(mopo_sac_t h, int enable);
+/* Synchronises the device and reads the fused step's sticky hand-off timeout word (no reference
+ * counterpart: the reference's TF session has no in-launch hand-offs).  A bounded wait that gave up
+ * makes every later step hold its parameter / Adam / target updates and write NaN logs; this call
+ * reports it (*timed_out = 1, returns -1 with mopo_last_error() set) and clears the word. */
+int mopo_sac_check(mopo_sac_t h, int* timed_out);
+/* Fault injection for tests: sets the timeout word as a give-up would. */
+int mopo_sac_inject_timeout(mopo_sac_t h);
 /* Target-network schedule (mopo.py:834-845 `if iteration % target_update_interval == 0:
  * _update_target()`, iteration = the epoch-local timestep of mopo.py:545-571, shared by the
  * n_train_repeat steps of a timestep, :790-795): the step whose device step counter is c updates the

@@ -81,7 +81,6 @@ SIGNATURES = {
     'mopo_bnn_train_restore': (c_int, [c_void_p, c_void_p]),
     'mopo_bnn_train_logs': (c_int, [c_void_p, c_void_p, c_int]),
     'mopo_bnn_train_tile_lists': (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_i64]),
-    'mopo_bnn_train_tile_lists_step': (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_i64]),
     'mopo_bnn_train_debug_stamps': (c_int, [c_void_p, c_i64]),
     'mopo_rollout_create': (c_int, [C.POINTER(c_void_p), c_void_p, c_i64, c_int]),
     'mopo_rollout_destroy': (c_int, [c_void_p]),
@@ -96,6 +95,8 @@ SIGNATURES = {
     'mopo_sac_step': (c_int, [c_void_p, C.POINTER(PoolDesc), C.POINTER(PoolDesc), c_int, c_u64, c_void_p,
                               c_void_p, c_void_p, c_void_p]),
     'mopo_sac_set_graph': (c_int, [c_void_p, c_int]),
+    'mopo_sac_check': (c_int, [c_void_p, C.POINTER(c_int)]),
+    'mopo_sac_inject_timeout': (c_int, [c_void_p]),
     'mopo_sac_set_target_schedule': (c_int, [c_void_p, c_i64, c_i64, c_i64, c_void_p]),
     'mopo_sac_set_action_prior': (c_int, [c_void_p, c_int]),
     'mopo_sac_copy': (c_int, [c_void_p, c_int, c_int, c_void_p, c_i64, c_void_p]),

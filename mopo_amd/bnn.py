@@ -22,9 +22,11 @@ import numpy as np
 from . import _lib as L
 
 # ensemble-forward arithmetic (mopo_bnn_create dtype): 'fp32' f32 MFMA; 'bf16' bf16 operands;
-# 'bf16x3' / 'bf16x6' f32 operands split into 2 / 3 bf16 parts (3 / 6 bf16 MFMAs per product,
-# f32 accumulate; bf16x6 ~22-bit operands, bf16x3 ~17 significand bits); 'f16x3' f32 operands as
-# 2 fp16 parts under power-of-two scales (3 f16 MFMAs per product, ~22-bit operands like bf16x6).
+# 'bf16x3' / 'bf16x6' f32 operands split into 2 / 3 round-to-nearest bf16 parts (3 / 6 bf16 MFMAs per
+# product, f32 accumulate): bf16x6's split is EXACT (x0 + x1 + x2 == x for 2^-100 <= |x| < 2^127,
+# csrc/mlp_tile.h split_bf16, tests/test_split.py) and its 3 dropped products total <= 2^-23 |x w|;
+# bf16x3 keeps ~17 significand bits; 'f16x3' f32 operands as 2 fp16 parts under power-of-two scales
+# (3 f16 MFMAs per product, ~22-bit operands, the dropped product <= 2^-22 |x w|).
 _DTYPES = {'fp32': 0, 'bf16': 1, 'bf16x3': 2, 'bf16x6': 3, 'f16x3': 4}
 DTYPES = tuple(_DTYPES)
 # what MOPO (and so `mopo run_local` and bench.py's headline) runs unless told otherwise: the f16x3
@@ -412,6 +414,9 @@ class BNN:
         side = None if os.environ.get('MOPO_TRAIN_SHUFFLE_SIDE') == '0' else self._side_stream()
         if side is not None:
             keys.record_stream(side)
+            # the block may have been in use on the current stream until just now: the side stream's first
+            # write of it must wait for that (record_stream only protects the free)
+            side.wait_stream(torch.cuda.current_stream())
         t0 = time.time()
         for epoch in (range(max_epochs) if max_epochs is not None else itertools.count()):
             L.check(L.lib().mopo_bnn_train_epoch(t, L.ptr(x), L.ptr(y), L.ptr(idxs), n, int(batch_size), None))

@@ -601,6 +601,9 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? BNN_F16_MINB_WIDE : BNN_F16_
 #ifndef BNN_F16H_MINB
 #define BNN_F16H_MINB 2
 #endif
+#ifndef BNN_F16H_FENCE
+#define BNN_F16H_FENCE 1
+#endif
 #ifndef BNN_F16H_XCDMEM
 #define BNN_F16H_XCDMEM 1  // E % 8 == 0: each XCD owns E / 8 members (their weights fetched into one L2)
 #endif
@@ -711,8 +714,16 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd
     to_input(lds_bias, inv_row * w.wscale[(1 + l) * E + e]);
   }
   f32x4 hd[NBO];
+#if BNN_F16H_FENCE
+  // the rollout epilogue's address arithmetic stays behind the last layer (hoisted into the layers it held 3
+  // more VGPRs there: 12 B of scratch per lane)
+  __builtin_amdgcn_sched_barrier(0);
+#endif
   layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, 1, true, NBO, KH>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd,
                                                                  lds, wv, lane, s_in);
+#if BNN_F16H_FENCE
+  __builtin_amdgcn_sched_barrier(0);
+#endif
   const float f = inv_row * w.wscale[4 * E + e] * kNegLn2;  // the head's input is y' = -log2(e) y
 #pragma unroll
   for (int nb = 0; nb < NBO; ++nb) hd[nb] *= f;
@@ -857,6 +868,9 @@ __global__ __launch_bounds__(WAVES * 64, R == 1 ? 2 : 1) void bnn_fwd_f16r_kerne
 #ifndef BNN_RING_DEPTH_BF16
 #define BNN_RING_DEPTH_BF16 3
 #endif
+#ifndef BNN_BF16X6_RING
+#define BNN_BF16X6_RING 1   // bf16x6 (the exact 3-part split) on the ring kernel at H <= 256
+#endif
 #ifndef BNN_F16_FOLD
 #define BNN_F16_FOLD 1   // with BNN_F16Q_DEFER: the ring kernel's row scale folded into the swish (bnn_fwd_ring_kernel)
 #endif
@@ -873,10 +887,14 @@ __global__ __launch_bounds__(WAVES * 64, R == 1 ? 2 : 1) void bnn_fwd_f16r_kerne
 #ifndef BNN_RING_MINB
 #define BNN_RING_MINB 3  // 4-wave workgroups per CU the ring kernel's registers are capped for (LDS admits 3)
 #endif
+#ifndef BNN_RING_MINB_X6
+#define BNN_RING_MINB_X6 3  // the same for bf16x6 (P = 3; 158 VGPRs with the dot2 residuals, no scratch)
+#endif
 template <int NB2, int NBO, int MODE, int WAVES, int P, int DEPTH, int NBU = NB2>
-__global__ __launch_bounds__(WAVES * 64, BNN_RING_MINB * 4 / WAVES > 0 ? BNN_RING_MINB * 4 / WAVES : 1) void bnn_fwd_ring_kernel(const BnnDev w,
+__global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_MINB) * 4 / WAVES > 0)
+                                             ? (P == 3 ? BNN_RING_MINB_X6 : BNN_RING_MINB) * 4 / WAVES : 1) void bnn_fwd_ring_kernel(const BnnDev w,
                                                                                             const FwdArgs a) {
-  static_assert(P == 1 || P == 2, "1: bf16, 2: f16x3");
+  static_assert(P == 1 || P == 2 || P == 3, "1: bf16, 2: f16x3, 3: bf16x6 (the exact 3-part bf16 split)");
   static_assert(DEPTH >= 3, "ring of at least 3 slots");
   constexpr bool F16 = P == 2;
   constexpr int KG = NB2 / 2, NS = P + 4 * KG * P;
@@ -1019,6 +1037,17 @@ __global__ __launch_bounds__(WAVES * 64, BNN_RING_MINB * 4 / WAVES > 0 ? BNN_RIN
       }
       cur[0] = __builtin_bit_cast(bf16x8, h4);
       cur[P - 1] = __builtin_bit_cast(bf16x8, l4);
+    } else if constexpr (P == 3) {   // the exact RN split (mlp_tile.h split_bf16_pair): x0 + x1 + x2 == x
+      u32x4v p4[3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t pr[3];
+        split_bf16_pair<3>(v[2 * q], v[2 * q + 1], pr);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) p4[k][q] = pr[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) cur[k] = __builtin_bit_cast(bf16x8, p4[k]);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) cur[0][j] = to_bf16(v[j]);
@@ -1068,13 +1097,13 @@ __global__ __launch_bounds__(WAVES * 64, BNN_RING_MINB * 4 / WAVES > 0 ? BNN_RIN
         for (int q = P - 1 - p; q >= 0; --q)
           acc[nb] = (KHL && kg + 1 == KGL) ? mfma_16x16x16_lo<F16>(fr, cur[q], acc[nb])
                                            : mfma_16x16x32<F16>(fr, cur[q], acc[nb]);
-        // the next k-group's activations, spread over this k-group's P slices: values 8 p / P ..,
-        // value v after fragment max((v + 1) NBUL / V - 1, 0) (V = 8 / P per slice)
+        // the next k-group's activations, spread over this k-group's P slices: values V p .. V p + V - 1,
+        // value v after fragment max((v + 1) NBUL / V - 1, 0) (V = ceil(8 / P) per slice)
         if constexpr (DEFER && kg + 1 < KGL) {
-          constexpr int V = 8 / P;
+          constexpr int V = (8 + P - 1) / P;
 #pragma unroll
           for (int v = 0; v < V; ++v)
-            if (nb == ((v + 1) * NBUL / V - 1 > 0 ? (v + 1) * NBUL / V - 1 : 0)) act(kg + 1, V * p + v);
+            if (V * p + v < 8 && nb == ((v + 1) * NBUL / V - 1 > 0 ? (v + 1) * NBUL / V - 1 : 0)) act(kg + 1, V * p + v);
         }
       }
     });
@@ -1179,6 +1208,8 @@ template <int NB2, int NBO, int P>
 static int launch_bf16_p(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   if constexpr (P == 1 && BNN_BF16_RING && NB2 <= 16)
     if (ring_shape<NB2>(h)) return launch_ring<NB2, NBO, 1, BNN_RING_DEPTH_BF16>(h, mode, a, s);
+  if constexpr (P == 3 && BNN_BF16X6_RING && NB2 <= 16)
+    if (ring_shape<NB2>(h)) return launch_ring<NB2, NBO, 3, BNN_RING_DEPTH_BF16>(h, mode, a, s);
   constexpr int WV = P == 1 ? FWD_WAVES : BNN_SPLIT_WAVES;
   constexpr int PS = P == 1 ? 1 : (BNN_SPLIT_PS == 0 ? P : BNN_SPLIT_PS);
   a.ntiles = (int)ceil_div((int)a.B, 16);

@@ -77,10 +77,6 @@ struct Train {
   int32_t* wlist = nullptr;    // weight-gradient tiles per XCD (train_wgrad2_kernel): [8][wl_per_x], counts [8]
   int32_t* wcnt = nullptr;
   int wl_per_x = 0;
-  int32_t* wlist_s = nullptr;  // the single-launch step's lists (make_wlist order 2), counts; its counters
-  int32_t* wcnt_s = nullptr;
-  int wl_per_x_s = 0;
-  unsigned* tsync = nullptr;
   // graphs (full-batch steps), keyed by the epoch's data pointers
   hipStream_t gs = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
@@ -701,263 +697,6 @@ static __global__ __launch_bounds__(NT, TRAIN_WG2_MINW > 0 ? TRAIN_WG2_MINW : (N
   }
 }
 
-// ---- the whole minibatch step as ONE launch (MOPO_TRAIN_STEP1) ------------------------------------------
-// Workgroups [0, nrw): the row blocks (train_rows_body<SIG = true>: member e's blocks on XCD e mod 8, each
-// stage handed off on ready[e][l]); workgroup nrw: the batch-level tail (the loss partials once every
-// member's row blocks are past their output gradient, the log-var bounds' Adam), which then waits for every
-// other workgroup of the launch before it advances the beta powers and the minibatch counter (every
-// workgroup derives this step's lr_t from them at its start) and zeroes the launch's counters; the rest:
-// weight-gradient tile workgroups, nwx per XCD, taking the entries of their XCD's list (tiles in readiness
-// order: layer NHID first) from a per-XCD work counter, each tile waiting until all nrb row blocks of its
-// (member, layer) have signalled -- so the heads' and the top hidden layers' tiles run on the CUs the 7 x 16
-// row blocks leave idle while the row blocks are still in their backward chain.  The tiles wait only on row
-// blocks (lower ids, dispatched first, never waiting themselves) and nothing waits on the tail, so the
-// launch drains whatever the placement; every spin is bounded (a give-up sets the timeout word; the tail then
-// writes NaN to the loss log).  Handed-off rows are stored write-through by the producers and read by the
-// tiles with sc1 loads (cdna_hip_programming.md Guideline 16, R1 form).
-struct TrainStep {
-  TrainRows r;
-  TrainWg2 g;
-  unsigned* sync;        // ready[E (NHID + 1)] | work[8] | done | timeout, TS_STRIDE apart
-  int nrw;               // row-block workgroups (8 nrb ceil(E / 8))
-};
-constexpr int TS_WORK = 0, TS_DONE = 8, TS_TMO = 9, TS_GLOBAL = 10;   // after the E (NHID + 1) ready counters
-constexpr unsigned TS_SPIN_LIMIT = 1u << 20;
-
-static __device__ __forceinline__ f32x4 bload4_sc1(__amdgpu_buffer_rsrc_t d, int idx) {   // idx < 0: zeros
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(d, idx * 4, 0, 16));
-}
-static __device__ __forceinline__ float bload_sc1(__amdgpu_buffer_rsrc_t d, int idx) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(d, idx * 4, 0, 16));
-}
-// wg2_issue with the operand rows read past the caches (they were handed over inside the launch)
-template <int NT>
-static __device__ __forceinline__ void wg2_issue_sc1(const Wg2Tile& t, int M, int kc, int tid, f32x4 (&va)[Wg2<NT>::NQ],
-                                                     f32x4 (&vb)[Wg2<NT>::NQ]) {
-  const auto dA = rsrc(t.A, (int64_t)M * t.K), dB = rsrc(t.B, (int64_t)M * t.N);
-  const int r0 = 4 * (tid & 7), k0 = kc + (tid >> 3);
-  const bool a4 = (t.K & 3) == 0, b4 = (t.N & 3) == 0;
-#pragma unroll
-  for (int q = 0; q < Wg2<NT>::NQ; ++q) {
-    const int k = k0 + (NT / 8) * q;
-    const int ia = k * t.K + t.i0 + r0, ib = k * t.N + t.j0 + r0;
-    if (a4) va[q] = bload4_sc1(dA, ia);
-    else va[q] = f32x4{bload_sc1(dA, ia), bload_sc1(dA, ia + 1), bload_sc1(dA, ia + 2), bload_sc1(dA, ia + 3)};
-    if (b4) vb[q] = bload4_sc1(dB, ib);
-    else vb[q] = f32x4{bload_sc1(dB, ib), bload_sc1(dB, ib + 1), bload_sc1(dB, ib + 2), bload_sc1(dB, ib + 3)};
-  }
-}
-
-static __device__ __forceinline__ unsigned ts_load(const unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// every wave polls the tile's counter itself (its loads are ordered after its own observation)
-static __device__ __forceinline__ void ts_wait(const unsigned* c, unsigned target, unsigned* tmo) {
-  unsigned spins = 0;
-  while (__builtin_amdgcn_readfirstlane(ts_load(c)) < target) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > TS_SPIN_LIMIT) {
-      __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-  }
-}
-
-template <int NT>
-static __device__ __forceinline__ void ts_tiles(const TrainStep& s, float* As, float* Bs, int* slot, int x) {
-  using C = Wg2<NT>;
-  const TrainWg2& g = s.g;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int E = s.r.E, nrb = s.r.nrb;
-  unsigned* work = s.sync + (E * (NHID + 1) + TS_WORK + x) * TS_STRIDE;
-  unsigned* tmo = s.sync + (E * (NHID + 1) + TS_TMO) * TS_STRIDE;
-  auto ready = [&](const Wg2Tile& t) { return s.sync + (t.e * (NHID + 1) + t.l) * TS_STRIDE; };
-  const int cnt = g.cnt[x];
-  const int32_t* lst = g.list + (int64_t)x * g.per_x;
-  const int M = g.M;
-  const AdamCtx& ad = g.ad;
-  const float b1p = s.r.beta_pow[0], b2p = s.r.beta_pow[1];
-  const float lr_t = s.r.lr * sqrtf(1.f - b2p) / (1.f - b1p);     // train_rows_kernel's block 0 expression
-  const int qd = w & 3, qi = qd >> 1, qj = qd & 1, kq = w >> 2, li = lane & 15, lk = lane >> 4;
-  // the list entries this workgroup runs come from the XCD's work counter, two ahead: the entry after the
-  // next one is requested at the top of each tile and read at the top of the following one
-  if (tid == 0) {
-    slot[0] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    slot[1] = (int)__hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const int i = slot[0];
-  int inx = __builtin_amdgcn_readfirstlane(slot[1]);
-  __syncthreads();
-  if (i >= cnt) return;
-  unsigned pend = 0;
-  if (tid == 0) pend = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  Wg2Tile cur = wg2_tile(g, __builtin_amdgcn_readfirstlane(lst[i]));
-  AdamIn a_in[C::NE], c_in;
-  wg2_adam_in<NT>(ad, cur, tid, a_in, c_in);          // not produced in this launch: ahead of the wait
-  ts_wait(ready(cur), (unsigned)nrb, tmo);
-  tstamp(1);
-  int ntile = 1;
-  f32x4 va[C::NQ], vb[C::NQ];
-  wg2_issue_sc1<NT>(cur, M, 0, tid, va, vb);
-  while (true) {
-    int after = cnt;
-    bool pref = false;
-    Wg2Tile nx = cur;
-    AdamIn a_nx[C::NE], c_nx{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int h = 0; h < C::NE; ++h) a_nx[h] = AdamIn{0.f, 0.f, 0.f, 0.f};
-    f32x4 acc0 = zero4(), acc1 = zero4();
-    float cs = 0.f;
-    for (int kc = 0; kc < M; kc += TW2_KC) {
-      int tt = tid;
-      asm volatile("" : "+v"(tt));
-      {
-        const int r0 = 4 * (tt & 7), k0 = tt >> 3;
-#pragma unroll
-        for (int q = 0; q < C::NQ; ++q)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            As[tw2_at(r0 + u, k0 + (NT / 8) * q)] = va[q][u];
-            Bs[tw2_at(r0 + u, k0 + (NT / 8) * q)] = vb[q][u];
-          }
-      }
-      if (kc == 0 && tid == 0) slot[0] = (int)pend;   // requested a whole tile ago
-      lds_barrier();
-      if (kc == 0) {
-        after = __builtin_amdgcn_readfirstlane(slot[0]);
-        if (tid == 0) pend = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (kc + TW2_KC < M) {
-        wg2_issue_sc1<NT>(cur, M, kc + TW2_KC, tt, va, vb);
-      } else if (inx < cnt) {
-        nx = wg2_tile(g, __builtin_amdgcn_readfirstlane(lst[inx]));
-        wg2_adam_in<NT>(ad, nx, tt, a_nx, c_nx);
-        // the next tile's operand rows only when they are already complete (else after this epilogue)
-        if (__builtin_amdgcn_readfirstlane(ts_load(ready(nx))) >= (unsigned)nrb) {
-          pref = true;
-          wg2_issue_sc1<NT>(nx, M, 0, tt, va, vb);
-        }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < C::KW / 16; ++s2) {
-        const int k = C::KW * kq + (C::KW / 4) * lk + 4 * s2;
-        const f32x4 a4 = ld4(As + tw2_at(16 * qi + li, k)), b4 = ld4(Bs + tw2_at(16 * qj + li, k));
-        acc0 = mfma4(a4[0], b4[0], acc0);
-        acc1 = mfma4(a4[1], b4[1], acc1);
-        acc0 = mfma4(a4[2], b4[2], acc0);
-        acc1 = mfma4(a4[3], b4[3], acc1);
-      }
-      if (cur.cs) {
-        const int crow = tid / C::CT, ck0 = C::CK * (tid % C::CT);
-#pragma unroll
-        for (int v = 0; v < C::CK; v += 4) {
-          const f32x4 x0 = ld4(Bs + tw2_at(crow, ck0 + v));
-          cs += (x0[0] + x0[1]) + (x0[2] + x0[3]);
-        }
-      }
-      lds_barrier();
-    }
-    float* part = As;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) part[kq * 1024 + (16 * qi + 4 * lk + r) * 32 + 16 * qj + li] = acc0[r] + acc1[r];
-    if (cur.cs) {
-#pragma unroll
-      for (int off = C::CT / 2; off > 0; off >>= 1) cs += __shfl_xor(cs, off);
-    }
-    lds_barrier();
-#pragma unroll
-    for (int h = 0; h < C::NE; ++h) {
-      const int e = tid + NT * h;
-      float v = part[e];
-#pragma unroll
-      for (int q = 1; q < C::NKQ; ++q) v += part[1024 * q + e];
-      const int gi = cur.i0 + (e >> 5), gj = cur.j0 + (e & 31);
-      if (gi < cur.K && gj < cur.N)
-        adam_apply(ad, cur.w0 + (int64_t)gi * cur.N + gj, v + cur.wd * a_in[h].p, a_in[h], lr_t);   // fc.py:156-157
-    }
-    {
-      const int cj = cur.j0 + tid / C::CT;
-      if (cur.cs && tid % C::CT == 0 && cj < cur.N) adam_apply(ad, cur.b0 + cj, cs, c_in, lr_t);
-    }
-    if (inx >= cnt) break;
-    ++ntile;
-    if (!pref) {
-      ts_wait(ready(nx), (unsigned)nrb, tmo);
-      wg2_issue_sc1<NT>(nx, M, 0, tid, va, vb);
-    }
-    lds_barrier();                                   // the partials are read before the next panels land
-    cur = nx;
-    inx = after;
-    for (int h = 0; h < C::NE; ++h) a_in[h] = a_nx[h];
-    c_in = c_nx;
-  }
-  tstamp(2);
-  tstamp(3, ntile);
-}
-
-template <int G0, int GH, int GD>
-static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_step_kernel(const TrainStep s) {
-  static_assert(TR_WAVES * 64 == 512, "the tiles run Wg2<512> in the row blocks' workgroup shape");
-  __shared__ __attribute__((aligned(16))) float lds[TR_LDS_FLOATS > 2 * TW2_T * TW2_KP + 64 ? TR_LDS_FLOATS
-                                                                                           : 2 * TW2_T * TW2_KP + 64];
-  const int b = blockIdx.x, E = s.r.E;
-  unsigned* glob = s.sync + E * (NHID + 1) * TS_STRIDE;
-  tstamp(0);
-  if (b == s.nrw) {   // the batch-level tail, right after the row blocks: its loss sums run beside the tiles
-    if (threadIdx.x < 64) {        // every member's row blocks are past their output gradient
-      const int e = threadIdx.x;
-      unsigned spins = 0;
-      while (!__all(e >= E || ts_load(s.sync + (e * (NHID + 1) + NHID) * TS_STRIDE) >= (unsigned)s.r.nrb)) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > TS_SPIN_LIMIT) {
-          if (threadIdx.x == 0) __hip_atomic_store(glob + TS_TMO * TS_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    __syncthreads();
-    tstamp(1);
-    train_loss_tail<TrainTail, true>(s.g.t, lds);
-    tstamp(2);
-    if (threadIdx.x == 0) {   // every other workgroup has read the beta powers and the counters
-      const unsigned others = gridDim.x - 1;
-      unsigned spins = 0;
-      while (ts_load(glob + TS_DONE * TS_STRIDE) < others) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > TS_SPIN_LIMIT) {
-          __hip_atomic_store(glob + TS_TMO * TS_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-      const TrainTail& t = s.g.t;
-      const float b1p = t.beta_pow[0], b2p = t.beta_pow[1];
-      t.beta_pow[2] = t.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-      t.beta_pow[0] = b1p * 0.9f;
-      t.beta_pow[1] = b2p * 0.999f;
-      if (t.bstep_inc) *t.bstep_inc += 1;
-      if (ts_load(glob + TS_TMO * TS_STRIDE)) t.logs[0] = __builtin_nanf("");   // a give-up: poison the loss log
-      for (int c = 0; c < E * (NHID + 1); ++c) s.sync[c * TS_STRIDE] = 0u;
-      for (int c = 0; c < 8; ++c) glob[(TS_WORK + c) * TS_STRIDE] = 0u;
-      glob[TS_DONE * TS_STRIDE] = 0u;
-    }
-    tstamp(3);
-    return;
-  }
-  if (b < s.nrw) {
-    int e, rb;
-    if (tr_block(b, s.r.nrb, E, e, rb)) train_rows_body<G0, GH, GD, true>(s.r, lds, s.sync, e, rb);
-  } else {
-    ts_tiles<512>(s, lds, lds + TW2_T * TW2_KP, reinterpret_cast<int*>(lds + 2 * TW2_T * TW2_KP), b & 7);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(glob + TS_DONE * TS_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // MOPO_TRAIN_WG2 (default 1): the persistent XCD-local weight-gradient launch; 0: train_wgrad_kernel
 int train_wg2() {
   static const int v = [] {
@@ -979,35 +718,8 @@ std::vector<int32_t> make_wlist(int E, int IN, int H, int D, int order, int* per
     total += E * ceil_div(K, TW2_T) * ceil_div(N, TW2_T);
   }
   const int target = ceil_div(total, 8);
-  if (order == 2) {
-    // train_step_kernel: each member's tiles in readiness order (layer NHID .. 0) on its home XCD; an XCD
-    // over the even share hands its EARLIEST-ready tiles to the XCDs under it (the least loaded first), so
-    // XCDs with no member of their own work while the row blocks still run; then every list is ordered by
-    // layer, NHID first (the order the work counter hands them out)
-    for (int e = 0; e < E; ++e)
-      for (int l = NHID; l >= 0; --l) {
-        const int K = l == 0 ? IN : H, N = l == NHID ? 2 * D : H;
-        for (int tm = 0; tm < ceil_div(K, TW2_T); ++tm)
-          for (int tn = 0; tn < ceil_div(N, TW2_T); ++tn) xl[e % 8].push_back(l | (e << 3) | (tm << 7) | (tn << 12));
-      }
-    for (int x = 0; x < 8; ++x)
-      if ((int)xl[x].size() > target) {
-        const int n = (int)xl[x].size() - target;
-        over.insert(over.end(), xl[x].begin(), xl[x].begin() + n);
-        xl[x].erase(xl[x].begin(), xl[x].begin() + n);
-      }
-    std::stable_sort(over.begin(), over.end(), [](int32_t a, int32_t b) { return (a & 7) > (b & 7); });
-    for (int32_t v : over) {
-      int best = 0;
-      for (int x = 1; x < 8; ++x)
-        if (xl[x].size() < xl[best].size()) best = x;
-      xl[best].push_back(v);
-    }
-    for (auto& v : xl) std::stable_sort(v.begin(), v.end(), [](int32_t a, int32_t b) { return (a & 7) > (b & 7); });
-    over.clear();
-  }
   int rr = 0;
-  for (int e = 0; e < E && order != 2; ++e) {
+  for (int e = 0; e < E; ++e) {
     auto& home = xl[e % 8];
     for (int l = NHID; l >= 0; --l) {
       const int K = l == 0 ? IN : H, N = l == NHID ? 2 * D : H;
@@ -1049,11 +761,6 @@ int build_wlist(Train* h) {
   h->wcnt = h->wlist + (size_t)8 * per;
   h->wl_per_x = per;
   MOPO_HIP(hipMemcpy(h->wlist, host.data(), host.size() * 4, hipMemcpyHostToDevice));
-  const std::vector<int32_t> hs = make_wlist(L.E, L.IN, L.H, L.D, 2, &per);
-  if (hipMalloc(&h->wlist_s, hs.size() * 4) != hipSuccess) return fail("bnn train: out of device memory (tile list)");
-  h->wcnt_s = h->wlist_s + (size_t)8 * per;
-  h->wl_per_x_s = per;
-  MOPO_HIP(hipMemcpy(h->wlist_s, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -1072,23 +779,6 @@ int train_wg2_nwx() {
     const char* e = std::getenv("MOPO_TRAIN_WG2_NWX");
     // the resident workgroups: three 512-thread ones per CU (TRAIN_WG2_KC), one 1024-thread one
     return e ? std::max(1, std::atoi(e)) : (train_wg2_nt() == 1024 ? 32 : train_wg2_nt() == 256 ? 192 : 96);
-  }();
-  return v;
-}
-
-// MOPO_TRAIN_STEP1 (default 0): the whole minibatch step as one launch (train_step_kernel); its tile
-// workgroups per XCD: MOPO_TRAIN_STEP_NWX (default 32, one per CU)
-int train_step1() {
-  static const int v = [] {
-    const char* e = std::getenv("MOPO_TRAIN_STEP1");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-int train_step_nwx() {
-  static const int v = [] {
-    const char* e = std::getenv("MOPO_TRAIN_STEP_NWX");
-    return e ? std::max(1, std::atoi(e)) : 32;
   }();
   return v;
 }
@@ -1133,41 +823,6 @@ int step_rows(Train* h, int par, const float* in, const float* tg, const int32_t
   a.lr = h->lr; a.G = h->G; a.ad = ad;
   const int grid = 8 * a.nrb * ceil_div(E, 8);   // train_rows.h tr_block: a member's row blocks on one XCD
   const int g0 = ceil_div(IN, 16), gh = ceil_div(H, 16), gd = ceil_div(D2, 16);
-  if (MOPO_TRAIN_FUSED && train_step1()) {
-    TrainStep st{};
-    st.r = a;
-    st.sync = h->tsync;
-    st.nrw = grid;
-    TrainWg2& g = st.g;
-    g.M = M;
-    g.nwx = train_step_nwx();
-    g.per_x = h->wl_per_x_s;
-    g.list = h->wlist_s;
-    g.cnt = h->wcnt_s;
-    for (int l = 0; l <= NHID; ++l) {
-      g.K[l] = l == 0 ? IN : H;
-      g.N[l] = l == NHID ? D2 : H;
-      g.A[l] = l == 0 ? a.X : h->Hh[l - 1];
-      g.B[l] = l == NHID ? h->dOUT : h->dZ[l];
-      g.W[l] = L.W[l];
-      g.b[l] = L.b[l];
-      g.wd[l] = WDECAY[l];
-    }
-    g.ad = ad;
-    TrainTail& t = g.t;
-    t.E = E; t.nrb = a.nrb; t.D = D; t.lpart = h->lpart; t.mx = L.mx; t.mn = L.mn;
-    t.logs = h->logs; t.beta_pow = h->beta_pow; t.bstep_inc = a.bstep_inc; t.lr = h->lr; t.G = h->G; t.ad = ad;
-    const dim3 sgrid(grid + 8 * g.nwx + 1);
-#define MOPO_TRS(G0, GH, GD)                                                                                 \
-    if (g0 == G0 && gh == GH && gd == GD) {                                                                  \
-      hipLaunchKernelGGL((train_step_kernel<G0, GH, GD>), sgrid, dim3(TR_WAVES * 64), 0, s, st);             \
-      MOPO_HIP(hipGetLastError());                                                                           \
-    } else
-    MOPO_TRS(2, 13, 3) MOPO_TRS(1, 13, 2) MOPO_TRS(1, 2, 2) MOPO_TRS(2, 2, 3) MOPO_TRS(2, 16, 3) MOPO_TRS(1, 16, 2)
-    return fail("bnn train: no row-block instantiation for these widths (use_rows)");
-#undef MOPO_TRS
-    return 0;
-  }
   if (MOPO_TRAIN_FUSED) {
 #define MOPO_TRF(G0, GH, GD)                                                                                 \
     if (g0 == G0 && gh == GH && gd == GD) {                                                                  \
@@ -1279,7 +934,7 @@ int capture(Train* h, int which, const float* in, const float* tg, const int32_t
   int rc = 0;
   for (int i = 0; i < steps && !rc; ++i) {
     if (use_rows(h)) {
-      rc = step_rows(h, i & 1, in, tg, idx, n_idx, true, batch, batch, gs, train_stage(h) && !train_step1());
+      rc = step_rows(h, i & 1, in, tg, idx, n_idx, true, batch, batch, gs, train_stage(h));
     } else {
       rc = launch_gather(h, in, tg, idx, n_idx, true, batch, batch, gs);
       if (!rc) rc = step_impl(h, i & 1, batch, true, gs);
@@ -1321,7 +976,6 @@ extern "C" int mopo_bnn_train_create(mopo_bnn_train_t* out, int E, int obs_dim, 
   f(&h->beta_pow, 3); f(&h->part, 4 * (int64_t)loss_blocks);
   f(&h->lpart, 4 * (int64_t)E * ceil_div(max_batch, 16) * L.D); f(&h->logs, 4); f(&h->mu, L.IN); f(&h->sigma, L.IN);
   reg.push_back({(void**)&h->bstep, 4});
-  reg.push_back({(void**)&h->tsync, (size_t)(E * (NHID + 1) + TS_GLOBAL) * TS_STRIDE * 4});   // zeroed below
   reg.push_back({(void**)&h->ticket, 4});
   f(&h->X, E * mM * L.IN); f(&h->T, E * mM * L.D); f(&h->X2, E * max_batch * L.IN); f(&h->T2, E * max_batch * L.D); f(&h->OUT, E * mM * 2 * L.D); f(&h->dOUT, E * mM * 2 * L.D);
   for (int l = 0; l < NHID; ++l) { f(&h->Z[l], E * mM * L.H); f(&h->Hh[l], E * mM * L.H); f(&h->dZ[l], E * mM * L.H); }
@@ -1345,9 +999,6 @@ static int tile_lists(int E, int obs_dim, int act_dim, int hidden, int order, in
 extern "C" int mopo_bnn_train_tile_lists(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap) {
   return tile_lists(E, obs_dim, act_dim, hidden, 0, out, cap);
 }
-extern "C" int mopo_bnn_train_tile_lists_step(int E, int obs_dim, int act_dim, int hidden, int32_t* out, int64_t cap) {
-  return tile_lists(E, obs_dim, act_dim, hidden, 2, out, cap);
-}
 static int tile_lists(int E, int obs_dim, int act_dim, int hidden, int order, int32_t* out, int64_t cap) {
   MOPO_REQUIRE(E >= 1 && E <= 16 && obs_dim >= 1 && act_dim >= 1 && hidden >= 1 && obs_dim + 1 <= 64,
                "mopo_bnn_train_tile_lists: bad dims");
@@ -1364,9 +1015,8 @@ static int tile_lists(int E, int obs_dim, int act_dim, int hidden, int order, in
   return per;
 }
 
-// Diagnostic builds only (MOPO_TRAIN_STAMPS=1; otherwise -1): the single-launch step's per-workgroup stamps
-// of the last step ([block][8]: rows 0 start, 1..5 the hand-offs l = NHID .. 0; tiles 0 start, 1 first
-// wait done, 2 end, 3 tiles done; the tail 0 start, 1 rows ready, 2 loss tail done, 3 end), 100 MHz clock
+// Diagnostic builds only (MOPO_TRAIN_STAMPS=1; otherwise -1): the rows launch's per-workgroup phase stamps
+// of the last step ([block][8]: 0 start, 1 gathered, 2 layer 0, 3 forward, 4 loss, 5 / 6 / 7 backward), 100 MHz clock
 extern "C" int mopo_bnn_train_debug_stamps(uint64_t* h_out, int64_t n) {
 #if MOPO_TRAIN_STAMPS
   MOPO_REQUIRE(h_out && n >= 0 && n <= 2048 * 8, "mopo_bnn_train_debug_stamps: bad output");
@@ -1390,7 +1040,6 @@ extern "C" int mopo_bnn_train_destroy(mopo_bnn_train_t hh) {
   if (h->gs) (void)hipStreamDestroy(h->gs);
   if (h->sort_keys) (void)hipFree(h->sort_keys);  // one allocation (keys | values | offsets | temp)
   if (h->wlist) (void)hipFree(h->wlist);
-  if (h->wlist_s) (void)hipFree(h->wlist_s);
   if (h->mem) (void)hipFree(h->mem);
   delete h;
   return 0;
@@ -1515,7 +1164,7 @@ extern "C" int mopo_bnn_train_epoch(mopo_bnn_train_t hh, const float* d_in, cons
       h->gkey[0] = d_in; h->gkey[1] = d_tg; h->gkey[2] = d_idxs; h->gkey_n = n_idx; h->gkey_b = batch;
     }
     // staged steps: the epoch's first minibatch is gathered here, every later one by the step before it
-    if (use_rows(h) && train_stage(h) && !train_step1() && launch_gather(h, d_in, d_tg, d_idxs, n_idx, true, batch, batch, gs))
+    if (use_rows(h) && train_stage(h) && launch_gather(h, d_in, d_tg, d_idxs, n_idx, true, batch, batch, gs))
       return -1;
     int64_t i = 0;
     for (; i + TRAIN_GRAPH_STEPS <= nfull; i += TRAIN_GRAPH_STEPS) MOPO_HIP(hipGraphLaunch(h->gexec[0], gs));

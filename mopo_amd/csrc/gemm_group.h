@@ -121,8 +121,16 @@ static __device__ __forceinline__ AdamIn adam_load(const AdamCtx& ad, int64_t i)
 
 // TF1 Adam (m += (g - m)(1 - b1), v += (g^2 - v)(1 - b2), p -= lr_t m / (sqrt(v) + eps)) + Polyak.
 // Returns the new parameter; *t_new (when given) the new target, or the old one where it did not move.
+// hold: the step's operands are not trusted (a fused SAC launch gave up waiting on a hand-off, sac_rows.h
+// handoff_wait): the parameter carries over unchanged into the other ping-pong copy, the moments and the target
+// stay, so a give-up never applies an update computed from stale data.
 static __device__ __forceinline__ float adam_apply(const AdamCtx& ad, int64_t i, float g, AdamIn a, float lr_t,
-                                                   float* t_new = nullptr) {
+                                                   float* t_new = nullptr, bool hold = false) {
+  if (hold) {
+    ad.Pn[i] = a.p;
+    if (t_new) *t_new = a.t;
+    return a.p;
+  }
   const float m = a.m + (g - a.m) * (1.f - 0.9f);
   const float v = a.v + (g * g - a.v) * (1.f - 0.999f);
   const float p = a.p - (m * lr_t) / (sqrtf(v) + 1e-8f);

@@ -272,22 +272,54 @@ __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, con
 }
 
 // ---- split-bf16 variant: f32 operands as P bf16 parts (x = x0 + x1 [+ x2]) ---------------------
-// Part p of a value is its residual after parts 0..p-1, truncated to bf16 (the last part rounded),
-// so P = 3 carries 8 + 8 + 8 significand bits plus the rounding of the last: f32-accurate.  The
-// layer runs the products W_p x X_q with p + q < P (P = 2: 3 MFMAs, P = 3: 6 MFMAs per k-group
-// and block) on v_mfma_f32_16x16x32_bf16 with f32 accumulate.  Weight fragments are packed
-// [kg][p][nb] (pack_frags_bf16_kernel with P parts), so the pipeline streams KG * P slices of NB
-// fragments through the same double-buffered LDS slot as the bf16 layer: slice (kg, p) feeds the
-// (P - p) activation parts of k-group kg.
+// Part p of a value is the round-to-nearest-even bf16 of its residual after parts 0..p-1 (each residual is
+// exact in f32).  P = 3 is an EXACT split: x0 + x1 + x2 == x for every f32 with 2^-100 <= |x| < 2^127 (and
+// x = 0): x0 takes the top 8 significand bits, the residual x - x0 is a multiple of ulp(x) of at most 2^15
+// ulps, x1 takes its top 8 bits, and what is left is a multiple of ulp(x) of at most 2^7 ulps -- 8 bits, so
+// x2 holds it exactly (above 2^-100 every part is a normal bf16).  The layer runs the products W_p x X_q
+// with p + q < P (P = 2: 3 MFMAs, P = 3: 6 MFMAs per k-group and block) on v_mfma_f32_16x16x32_bf16 with f32
+// accumulate; the three dropped products x1 w2 + x2 w1 + x2 w2 are <= (2^-24 + 2^-24 + 2^-32) |x w| with
+// RN parts (|x1| <= 2^-8 |x|, |x2| <= 2^-16 |x|), under f32's own rounding of the sums.  Weight fragments
+// are packed [kg][p][nb] (pack_frags_bf16_kernel with P parts), so the pipeline streams KG * P slices of NB
+// fragments through the same LDS slots as the bf16 layer: slice (kg, p) feeds the (P - p) activation parts
+// of k-group kg.  (tests/test_split.py holds the CPU restatement of this split to the exactness claim.)
+__device__ __forceinline__ float from_bf16(short s) { return __builtin_bit_cast(float, (uint32_t)(uint16_t)s << 16); }
 template <int P>
 __device__ __forceinline__ void split_bf16(float v, short (&out)[P]) {
   float r = v;
 #pragma unroll
   for (int p = 0; p < P; ++p) {
-    const uint32_t u = __builtin_bit_cast(uint32_t, r);
-    const short s = p + 1 < P ? (short)(u >> 16) : to_bf16(r);
+    const short s = to_bf16(r);
     out[p] = s;
-    if (p + 1 < P) r -= __builtin_bit_cast(float, (uint32_t)(uint16_t)s << 16);
+    if (p + 1 < P) r -= from_bf16(s);
+  }
+}
+// two values at once into whole dwords (part p of a in the low half, of b in the high half): v_cvt_pk_bf16_f32
+// rounds to nearest even; each residual is ONE v_dot2_f32_bf16 -- a + (-1) * part_lo + 0 * part_hi (b: the
+// halves swapped) -- whose exact result (the bf16 x bf16 products are exact, the sum is representable) is what
+// the shift / mask + subtract pair computed, at half the VALU issue
+#ifndef MOPO_SPLIT_DOT2
+#define MOPO_SPLIT_DOT2 1
+#endif
+template <int P>
+__device__ __forceinline__ void split_bf16_pair(float a, float b, uint32_t (&out)[P]) {
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    uint32_t h;
+    asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(h) : "v"(a), "v"(b));
+    out[p] = h;
+    if (p + 1 < P) {
+      if (MOPO_SPLIT_DOT2) {
+        float ra, rb;
+        asm volatile("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(ra) : "v"(h), "s"(0x0000BF80u), "v"(a));
+        asm volatile("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(rb) : "v"(h), "s"(0xBF800000u), "v"(b));
+        a = ra;
+        b = rb;
+      } else {
+        a -= __builtin_bit_cast(float, h << 16);
+        b -= __builtin_bit_cast(float, h & 0xffff0000u);
+      }
+    }
   }
 }
 

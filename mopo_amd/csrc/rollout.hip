@@ -377,25 +377,6 @@ static int split_parts() {  // MOPO_ROLLOUT_SPLIT=<parts> (0 or 1: one stream); 
   return v;
 }
 
-// MOPO_ROLLOUT_PRIO=1 (A/B): parts 1.. of the split on the greatest-priority stream
-static int split_prio() {
-  static const int v = [] {
-    const char* e = std::getenv("MOPO_ROLLOUT_PRIO");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
-// MOPO_ROLLOUT_PART0=<permille> (A/B): part 0's share of the rows in a 2-part split (default 500)
-static int split_part0_permille() {
-  static const int v = [] {
-    const char* e = std::getenv("MOPO_ROLLOUT_PART0");
-    const int n = e ? std::atoi(e) : 500;
-    return n < 100 ? 100 : (n > 900 ? 900 : n);
-  }();
-  return v;
-}
-
 // Horizon steps [i0, i1) of one rollout.  i0 == 0 draws the start states and repacks the policy;
 // later ranges continue from the state the previous call left (obs ping-pong, live counts).  Staged
 // rows of step i go to rows (i - i0) * B of the staging descriptor.
@@ -432,7 +413,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
   const int nsplit = !compact && !h->profile && a->horizon > 1 ? std::min<int>(split_parts(), (int)(B / 2048)) : 1;
   const bool split = nsplit > 1;
   const int64_t bpart = !split ? B
-                       : nsplit == 2 ? (B * split_part0_permille() / 1000 + 63) / 64 * 64 : (B / nsplit + 63) / 64 * 64;
+                       : (B / nsplit + 63) / 64 * 64;   // equal parts (unequal halves measured slower)
   if (i0 == 0) {
     h->oc = 0;
     h->uc = 0;
@@ -529,13 +510,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
   if (split) {
     for (int k = 1; k < nsplit; ++k)
       if (!h->sp[k]) {
-        if (split_prio()) {   // A/B: the later part's chain on the greatest-priority stream
-          int least = 0, greatest = 0;
-          MOPO_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-          MOPO_HIP(hipStreamCreateWithPriority(&h->sp[k], hipStreamNonBlocking, greatest));
-        } else {
-          MOPO_HIP(hipStreamCreateWithFlags(&h->sp[k], hipStreamNonBlocking));
-        }
+        MOPO_HIP(hipStreamCreateWithFlags(&h->sp[k], hipStreamNonBlocking));
         MOPO_HIP(hipEventCreateWithFlags(&h->ev_fork[k], hipEventDisableTiming));
         MOPO_HIP(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
       }

@@ -77,8 +77,7 @@ struct Sac {
   uint64_t* stamps = nullptr;     // MOPO_SAC_STAMPS builds: [slot][block][8]
   unsigned* sync = nullptr;       // fused F2 + B1 launch: [nrb][2] row-block counters, then the timeout word
                                   //   (each on its own 128-B line: sac_rows.h SYNC_STRIDE)
-  int fuse = 2;                   // 0: F1, F2, B1 separate; 1: F2 + B1 one launch; 2: F1 + F2 + B1 one launch;
-                                  // 3: the whole step (+ the weight gradients and the loss tail) one launch
+  int fuse = 2;                   // 0: F1, F2, B1 separate; 1: F2 + B1 one launch; 2: F1 + F2 + B1 one launch
   float *dhead, *dh2p, *dh1p;
   // graph
   bool use_graph = true;
@@ -170,14 +169,14 @@ static int launch_gather(Sac* h, int par, const mopo_pool_desc* env, const mopo_
 // Pb[1 - par].  With `prefetch`, B1 also gathers the next step's batch into bt[1 - par] (a separate
 // gather launch, or a forked graph branch, costs more than it hides).
 #ifndef MOPO_SAC_FUSE
-#define MOPO_SAC_FUSE 2   // 0: F1, F2, B1 as three launches; 1: F2 + B1 fused; 2: F1 + F2 + B1 fused; 3: the
-                          // whole step as one launch (the environment variable MOPO_SAC_FUSE overrides it at
-                          // mopo_sac_create; 3 needs batch <= 256, else 2)
+#define MOPO_SAC_FUSE 2   // 0: F1, F2, B1 as three launches; 1: F2 + B1 fused; 2: F1 + F2 + B1 fused (the
+                          // environment variable MOPO_SAC_FUSE overrides it at mopo_sac_create: the separate
+                          // launches are the fused form's bit-identical cross-check in tests/test_gpu_sac.py)
 #endif
 static int sac_fuse_default() {
   const char* e = std::getenv("MOPO_SAC_FUSE");
   const int v = e ? std::atoi(e) : MOPO_SAC_FUSE;
-  return v < 0 ? 0 : v > 3 ? 3 : v;
+  return v < 0 ? 0 : v > 2 ? 2 : v;
 }
 
 static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_pool_desc* mod, uint64_t seed,
@@ -298,9 +297,7 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     if (ncq1 * nrb < 2 && prefetch) return fail("sac: B1 needs at least one gather block");
     static_assert(B1_COLS == RB_COLS && B1_WAVES == 4, "the fused launches share the F1 / F2 grid");
     f2.st = Stamps{h->stamps, h->fuse >= 2 ? 0 : 1};
-    if (h->fuse == 3) {
-      // the single-launch step: launched below, with the weight-gradient blocks
-    } else if (h->fuse == 2) {
+    if (h->fuse == 2) {
       hipLaunchKernelGGL(sac_f12b1_kernel, dim3(ncq, nrb, 12), dim3(256), 0, s, f1, f2, d);
     } else if (h->fuse == 1) {
       hipLaunchKernelGGL(sac_f2b1_kernel, dim3(ncq, nrb, 8), dim3(256), 0, s, f2, d);
@@ -344,15 +341,10 @@ static int sac_step_impl(Sac* h, int par, const mopo_pool_desc* env, const mopo_
     g.prior = h->prior; g.eps_s = h->eps_s;
     g.sync_tmo = h->fuse ? h->sync + (SYNC_N * nrb + SYNC_TMO) * SYNC_STRIDE : nullptr;
     if (h->fuse == 2) { g.sync_reset = h->sync; g.n_sync = SYNC_N * nrb; }
-    g.st = Stamps{h->stamps, h->fuse == 3 ? 0 : 3};
+    g.st = Stamps{h->stamps, 3};
     if (tot > h->nslots_cap) return fail("sac: grad-norm slots exceed the allocation");
     h->nslots = tot;
-    if (h->fuse == 3) {
-      const int zb2 = ceil_div(1 + tot, ncq * nrb);
-      hipLaunchKernelGGL(sac_step_kernel, dim3(ncq, nrb, 12 + zb2), dim3(256), 0, s, f1, f2, b1a, g);
-    } else {
-      hipLaunchKernelGGL(sac_wgrad_kernel, dim3(1 + tot), dim3(1024), 0, s, g);
-    }
+    hipLaunchKernelGGL(sac_wgrad_kernel, dim3(1 + tot), dim3(1024), 0, s, g);
     MOPO_HIP(hipGetLastError());
   }
   return 0;
@@ -408,7 +400,6 @@ extern "C" int mopo_sac_create(mopo_sac_t* out, int O, int A, int H, int batch, 
   f(&h->logp_s, 2 * ns); f(&h->logp_n, 2 * ns); f(&h->eps_s, ns * EPW); f(&h->eps_n, ns * EPW);
   reg.push_back({(void**)&h->sync, (size_t)(SYNC_N * (ns / 16) + SYNC_GLOBAL) * SYNC_STRIDE * 4});
   h->fuse = sac_fuse_default();
-  if (h->fuse == 3 && batch > WG_KC) h->fuse = 2;   // the single-launch tiles stage one K chunk
   for (int i = 0; i < 4; ++i) { f(&h->dq[i], n); f(&h->dh1[i], n * H); }
   f(&h->dhead, n * 2 * A); f(&h->dh2p, n * H); f(&h->dh1p, n * H);
   size_t total = 0;
@@ -485,6 +476,32 @@ extern "C" int mopo_sac_set_graph(mopo_sac_t hh, int enable) {
   Sac* h = reinterpret_cast<Sac*>(hh);
   MOPO_REQUIRE(h, "mopo_sac_set_graph: NULL handle");
   h->use_graph = enable != 0;
+  return 0;
+}
+
+extern "C" int mopo_sac_check(mopo_sac_t hh, int* timed_out) {
+  Sac* h = reinterpret_cast<Sac*>(hh);
+  MOPO_REQUIRE(h && timed_out, "mopo_sac_check: NULL argument");
+  MOPO_HIP(hipDeviceSynchronize());
+  unsigned* w = h->sync + (SYNC_N * ceil_div(h->d.n, 16) + SYNC_TMO) * SYNC_STRIDE;
+  unsigned v = 0;
+  MOPO_HIP(hipMemcpy(&v, w, 4, hipMemcpyDeviceToHost));
+  *timed_out = v != 0;
+  if (v) {
+    MOPO_HIP(hipMemset(w, 0, 4));
+    MOPO_HIP(hipDeviceSynchronize());
+    return fail("sac: an in-launch hand-off wait of the fused step timed out; the parameter, Adam and target "
+                "updates of the steps since then were held (not applied) and their logs are NaN");
+  }
+  return 0;
+}
+
+extern "C" int mopo_sac_inject_timeout(mopo_sac_t hh) {
+  Sac* h = reinterpret_cast<Sac*>(hh);
+  MOPO_REQUIRE(h, "mopo_sac_inject_timeout: NULL handle");
+  MOPO_HIP(hipDeviceSynchronize());
+  const unsigned one = 1;
+  MOPO_HIP(hipMemcpy(h->sync + (SYNC_N * ceil_div(h->d.n, 16) + SYNC_TMO) * SYNC_STRIDE, &one, 4, hipMemcpyHostToDevice));
   return 0;
 }
 

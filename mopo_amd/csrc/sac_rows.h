@@ -133,9 +133,9 @@ constexpr bool B1_LATE = MOPO_SAC_B1_LATE != 0;
 // F1 blocks: pi(s), pi(s'), Q(s, a); F2: main / target critics; B1: step control + gather, critic dh1, policy rows
 enum { SYNC_PI_S = 0, SYNC_PI_N = 1, SYNC_Q_SA = 2, SYNC_F2_MAIN = 3, SYNC_F2_TGT = 4, SYNC_B1_CTL = 5, SYNC_B1_Q = 6,
        SYNC_B1_PI = 7, SYNC_N = 8 };
-// global words after the per-row-block counters (x SYNC_STRIDE): the sticky timeout word, then the single-launch
-// step's count of finished weight-gradient tiles
-enum { SYNC_TMO = 0, SYNC_B2_DONE = 1, SYNC_GLOBAL = 2 };
+// global words after the per-row-block counters (x SYNC_STRIDE): the sticky timeout word (set by a give-up, read
+// and cleared by the host: mopo_sac_check)
+enum { SYNC_TMO = 0, SYNC_GLOBAL = 1 };
 static __device__ __forceinline__ unsigned* sync_at(unsigned* sync, int rb, int c) {
   return sync + (SYNC_N * rb + c) * SYNC_STRIDE;
 }
@@ -165,41 +165,6 @@ static __device__ __forceinline__ void handoff_wait_rows(unsigned* sync, int nrb
     }
 #if MOPO_SAC_FUSE_ACQ
     if (r == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-#endif
-  }
-  __syncthreads();
-}
-
-// wave 0 polls two classes of every row block (lane r: row block r; nrb <= 64) and, when ctl_target > 0, the
-// step-control counter of row block 0, with a long sleep between polls (for blocks that expect to wait long);
-// ONE acquire when all are done (acq = false: none -- the caller reads nothing the producers wrote)
-static __device__ __forceinline__ void handoff_wait_all(unsigned* sync, int nrb, int c1, unsigned t1, int c2,
-                                                        unsigned t2, unsigned ctl_target, unsigned* tmo, bool acq) {
-  if (threadIdx.x < 64) {
-    const int r = threadIdx.x;
-    unsigned spins = 0;
-    while (true) {
-      bool ok = true;
-      if (r < nrb) {
-        ok = __hip_atomic_load(sync + (SYNC_N * r + c1) * SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= t1 &&
-             (t2 == 0u || __hip_atomic_load(sync + (SYNC_N * r + c2) * SYNC_STRIDE, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT) >= t2);
-        if (r == 0 && ctl_target)
-          ok = ok && __hip_atomic_load(sync + SYNC_B1_CTL * SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                         ctl_target;
-      }
-      if (__all(ok)) break;
-      __builtin_amdgcn_s_sleep(8);
-      if (++spins > SAC_SPIN_LIMIT) {
-        if (r == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-#if MOPO_SAC_FUSE_ACQ
-    if (r == 0 && acq) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -389,8 +354,8 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
       dls = -g + dstd * sd;
       if (!(raw >= -20.f && raw <= 2.f)) dls = 0.f;                 // clip_by_value grad
       if (cq == 0) {
-        hstore<FZ == 3>(&c.dhead[(int64_t)hrow * 2 * A + hj], dmu);
-        hstore<FZ == 3>(&c.dhead[(int64_t)hrow * 2 * A + A + hj], dls);
+        hstore<false>(&c.dhead[(int64_t)hrow * 2 * A + hj], dmu);
+        hstore<false>(&c.dhead[(int64_t)hrow * 2 * A + A + hj], dls);
       }
     }
     dmu_s[tid] = dmu;
@@ -417,7 +382,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
           const int row = 4 * lk + i;
           const float v = h2v[q][i] > 0.f ? d[i] : 0.f;
           S[row * HS + c2] = v;
-          if (cq == 0 && r0 + row < n) hstore<FZ == 3>(&c.dh2p[(int64_t)(r0 + row) * H + c2], v);
+          if (cq == 0 && r0 + row < n) hstore<false>(&c.dh2p[(int64_t)(r0 + row) * H + c2], v);
         }
       }
     }
@@ -439,7 +404,7 @@ static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, in
     const int row = r0 + 4 * lk + i;                                // D: col li, row 4 lk + i
     if (row < n && col < H) {
       const float v = acc[0][i] + acc[1][i] + acc[2][i] + acc[3][i];
-      hstore<FZ == 3>(&c.dh1p[(int64_t)row * H + col], m1[i] > 0.f ? v : 0.f);
+      hstore<false>(&c.dh1p[(int64_t)row * H + col], m1[i] > 0.f ? v : 0.f);
     }
   }
 }
@@ -996,17 +961,16 @@ struct Dh1Args {
 // shares it: identical step counts), the beta powers of the next step, and whether this step's timestep
 // moves the targets (mopo.py:780-799, 843-845: n_train_repeat steps share one timestep).  The step counter
 // itself advances in the loss tail of the next launch (sac_wgrad.h), after every reader of this step's.
-template <bool SC>
 static __device__ __forceinline__ void step_control(const Dh1Args& a) {
   if (threadIdx.x != 0) return;
   const float b1p = a.beta_pow[0], b2p = a.beta_pow[1];
   const int64_t it = *a.iter, base = a.tctl[0];
   const int64_t rep = a.tctl[1] > 0 ? a.tctl[1] : 1, every = a.tctl[2] > 0 ? a.tctl[2] : 1;
-  hstore<SC>(&a.beta_pow[2], a.lr * sqrtf(1.f - b2p) / (1.f - b1p));   // TF1 Adam step size
+  hstore<false>(&a.beta_pow[2], a.lr * sqrtf(1.f - b2p) / (1.f - b1p));   // TF1 Adam step size
   a.beta_pow[0] = b1p * 0.9f;
   a.beta_pow[1] = b2p * 0.999f;
   const int64_t ts = (it - base) / rep;
-  hstore<SC>(&a.beta_pow[3], ((ts % every) + every) % every == 0 ? 1.f : 0.f);
+  hstore<false>(&a.beta_pow[3], ((ts % every) + every) % every == 0 ? 1.f : 0.f);
 }
 
 // LDS of one B1 workgroup
@@ -1031,19 +995,17 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args a, int x, int y, 
   if (z == 0) {
     const int zb = x + a.ncq1 * y;
     if (zb == 0) {
-      step_control<FZ == 3>(a);
+      step_control(a);
     } else if (a.gather) {
       const GatherArgs& g = a.ga;
       const int C = 2 * g.O + g.A + 2, tot = g.n * C, stride = (a.ncq1 * a.nrb - 1) * (int)blockDim.x;
       for (int e = (zb - 1) * blockDim.x + tid; e < tot; e += stride) gather_elem(g, e / C, e % C);
     }
-    if constexpr (FZ == 3) handoff_signal(sync_at(a.sync, y, SYNC_B1_CTL));   // read iter / wrote lr_t
     stamp(a.st, 4);
     return;
   }
   if (z == 3) {                       // the policy-row blocks: the action-gradient partials came from F2
     policy_rows_block<FZ>(a.pr, y * a.ncq1 + x, As, Ts, a.st, a.sync, a.nrb);
-    if constexpr (FZ == 3) handoff_signal(sync_at(a.sync, y, SYNC_B1_PI));
     stamp(a.st, 4);
     return;
   }
@@ -1112,7 +1074,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args a, int x, int y, 
     if (i0 + tid < n) {
       const RowQ rq = row_losses(a.L, rin);
       dq = ((p.kind == 0 ? rq.q[0] : rq.q[1]) - rq.y) * (1.f / (float)n);
-      if (cq == 0) hstore<FZ == 3>(&p.dq[i0 + tid], dq);
+      if (cq == 0) hstore<false>(&p.dq[i0 + tid], dq);
     }
     dqs[tid] = dq;
   }
@@ -1141,9 +1103,8 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args a, int x, int y, 
   for (int rr = 0; rr < 4; ++rr) {
     const int orow = i0 + 4 * lk + rr;
     const float v = (col < H && orow < n && m1[rr] > 0.f) ? acc[0][rr] + acc[1][rr] + acc[2][rr] + acc[3][rr] : 0.f;
-    if (orow < n && col < H) hstore<FZ == 3>(&p.dh1[(int64_t)orow * H + col], v);
+    if (orow < n && col < H) hstore<false>(&p.dh1[(int64_t)orow * H + col], v);
   }
-  if constexpr (FZ == 3) handoff_signal(sync_at(a.sync, rb, SYNC_B1_Q));
   stamp(a.st, 4);
 }
 

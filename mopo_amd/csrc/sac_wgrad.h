@@ -129,9 +129,10 @@ static __device__ __forceinline__ void wgrad_loss_tail(const WgradArgs& a, float
   const float m1 = red[2] / fn, m2 = red[3] / fn, mlp = red[4] / fn, ment = red[5] / fn;
   const float pil = red[6] / fn;                                      // mopo.py:371-377
   const float ga = -(mlp + a.tent);                                   // d/dlog_alpha of -mean(la*(logp+H))
-  if (a.sync_tmo && *a.sync_tmo) {    // a fused launch gave up waiting (sac_rows.h handoff_wait): poison the logs
-    const float nan = __builtin_nanf("");
-    for (int i = 0; i < LOG_N; ++i) a.logs[i] = nan;
+  if (a.sync_tmo && *a.sync_tmo) {    // a fused launch gave up waiting (sac_rows.h handoff_wait): poison the logs,
+    const float nan = __builtin_nanf("");   // hold log_alpha (as the tiles hold every parameter); the host's
+    for (int i = 0; i < LOG_N; ++i) a.logs[i] = nan;   // mopo_sac_check reports it and clears the word
+    adam_apply(ad, ad.total, ga, al, lr_t, nullptr, true);
     *a.iter += 1;
     return;
   }
@@ -179,6 +180,7 @@ static __global__ __launch_bounds__(1024, 1) void sac_wgrad_kernel(const WgradAr
   AdamIn c_in{0.f, 0.f, 0.f, 0.f};
   if (c_on) c_in = adam_load(ad, c_idx);
   const float lr_t = *ad.lr_t;
+  const bool hold = g.sync_tmo && *g.sync_tmo;   // a give-up in the fused launch: no update from stale operands
   asm volatile("" : "+v"(a_in.p), "+v"(a_in.m), "+v"(a_in.v), "+v"(a_in.t));
   const int qd = w & 3, qi = qd >> 1, qj = qd & 1, kq = w >> 2;
   const int li = lane & 15, lk = lane >> 4;
@@ -242,13 +244,13 @@ static __global__ __launch_bounds__(1024, 1) void sac_wgrad_kernel(const WgradAr
     const float v = (part[tid] + part[1024 + tid]) + (part[2048 + tid] + part[3072 + tid]);
     if (e_on) {
       p.C[(int64_t)gi * p.ldc + gj] = v;
-      adam_apply(ad, a_idx, v, a_in, lr_t);
+      adam_apply(ad, a_idx, v, a_in, lr_t, nullptr, hold);
       gsq = v * v;
     }
   }
   if (c_on) {
     p.colsum[j0 + cj] = cs;
-    adam_apply(ad, c_idx, cs, c_in, lr_t);
+    adam_apply(ad, c_idx, cs, c_in, lr_t, nullptr, hold);
     gsq += cs * cs;
   }
   if (ad.norm_part) {  // per-block squared-gradient partial (grad-norm logs; summed by sac_logs_kernel)
@@ -266,310 +268,6 @@ static __global__ __launch_bounds__(1024, 1) void sac_wgrad_kernel(const WgradAr
     }
   }
   stamp(g.st, 4);
-}
-
-// ---- the single-launch SAC step (MOPO_SAC_FUSE=3, sac_step_kernel): the weight-gradient tiles and the loss
-// tail as 4-wave workgroups of the same launch as F1, F2 and B1.  A tile computes exactly sac_wgrad_kernel's
-// arithmetic -- the same MFMA sequence into the same accumulator chains (wave w's K quarter of the 16-wave
-// tile becomes accumulator pair kq of the quadrant's wave), the same K-quarter association, the same column-sum
-// tree -- so its results are bit-identical (tests/test_gpu_sac.py::test_sac_fused_launches_bit_identical_...).
-// Its A panel (F1's activations or the batch) is staged in LDS once F1 is done for every row block; the B
-// operand (B1's gradients, or a critic's rank-1 masked dh2) goes straight into registers, one K quarter at a
-// time, once B1 is done; the Adam state of its outputs is loaded at the start.  n <= WG_KC.
-struct Wg4Lds {
-  float As[WG_TILE * WG_KP];         // A panel [i][k]
-  float csl[WG_TILE][33];            // the 32 k-slice sums of each column (tile-row 0 of a problem with a bias)
-  float red[8];
-};
-
-static __device__ __forceinline__ void wgrad_tile4(const WgradArgs g, int bid, Wg4Lds& L, unsigned* sync, int nrb,
-                                                   int ncq) {
-  unsigned* tmo = sync + (SYNC_N * nrb + SYNC_TMO) * SYNC_STRIDE;
-  stamp(g.st, 0);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int pi = 0;
-  while (pi + 1 < g.np && bid >= g.prefix[pi + 1]) ++pi;
-  const WgProb& p = g.p[pi];
-  const int t = bid - g.prefix[pi];
-  const int tn_cnt = ceil_div(p.N, WG_TILE);
-  const int tm = t / tn_cnt, tn = t % tn_cnt;
-  const int i0 = tm * WG_TILE, j0 = tn * WG_TILE;
-  const int n = g.n;
-  const bool do_cs = p.colsum && tm == 0;
-  const int qi = w >> 1, qj = w & 1, li = lane & 15, lk = lane >> 4;
-  const AdamCtx& ad = g.ad;
-  // ---- the Adam state of this lane's outputs first: rows 16 qi + 4 lk + r, column 16 qj + li of the tile
-  const int gj = j0 + 16 * qj + li;
-  AdamIn ain[4];
-  int64_t aidx[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int gi = i0 + 16 * qi + 4 * lk + r;
-    aidx[r] = (int64_t)(p.C - ad.G) + (int64_t)min(gi, p.M - 1) * p.ldc + min(gj, p.N - 1);
-    ain[r] = adam_load(ad, aidx[r]);
-  }
-  const bool c_on = do_cs && qi == 0 && lk == 0 && gj < p.N;        // the bias gradient of column gj
-  const int64_t c_idx = p.colsum ? (int64_t)(p.colsum - ad.G) + min(gj, p.N - 1) : 0;
-  AdamIn c_in{0.f, 0.f, 0.f, 0.f};
-  if (c_on) c_in = adam_load(ad, c_idx);
-  // ---- B1 done for every row block (so F1 and F2 too: B1's blocks waited on them) and the step control
-  //      (lr_t, the target flag): ONE acquire, then the A panel (element e = tid + 256 q: row e % 32, k e / 32)
-  stamp(g.st, 5);
-  handoff_wait_all(sync, nrb, p.cls ? SYNC_B1_PI : SYNC_B1_Q, p.cls ? (unsigned)ncq : 2u * (unsigned)ncq,
-                   p.cls ? SYNC_B1_Q : SYNC_B1_PI, 0u, (unsigned)ncq, tmo, true);
-  stamp(g.st, 6);
-  const auto dA = rsrc(p.A, (int64_t)(n - 1) * p.lda + p.M);
-  const float lr_t = *ad.lr_t;
-  const bool r1 = p.bu != nullptr;
-  const auto dB = rsrc(r1 ? p.bm : p.B, (int64_t)(n - 1) * (r1 ? p.bldm : p.ldb) + p.N);
-  const auto dU = rsrc(p.bu, r1 ? n : 0);
-  const float bv = r1 ? bload(rsrc(p.bv, p.N), gj) : 0.f;
-  // B of K quarters kq0, kq0 + 1 straight into registers (a rank-1 masked B: the mask operand and dq, both
-  // loaded unconditionally so no load waits on another)
-  float vb[2][4][4], vu[2][4][4];
-  auto load_b = [&](int kq0) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int k = 64 * (kq0 + h) + 16 * lk + 4 * s2 + u;
-          vb[h][s2][u] = bload(dB, k * (r1 ? p.bldm : p.ldb) + gj);
-          vu[h][s2][u] = r1 ? bload(dU, k) : 0.f;
-        }
-  };
-  load_b(0);
-  {
-    float va[32];
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      const int e = tid + 256 * q;
-      va[q] = bload(dA, (e >> 5) * p.lda + i0 + (e & 31));
-    }
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      const int e = tid + 256 * q;
-      L.As[(e & 31) * WG_KP + (e >> 5)] = va[q];
-    }
-  }
-  lds_barrier();
-  f32x4 acc0[4], acc1[4];
-#pragma unroll
-  for (int kq = 0; kq < 4; ++kq) {
-    if (kq == 2) load_b(2);
-    const int h = kq & 1;
-    acc0[kq] = zero4();
-    acc1[kq] = zero4();
-    float b[4][4];
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) b[s2][u] = r1 ? (vb[h][s2][u] > 0.f ? vu[h][s2][u] * bv : 0.f) : vb[h][s2][u];
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) {
-      const f32x4 a4 = ld4(L.As + (16 * qi + li) * WG_KP + 64 * kq + 16 * lk + 4 * s2);
-      acc0[kq] = mfma4(a4[0], b[s2][0], acc0[kq]);
-      acc1[kq] = mfma4(a4[1], b[s2][1], acc1[kq]);
-      acc0[kq] = mfma4(a4[2], b[s2][2], acc0[kq]);
-      acc1[kq] = mfma4(a4[3], b[s2][3], acc1[kq]);
-    }
-    if (do_cs && qi == 0) {          // k-slices t = 8 kq + 2 lk + sp of column 16 qj + li
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp)
-        L.csl[16 * qj + li][8 * kq + 2 * lk + sp] = ((b[2 * sp][0] + b[2 * sp][1]) + (b[2 * sp][2] + b[2 * sp][3])) +
-                                                     ((b[2 * sp + 1][0] + b[2 * sp + 1][1]) + (b[2 * sp + 1][2] + b[2 * sp + 1][3]));
-    }
-  }
-  lds_barrier();
-  float gsq = 0.f;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int gi = i0 + 16 * qi + 4 * lk + r;
-    const float v = ((acc0[0][r] + acc1[0][r]) + (acc0[1][r] + acc1[1][r])) +
-                    ((acc0[2][r] + acc1[2][r]) + (acc0[3][r] + acc1[3][r]));
-    if (gi < p.M && gj < p.N) {
-      p.C[(int64_t)gi * p.ldc + gj] = v;
-      adam_apply(ad, aidx[r], v, ain[r], lr_t);
-      gsq += v * v;
-    }
-  }
-  if (c_on) {                        // sac_wgrad_kernel's column sum: the 32-lane xor tree, read at slice 0
-    const float* S = L.csl[16 * qj + li];
-    float a8[16], b4[8], c2[4];
-#pragma unroll
-    for (int x = 0; x < 16; ++x) a8[x] = S[x] + S[x ^ 16];
-#pragma unroll
-    for (int x = 0; x < 8; ++x) b4[x] = a8[x] + a8[x ^ 8];
-#pragma unroll
-    for (int x = 0; x < 4; ++x) c2[x] = b4[x] + b4[x ^ 4];
-    const float cs = (c2[0] + c2[2]) + (c2[1] + c2[3]);
-    p.colsum[gj] = cs;
-    adam_apply(ad, c_idx, cs, c_in, lr_t);
-    gsq += cs * cs;
-  }
-  if (ad.norm_part) {                // per-tile squared-gradient partial (grad-norm logs, sac_logs_kernel)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) gsq += __shfl_xor(gsq, off);
-    if (lane == 0) L.red[w] = gsq;
-    lds_barrier();
-    if (tid == 0) {
-      const float bsum = (L.red[0] + L.red[1]) + (L.red[2] + L.red[3]);
-      const int64_t off = (int64_t)(p.C - ad.G);
-      float* np_ = ad.norm_part + 2 * (int64_t)(ad.slot0 + bid);
-      np_[0] = off >= 0 && off < ad.n_pi ? bsum : 0.f;
-      np_[1] = off >= ad.n_pi && off < ad.n_pi + ad.n_q ? bsum : 0.f;
-    }
-  }
-  handoff_signal(sync + (SYNC_N * nrb + SYNC_B2_DONE) * SYNC_STRIDE);
-  stamp(g.st, 4);
-}
-
-// The loss tail of the single-launch step with 256 threads, exactly sac_wgrad_kernel's 1024-thread sums: thread
-// tid plays the 1024-thread block's threads tid + 256 q (q < 4), i.e. lane tid % 64 of virtual wave w + 4 q, and
-// the virtual waves' partials are added in wave order.  It then waits for every tile, zeroes the step's counters
-// (nothing of this launch polls them any more) and advances the step counter.
-static __device__ __forceinline__ void wgrad_loss_tail4(const WgradArgs a, float* sh, unsigned* sync, int nrb,
-                                                        int ncq, int ntiles) {
-  unsigned* tmo = sync + (SYNC_N * nrb + SYNC_TMO) * SYNC_STRIDE;
-  stamp(a.st, 0);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int n = a.n, A = a.A;
-  const AdamCtx& ad = a.ad;
-  AdamIn al{0.f, 0.f, 0.f, 0.f};
-  if (tid == 0) al = adam_load(ad, ad.total);                       // log_alpha = the last parameter
-  // B1 done (critic and policy blocks; F1 and F2 before them), then every step-control / gather block (the
-  // readers of the step counter): ONE acquire
-  handoff_wait_all(sync, nrb, SYNC_B1_Q, 2u * (unsigned)ncq, SYNC_B1_PI, (unsigned)ncq, 0u, tmo, false);
-  handoff_wait_all(sync, nrb, SYNC_B1_CTL, (unsigned)ncq, SYNC_B1_CTL, 0u, 0u, tmo, true);
-  const float lr_t = *ad.lr_t;
-  float red[4][7];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int i = 0; i < 7; ++i) red[q][i] = 0.f;
-  const auto dls = rsrc(a.L.head_s, (int64_t)n * 2 * A), dlp = rsrc(a.L.logp_s, 2 * rows_ns(n));
-  const auto dep = rsrc(a.eps_s, (int64_t)n * EPW);
-  for (int r0 = 0; r0 < n; r0 += 1024) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = r0 + tid + 256 * q;
-      const bool on = r < n;
-      const RowIn in = row_losses_load(a.L, n, a.ncq, r, on);
-      const float lps = bload(dlp, on ? lp_idx(r) : -1);
-      float lsv[8], muv[8], epv[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        lsv[j] = bload(dls, (on && j < A) ? r * 2 * A + A + j : -1);
-        muv[j] = bload(dls, (a.prior && on && j < A) ? r * 2 * A + j : -1);
-        epv[j] = bload(dep, (a.prior && on && j < A) ? r * EPW + j : -1);
-      }
-      if (!on) continue;
-      const RowQ o = row_losses(a.L, in);
-      const float q1 = o.q[0], q2 = o.q[1], q1p = o.q[2], q2p = o.q[3];
-      float ent = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (j >= A) break;
-        const float ls = fminf(fmaxf(lsv[j], -20.f), 2.f);
-        ent += logf(expf(ls) + 1e-8f) + 0.5f * logf(2.f * 3.14159265358979f * 2.718281828459045f);
-      }
-      red[q][0] += (q1 - o.y) * (q1 - o.y); red[q][1] += (q2 - o.y) * (q2 - o.y); red[q][2] += q1; red[q][3] += q2;
-      float lprior = 0.f;
-      if (a.prior) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (j >= A) break;
-          const float act = tanhf(muv[j] + epv[j] * expf(fminf(fmaxf(lsv[j], -20.f), 2.f)));
-          lprior -= 0.5f * act * act;
-        }
-        lprior -= 0.5f * (float)A * 1.8378770664093453f;
-      }
-      red[q][4] += lps; red[q][5] += ent; red[q][6] += o.alpha * lps - fminf(q1p, q2p) - lprior;
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) red[q][i] += __shfl_xor(red[q][i], off);
-      if (lane == 0) sh[(w + 4 * q) * 8 + i] = red[q][i];
-    }
-  lds_barrier();
-  if (tid == 0) {
-    float tot[7];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {                                   // virtual-wave partials in wave order
-      float t = 0.f;
-      for (int q = 0; q < 16; ++q) t += sh[8 * q + i];
-      tot[i] = t;
-    }
-    const float fn = (float)n;
-    const float l1 = tot[0] / fn * 0.5f, l2 = tot[1] / fn * 0.5f;    // mopo.py:403-404
-    const float m1 = tot[2] / fn, m2 = tot[3] / fn, mlp = tot[4] / fn, ment = tot[5] / fn;
-    const float pil = tot[6] / fn;                                  // mopo.py:371-377
-    const float ga = -(mlp + a.tent);
-    const_cast<float*>(ad.G)[ad.total] = ga;
-    float* logs = a.logs;
-    logs[LOG_Q1_LOSS] = l1; logs[LOG_Q2_LOSS] = l2; logs[LOG_Q1] = m1; logs[LOG_Q2] = m2;
-    logs[LOG_ALPHA] = expf(al.p); logs[LOG_ENTROPY] = ment; logs[LOG_LOGP] = mlp; logs[LOG_PI_LOSS] = pil;
-    adam_apply(ad, ad.total, ga, al, lr_t);
-  }
-  // every tile is done with the counters: zero them for the next step, then advance the step counter (nothing
-  // the tiles wrote is read here: no acquire)
-  if (tid == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(sync + (SYNC_N * nrb + SYNC_B2_DONE) * SYNC_STRIDE, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT) < (unsigned)ntiles) {
-      __builtin_amdgcn_s_sleep(8);
-      if (++spins > SAC_SPIN_LIMIT) {
-        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  if (*tmo && tid == 0) {            // a wait gave up (sac_rows.h handoff_wait): poison the logs
-    const float nan = __builtin_nanf("");
-    for (int i = 0; i < LOG_N; ++i) a.logs[i] = nan;
-  }
-  for (int i = tid; i < SYNC_N * nrb; i += blockDim.x) sync[i * SYNC_STRIDE] = 0u;
-  if (tid == 0) {
-    sync[(SYNC_N * nrb + SYNC_B2_DONE) * SYNC_STRIDE] = 0u;
-    *a.iter += 1;
-  }
-  stamp(a.st, 4);
-}
-
-// The whole SAC step as ONE launch, grid (ncq, nrb, 12 + zb2): z < 4 F1, 4 <= z < 8 F2, 8 <= z < 12 B1, then
-// the weight-gradient blocks b = x + ncq (y + nrb (z - 12)): b = 0 the loss tail, 1 <= b <= ntiles tile b - 1.
-// Every block waits only on blocks with lower linear ids (dispatched first), every wait is bounded.
-union StepLds {
-  F2B1Lds a;
-  Wg4Lds b;
-};
-#ifndef MOPO_SAC_STEP_MINB
-#define MOPO_SAC_STEP_MINB 2   // workgroups per CU the single-launch step's registers are capped for
-#endif
-static __global__ __launch_bounds__(256, MOPO_SAC_STEP_MINB) void sac_step_kernel(const FwdArgsR f1, const FwdArgsR f2, const Dh1Args d,
-                                                                 const WgradArgs g) {
-  __shared__ __attribute__((aligned(16))) StepLds S;
-  const int z = blockIdx.z;
-  if (z < 4) {
-    fwd_block<false, 3>(f1, blockIdx.x, blockIdx.y, z, S.a.f);
-  } else if (z < 8) {
-    fwd_block<true, 3>(f2, blockIdx.x, blockIdx.y, z - 4, S.a.f);
-  } else if (z < 12) {
-    dh1_block<3>(d, blockIdx.x, blockIdx.y, z - 8, S.a.b);
-  } else {
-    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * (z - 12));
-    const int ntiles = g.prefix[g.np];
-    if (b == 0)
-      wgrad_loss_tail4(g, S.b.As, d.sync, d.nrb, d.ncq, ntiles);
-    else if (b <= ntiles)
-      wgrad_tile4(g, b - 1, S.b, d.sync, d.nrb, d.ncq);
-  }
 }
 
 static inline WgProb wprob(int M, int N, const float* A, int lda, const float* B, int ldb, float* C, int ldc,

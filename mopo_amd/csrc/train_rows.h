@@ -539,15 +539,9 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_bwd_rows_kernel
 #ifndef TR_XPF
 #define TR_XPF 1   // the next layer's first weight k-groups issued before this layer's epilogue (rows_pre)
 #endif
-// The fused rows body, shared by train_rows_kernel and the single-launch step (bnn_train.hip
-// train_step_kernel, SIG = true).  SIG: the rows another workgroup of the launch reads (X, the swish
-// outputs, the heads' and the hidden layers' output gradients, the loss partials) are stored write-through
-// (sc1) and each stage ends in a hand-off (cdna_hip_programming.md Guideline 16): every wave drains its
-// stores, the workgroup barrier, then one agent-scope add to ready[(e (NHID + 1) + l) TS_STRIDE], the count
-// of row blocks of member e whose layer-l weight-gradient operands are complete (l = NHID after the output
-// gradient, l - 1 after the backward of layer l).
+// The fused rows body of train_rows_kernel.
 #ifndef MOPO_TRAIN_STAMPS
-#define MOPO_TRAIN_STAMPS 0   // diagnostic builds: per-workgroup phase stamps of train_step_kernel
+#define MOPO_TRAIN_STAMPS 0   // diagnostic builds: per-workgroup phase stamps of train_rows_kernel
 #endif
 #if MOPO_TRAIN_STAMPS
 __device__ uint64_t g_train_stamps[2048 * 8];
@@ -562,40 +556,13 @@ static __device__ __forceinline__ void tstamp(int i, int64_t v = -1) {
   (void)i; (void)v;
 #endif
 }
-constexpr int TS_STRIDE = 32;   // one counter per 128-B line
 constexpr int TR_LDS_FLOATS = (2 + TR_NHID) * 16 * TR_LD + 3 * 64 * 17;
-template <bool SC>
-static __device__ __forceinline__ void st_h(float* p, float v) {
-  if constexpr (SC) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <bool SC, int TW>
-static __device__ __forceinline__ void st_tw_h(float* p, const float (&v)[TW]) {
-  if constexpr (SC) {
-#pragma unroll
-    for (int q = 0; q < TW; ++q) __hip_atomic_store(p + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    st_tw<TW>(p, v);
-  }
-}
-static __device__ __forceinline__ void rows_signal(unsigned* c) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int G0, int GH, int GD, bool SIG>
-static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float* lds, unsigned* ready, int e, int rb) {
+template <int G0, int GH, int GD>
+static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float* lds, int e, int rb) {
   float (*buf)[16 * TR_LD] = reinterpret_cast<float (*)[16 * TR_LD]>(lds);
   float (*zb)[16 * TR_LD] = reinterpret_cast<float (*)[16 * TR_LD]>(lds + 2 * 16 * TR_LD);
   float (*red)[64][17] = reinterpret_cast<float (*)[64][17]>(lds + (2 + TR_NHID) * 16 * TR_LD);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15;
-  auto signal = [&](int l) {
-    if constexpr (SIG) {
-      rows_signal(ready + (e * (TR_NHID + 1) + l) * TS_STRIDE);
-      tstamp(1 + TR_NHID - l);
-    }
-  };
   const int M = a.M, IN = a.IN, H = a.H, D = a.D, i0 = rb * 16;
   const int c0 = 64 * (w & 3) + 4 * li + TR_TW * (w >> 2);   // this lane's first column
   auto wfwd = [&](int l) {
@@ -612,7 +579,7 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
   constexpr int NPF = 2;
   float pf_v[NPF];
   int pf_src[NPF];
-  bool staged = !SIG && a.staged;
+  const bool staged = a.staged;
   if (staged) {   // the indices now; the rows they name after layer 0; the stores at the end
     const int W = IN + D;
     const int64_t nb = (int64_t)(*a.bstep + 1) * a.batch;
@@ -621,8 +588,9 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     for (int q = 0; q < NPF; ++q) {
       const int i = tid + q * TR_WAVES * 64, row = i0 + (i / W);
       // past the index array: row 0 (the last full step prefetches for a minibatch that does not come)
-      pf_src[q] = i < 16 * W ? __builtin_bit_cast(int, __builtin_amdgcn_raw_buffer_load_b32(
-                                   drows, (int)((e * a.stride + nb + row) * 4), 0, 0)) : 0;
+      // rows past the member's batch (batch % 16 != 0) are neither loaded nor stored
+      pf_src[q] = i < 16 * W && row < M ? __builtin_bit_cast(int, __builtin_amdgcn_raw_buffer_load_b32(
+                                              drows, (int)((e * a.stride + nb + row) * 4), 0, 0)) : 0;
     }
   }
   auto prefetch_rows = [&]() {
@@ -632,7 +600,7 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     for (int q = 0; q < NPF; ++q) {
       const int i = tid + q * TR_WAVES * 64, c = i % W;
       const int64_t src = pf_src[q];
-      pf_v[q] = i >= 16 * W ? 0.f : c < IN ? (a.inputs[src * IN + c] - a.mu[c]) / a.sigma[c]   // utils.py:96
+      pf_v[q] = i >= 16 * W || i0 + i / W >= M ? 0.f : c < IN ? (a.inputs[src * IN + c] - a.mu[c]) / a.sigma[c]   // utils.py:96
                                            : a.targets[src * D + (c - IN)];
     }
   };
@@ -644,7 +612,7 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     if (staged) {
       for (int i = tid; i < 16 * IN; i += TR_WAVES * 64) {
         const int r = i / IN, c = i % IN;
-        buf[0][r * TR_LD + c] = a.X[((int64_t)e * M + i0 + r) * IN + c];
+        if (i0 + r < M) buf[0][r * TR_LD + c] = a.X[((int64_t)e * M + i0 + r) * IN + c];   // padding rows stay 0
       }
     } else
     for (int i = tid; i < 16 * W; i += TR_WAVES * 64) {
@@ -654,7 +622,7 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
       const int64_t er = (int64_t)e * M + row;
       if (c < IN) {
         const float x = (a.inputs[src * IN + c] - a.mu[c]) / a.sigma[c];   // utils.py:96
-        st_h<SIG>(&a.X[er * IN + c], x);
+        *(&a.X[er * IN + c]) = x;
         buf[0][r * TR_LD + c] = x;
       } else {
         a.T[er * D + (c - IN)] = a.targets[src * D + (c - IN)];
@@ -690,7 +658,7 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
           st_tw<TR_TW>(zb[l] + r * TR_LD + c0, v);             // pre-activation, for swish' below
 #pragma unroll
           for (int q = 0; q < TR_TW; ++q) v[q] = swish_fast(v[q]);
-          if (ok) st_tw_h<SIG, TR_TW>(a.Hh[l] + ((int64_t)e * M + row) * H + c0, v);
+          if (ok) st_tw<TR_TW>(a.Hh[l] + ((int64_t)e * M + row) * H + c0, v);
         } else if (ok) {
           st_tw<TR_TW>(a.OUT + ((int64_t)e * M + row) * 2 * D + c0, v);
         }
@@ -702,12 +670,12 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     }
     lds_barrier();
   };
-  if constexpr (!SIG) tstamp(1);
+  tstamp(1);
   fwd(std::integral_constant<int, G0>{}, 0);
   prefetch_rows();
-  if constexpr (!SIG) tstamp(2);
+  tstamp(2);
   for (int l = 1; l <= TR_NHID; ++l) fwd(std::integral_constant<int, GH>{}, l);
-  if constexpr (!SIG) tstamp(3);
+  tstamp(3);
   // ---- output gradient and the block's partial sums (train_fwd_rows_kernel); dY of the heads also into
   //      buf[0] (the backward's input; zero-padded to a multiple of 16 columns)
   const float* o = buf[(TR_NHID + 1) & 1];
@@ -730,8 +698,8 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
       const float dlv1 = dlv * sb;
       g_mean = 2.f * err * inv * s;
       g_lv = dlv1 * sa;
-      st_h<SIG>(&a.dOUT[er * 2 * D + d], g_mean);
-      st_h<SIG>(&a.dOUT[er * 2 * D + D + d], g_lv);
+      *(&a.dOUT[er * 2 * D + d]) = g_mean;
+      *(&a.dOUT[er * 2 * D + D + d]) = g_lv;
       c_mn = dlv * (1.f - sb);
       c_mx = dlv1 * (1.f - sa);
       c_loss = (err * err * inv + lv) * s;
@@ -750,13 +718,9 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     for (int k = 0; k < 3; ++k)
       for (int r = 0; r < 16; ++r) t3[k] += red[k][tid][r];
     float* pp = a.lpart + (((int64_t)e * a.nrb + rb) * D + tid) * 4;
-    st_h<SIG>(pp, t3[0]); st_h<SIG>(pp + 1, t3[1]); st_h<SIG>(pp + 2, t3[2]);
+    *(pp) = t3[0]; *(pp + 1) = t3[1]; *(pp + 2) = t3[2];
   }
-  // the hand-offs are signalled one stage late, right after the next layer's MFMAs: by then the stage's
-  // write-through stores have long completed, so the drain in front of the signal costs nothing (signalled
-  // at once it stalled every wave on its stores, ~1 us per stage); the last one goes out at the end
-  if constexpr (!SIG) tstamp(4);
-  int pending = TR_NHID;   // the heads' weight-gradient operands (Hh[NHID - 1], dOUT) and the loss partials
+  tstamp(4);
   // ---- the activation-gradient chain (train_bwd_rows_kernel), swish'(Z) from LDS; dY of layer l sits in
   //      buf[(TR_NHID - l) & 1] as in that kernel (dy = buf[TR_NHID & 1] = buf[0] for 4 hidden layers)
   static_assert((TR_NHID & 1) == 0, "the backward's first input buffer is buf[0]");
@@ -774,11 +738,9 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
     f32x4 acc[TR_TW];
     if (TR_XPF) {
       rows_gemm_pre<true, G, TR_TW>(buf[(TR_NHID - l) & 1], wbwd(l), c0, lane, pre, acc);
-      if constexpr (SIG) signal(pending);
       if (l > 1) rows_pre<true, GH, TR_TW>(wbwd(l - 1), c0, lane, pre);
     } else {
       rows_gemm<true, G, TR_TW>(buf[(TR_NHID - l) & 1], Wl, Nl, Kl, Nl, c0, lane, acc);
-      if constexpr (SIG) signal(pending);
     }
     float* out = buf[(TR_NHID - l + 1) & 1];
     if (__builtin_amdgcn_readfirstlane(c0 - 4 * li) < Kl) {
@@ -789,34 +751,31 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
         float v[TR_TW];
 #pragma unroll
         for (int q = 0; q < TR_TW; ++q) v[q] = ok ? acc[q][i] * dswish_fast(zm[i][q]) : 0.f;
-        if (ok) st_tw_h<SIG, TR_TW>(a.dZ[l - 1] + ((int64_t)e * M + row) * H + c0, v);
+        if (ok) st_tw<TR_TW>(a.dZ[l - 1] + ((int64_t)e * M + row) * H + c0, v);
         st_tw<TR_TW>(out + r * TR_LD + c0, v);
       }
     }
-    pending = l - 1;   // layer l - 1's operands (Hh[l - 2] or X, dZ[l - 1])
     lds_barrier();
   };
   bwd(std::integral_constant<int, GD>{}, TR_NHID);
-  if constexpr (!SIG) tstamp(5);
+  tstamp(5);
   for (int l = TR_NHID - 1; l >= 1; --l) {
     bwd(std::integral_constant<int, GH>{}, l);
-    if (!SIG && l == 2) tstamp(6);
+    if (l == 2) tstamp(6);
   }
-  if constexpr (!SIG) tstamp(7);
-  if constexpr (SIG) signal(pending);
+  tstamp(7);
   if (staged) {   // the next step's rows, loaded at the start
     const int W = IN + D;
 #pragma unroll
     for (int q = 0; q < NPF; ++q) {
       const int i = tid + q * TR_WAVES * 64, r = i / W, c = i % W;
       const int64_t er = (int64_t)e * M + i0 + r;
-      if (i < 16 * W) {
+      if (i < 16 * W && i0 + r < M) {   // never into the next member's rows (or past the last member's)
         if (c < IN) a.Xn[er * IN + c] = pf_v[q];
         else a.Tn[er * D + (c - IN)] = pf_v[q];
       }
     }
   }
-  (void)pending;
 }
 
 template <int G0, int GH, int GD>
@@ -829,7 +788,7 @@ static __global__ __launch_bounds__(TR_WAVES * 64, 1) void train_rows_kernel(con
   }
   if (!tr_block(blockIdx.x, a.nrb, a.E, e, rb)) return;
   tstamp(0);
-  train_rows_body<G0, GH, GD, false>(a, lds, nullptr, e, rb);
+  train_rows_body<G0, GH, GD>(a, lds, e, rb);
 }
 
 }  // namespace mopo

@@ -193,9 +193,16 @@ class SAC:
     def logs(self):
         """Fetches of the last step (mopo.py:453-463 names, plus policy_loss); synchronises."""
         v = self._copy(5, len(LOG_KEYS)).cpu().numpy()
+        self.check()
         d = OrderedDict((k, float(x)) for k, x in zip(LOG_KEYS, v))
         d['sac_pi/std'] = d['sac_pi/logp_pi']   # the reference logs logp_pi under this key (mopo.py:463)
         return d
+
+    def check(self):
+        """Raises if a fused step's bounded hand-off wait gave up since the last check (the device then held
+        every parameter / Adam / target update instead of applying one from stale operands); synchronises."""
+        flag = C.c_int(0)
+        L.check(L.lib().mopo_sac_check(self._h, C.byref(flag)))
 
     def _do_training(self, iteration, env_pool=None, model_pool=None, n_steps=1, seed=0, idx=None, eps_s=None,
                      eps_n=None, stream=None, n_train_repeat=1):

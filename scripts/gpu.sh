@@ -12,7 +12,7 @@
 #   train_so_ab BNN.train parity on each abv/<v>.so of $AB, then the train leg alternating them
 #   env_ab      bench (SAC + headline) alternating the env settings in $VARS (comma-joined per variant)
 #   stamps      SAC phase stamps from abv/sac_stamps.so (scripts/sac_stamps.py)
-#   train_stamps  single-launch BNN.train step stamps from abv/train_stamps.so (scripts/train_timeline.py)
+#   train_stamps  BNN.train rows-launch phase stamps from abv/train_stamps.so (scripts/train_timeline.py)
 # usage: bash scripts/gpu.sh tests bench ;  AB="new old" bash scripts/gpu.sh sac_ab
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
@@ -30,7 +30,7 @@ for step in "$@"; do
       tail -4 gpurun_out/pytest_k.log ;;
     bench)
       timeout -k 10 400 python bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err; rc=$?
-      [ $rc -eq 0 ] && python scripts/bench_brief.py gpurun_out/bench_full.json || tail -5 gpurun_out/bench_full.err ;;
+      [ $rc -eq 0 ] && python scripts/bench_brief.py gpurun_out/bench_full.json gpurun_out/bench_detail.json || tail -5 gpurun_out/bench_full.err ;;
     profile)
       bash scripts/gpu_profile.sh; rc=$? ;;
     probe)
@@ -109,7 +109,7 @@ for step in "$@"; do
       keep; : > gpurun_out/train_timeline.txt; rc=0
       for so in ${SOS:-train_stamps}; do
         cp abv/$so.so mopo_amd/libmopo_hip.so
-        for v in ${VARS:-MOPO_TRAIN_STEP1=1}; do
+        for v in ${VARS:-MOPO_TRAIN_STAGE=1}; do
           echo "== $so $v" >> gpurun_out/train_timeline.txt
           env ${v//,/ } timeout -k 10 120 python scripts/train_timeline.py >> gpurun_out/train_timeline.txt 2>&1 || { rc=1; break 2; }
         done

@@ -1,7 +1,7 @@
-"""Timeline of one BNN.train minibatch step run as the single launch (MOPO_TRAIN_STEP1=1) from the
-per-workgroup stamps of a MOPO_TRAIN_STAMPS=1 build: per group (row blocks, tile workgroups, the tail) the
-p50 / max of each stamp, us after the step's first workgroup start.  The epoch holds whole minibatches
-only, so the stamps are a graph-replayed full step's.  usage: MOPO_TRAIN_STEP1=1 python scripts/train_timeline.py"""
+"""Timeline of one BNN.train minibatch step's rows launch (train_rows_kernel) from the per-workgroup stamps
+of a MOPO_TRAIN_STAMPS=1 build: the p50 / max of each phase stamp, us after the step's first workgroup start.
+The epoch holds whole minibatches only, so the stamps are a graph-replayed full step's.
+usage: python scripts/train_timeline.py"""
 import os
 import sys
 
@@ -34,25 +34,14 @@ def main():
     t0 = st[:nblk, 0][st[:nblk, 0] > 0].min()
     us = lambda v: (v - t0) * 0.01
     rows = [b for b in range(nrw) if (b & 7) + 8 * ((b >> 3) // nrb) < E]
-    tiles = list(range(nrw + 1, nblk))        # workgroup nrw is the tail
     def show(name, idx, cols, labels):
         for c, lab in zip(cols, labels):
             v = np.array([us(st[b, c]) for b in idx if st[b, c] > 0])
             if len(v):
                 print('%-8s %-22s p50 %7.2f  min %7.2f  max %7.2f  (n=%d)' % (name, lab, np.median(v), v.min(), v.max(), len(v)))
-    if os.environ.get('MOPO_TRAIN_STEP1', '0') == '0':   # the rows launch of the two-launch step alone
-        print('rows launch (two-launch step), %d row blocks, us' % len(rows))
-        show('rows', rows, range(8), ['start', 'gather done', 'layer 0', 'hidden + heads', 'loss + dY',
-                                      'bwd l4', 'bwd l3, l2', 'bwd l1 (end)'])
-        return
-    print('single-launch train step, %d workgroups (%d row blocks, %d tile workgroups, 1 tail), us' % (nblk, len(rows), len(tiles)))
-    show('rows', rows, range(6), ['start', 'fwd+loss (l=4 ready)', 'bwd l4 (l=3 ready)', 'bwd l3 (l=2 ready)',
-                                  'bwd l2 (l=1 ready)', 'bwd l1 (l=0 ready)'])
-    show('tiles', tiles, range(3), ['start', 'first wait done', 'end'])
-    nt = st[tiles, 3]
-    print('tiles    tiles per workgroup: mean %.2f  max %d  zero %d' % (nt.mean(), nt.max(), int((nt == 0).sum())))
-    show('tail', [nrw], range(4), ['start', 'rows ready', 'loss tail done', 'end'])
-
+    print('rows launch, %d row blocks, us' % len(rows))
+    show('rows', rows, range(8), ['start', 'gather done', 'layer 0', 'hidden + heads', 'loss + dY',
+                                  'bwd l4', 'bwd l3, l2', 'bwd l1 (end)'])
 
 if __name__ == '__main__':
     main()

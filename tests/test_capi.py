@@ -105,16 +105,14 @@ def test_error_reporting():
     assert b'num_networks' in L.mopo_last_error()
 
 
-@pytest.mark.parametrize('step', [False, True])
 @pytest.mark.parametrize('E,O,A,H', [(7, 17, 6, 200), (7, 11, 3, 200), (5, 17, 6, 256), (16, 17, 6, 32), (1, 3, 1, 8)])
-def test_train_weight_gradient_tile_lists(E, O, A, H, step):
+def test_train_weight_gradient_tile_lists(E, O, A, H):
     """The training step's weight-gradient tiles (bnn_train.hip make_wlist, host only): every (layer,
     member, tile row, tile column) of the 5 layers exactly once over the 8 XCD lists, the lists within one
-    tile of an even share, and -- except the overflow past that share -- member e's tiles on list e mod 8.
-    step: the single-launch step's lists (order 2), whose entries are also ordered by layer, heads first."""
+    tile of an even share, and -- except the overflow past that share -- member e's tiles on list e mod 8."""
     from mopo_amd import _lib
     L = _lib.lib()
-    fn = L.mopo_bnn_train_tile_lists_step if step else L.mopo_bnn_train_tile_lists
+    fn = L.mopo_bnn_train_tile_lists
     per = fn(E, O, A, H, None, 0)
     assert per > 0
     out = np.empty(8 * per + 8, np.int32)
@@ -128,8 +126,6 @@ def test_train_weight_gradient_tile_lists(E, O, A, H, step):
     for x in range(8):
         lst = out[x * per:x * per + cnt[x]]
         assert np.all(out[x * per + cnt[x]:(x + 1) * per] == -1)
-        if step:
-            assert np.all(np.diff(lst & 7) <= 0)
         for v in lst:
             t = (v & 7, (v >> 3) & 15, (v >> 7) & 31, (v >> 12) & 31)
             got.append(t)

@@ -508,10 +508,10 @@ def test_empty_batches():
     assert steps.cpu().numpy().tolist() == [0, 0, 0] and pool.size == 0
 
 
+# the C2 workload itself (halfcheetah, E=7, H=200, B=50,000, h=5) is compared row for row over the whole pool
+# below (test_full_pool_c2_rollout_vs_oracle); these sample 192 rows of the other full-size workloads
 FULL_SIZE = [
-    ('halfcheetah', 'fp32', 7, 200, 50000, 5, 1.0, 40000), ('walker2d', 'fp32', 7, 200, 50000, 5, 1.0, 40000),
-    ('halfcheetah', 'bf16x6', 7, 200, 50000, 5, 1.0, 40000), ('walker2d', 'bf16x6', 7, 200, 50000, 5, 1.0, 40000),
-    ('halfcheetah', 'f16x3', 7, 200, 50000, 5, 1.0, 40000),                                 # C2 (headline)
+    ('walker2d', 'fp32', 7, 200, 50000, 5, 1.0, 40000), ('walker2d', 'bf16x6', 7, 200, 50000, 5, 1.0, 40000),
     ('walker2d', 'f16x3', 7, 200, 50000, 5, 1.0, 40000),
     ('walker2d', 'bf16', 7, 200, 100000, 1, 1.0, 40000),                                     # C3
     ('halfcheetah', 'f16x3', 7, 200, 50000, 5, 5.0, 1000000),     # C4 per GPU: medium-expert, 1e6-row env pool
@@ -538,14 +538,109 @@ def test_full_size_perf_mode_rows_vs_oracle(domain, dtype, E, H, B, h, coeff, en
     _full_size_rows(domain, dtype, E, H, B, h, coeff, env_n)
 
 
-def test_full_size_f16x3_error_distribution_matches_fp32():
-    """The C2 headline at full size (B=50,000, h=5) in the product default f16x3 and in exact-f32 MFMA:
-    the scaled errors of the 192 sampled rows' next states (every step) against the f64 oracle have
-    quantiles (50 / 90 / 99 / 100 %) within 2x of the fp32 kernel's, floor 2^-23 (same seeds, same rows)."""
-    e16 = np.concatenate(_full_size_rows('halfcheetah', 'f16x3', 7, 200, 50000, 5, 1.0, 40000))
-    e32 = np.concatenate(_full_size_rows('halfcheetah', 'fp32', 7, 200, 50000, 5, 1.0, 40000))
-    q16, q32 = (np.quantile(e, (0.5, 0.9, 0.99, 1.0)) for e in (e16, e32))
-    assert np.all(q16 <= np.maximum(2 * q32, 2.0 ** -23)), (q16, q32)
+_POOL_ERRS = {}
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16x6', 'f16x3'])
+def test_full_pool_c2_rollout_vs_oracle(dtype):
+    """C2 at full size (halfcheetah-mixed: E=7, H=200, B=50,000, h=5, learned-var penalty, perf-mode Philox
+    streams, split rollout): EVERY one of the 250,000 pool rows is recomputed by the oracle from the restated
+    streams (oracle/rng.py) -- start rows bit-exact, terminals bit-exact, observations, actions, next
+    observations and rewards within the fp32 parity tolerance 5e-5 (1 + |ref|) -- in exact-f32 MFMA, the
+    exact-split bf16x6 and the f16x3 default."""
+    _POOL_ERRS[dtype] = _full_pool_c2(dtype)
+
+
+def test_full_size_16bit_error_distributions_match_fp32():
+    """The C2 pool's scaled next-state errors against the f64 oracle (all 250,000 rows) in bf16x6 and f16x3
+    have quantiles (50 / 90 / 99 / 100 %) within 2x of the exact-f32 MFMA kernel's, floor 2^-23."""
+    for d in ('fp32', 'bf16x6', 'f16x3'):
+        if d not in _POOL_ERRS:
+            _POOL_ERRS[d] = _full_pool_c2(d)
+    q32 = np.quantile(_POOL_ERRS['fp32'], (0.5, 0.9, 0.99, 1.0))
+    for d in ('bf16x6', 'f16x3'):
+        q = np.quantile(_POOL_ERRS[d], (0.5, 0.9, 0.99, 1.0))
+        assert np.all(q <= np.maximum(2 * q32, 2.0 ** -23)), (d, q, q32)
+
+
+C2_FULL = dict(O=17, A=6, E=7, H=200, B=50000, h=5, env_n=40000, coeff=1.0, seed=0x1234567890ab, epoch=3,
+               elites=[4, 1, 0, 6, 2])
+_C2_ORACLE = {}
+
+
+def _c2_inputs():
+    from mopo_amd.rollout import init_sac_params
+    c = C2_FULL
+    rs = np.random.RandomState(21)
+    env_obs = rs.normal(size=(c['env_n'], c['O'])).astype(np.float32)
+    mats = obnn.to_mat_list(obnn.init_params(c['E'], c['O'], c['A'], hidden=c['H'], seed=22,
+                                             inputs=np.concatenate([env_obs[:2000], rs.uniform(-1, 1, (2000, c['A']))], 1)))
+    return env_obs, mats, init_sac_params(c['O'], c['A'], 256, seed=23)
+
+
+def _c2_oracle(chunk=12500):
+    """The oracle's C2 rollout of all B rows (same inputs and streams for every dtype: computed once)."""
+    if _C2_ORACLE:
+        return _C2_ORACLE
+    from oracle import rng as orng
+    from mopo_amd.rollout import split_params
+    c = C2_FULL
+    O, A, E, B, h, seed, epoch = c['O'], c['A'], c['E'], c['B'], c['h'], c['seed'], c['epoch']
+    env_obs, mats, flat = _c2_inputs()
+    p = obnn.from_mat_list(mats)
+    P = [q.astype(np.float64) for q in split_params(flat, O, A)[:8]]
+    out = {k: [[] for _ in range(h)] for k in ('obs', 'act', 'nobs', 'rew', 'term')}
+    for c0 in range(0, B, chunk):
+        rows = np.arange(c0, min(B, c0 + chunk))
+        obs = env_obs[orng.start_rows(rows, seed, epoch * 4096, c['env_n'])].astype(np.float64)
+        for i in range(h):
+            st = epoch * 4096 + 1 + i
+            ea = orng.act_noise(rows, seed, st, A).astype(np.float64)
+            act, _ = osac.actor_act(P, obs.astype(np.float32).astype(np.float64), ea)
+            act = act.astype(np.float32)
+            sel = orng.model_choice(rows, seed, st, c['elites'])
+            noise = np.broadcast_to(orng.obs_noise(rows, seed, st, O + 1).astype(np.float64), (E, len(rows), O + 1))
+            nobs, rew, term, _ = ofe.step(p, c['elites'], obs, act, ofe.TERMINATION['halfcheetah'],
+                                          penalty_coeff=c['coeff'], penalty_learned_var=True, noise=noise, model_inds=sel)
+            for k, v in (('obs', obs), ('act', act), ('nobs', nobs), ('rew', rew), ('term', term)):
+                out[k][i].append(v)
+            obs = nobs
+    for k in out:
+        _C2_ORACLE[k] = [np.concatenate(v) for v in out[k]]
+    return _C2_ORACLE
+
+
+def _full_pool_c2(dtype):
+    """One full-size C2 rollout, every pool row against the oracle; returns the next-state scaled errors."""
+    import torch
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.rollout import ModelRollout
+    from mopo_amd.static import static_fns
+    c = C2_FULL
+    B, h, tol = c['B'], c['h'], 5e-5
+    env_obs, mats, flat = _c2_inputs()
+    model = make_model(mats, c['E'], c['H'], dtype=dtype)
+    pool = SimpleReplayPool(obs_dim=c['O'], act_dim=c['A'], max_size=B * h)
+    ro = ModelRollout(model, B, h)
+    steps = ro.run(torch.from_numpy(env_obs).cuda(), torch.from_numpy(flat).cuda(), pool, B, h,
+                   static_fns['halfcheetah'].term_kind, c['coeff'], c['elites'], seed=c['seed'],
+                   epoch=c['epoch']).cpu().numpy()
+    assert steps.tolist() == [B] * h and pool.size == B * h    # halfcheetah never terminates: no compaction
+    dev = {k: v[:pool.size].cpu().numpy() for k, v in pool.fields.items()}
+    ref = _c2_oracle()
+    errs = []
+    for i in range(h):
+        got = {k: v[i * B:(i + 1) * B] for k, v in dev.items()}
+        obs, act, nobs = ref['obs'][i], ref['act'][i], ref['nobs'][i]
+        if i == 0:   # the start rows: an exact copy of the Philox-chosen env rows
+            np.testing.assert_array_equal(got['observations'], obs.astype(np.float32))
+        close(got['observations'], obs, tol)
+        close(got['actions'], act, 5e-5 if i == 0 else tol)
+        close(got['next_observations'], nobs, tol)
+        close(got['rewards'], ref['rew'][i], tol)
+        np.testing.assert_array_equal(got['terminals'], ref['term'][i])
+        errs.append((np.abs(got['next_observations'] - nobs) / (1 + np.abs(nobs))).ravel())
+    return np.concatenate(errs)
 
 
 def _full_size_rows(domain, dtype, E, H, B, h, coeff, env_n):

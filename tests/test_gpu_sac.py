@@ -388,7 +388,7 @@ def test_sac_fused_launches_bit_identical_to_separate_launches(o, a, h, n, monke
         pl.append(p)
     fl = flat(osac.init_params(o, a, h, seed=3)).astype(np.float32)
     out = {}
-    for fuse in ('0', '1', '2', '3'):
+    for fuse in ('0', '1', '2'):
         monkeypatch.setenv('MOPO_SAC_FUSE', fuse)
         sac = SAC(o, a, h, batch_size=n, real_ratio=0.05, target_entropy=-3, params=fl)
         sac._do_training(0, pl[0], pl[1], n_steps=300, seed=19)
@@ -396,6 +396,53 @@ def test_sac_fused_launches_bit_identical_to_separate_launches(o, a, h, n, monke
         lg = sac.logs()
         assert all(np.isfinite(v) for v in lg.values()), (fuse, lg)
         out[fuse] = {k: v.cpu().numpy() for k, v in sac.state_dict().items()}
-    for f in ('1', '2', '3'):
+    for f in ('1', '2'):
         for k in out['0']:
             np.testing.assert_array_equal(out[f][k], out['0'][k], err_msg='MOPO_SAC_FUSE=%s %s' % (f, k))
+
+
+def test_sac_handoff_timeout_holds_updates_and_is_reported():
+    """A bounded hand-off wait that gives up (sac_rows.h handoff_wait) sets the sticky timeout word: every later
+    step must then hold its parameter / Adam / target updates (no update computed from stale operands), write
+    NaN logs, and SAC.check() / logs() must raise once and clear the word, after which steps update again."""
+    import ctypes as C
+
+    import torch
+    from mopo_amd import _lib as L
+    from mopo_amd.replay_pool import SimpleReplayPool
+    from mopo_amd.sac import SAC
+    o, a, h, n = 11, 3, 64, 100
+    rs = np.random.RandomState(23)
+    pl = []
+    for rows in (400, 2000):
+        s = {'observations': rs.normal(size=(rows, o)).astype(np.float32),
+             'actions': rs.uniform(-1, 1, (rows, a)).astype(np.float32),
+             'next_observations': rs.normal(size=(rows, o)).astype(np.float32),
+             'rewards': rs.normal(size=(rows, 1)).astype(np.float32),
+             'terminals': rs.uniform(size=(rows, 1)) < 0.1}
+        p = SimpleReplayPool(obs_dim=o, act_dim=a, max_size=rows)
+        p.add_samples(s)
+        pl.append(p)
+    sac = SAC(o, a, h, batch_size=n, real_ratio=0.05, target_entropy=-3,
+              params=flat(osac.init_params(o, a, h, seed=3)).astype(np.float32))
+    sac._do_training(0, pl[0], pl[1], n_steps=5, seed=19)
+    sac.check()                                          # no give-up so far
+    before = {k: v.cpu().numpy() for k, v in sac.state_dict().items()}
+    L.check(L.lib().mopo_sac_inject_timeout(sac._h))
+    sac._do_training(5, pl[0], pl[1], n_steps=9, seed=19)
+    torch.cuda.synchronize()
+    held = {k: v.cpu().numpy() for k, v in sac.state_dict().items()}
+    for k in before:
+        np.testing.assert_array_equal(held[k], before[k], err_msg=k)
+    v = sac._copy(5, 10).cpu().numpy()
+    assert np.all(np.isnan(v[[0, 1, 2, 3, 4, 5, 6, 9]])), v   # losses, means, alpha (7, 8: the gradient norms)
+    with pytest.raises(RuntimeError, match='timed out'):
+        sac.logs()
+    flag = C.c_int(-1)
+    L.check(L.lib().mopo_sac_check(sac._h, C.byref(flag)))   # cleared by the report
+    assert flag.value == 0
+    sac._do_training(14, pl[0], pl[1], n_steps=3, seed=19)
+    lg = sac.logs()
+    assert all(np.isfinite(x) for x in lg.values()), lg
+    after = sac.state_dict()['params'].cpu().numpy()
+    assert np.abs(after - before['params']).max() > 0
