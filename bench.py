@@ -44,6 +44,14 @@ DTYPE_DESC = {'fp32': 'fp32 (f32 MFMA 16x16x4)',
                        'accumulate: ~22-bit operands like bf16x6, held to the fp32 parity tolerances)'}
 
 
+def dtype_desc(ensemble_dtype, actor_dtype=None):
+    """The line's dtype: the ensemble forward's arithmetic and the rollout actor's (rollout.default_actor_dtype)."""
+    from mopo_amd.rollout import default_actor_dtype
+    act = actor_dtype or default_actor_dtype(ensemble_dtype)
+    return '%s; rollout actor: %s' % (DTYPE_DESC[ensemble_dtype], 'exact f32 MFMA' if act == 'fp32' else
+                                      'f16x3 (~22-bit operands)')
+
+
 # BASELINE.json configs (SURVEY 8(d) table).  B_total = the config's rollout_batch; 'sharded': the batch is
 # split over the ranks (C4, C5: 400k / 1M over 8 GPUs), otherwise every GPU runs B_total rows (weak scaling).
 CONFIGS = {
@@ -105,6 +113,9 @@ def parse():
         a.horizon = spec['h']
         if a.ensemble_dtype == DEFAULT_ENSEMBLE_DTYPE and spec.get('dtype'):
             a.ensemble_dtype = spec['dtype']
+        elif a.ensemble_dtype == DEFAULT_ENSEMBLE_DTYPE:   # the product default at this width (bf16x6: H <= 256)
+            from mopo_amd.bnn import default_ensemble_dtype
+            a.ensemble_dtype = default_ensemble_dtype(spec['H'])
     return a
 
 
@@ -380,7 +391,7 @@ def alt_headline_leg(args, dev, dtype, reps=10):
     a2.ensemble_dtype = dtype
     n, dt, kms = timed_leg(a2, dev, reps, 2, max(args.prof_steps // 2, 4))
     return {'metric': 'model-rollout transitions/s (halfcheetah-mixed, %s ensemble)' % dtype, 'value': n / dt,
-            'unit': 'transitions/s', 'dtype': DTYPE_DESC[dtype], 'ms_per_rollout': dt / reps * 1e3,
+            'unit': 'transitions/s', 'dtype': dtype_desc(dtype), 'ms_per_rollout': dt / reps * 1e3,
             'kernel_ms_avg': kms, 'roofline': leg_roofline(a2, kms)}
 
 
@@ -396,7 +407,7 @@ def config_leg(args, dev, name, dtype, reps=5, warm=3):
     v = n / dt
     share = ' (one GPU of eight: %d of %d rows)' % (a2.batch, spec['B_total']) if spec.get('sharded') else ''
     out = {'metric': 'model-rollout transitions/s (%s: %s%s)' % (name, spec['name'], share), 'value': v,
-           'unit': 'transitions/s', 'dtype': DTYPE_DESC[dtype], 'ms_per_rollout': dt / reps * 1e3,
+           'unit': 'transitions/s', 'dtype': dtype_desc(dtype), 'ms_per_rollout': dt / reps * 1e3,
            'config': {'workload': 'E=%d, H=%d, obs=17, act=6, rollout_batch=%d per GPU, horizon=%d, %s terminations, '
                                   'penalty_coeff=%g, env pool %d rows' % (spec['E'], spec['H'], a2.batch, spec['h'],
                                                                            spec['domain'], spec['penalty'],
@@ -591,7 +602,8 @@ def main():
     sac_rate = sac_leg(args, pool, env, dev, world)
     extra = {}
     if rank == 0 and world == 1 and not args.no_c3 and args.config == 'C2':
-        for key, name, dty in (('N2', 'N2', args.ensemble_dtype), ('N2_fp32', 'N2', 'fp32'), ('C3', 'C3', 'bf16'),
+        for key, name, dty in (('N2', 'N2', args.ensemble_dtype), ('N2_fp32', 'N2', 'fp32'), ('N2_f16x3', 'N2', 'f16x3'),
+                               ('C3', 'C3', 'bf16'),
                                ('C4_per_gpu', 'C4', args.ensemble_dtype), ('C5_per_gpu', 'C5', 'fp32'),
                                ('C5_f16x3_per_gpu', 'C5', 'f16x3'), ('C5_bf16_per_gpu', 'C5', 'bf16')):
             extra[key] = config_leg(args, dev, name, dty)
@@ -612,7 +624,7 @@ def main():
                   'model-rollout transitions/s (%s: %s)' % (args.config, spec['name']),
         'value': value, 'unit': 'transitions/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': DTYPE_DESC[args.ensemble_dtype], 'data': 'synthetic (random-init weights, N(0,1) env pool; D4RL/.mat unavailable offline)',
+        'dtype': dtype_desc(args.ensemble_dtype, args.actor_dtype), 'data': 'synthetic (random-init weights, N(0,1) env pool; D4RL/.mat unavailable offline)',
         'config': {'workload': '%s rollout: E=%d (5 elites), H=%d smv, obs=17, act=6, rollout_batch=%d per GPU, '
                                'horizon=%d, penalty_coeff=%g, learned-var penalty, env pool %d rows'
                                % (args.config, spec['E'], spec['H'], args.batch, args.horizon, spec['penalty'],

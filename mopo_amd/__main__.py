@@ -21,7 +21,7 @@ import json
 import os
 import sys
 
-from .bnn import DEFAULT_ENSEMBLE_DTYPE, DTYPES
+from .bnn import DTYPES, default_ensemble_dtype
 
 EXAMPLES = ('examples.development',)
 COMMANDS = ('run_local', 'run_example_dry', 'run_example_debug')
@@ -71,7 +71,7 @@ def variant_spec(args):
     for k in ('ensemble_dtype', 'actor_dtype'):
         if getattr(args, k) is not None:
             kw[k] = getattr(args, k)
-    kw.setdefault('ensemble_dtype', DEFAULT_ENSEMBLE_DTYPE)
+    kw.setdefault('ensemble_dtype', default_ensemble_dtype(kw.get('hidden_dim', 200)))
     seeds = [args.seed + i for i in range(max(args.num_samples, 1))]
     return {'algorithm_params': params, 'run_params': {'seeds': seeds, 'checkpoint_frequency': args.checkpoint_frequency},
             'model_dir': args.model_dir, 'epochs': args.epochs}

@@ -29,10 +29,18 @@ from . import _lib as L
 # (3 f16 MFMAs per product, ~22-bit operands, the dropped product <= 2^-22 |x w|).
 _DTYPES = {'fp32': 0, 'bf16': 1, 'bf16x3': 2, 'bf16x6': 3, 'f16x3': 4}
 DTYPES = tuple(_DTYPES)
-# what MOPO (and so `mopo run_local` and bench.py's headline) runs unless told otherwise: the f16x3
-# split is held to the fp32 parity tolerances (tests/test_gpu_ref.py, tests/test_gpu_rollout.py)
-# and runs ~2.2x the exact-f32 MFMA kernel; 'fp32' stays selectable everywhere (ensemble_dtype).
-DEFAULT_ENSEMBLE_DTYPE = 'f16x3'
+# what MOPO (and so `mopo run_local` and bench.py's headline) runs unless told otherwise: the exact
+# bf16x6 split -- the reference's f32 operands exactly, 6 bf16 MFMA products per f32 product, f32
+# accumulate, held to the fp32 parity tolerances over whole rollouts (tests/test_gpu_rollout.py) -- at
+# ~1.5x the exact-f32 MFMA kernel's rate (the f32 MFMA peak caps that one below it).  bf16x6 has no H > 256
+# form: there the default is 'fp32' (default_ensemble_dtype).  'f16x3' (~22-bit operands, ~2.4x fp32) and
+# 'fp32' stay selectable everywhere (ensemble_dtype).
+DEFAULT_ENSEMBLE_DTYPE = 'bf16x6'
+
+
+def default_ensemble_dtype(hidden_dim):
+    """The product default for an ensemble of this width: bf16x6 up to H = 256, exact-f32 MFMA above."""
+    return DEFAULT_ENSEMBLE_DTYPE if int(hidden_dim) <= 256 else 'fp32'
 
 N_HIDDEN = 4
 

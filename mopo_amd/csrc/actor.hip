@@ -322,7 +322,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64, NBP == 16 ? ACT_F32_OCC : 2) void a
   __shared__ float head[ACT_WAVES][16][25];  // head outputs [0, 16), then the actions [16, 16 + A)
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + (NBP * 4 + 63) / 64 * 256];  // one array (bnn.hip)
   float* lds_bias = lds + 2 * SLOT;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   if ((int64_t)blockIdx.x * ACT_WAVES * 16 >= count) return;  // whole workgroup past the live rows
   const int64_t row0 = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16;
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16_kernel(const Acto
   constexpr int SLOT = Stage<PS * NBP, ACT_WAVES>::SLOTS * 256;
   __shared__ float head[ACT_WAVES][16][25];
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   if ((int64_t)blockIdx.x * ACT_WAVES * 16 >= count) return;  // whole workgroup past the live rows
   const int64_t row = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16 + m;
@@ -503,7 +503,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64, R == 1 ? 2 : 1) void actor_f16r_ker
   constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;   // also holds the head's 2 KG = NBP fragments
   __shared__ float head[ACT_WAVES][16][25];
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   if ((int64_t)blockIdx.x * ACT_WAVES * 16 * R >= count) return;  // whole workgroup past the live rows
   const int64_t row0 = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16 * R + m;   // row block r: row0 + 16 r
@@ -602,7 +602,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16q_kernel(const Act
   constexpr int BQ = (2 * NBP * 16 + 16) / 4;   // b1 | b2 | bh quads (contiguous in the packing)
   __shared__ __attribute__((aligned(16))) float lds[3 * SLOT + (BQ + 63) / 64 * 256];  // one array (see layer_lds)
   float* lds_bias = lds + 3 * SLOT;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   if ((int64_t)blockIdx.x * ACT_WAVES * 16 >= count) return;  // whole workgroup past the live rows
   const int64_t row = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16 + m;

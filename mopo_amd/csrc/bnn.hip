@@ -214,7 +214,7 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES >= 8 || NBH > 16) ? BNN_MINB_WID
   // draining the next slice's copy instead of overlapping it with the MFMAs
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + (BIASQ + 63) / 64 * 256];
   float* lds_bias = lds + 2 * SLOT;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
   const int e = blockIdx.x / groups, grp = blockIdx.x % groups;
@@ -336,12 +336,24 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
   constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;  // the layer's bias (stage_bias pieces)
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + BIAS_LDS];  // one array (see layer_lds)
   float* lds_bias = lds + 2 * SLOT;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
-  const int e = blockIdx.x / groups, grp = blockIdx.x % groups;
+  // member-major over the grid; or (a.xcd_members, E % 8 == 0) XCD x owns members x, x + 8, ... (workgroup b
+  // runs on XCD b mod 8), member-major within the XCD.  C5 bf16 (E = 32, H = 400, 125k rows): 20.45 vs 20.42M
+  // transitions/s member-major over the grid; row-group-major within the XCD (a row group's inputs read once
+  // per XCD) 19.3M (same box, profiles/r06_c5_bf16_order_ab.txt)
+  int e, grp;
+  if (a.xcd_members) {   // member-major within the XCD: each owned member's weights are fetched into ONE L2
+    const int j = blockIdx.x >> 3;
+    e = (blockIdx.x & 7) + 8 * (j / groups);
+    grp = j % groups;
+  } else {
+    e = blockIdx.x / groups;
+    grp = blockIdx.x % groups;
+  }
   const int64_t row = (int64_t)(grp * WAVES + wv) * 16 + m;
-  if ((int64_t)grp * WAVES * 16 >= count) return;
+  if (grp >= groups || (int64_t)grp * WAVES * 16 >= count) return;
   const int IN = w.IN, O = w.O;
   const bool ok = row < count;
   bf16x8 x0[P][1];
@@ -480,7 +492,7 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? BNN_F16_MINB_WIDE : BNN_F16_
   constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;  // the layer's bias (stage_bias pieces)
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + BIAS_LDS];  // one array (see layer_lds)
   float* lds_bias = lds + 2 * SLOT;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
 #if BNN_F16_XCD
@@ -601,8 +613,8 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? BNN_F16_MINB_WIDE : BNN_F16_
 #ifndef BNN_F16H_MINB
 #define BNN_F16H_MINB 2
 #endif
-#ifndef BNN_F16H_FENCE
-#define BNN_F16H_FENCE 1
+#ifndef BNN_BF16_XCDMEM
+#define BNN_BF16_XCDMEM 1  // bnn_fwd_bf16_kernel, E % 8 == 0: XCD-owned members (member-major within the XCD)
 #endif
 #ifndef BNN_F16H_XCDMEM
 #define BNN_F16H_XCDMEM 1  // E % 8 == 0: each XCD owns E / 8 members (their weights fetched into one L2)
@@ -618,7 +630,7 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd
   constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + BIAS_LDS];  // one array (see layer_lds)
   float* lds_bias = lds + 2 * SLOT;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const int m = lane & 15;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
@@ -633,7 +645,7 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd
   const int e = own ? xcd + 8 * (j / groups) : j / C;
   const int grp = own ? j % groups : xcd * C + j % C;
   if (grp >= groups || e >= E) return;
-  const int64_t row = (int64_t)(grp * WAVES + wv) * 16 + m;
+  const int row = (grp * WAVES + wv) * 16 + m;   // < 2^31 (B <= max_batch)
   if ((int64_t)grp * WAVES * 16 >= count) return;
   const bool ok = row < count;
   auto row_max = [&](float mx) {
@@ -682,8 +694,8 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd
   constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.6931471805599453f;
   float x1[1][8];
   if (a.xs) {
-    const f32x4 lo = ok ? ld4(a.xs + row * XS_STRIDE + 4 * g) : zero4();
-    const f32x4 hi = ok ? ld4(a.xs + row * XS_STRIDE + 16 + 4 * g) : zero4();
+    const f32x4 lo = ok ? ld4(a.xs + (int64_t)row * XS_STRIDE + 4 * g) : zero4();
+    const f32x4 hi = ok ? ld4(a.xs + (int64_t)row * XS_STRIDE + 16 + 4 * g) : zero4();
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       x1[0][t] = lo[t];
@@ -695,8 +707,8 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd
       const int k = slot_feat(bf16_kperm(g, jj), IN);
       float v = 0.f;
       if (ok && k >= 0) {
-        float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, row * a.in.sa + k)
-                          : load_feat(a.in.xb, a.in.xb_f64, row * a.in.sb + (k - O));
+        float raw = k < O ? load_feat(a.in.xa, a.in.xa_f64, (int64_t)row * a.in.sa + k)
+                          : load_feat(a.in.xb, a.in.xb_f64, (int64_t)row * a.in.sb + (k - O));
         v = (raw - w.mu[k]) / w.sigma[k];
       }
       x1[0][jj] = v;
@@ -714,21 +726,19 @@ __global__ __launch_bounds__(WAVES * 64, BNN_F16H_MINB * 4 / WAVES) void bnn_fwd
     to_input(lds_bias, inv_row * w.wscale[(1 + l) * E + e]);
   }
   f32x4 hd[NBO];
-#if BNN_F16H_FENCE
-  // the rollout epilogue's address arithmetic stays behind the last layer (hoisted into the layers it held 3
-  // more VGPRs there: 12 B of scratch per lane)
-  __builtin_amdgcn_sched_barrier(0);
-#endif
   layer_lds_split_f32<KG, NBO, WAVES, SLOT, P, 1, true, NBO, KH>(w.whdb + (int64_t)e * KG * P * NBO * 256, hf, hd,
                                                                  lds, wv, lane, s_in);
-#if BNN_F16H_FENCE
-  __builtin_amdgcn_sched_barrier(0);
-#endif
   const float f = inv_row * w.wscale[4 * E + e] * kNegLn2;  // the head's input is y' = -log2(e) y
 #pragma unroll
   for (int nb = 0; nb < NBO; ++nb) hd[nb] *= f;
-  head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
-                           (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
+  // the row index again from a fresh lane id (v_mbcnt in volatile asm: not merged with the one at the top), so
+  // no row value lives across the layers -- kept live, it was the value spilled (8 B per lane in rollout mode)
+  int lane_e;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_e));
+  const int64_t row_e = (int64_t)((grp * WAVES + __builtin_amdgcn_readfirstlane(wv)) * 16 + (lane_e & 15));
+  const bool ok_e = row_e < count;
+  head_epilogue<NBO, MODE>(w, a, hd, e, row_e, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
+                           (MODE == FWD_ROLLOUT && a.sel && ok_e) ? a.sel[row_e] : -1);
 }
 
 // ---- f16x3 forward over R row blocks per wave (R = 2: 32 rows per wave, 128 per 4-wave workgroup, one
@@ -749,7 +759,7 @@ __global__ __launch_bounds__(WAVES * 64, R == 1 ? 2 : 1) void bnn_fwd_f16r_kerne
   constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;
   __shared__ __attribute__((aligned(16))) float lds[2 * SLOT + BIAS_LDS];
   float* lds_bias = lds + 2 * SLOT;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);  // ntiles: tiles of 16 R rows
   const int C = ceil_div(groups, 8);             // XCD-aware order (bnn_fwd_f16s_kernel)
@@ -888,7 +898,7 @@ __global__ __launch_bounds__(WAVES * 64, R == 1 ? 2 : 1) void bnn_fwd_f16r_kerne
 #define BNN_RING_MINB 3  // 4-wave workgroups per CU the ring kernel's registers are capped for (LDS admits 3)
 #endif
 #ifndef BNN_RING_MINB_X6
-#define BNN_RING_MINB_X6 3  // the same for bf16x6 (P = 3; 158 VGPRs with the dot2 residuals, no scratch)
+#define BNN_RING_MINB_X6 3  // the same for bf16x6 (P = 3)
 #endif
 template <int NB2, int NBO, int MODE, int WAVES, int P, int DEPTH, int NBU = NB2>
 __global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_MINB) * 4 / WAVES > 0)
@@ -906,7 +916,8 @@ __global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_
   // has a whole layer of slice waits behind it whatever the depth
   __shared__ __attribute__((aligned(16))) float lds[DEPTH * SLOT + 2 * BIAS_LDS];  // one array (see layer_lds)
   float* lds_bias0 = lds + DEPTH * SLOT;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = lane & 15, g = lane >> 4;
+  // the wave index in an SGPR (uniform): it and the row base computed from it hold no VGPRs
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), m = lane & 15, g = lane >> 4;
   const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
   const int groups = ceil_div(a.ntiles, WAVES);
   const int C = ceil_div(groups, 8);  // XCD-aware order (bnn_fwd_f16s_kernel)
@@ -1129,8 +1140,14 @@ __global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_
   const float f = inv_row * wsc[4] * kNegLn2;  // the head's input is y' = -log2(e) y
 #pragma unroll
   for (int nb = 0; nb < NBO; ++nb) hd[nb] = acc[nb] * f;
-  head_epilogue<NBO, MODE>(w, a, hd, e, row, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
-                           (MODE == FWD_ROLLOUT && a.sel && ok) ? a.sel[row] : -1);
+  // the row index again from a fresh lane id (volatile asm: not merged with the one at the top), so no 64-bit
+  // row value lives across the layers (bnn_fwd_f16h_kernel: it was the value spilled there)
+  int lane_e;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_e));
+  const int64_t row_e = (int64_t)(grp * WAVES + wv) * 16 + (lane_e & 15);
+  const bool ok_e = row_e < count;
+  head_epilogue<NBO, MODE>(w, a, hd, e, row_e, count, g, w.bhd + (int64_t)e * 3 * NBO * 16,
+                           (MODE == FWD_ROLLOUT && a.sel && ok_e) ? a.sel[row_e] : -1);
 }
 
 template <int NB2, int NBO, int P, int DEPTH>
@@ -1214,7 +1231,8 @@ static int launch_bf16_p(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   constexpr int PS = P == 1 ? 1 : (BNN_SPLIT_PS == 0 ? P : BNN_SPLIT_PS);
   a.ntiles = (int)ceil_div((int)a.B, 16);
   if (a.ntiles == 0) return 0;
-  dim3 grid(ceil_div(a.ntiles, WV) * h->E), block(64 * WV);
+  dim3 grid(ceil_div(a.ntiles, WV) * h->E), block(64 * WV);   // = 8 groups (E / 8) when the XCDs own members
+  a.xcd_members = (BNN_BF16_XCDMEM && h->E % 8 == 0) ? 1 : 0;
   // odd hidden-block count (e.g. H = 200): the last block is padding and is skipped (NBU = NB2 - 1); not at
   // H = 400 (25 of 26), where the skipping variant takes 256 VGPRs and spills
   // NB2 = 14: H = 200 only (13 blocks used); the whole-block form is not instantiated (it spilled 8-12 B)

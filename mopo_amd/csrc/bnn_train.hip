@@ -595,7 +595,7 @@ static __global__ __launch_bounds__(NT, TRAIN_WG2_MINW > 0 ? TRAIN_WG2_MINW : (N
   using C = Wg2<NT>;
   __shared__ __attribute__((aligned(16))) float As[TW2_T * TW2_KP];   // [i][k]; later the K-part partials
   __shared__ __attribute__((aligned(16))) float Bs[TW2_T * TW2_KP];   // [j][k]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (blockIdx.x == gridDim.x - 1) {   // the batch-level tail
     train_loss_tail(g.t, As);
     return;

@@ -295,12 +295,8 @@ __device__ __forceinline__ void split_bf16(float v, short (&out)[P]) {
   }
 }
 // two values at once into whole dwords (part p of a in the low half, of b in the high half): v_cvt_pk_bf16_f32
-// rounds to nearest even; each residual is ONE v_dot2_f32_bf16 -- a + (-1) * part_lo + 0 * part_hi (b: the
-// halves swapped) -- whose exact result (the bf16 x bf16 products are exact, the sum is representable) is what
-// the shift / mask + subtract pair computed, at half the VALU issue
-#ifndef MOPO_SPLIT_DOT2
-#define MOPO_SPLIT_DOT2 1
-#endif
+// rounds to nearest even; the residuals are exact subtractions of the parts' f32 values (a v_dot2_f32_bf16
+// form of the subtraction, a + (-1) * part, measured WRONG on gfx950: errors of 0.03-1 in the ensemble output)
 template <int P>
 __device__ __forceinline__ void split_bf16_pair(float a, float b, uint32_t (&out)[P]) {
 #pragma unroll
@@ -309,16 +305,8 @@ __device__ __forceinline__ void split_bf16_pair(float a, float b, uint32_t (&out
     asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(h) : "v"(a), "v"(b));
     out[p] = h;
     if (p + 1 < P) {
-      if (MOPO_SPLIT_DOT2) {
-        float ra, rb;
-        asm volatile("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(ra) : "v"(h), "s"(0x0000BF80u), "v"(a));
-        asm volatile("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(rb) : "v"(h), "s"(0xBF800000u), "v"(b));
-        a = ra;
-        b = rb;
-      } else {
-        a -= __builtin_bit_cast(float, h << 16);
-        b -= __builtin_bit_cast(float, h & 0xffff0000u);
-      }
+      a -= __builtin_bit_cast(float, h << 16);
+      b -= __builtin_bit_cast(float, h & 0xffff0000u);
     }
   }
 }

@@ -220,7 +220,7 @@ template <int FZ = 0>
 static __device__ __forceinline__ void policy_rows_block(const PolicyRows& c, int x, float* S, float* hs,
                                                          const Stamps& st, unsigned* sync = nullptr,
                                                          int nrb = 0) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = c.H, A = c.A, HS = H + 4, n = c.n;
   const int pcols = 16 * (int)(blockDim.x >> 6);   // dh1p columns of the block: one 16-wide tile per wave
   const int ncq = (H + pcols - 1) / pcols;
@@ -646,7 +646,7 @@ static __device__ __forceinline__ void fwd_block(const FwdArgsR a, int cq, int r
   auto& act_s = L.act_s;
   auto& da_s = L.da_s;
   stamp(a.st, 0);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const FwdInst p = pick4(a.in, ii);
   if (!HEAD && a.sync_reset && cq == 0 && rb == 0 && ii == 0 && tid < a.n_sync) a.sync_reset[tid * SYNC_STRIDE] = 0u;
   const int n = a.n, H = a.H, A = a.A;
@@ -991,7 +991,7 @@ static __device__ __forceinline__ void dh1_block(const Dh1Args a, int x, int y, 
   float* Ts = S.Ts;
   float* dqs = S.dqs;
   stamp(a.st, 0);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (z == 0) {
     const int zb = x + a.ncq1 * y;
     if (zb == 0) {

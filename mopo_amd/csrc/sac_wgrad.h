@@ -156,7 +156,7 @@ static __global__ __launch_bounds__(1024, 1) void sac_wgrad_kernel(const WgradAr
     return;
   }
   const int bid = (int)blockIdx.x - 1;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   int pi = 0;
   while (pi + 1 < g.np && bid >= g.prefix[pi + 1]) ++pi;
   const WgProb& p = g.p[pi];

@@ -562,7 +562,7 @@ static __device__ __forceinline__ void train_rows_body(const TrainRows& a, float
   float (*buf)[16 * TR_LD] = reinterpret_cast<float (*)[16 * TR_LD]>(lds);
   float (*zb)[16 * TR_LD] = reinterpret_cast<float (*)[16 * TR_LD]>(lds + 2 * 16 * TR_LD);
   float (*red)[64][17] = reinterpret_cast<float (*)[64][17]>(lds + (2 + TR_NHID) * 16 * TR_LD);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), li = lane & 15;
   const int M = a.M, IN = a.IN, H = a.H, D = a.D, i0 = rb * 16;
   const int c0 = 64 * (w & 3) + 4 * li + TR_TW * (w >> 2);   // this lane's first column
   auto wfwd = [&](int l) {

@@ -19,7 +19,7 @@ from collections import OrderedDict
 
 import numpy as np
 
-from .bnn import DEFAULT_ENSEMBLE_DTYPE, construct_model
+from .bnn import DEFAULT_ENSEMBLE_DTYPE, construct_model, default_ensemble_dtype
 from .fake_env import FakeEnv
 from .replay_pool import SimpleReplayPool
 from .rollout import ModelRollout
@@ -36,9 +36,10 @@ class MOPO:
                  rollout_random=False, evaluation_environment=None, eval_n_episodes=10, eval_deterministic=True,
                  max_path_length=1000, ensemble_dtype=None, actor_dtype=None, **kwargs):
         """``ensemble_dtype``: the ensemble forward's arithmetic (``mopo_amd.bnn.DTYPES``), default
-        ``DEFAULT_ENSEMBLE_DTYPE`` ('f16x3': f32 operands as two fp16 parts, f32 accumulate, held to
-        the fp32 parity tolerances); 'fp32' runs exact-f32 MFMA.  ``actor_dtype``: the rollout
-        policy forward ('fp32' / 'f16x3'; default fp32 with the fp32 ensemble, else f16x3:
+        ``DEFAULT_ENSEMBLE_DTYPE`` ('bf16x6': the f32 operands split exactly into 3 bf16 parts, 6 bf16
+        MFMA products, f32 accumulate; 'fp32' above H = 256: ``bnn.default_ensemble_dtype``); 'fp32' runs
+        exact-f32 MFMA, 'f16x3' ~22-bit operands.  ``actor_dtype``: the rollout policy forward ('fp32' /
+        'f16x3'; default fp32 beside the exact-operand ensembles fp32 and bf16x6, else f16x3:
         ``rollout.default_actor_dtype``)."""
         if kwargs.get('action_prior', 'uniform') != 'uniform':   # mopo.py:364 asserts the uniform prior
             raise AssertionError("MOPO's policy loss supports action_prior='uniform' only (mopo.py:364)")
@@ -49,7 +50,7 @@ class MOPO:
                                       num_networks=num_networks, num_elites=num_elites,
                                       separate_mean_var=separate_mean_var, name=model_name,
                                       load_dir=model_load_dir, deterministic=deterministic,
-                                      dtype=ensemble_dtype or DEFAULT_ENSEMBLE_DTYPE, seed=seed)   # the run seed (simple_run/main.py:180 set_seed) fixes the init
+                                      dtype=ensemble_dtype or default_ensemble_dtype(hidden_dim), seed=seed)   # the run seed (simple_run/main.py:180 set_seed) fixes the init
         self.fake_env = FakeEnv(self._model, static_fns, penalty_coeff=penalty_coeff,
                                 penalty_learned_var=penalty_learned_var)
         self._rollout_schedule = [20, 100, rollout_length, rollout_length]                 # mopo.py:137

@@ -93,10 +93,11 @@ _ACTOR_DTYPES = {'fp32': 0, 'f16x3': 4}
 
 
 def default_actor_dtype(ensemble_dtype):
-    """The rollout policy's arithmetic for an ensemble dtype: exact f32 beside the exact-f32 ensemble,
-    else the f16x3 actor (f32-class operands on the f16 MFMA, held to the fp32 actor tolerances) -- a
-    16-bit ensemble (f16x3, bf16x6, bf16x3, bf16) gets a 16-bit-MFMA actor, not the 9x slower f32 one."""
-    return 'fp32' if ensemble_dtype == 'fp32' else 'f16x3'
+    """The rollout policy's arithmetic for an ensemble dtype: exact-f32 MFMA beside the exact-operand
+    ensembles (fp32, bf16x6), so the whole rollout computes on the reference's f32 operands; else the f16x3
+    actor (~22-bit operands on the f16 MFMA, held to the fp32 actor tolerances) beside the reduced-operand
+    ensembles (f16x3, bf16x3, bf16)."""
+    return 'fp32' if ensemble_dtype in ('fp32', 'bf16x6') else 'f16x3'
 
 
 class ModelRollout:

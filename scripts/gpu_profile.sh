@@ -7,20 +7,21 @@
 # usage: TAG=r05 LEGS="C2_f16x3 C2_fp32" bash scripts/gpu_profile.sh
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 NOX="--no-cpu-baseline --no-c3 --no-alt-dtypes"
 declare -A A
 A[C2_f16x3]="--ensemble-dtype f16x3 --train-epochs 2"
+A[C2_bf16x6]="--ensemble-dtype bf16x6 --train-epochs 0 --sac-steps 16"
 A[C2_fp32]="--ensemble-dtype fp32 --train-epochs 0 --sac-steps 16"
 A[C3_bf16]="--config C3 --ensemble-dtype bf16 --train-epochs 0 --sac-steps 16"
 A[N2_f16x3]="--config N2 --ensemble-dtype f16x3 --train-epochs 0 --sac-steps 16"
 A[C5_fp32]="--config C5 --shards 8 --ensemble-dtype fp32 --train-epochs 0 --sac-steps 16 --steps 5 --warmup 2"
 A[C5_f16x3]="--config C5 --shards 8 --ensemble-dtype f16x3 --train-epochs 0 --sac-steps 16 --steps 5 --warmup 2"
 A[C5_bf16]="--config C5 --shards 8 --ensemble-dtype bf16 --train-epochs 0 --sac-steps 16 --steps 5 --warmup 2"
-LEGS=${LEGS:-"C2_f16x3 C2_fp32 C3_bf16 C5_fp32 C5_f16x3 C5_bf16"}
+LEGS=${LEGS:-"C2_f16x3 C2_bf16x6 C2_fp32 C3_bf16 C5_fp32 C5_f16x3 C5_bf16"}
 for L in $LEGS; do
   D=$R/$OUT/$L
   rm -rf $D && mkdir -p $D

@@ -101,7 +101,7 @@ def test_user_config_module_is_imported(tmp_path, monkeypatch, capsys):
     assert kw['hidden_dim'] == 64 and kw['n_epochs'] == 1000                # module value / default underneath
     assert kw['network_kwargs'] == {'hidden_sizes': [128, 128], 'activation': 'relu', 'output_activation': None}
     assert kw['model_name'] == 'walker2d-my-sweep_smv_1_0'
-    assert kw['ensemble_dtype'] == 'f16x3'
+    assert kw['ensemble_dtype'] == 'bf16x6'                                  # the product default at H <= 256
 
 
 def test_user_config_errors(tmp_path, monkeypatch):
