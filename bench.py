@@ -30,7 +30,7 @@ O, A, E, ELITES, H, HP = 17, 6, 7, 5, 200, 256
 ENV_ROWS = 101000
 FLOP_BNN_ROW = 2 * E * ((O + A) * H + 3 * H * H + 2 * H * (O + 1))       # 1,845,200
 FLOP_ACTOR_ROW = 2 * (O * HP + HP * HP + HP * 2 * A)                      # 145,920
-PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r05_pmc_summary.json')
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r06_pmc_summary.json')
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
 # ensemble dtype -> (bf16 parts per operand, bf16 products per f32 product); fp32 runs f32 MFMA
 SPLIT = {'bf16': (1, 1), 'bf16x3': (2, 3), 'bf16x6': (3, 6), 'f16x3': (2, 3)}
@@ -501,10 +501,10 @@ def sac_roofline(rate):
 def sac_pmc_traffic():
     """HBM bytes per SAC step from the committed PMC summary: the per-dispatch bytes of every per-step SAC
     launch (all ``mopo::sac_*`` kernels but the one-off batch gather and the logs read) summed, on the
-    default C2 f16x3 workload whose passes run 200 SAC steps (scripts/gpu_profile.sh)."""
+    default C2 workload (product-default dtype) whose passes run 200 SAC steps (scripts/gpu_profile.sh)."""
     if not os.path.exists(PMC_SUMMARY):
         return None
-    w = json.load(open(PMC_SUMMARY)).get('workloads', {}).get('C2 B=50000 h=5 dtype=f16x3')
+    w = json.load(open(PMC_SUMMARY)).get('workloads', {}).get('C2 B=50000 h=5 dtype=%s' % DEFAULT_ENSEMBLE_DTYPE)
     if not w:
         return None
     ks = [v for k, v in w['kernels'].items()

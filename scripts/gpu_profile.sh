@@ -4,7 +4,7 @@
 #      reduced per (kernel, grid size) by scripts/trace_summary.py, and
 #   2. the PMC passes of scripts/pmc.sh on the same workload, merged into one summary.
 # Outputs: gpurun_out/prof_$TAG/<leg>/{bench.json, stats/, trace.json, trace.txt}, gpurun_out/prof_$TAG/pmc_summary.json
-# usage: TAG=r05 LEGS="C2_f16x3 C2_fp32" bash scripts/gpu_profile.sh
+# usage: TAG=r06 LEGS="C2_bf16x6 C2_fp32" bash scripts/gpu_profile.sh  (NO_PMC=1: traces only; PMC_ONLY=1: PMC only)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD
 TAG=${TAG:-r06}
@@ -13,16 +13,17 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 NOX="--no-cpu-baseline --no-c3 --no-alt-dtypes"
 declare -A A
-A[C2_f16x3]="--ensemble-dtype f16x3 --train-epochs 2"
-A[C2_bf16x6]="--ensemble-dtype bf16x6 --train-epochs 0 --sac-steps 16"
+A[C2_f16x3]="--ensemble-dtype f16x3 --train-epochs 0 --sac-steps 16"
+A[C2_bf16x6]="--ensemble-dtype bf16x6 --train-epochs 2"
 A[C2_fp32]="--ensemble-dtype fp32 --train-epochs 0 --sac-steps 16"
 A[C3_bf16]="--config C3 --ensemble-dtype bf16 --train-epochs 0 --sac-steps 16"
-A[N2_f16x3]="--config N2 --ensemble-dtype f16x3 --train-epochs 0 --sac-steps 16"
+A[N2_bf16x6]="--config N2 --ensemble-dtype bf16x6 --train-epochs 0 --sac-steps 16"
 A[C5_fp32]="--config C5 --shards 8 --ensemble-dtype fp32 --train-epochs 0 --sac-steps 16 --steps 5 --warmup 2"
 A[C5_f16x3]="--config C5 --shards 8 --ensemble-dtype f16x3 --train-epochs 0 --sac-steps 16 --steps 5 --warmup 2"
 A[C5_bf16]="--config C5 --shards 8 --ensemble-dtype bf16 --train-epochs 0 --sac-steps 16 --steps 5 --warmup 2"
-LEGS=${LEGS:-"C2_f16x3 C2_bf16x6 C2_fp32 C3_bf16 C5_fp32 C5_f16x3 C5_bf16"}
+LEGS=${LEGS:-"C2_bf16x6 C2_f16x3 C2_fp32 N2_bf16x6 C3_bf16 C5_fp32 C5_f16x3 C5_bf16"}
 for L in $LEGS; do
+  [ -n "$PMC_ONLY" ] && break
   D=$R/$OUT/$L
   rm -rf $D && mkdir -p $D
   (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $D/stats -o run -- \
@@ -37,6 +38,6 @@ done
 for L in $LEGS; do
   # the PMC passes time a short bench of the same workload (the train leg only where it was traced)
   EXTRA=""
-  [ "$L" = "C2_f16x3" ] && EXTRA="--train-epochs 1 --sac-steps 200"
+  [ "$L" = "C2_bf16x6" ] && EXTRA="--train-epochs 1 --sac-steps 200"
   bash scripts/pmc.sh $OUT/pmc_summary.json ${A[$L]} --steps 3 --warmup 1 --prof-steps 2 $EXTRA || exit $?
 done
