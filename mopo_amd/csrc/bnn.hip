@@ -1102,8 +1102,8 @@ __global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_
       for (int nb = 0; nb < NBUL; ++nb) {
         const bf16x8 fr = fr_next;
         if (nb + 1 < NBUL) fr_next = *reinterpret_cast<const bf16x8*>(b + ((nb + 1) * 64 + lane) * 4);
-        // f16x3: part 0 of W meets both activation parts (x1 first), part 1 only the high part (the
-        // product order of layer_lds_split_f32)
+        // part p of W meets the activation parts q < P - p, the lowest first (the product order of
+        // layer_lds_split_f32; bf16x6 with x0 first measured the same: 91.4-91.6 vs 91.2-91.6M/s)
 #pragma unroll
         for (int q = P - 1 - p; q >= 0; --q)
           acc[nb] = (KHL && kg + 1 == KGL) ? mfma_16x16x16_lo<F16>(fr, cur[q], acc[nb])
