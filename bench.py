@@ -48,8 +48,8 @@ def dtype_desc(ensemble_dtype, actor_dtype=None):
     """The line's dtype: the ensemble forward's arithmetic and the rollout actor's (rollout.default_actor_dtype)."""
     from mopo_amd.rollout import default_actor_dtype
     act = actor_dtype or default_actor_dtype(ensemble_dtype)
-    return '%s; rollout actor: %s' % (DTYPE_DESC[ensemble_dtype], 'exact f32 MFMA' if act == 'fp32' else
-                                      'f16x3 (~22-bit operands)')
+    return '%s; rollout actor: %s' % (DTYPE_DESC[ensemble_dtype], {'fp32': 'exact f32 MFMA', 'bf16x6': 'the same exact '
+                                      'bf16x6 split'}.get(act, 'f16x3 (~22-bit operands)'))
 
 
 # BASELINE.json configs (SURVEY 8(d) table).  B_total = the config's rollout_batch; 'sharded': the batch is
@@ -93,7 +93,7 @@ def parse():
     p.add_argument('--ensemble-dtype', default=DEFAULT_ENSEMBLE_DTYPE, choices=list(DTYPES),
                    help='headline ensemble-forward arithmetic (mopo_amd.bnn.DTYPES); the default is the one '
                         'MOPO.train runs (mopo_amd.bnn.DEFAULT_ENSEMBLE_DTYPE)')
-    p.add_argument('--actor-dtype', default=None, choices=['fp32', 'f16x3'],
+    p.add_argument('--actor-dtype', default=None, choices=['fp32', 'bf16x6', 'f16x3'],
                    help="the rollout policy's arithmetic (default: mopo_amd.rollout.default_actor_dtype of the "
                         'ensemble dtype)')
     p.add_argument('--no-alt-dtypes', action='store_true',

@@ -115,8 +115,9 @@ int64_t mopo_sac_param_count(int obs_dim, int act_dim, int hidden);
 int mopo_actor_forward(const float* d_pi_params, int obs_dim, int act_dim, int hidden,
                        const void* d_obs, int obs_f64, int64_t B, const float* d_eps,
                        uint64_t seed, uint32_t step, float* d_act, float* d_mu, void* stream);
-/* The same with the arithmetic chosen: dtype 0 = fp32 (f32 MFMA), 4 = f16x3 (f32 operands as 2 fp16
- * parts under power-of-two scales, 3 f16 MFMA products, ~22-bit operands; hidden 32 or 256). */
+/* The same with the arithmetic chosen: dtype 0 = fp32 (f32 MFMA), 3 = bf16x6 (f32 operands split exactly into
+ * 3 bf16 parts, 6 bf16 MFMA products), 4 = f16x3 (f32 operands as 2 fp16 parts under power-of-two scales,
+ * 3 f16 MFMA products, ~22-bit operands); hidden 32 or 256 for the split forms. */
 int mopo_actor_forward_dtype(const float* d_pi_params, int obs_dim, int act_dim, int hidden,
                              const void* d_obs, int obs_f64, int64_t B, const float* d_eps,
                              uint64_t seed, uint32_t step, float* d_act, float* d_mu, int dtype, void* stream);
@@ -238,7 +239,7 @@ typedef struct {
                                84-86); the selection streams are unused */
   int rollout_random;       /* 1: actions ~ U(-1, 1) instead of the policy's (mopo.py:736-738) */
   const float* d_act_uniform; /* parity mode with rollout_random: [horizon, B, A] injected uniforms, or NULL */
-  int actor_dtype;          /* policy forward arithmetic: 0 fp32, 4 f16x3 (mopo_actor_forward_dtype) */
+  int actor_dtype;          /* policy forward arithmetic: 0 fp32, 3 bf16x6, 4 f16x3 (mopo_actor_forward_dtype) */
 } mopo_rollout_args;
 
 int mopo_rollout_create(mopo_rollout_t* out, mopo_bnn_t bnn, int64_t max_batch, int max_horizon);

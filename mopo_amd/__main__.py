@@ -39,7 +39,7 @@ def get_parser():
     p.add_argument('--model-dir', default=None)
     p.add_argument('--epochs', type=int, default=None)
     p.add_argument('--ensemble-dtype', default=None, choices=DTYPES)
-    p.add_argument('--actor-dtype', default=None, choices=('fp32', 'f16x3'))
+    p.add_argument('--actor-dtype', default=None, choices=('fp32', 'bf16x6', 'f16x3'))
     for f in ('--cpus', '--gpus', '--trial-cpus', '--trial-extra-cpus', '--max-failures'):
         p.add_argument(f, type=int, default=None)
     for f in ('--trial-gpus', '--trial-extra-gpus'):

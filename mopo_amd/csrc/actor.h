@@ -30,7 +30,7 @@ struct ActorArgs {
   // Philox -- and replace the policy's (still computed, as the reference calls get_action_meta first)
   int rand_act; const float* act_uni;
   // 0: f32 MFMA on the fragment-major f32 packing; 4 (DT_F16X3): the f16x3 split (mlp_tile.h) on the
-  // f16 packing (pack_actor with f16 = 1)
+  // f16 packing (pack_actor with split = 1); 3 (DT_BF16X6): the exact 3-part bf16 split (split = 2)
   int dtype;
   // 1: no other launch runs beside this one (an unsplit rollout): the f16x3 ring actor (actor_f16q_kernel,
   // 203 VGPRs), faster alone, slower beside the other row part's ensemble launch
@@ -38,7 +38,7 @@ struct ActorArgs {
 };
 
 int launch_actor(const ActorArgs& a, hipStream_t s);
-__host__ __device__ int64_t actor_packed_floats(int O, int Hp, int f16 = 0);
-int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s, int f16 = 0);
+__host__ __device__ int64_t actor_packed_floats(int O, int Hp, int split = 0);
+int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s, int split = 0);
 
 }  // namespace mopo

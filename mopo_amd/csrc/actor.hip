@@ -19,9 +19,12 @@ namespace mopo {
 // then 3 inverse weight scales (+5 spare floats) and actor_wmax_kernel's WMAX_BLOCKS x 3 partial max-|W|
 constexpr int WMAX_BLOCKS = 64;   // actor_wmax_kernel's grid (<= 64: one wave reduces the partials)
 
-__host__ __device__ int64_t actor_packed_floats(int O, int Hp, int f16) {
+// split: 0 f32 fragments, 1 f16x3 (2 scaled fp16 parts), 2 bf16x6 (the exact 3-part bf16 split, no scales):
+// W1 [1][3][NB] | W2 [NB/2][3][NB] | head [NB/2][3][1] fragments, then the biases
+__host__ __device__ int64_t actor_packed_floats(int O, int Hp, int split) {
   const int KG0 = (O + 15) / 16, NB = (Hp + 15) / 16;
-  if (f16) return (int64_t)(2 * NB + NB * NB + NB) * 256 + 2LL * NB * 16 + 16 + 8 + 3 * WMAX_BLOCKS;
+  if (split == 2) return (int64_t)(3 * NB + 3 * (NB / 2) * NB + 3 * (NB / 2)) * 256 + 2LL * NB * 16 + 16;
+  if (split) return (int64_t)(2 * NB + NB * NB + NB) * 256 + 2LL * NB * 16 + 16 + 8 + 3 * WMAX_BLOCKS;
   return (int64_t)KG0 * NB * 256 + (int64_t)NB * NB * 256 + (int64_t)NB * 256 + 2LL * NB * 16 + 16;
 }
 
@@ -119,6 +122,57 @@ __global__ void pack_actor_f16_kernel(const float* __restrict__ P, int O, int A,
   }
 }
 
+// bf16x6 packing: part p of the exact split (split_bf16<3>) of each weight in the bf16 fragment layout
+// (k permutation of the ensemble's), [kg][p][nb] per matrix; the biases as in the f32 packing
+__global__ void pack_actor_x6_kernel(const float* __restrict__ P, int O, int A, int Hp, float* __restrict__ dst) {
+  constexpr int NP = 3;
+  const int NB = ceil_div(Hp, 16), KG = NB / 2;
+  const float* W1 = P;
+  const float* W2 = W1 + O * Hp + Hp;
+  const float* Wm = W2 + Hp * Hp + Hp;
+  const float* Wl = Wm + Hp * A + A;
+  const int64_t f1 = (int64_t)NP * NB, f2 = (int64_t)KG * NP * NB, fh = (int64_t)KG * NP;
+  const int64_t nfrag = (f1 + f2 + fh) * 512;  // bf16 elements
+  short* d16 = reinterpret_cast<short*>(dst);
+  float* tail = dst + (f1 + f2 + fh) * 256;
+  const int64_t total = nfrag + 2LL * NB * 16 + 16;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < nfrag) {
+      const int j = i & 7, lane = (int)((i >> 3) & 63), g = lane >> 4, r = lane & 15;
+      int64_t f = i >> 9;
+      int which, nbs;
+      if (f < f1) { which = 0; nbs = NB; }
+      else if (f < f1 + f2) { which = 1; f -= f1; nbs = NB; }
+      else { which = 2; f -= f1 + f2; nbs = 1; }
+      const int nb = (int)(f % nbs), p = (int)((f / nbs) % NP), kg = (int)(f / (NP * nbs));
+      int k = kg * 32 + bf16_kperm(g, j);
+      const int n = nb * 16 + r;
+      float v = 0.f;
+      if (which == 0) {
+        k = slot_feat(k, O);
+        if (k >= 0 && n < Hp) v = W1[k * Hp + n];
+      } else if (which == 1) {
+        if (k < Hp && n < Hp) v = W2[k * Hp + n];
+      } else if (k < Hp) {
+        v = r < A ? Wm[k * A + r] : (r < 2 * A ? Wl[k * A + (r - A)] : 0.f);
+      }
+      short parts[NP];
+      split_bf16<NP>(v, parts);
+      d16[i] = p == 0 ? parts[0] : (p == 1 ? parts[1] : parts[2]);
+    } else {
+      const int j = (int)(i - nfrag);  // b1 | b2 | [bmu | bls]
+      float v;
+      if (j < NB * 16) v = j < Hp ? W1[O * Hp + j] : 0.f;
+      else if (j < 2 * NB * 16) v = j - NB * 16 < Hp ? W2[Hp * Hp + j - NB * 16] : 0.f;
+      else {
+        const int q = j - 2 * NB * 16;
+        v = q < A ? Wm[Hp * A + q] : (q < 2 * A ? Wl[Hp * A + q - A] : 0.f);
+      }
+      tail[j] = v;
+    }
+  }
+}
+
 // One launch packs the whole policy (it is repacked at every rollout, after the SAC updates):
 // W1 (observation side in slot_feat order), W2, the combined head (n < A -> Wmu[:, n],
 // A <= n < 2A -> Wls[:, n - A]) fragment-major (mlp_tile.h), then the zero-padded biases.
@@ -162,7 +216,17 @@ __global__ void pack_actor_kernel(const float* __restrict__ P, int O, int A, int
   }
 }
 
-int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s, int f16) {
+int pack_actor(const float* P, int O, int A, int Hp, float* dst, hipStream_t s, int split) {
+  if (split == 2) {
+    MOPO_REQUIRE(Hp % 32 == 0, "actor bf16x6: hidden width must be a multiple of 32");
+    MOPO_REQUIRE(O <= 32 && 2 * A <= 16, "actor bf16x6: obs_dim <= 32, act_dim <= 8");
+    const int64_t tot = actor_packed_floats(O, Hp, 2) * 2;   // upper bound on the elements the kernel walks
+    hipLaunchKernelGGL(pack_actor_x6_kernel, dim3((int)std::min<int64_t>((tot + 255) / 256, 1024)), dim3(256), 0, s,
+                       P, O, A, Hp, dst);
+    MOPO_HIP(hipGetLastError());
+    return 0;
+  }
+  const int f16 = split;
   if (f16) {
     MOPO_REQUIRE(Hp % 32 == 0, "actor f16x3: hidden width must be a multiple of 32");
     MOPO_REQUIRE(O <= 32 && 2 * A <= 16, "actor f16x3: obs_dim <= 32, act_dim <= 8");
@@ -489,6 +553,68 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16_kernel(const Acto
   actor_finish(a, head, wv, m, g, row, ok);
 }
 
+// bf16x6 policy forward: every f32 operand split EXACTLY into 3 RN bf16 parts (mlp_tile.h split_bf16), the 6
+// products p + q < 3 per k-group on the bf16 MFMA, f32 accumulate and f32 epilogues -- the reference's f32
+// operands, like the bf16x6 ensemble beside it; the f16x3 kernel's structure without scales
+template <int NBP>
+__global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_x6_kernel(const ActorArgs a) {
+  constexpr int P = 3, KG = NBP / 2;
+  constexpr int SLOT = Stage<NBP, ACT_WAVES>::SLOTS * 256;
+  __shared__ float head[ACT_WAVES][16][25];
+  __shared__ __attribute__((aligned(16))) float lds[2 * SLOT];
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), m = lane & 15, g = lane >> 4;
+  const int64_t count = a.d_count ? (int64_t)*a.d_count : a.B;
+  if ((int64_t)blockIdx.x * ACT_WAVES * 16 >= count) return;  // whole workgroup past the live rows
+  const int64_t row = ((int64_t)blockIdx.x * ACT_WAVES + wv) * 16 + m;
+  const bool ok = row < count;
+  const int O = a.O;
+  const float* w1f = a.Wpk;
+  const float* w2f = w1f + P * NBP * 256;
+  const float* whf = w2f + KG * P * NBP * 256;
+  const float* b1 = whf + KG * P * 256;
+  const float* b2 = b1 + NBP * 16;
+  const float* bh = b2 + NBP * 16;
+  bf16x8 x0[P][1];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = slot_feat(bf16_kperm(g, j), O);
+    float v = 0.f;
+    if (ok && k >= 0)
+      v = a.obs_f64 ? (float)reinterpret_cast<const double*>(a.obs)[row * O + k]
+                    : reinterpret_cast<const float*>(a.obs)[row * O + k];
+    short parts[P];
+    split_bf16<P>(v, parts);
+#pragma unroll
+    for (int p = 0; p < P; ++p) x0[p][0][j] = parts[p];
+  }
+  f32x4 acc[NBP];
+  float hf[KG][8];
+  auto to_input = [&](const float* b) {  // acc + bias, relu (mopo.py:277-278, 301)
+#pragma unroll
+    for (int c = 0; c < KG; ++c) {
+      const f32x4 b0 = ld4(b + (2 * c) * 16 + 4 * g), bb1 = ld4(b + (2 * c + 1) * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        hf[c][t] = fmaxf(acc[2 * c][t] + b0[t], 0.f);
+        hf[c][4 + t] = fmaxf(acc[2 * c + 1][t] + bb1[t], 0.f);
+      }
+    }
+  };
+  layer_lds_split<1, NBP, ACT_WAVES, SLOT, P, 1, false>(w1f, x0, acc, lds, wv, lane);
+  to_input(b1);
+  layer_lds_split_f32<KG, NBP, ACT_WAVES, SLOT, P, 1, false>(w2f, hf, acc, lds, wv, lane);
+  to_input(b2);
+  f32x4 hd[1];
+  layer_lds_split_f32<KG, 1, ACT_WAVES, SLOT, P, 1, false>(whf, hf, hd, lds, wv, lane);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n = 4 * g + t;
+    head[wv][m][n] = hd[0][t] + bh[n];   // mu | log_std (mopo.py:302-303)
+  }
+  __syncthreads();
+  actor_finish(a, head, wv, m, g, row, ok);
+}
+
 // f16x3 policy forward over R row blocks per wave (layer_f16_rows): actor_f16_kernel's arithmetic,
 // product for product, with layer 2's first slice prefetched during layer 1's last one and the whole
 // head ([mu | log_std], 2 KG fragments) prefetched during layer 2's last slice, so no layer starts on
@@ -762,6 +888,13 @@ int launch_actor(const ActorArgs& a, hipStream_t s) {
     return 0;
   }
 #endif
+  if (a.dtype == DT_BF16X6) {
+    if (a.Hp == 256) hipLaunchKernelGGL(actor_x6_kernel<16>, grid, block, 0, s, a);
+    else if (a.Hp == 32) hipLaunchKernelGGL(actor_x6_kernel<2>, grid, block, 0, s, a);
+    else return fail("actor bf16x6: unsupported hidden size (256 or 32)");
+    MOPO_HIP(hipGetLastError());
+    return 0;
+  }
   if (a.dtype == DT_F16X3) {
 #if ACT_F16_RING
     if (a.alone && a.Hp == 256) hipLaunchKernelGGL(actor_f16q_kernel<16>, grid, block, 0, s, a);
@@ -804,13 +937,14 @@ extern "C" int mopo_actor_forward_dtype(const float* P, int O, int A, int H, con
                                         const float* eps, uint64_t seed, uint32_t step, float* act, float* mu,
                                         int dtype, void* stream) {
   MOPO_REQUIRE(P && obs, "mopo_actor_forward: NULL pointer");
-  MOPO_REQUIRE(dtype == DT_FP32 || dtype == DT_F16X3, "mopo_actor_forward: dtype must be 0 (fp32) or 4 (f16x3)");
+  MOPO_REQUIRE(dtype == DT_FP32 || dtype == DT_F16X3 || dtype == DT_BF16X6,
+               "mopo_actor_forward: dtype must be 0 (fp32), 3 (bf16x6) or 4 (f16x3)");
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int f16 = dtype == DT_F16X3;
+  const int split = dtype == DT_F16X3 ? 1 : (dtype == DT_BF16X6 ? 2 : 0);
   float* wpk = nullptr;
-  MOPO_HIP(hipMallocAsync((void**)&wpk, actor_packed_floats(O, H, f16) * sizeof(float), s));
-  int rc = pack_actor(P, O, A, H, wpk, s, f16);
+  MOPO_HIP(hipMallocAsync((void**)&wpk, actor_packed_floats(O, H, split) * sizeof(float), s));
+  int rc = pack_actor(P, O, A, H, wpk, s, split);
   if (rc == 0) {
     ActorArgs a{};
     a.P = P; a.Wpk = wpk; a.O = O; a.A = A; a.Hp = H; a.dtype = dtype;

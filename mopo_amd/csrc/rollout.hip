@@ -425,8 +425,9 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
   }
   if (i0 == 0) {
     MOPO_HIP(hipGetLastError());
-    MOPO_REQUIRE(a->actor_dtype == DT_FP32 || a->actor_dtype == DT_F16X3, "rollout: actor_dtype must be 0 or 4");
-    const int f16 = a->actor_dtype == DT_F16X3;
+    MOPO_REQUIRE(a->actor_dtype == DT_FP32 || a->actor_dtype == DT_F16X3 || a->actor_dtype == DT_BF16X6,
+                 "rollout: actor_dtype must be 0 (fp32), 3 (bf16x6) or 4 (f16x3)");
+    const int f16 = a->actor_dtype == DT_F16X3 ? 1 : (a->actor_dtype == DT_BF16X6 ? 2 : 0);   // pack_actor's split
     if (!h->wpk || h->wpk_hp != a->pi_hidden || h->wpk_f16 != f16) {
       if (h->wpk) (void)hipFree(h->wpk);
       MOPO_HIP(hipMalloc(&h->wpk, actor_packed_floats(O, a->pi_hidden, f16) * sizeof(float)));

@@ -39,7 +39,7 @@ class MOPO:
         ``DEFAULT_ENSEMBLE_DTYPE`` ('bf16x6': the f32 operands split exactly into 3 bf16 parts, 6 bf16
         MFMA products, f32 accumulate; 'fp32' above H = 256: ``bnn.default_ensemble_dtype``); 'fp32' runs
         exact-f32 MFMA, 'f16x3' ~22-bit operands.  ``actor_dtype``: the rollout policy forward ('fp32' /
-        'f16x3'; default fp32 beside the exact-operand ensembles fp32 and bf16x6, else f16x3:
+        'bf16x6' / 'f16x3'; default the ensemble's for fp32 and bf16x6, else f16x3:
         ``rollout.default_actor_dtype``)."""
         if kwargs.get('action_prior', 'uniform') != 'uniform':   # mopo.py:364 asserts the uniform prior
             raise AssertionError("MOPO's policy loss supports action_prior='uniform' only (mopo.py:364)")

@@ -89,15 +89,15 @@ def split_params(flat, O, A, H=256):
     return out
 
 
-_ACTOR_DTYPES = {'fp32': 0, 'f16x3': 4}
+_ACTOR_DTYPES = {'fp32': 0, 'bf16x6': 3, 'f16x3': 4}
 
 
 def default_actor_dtype(ensemble_dtype):
-    """The rollout policy's arithmetic for an ensemble dtype: exact-f32 MFMA beside the exact-operand
-    ensembles (fp32, bf16x6), so the whole rollout computes on the reference's f32 operands; else the f16x3
-    actor (~22-bit operands on the f16 MFMA, held to the fp32 actor tolerances) beside the reduced-operand
-    ensembles (f16x3, bf16x3, bf16)."""
-    return 'fp32' if ensemble_dtype in ('fp32', 'bf16x6') else 'f16x3'
+    """The rollout policy's arithmetic for an ensemble dtype: the exact-operand forms beside the exact-operand
+    ensembles -- f32 MFMA beside fp32, the exact bf16x6 split beside bf16x6 -- so the whole rollout computes on
+    the reference's f32 operands; else the f16x3 actor (~22-bit operands on the f16 MFMA, held to the fp32
+    actor tolerances) beside the reduced-operand ensembles (f16x3, bf16x3, bf16)."""
+    return ensemble_dtype if ensemble_dtype in ('fp32', 'bf16x6') else 'f16x3'
 
 
 class ModelRollout:
@@ -125,7 +125,7 @@ class ModelRollout:
         ``penalty_learned_var`` / ``deterministic``: FakeEnv's modes (fake_env.py:69-110; every D4RL
         config uses the learned-var penalty, not deterministic); ``rollout_random``: uniform actions
         (mopo.py:736-738), ``act_uniform`` [horizon, B, A] injects them in parity mode.
-        ``actor_dtype``: 'fp32' or 'f16x3' policy forward (default: f16x3 with an f16x3 ensemble)."""
+        ``actor_dtype``: 'fp32', 'bf16x6' or 'f16x3' policy forward (default: default_actor_dtype)."""
         import torch
         dev = env_obs.device
         B = int(batch_size)

@@ -24,9 +24,8 @@ def main(argv=None):
     p.add_argument('--ensemble-dtype', default=None, choices=DTYPES,
                    help='ensemble forward arithmetic (default: the config kwarg ensemble_dtype, else %s)'
                         % DEFAULT_ENSEMBLE_DTYPE)
-    p.add_argument('--actor-dtype', default=None, choices=('fp32', 'f16x3'),
-                   help='rollout policy forward (default: fp32 beside the exact-operand ensembles fp32 and bf16x6, '
-                        'else f16x3)')
+    p.add_argument('--actor-dtype', default=None, choices=('fp32', 'bf16x6', 'f16x3'),
+                   help='rollout policy forward (default: the ensemble dtype for fp32 and bf16x6, else f16x3)')
     a = p.parse_args(argv)
     from .config import DIMS, get_params
     from .loader import restore_pool

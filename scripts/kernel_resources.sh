@@ -4,7 +4,7 @@
 cd "$(dirname "$0")/../mopo_amd/csrc"
 T=$(mktemp -d)
 for f in *.hip; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 --cuda-device-only $( [ "$f" = bnn.hip ] && echo -mllvm -pragma-unroll-threshold=262144) -Rpass-analysis=kernel-resource-usage \
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 --cuda-device-only $( [ "$f" = bnn.hip -o "$f" = actor.hip ] && echo -mllvm -pragma-unroll-threshold=262144) -Rpass-analysis=kernel-resource-usage \
     -c "$f" -o /dev/null > "$T/$f.txt" 2>&1 &
 done
 wait

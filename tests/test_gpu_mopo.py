@@ -217,7 +217,7 @@ def test_mopo_epoch_vs_oracle_epoch(K, dtype):
     K = 50: p50 <= 1e-6, p99 <= 1e-4, max <= 1e-3 (measured 1e-8 / 2e-6 / 9e-5); K = 200: p50 <= 1e-4,
     p99 <= 2e-3, max <= 2e-2 (measured 3.4e-5 / 5.0e-4 / 4.3e-3); and the last step's losses (logs) within
     1e-3 relative.  The exact-f32 MFMA ensemble + actor, the product default (the exact bf16x6 split + the
-    exact-f32 actor: ``mopo run_local``'s arithmetic) and f16x3 (+ the f16x3 actor) are all held to these same
+    bf16x6 actor: ``mopo run_local``'s arithmetic) and f16x3 (+ the f16x3 actor) are all held to these same
     bounds against the f64 oracle."""
     import torch
     from oracle import fake_env as ofe
@@ -311,7 +311,7 @@ def test_16bit_splits_track_fp32_over_epochs():
     end-to-end effect of the 22-bit operands on what SAC learns is pinned, not only per step.  SAC's
     training dynamics amplify any rounding difference (test_mopo_epoch_vs_oracle_epoch: the f32 device
     against the f64 oracle reaches p50 3e-5 / p99 5e-4 after 200 steps).  For both splits -- bf16x6 (the
-    product default, exact operands, with the exact-f32 actor) and f16x3 (~22-bit operands, f16x3 actor) --
+    product default, exact operands, with the bf16x6 actor) and f16x3 (~22-bit operands, f16x3 actor) --
     the scaled SAC parameter difference |x - fp32| / (1 + |fp32|) must stay within p50 <= 3e-4, p99 <= 3e-3,
     and f16x3's last losses within 1e-2 relative of fp32's (measured on MI355X: p50 1.5e-4 / p99 1.5e-3 for
     both -- the same order as the fp32 device's own drift from the f64 oracle, 3.4e-5 / 5.0e-4 after 200

@@ -124,7 +124,7 @@ def test_sac_steps_vs_reference_graph(path):
             assert np.abs(tgt - t_ref).max() <= 2e-6 + 5e-3 * 2 * sum(lr_t[:k + 1])
 
 
-@pytest.mark.parametrize('dtype', [0, 4])   # fp32, f16x3
+@pytest.mark.parametrize('dtype', [0, 3, 4])   # fp32, bf16x6, f16x3
 @pytest.mark.parametrize('path', SAC, ids=[os.path.basename(p)[8:-4] for p in SAC])
 def test_actor_vs_reference_graph(path, dtype):
     """get_action_meta (mopo.py:468-485): pi and the deterministic mu for the step-0 batch."""

@@ -98,7 +98,7 @@ def test_fakeenv_step_vs_reference_golden(path):
         assert near.all()
 
 
-@pytest.mark.parametrize('dtype', [0, 4])   # fp32, f16x3
+@pytest.mark.parametrize('dtype', [0, 3, 4])   # fp32, bf16x6, f16x3
 def test_actor_forward_vs_oracle(dtype):
     import torch
     from mopo_amd import _lib as L
