@@ -129,6 +129,7 @@ extern "C" int mopo_fakeenv_step(mopo_bnn_t hh, const mopo_fakeenv_args* a, void
   MOPO_REQUIRE(h && a, "mopo_fakeenv_step: NULL argument");
   MOPO_REQUIRE(h->O + 1 <= MAXD, "mopo_fakeenv_step: obs_dim too large");
   MOPO_REQUIRE(a->B >= 0, "mopo_fakeenv_step: negative batch");
+  MOPO_REQUIRE(a->term_kind >= 0 && a->term_kind < MOPO_TERM_KINDS, "mopo_fakeenv_step: unknown term_kind");
   if (a->B == 0) return 0;  // empty batch: nothing to read or write (empty buffers may be NULL)
   MOPO_REQUIRE(a->d_ens_mean && a->d_ens_var, "mopo_fakeenv_step: ensemble workspaces required");
   MOPO_REQUIRE(a->deterministic || (a->d_noise_sel && a->d_model_inds),

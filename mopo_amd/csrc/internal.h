@@ -106,7 +106,18 @@ __device__ __forceinline__ bool term_fn_at(int kind, const F& nobs, int O) {
     bool not_done = fin && small && (hh > 0.7) && (fabs(an) < 0.2);
     return !not_done;
   }
-  return false;  // halfcheetah.py:9-10
+  if (kind == MOPO_TERM_ANT) {  // ant.py:9-15, antangle.py:9-15
+    bool fin = true;
+    for (int d = 0; d < O; ++d) fin = fin && isfinite(nobs(d));
+    double x = nobs(0);
+    bool not_done = fin && (x >= 0.2) && (x <= 1.0);
+    return !not_done;
+  }
+  if (kind == MOPO_TERM_HUMANOID) {  // humanoid.py:10-11 (NaN compares false: not done)
+    double z = nobs(0);
+    return (z < 1.0) || (z > 2.0);
+  }
+  return false;  // halfcheetah.py:9-10 and the other never-done domains
 }
 
 __device__ __forceinline__ bool term_fn(int kind, const double* nobs, int O) {

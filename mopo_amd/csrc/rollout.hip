@@ -385,6 +385,7 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
   MOPO_REQUIRE(a && p, "rollout: NULL argument");
   MOPO_REQUIRE(a->B >= 0 && a->B <= h->Bmax, "rollout: B exceeds the handle's max_batch");
   MOPO_REQUIRE(a->horizon >= 0 && a->horizon <= h->Hmax, "rollout: horizon exceeds max_horizon");
+  MOPO_REQUIRE(a->term_kind >= 0 && a->term_kind < MOPO_TERM_KINDS, "rollout: unknown term_kind");
   MOPO_REQUIRE(a->d_env_obs && a->env_size > 0, "rollout: empty env pool");
   MOPO_REQUIRE(a->d_pi_params, "rollout: NULL policy params");
   MOPO_REQUIRE(a->d_model_inds || (a->d_elites && a->n_elites > 0), "rollout: elites required");

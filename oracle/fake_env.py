@@ -4,7 +4,9 @@ Follows (reference xionghuichen/mopo):
   * ``FakeEnv.step``           mopo/models/fake_env.py:37-131
   * ``FakeEnv._get_logprob``   mopo/models/fake_env.py:20-35
   * ``BNN.random_inds``        mopo/models/bnn.py:342-344
-  * termination functions      mopo/static/halfcheetah.py:6-11, walker2d.py:6-17, hopper.py:6-18
+  * termination functions      mopo/static/halfcheetah.py:6-11, walker2d.py:6-17, hopper.py:6-18,
+                               ant.py:6-17, antangle.py:6-17, humanoid.py:7-15 and the never-done
+                               halfcheetahjump/vel/veljump, point2denv, point2dwallenv, pendulum
 
 Pinned against golden vectors from the reference's own ``FakeEnv.step`` and
 ``mopo/static`` (tests/golden/make_golden.py).
@@ -36,7 +38,25 @@ def term_hopper(obs, act, next_obs):
     return (~not_done)[:, None]
 
 
-TERMINATION = {'halfcheetah': term_halfcheetah, 'walker2d': term_walker2d, 'hopper': term_hopper}
+def term_ant(obs, act, next_obs):
+    # ant.py:6-17 (antangle.py is the same rule)
+    x = next_obs[:, 0]
+    not_done = np.isfinite(next_obs).all(axis=-1) * (x >= 0.2) * (x <= 1.0)
+    return (~not_done)[:, None]
+
+
+def term_humanoid(obs, act, next_obs):
+    # humanoid.py:7-15; bool + bool is logical or
+    z = next_obs[:, 0]
+    return ((z < 1.0) | (z > 2.0))[:, None]
+
+
+TERMINATION = {'halfcheetah': term_halfcheetah, 'walker2d': term_walker2d, 'hopper': term_hopper,
+               'ant': term_ant, 'antangle': term_ant, 'humanoid': term_humanoid}
+for _d in ('halfcheetahjump', 'halfcheetahvel', 'halfcheetahveljump', 'point2denv', 'point2dwallenv'):
+    TERMINATION[_d] = term_halfcheetah
+# pendulum.py:9 returns np.zeros((n, 1)) (float); its truth value is the never-done rule
+TERMINATION['pendulum'] = term_halfcheetah
 
 
 def get_logprob(x, means, variances):

@@ -74,6 +74,25 @@ def test_termination_vs_reference():
         np.testing.assert_array_equal(ofe.TERMINATION[d](dummy[0], dummy[1], nobs), z['done_' + d])
 
 
+def test_termination_more_domains_vs_reference():
+    """ant, antangle, humanoid and the never-done domains: oracle and the host StaticFns vs the reference's
+    own termination_fn outputs (tests/golden/make_termination_more.py)."""
+    from mopo_amd.static import static_fns, term_kind_of
+    z = np.load(os.path.join(GOLD, 'termination_more.npz'))
+    nobs = z['next_obs']
+    dummy = np.zeros((len(nobs), 17)), np.zeros((len(nobs), 6))
+    for d in ('ant', 'antangle', 'humanoid', 'halfcheetahjump', 'halfcheetahvel', 'halfcheetahveljump',
+              'point2denv', 'point2dwallenv', 'pendulum'):
+        ref = np.asarray(z['done_' + d]).astype(bool)         # pendulum.py returns float zeros
+        with np.errstate(invalid='ignore'):
+            np.testing.assert_array_equal(ofe.TERMINATION[d](dummy[0], dummy[1], nobs), ref)
+        np.testing.assert_array_equal(static_fns[d].termination_fn(dummy[0], dummy[1], nobs), ref)
+        # the reference's StaticFns classes map to the same device kind by module name
+        ref_like = type('StaticFns', (), {'__module__': 'ref_static_' + d})
+        assert term_kind_of(ref_like) == static_fns[d].term_kind
+    assert z['done_ant'].any() and z['done_humanoid'].any() and not z['done_ant'].all()
+
+
 def test_pool_vs_reference():
     z = np.load(os.path.join(GOLD, 'pool_trace.npz'))
     pool = opool.Pool(17, 6, int(z['max_size']))
