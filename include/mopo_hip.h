@@ -73,7 +73,7 @@ int64_t mopo_bnn_packed_bytes(mopo_bnn_t h);
 int mopo_bnn_packed_copy(mopo_bnn_t h, int to_handle, void* d_buf, int64_t nbytes, void* stream);
 
 /* ---- FakeEnv.step ------------------------------------------------------------------- */
-/* termination rules of mopo/static/*.py: NONE covers halfcheetah{,jump,vel,veljump}, point2denv,
+/* termination rules of mopo/static/<domain>.py: NONE covers halfcheetah{,jump,vel,veljump}, point2denv,
  * point2dwallenv and pendulum (never done); ANT covers ant.py / antangle.py; HUMANOID humanoid.py */
 enum { MOPO_TERM_NONE = 0, MOPO_TERM_HALFCHEETAH = 0, MOPO_TERM_WALKER2D = 1, MOPO_TERM_HOPPER = 2,
        MOPO_TERM_ANT = 3, MOPO_TERM_HUMANOID = 4, MOPO_TERM_KINDS = 5 };

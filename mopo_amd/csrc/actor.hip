@@ -556,6 +556,9 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_f16_kernel(const Acto
 // bf16x6 policy forward: every f32 operand split EXACTLY into 3 RN bf16 parts (mlp_tile.h split_bf16), the 6
 // products p + q < 3 per k-group on the bf16 MFMA, f32 accumulate and f32 epilogues -- the reference's f32
 // operands, like the bf16x6 ensemble beside it; the f16x3 kernel's structure without scales
+#ifndef ACT_X6_HEAD_PS
+#define ACT_X6_HEAD_PS 3
+#endif
 template <int NBP>
 __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_x6_kernel(const ActorArgs a) {
   constexpr int P = 3, KG = NBP / 2;
@@ -605,7 +608,8 @@ __global__ __launch_bounds__(ACT_WAVES * 64, 2) void actor_x6_kernel(const Actor
   layer_lds_split_f32<KG, NBP, ACT_WAVES, SLOT, P, 1, false>(w2f, hf, acc, lds, wv, lane);
   to_input(b2);
   f32x4 hd[1];
-  layer_lds_split_f32<KG, 1, ACT_WAVES, SLOT, P, 1, false>(whf, hf, hd, lds, wv, lane);
+  // the head's P parts of a k-group as one slice (3 fragments, contiguous in the packing): KG barriers, not P KG
+  layer_lds_split_f32<KG, 1, ACT_WAVES, SLOT, P, ACT_X6_HEAD_PS, false>(whf, hf, hd, lds, wv, lane);
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int n = 4 * g + t;

@@ -891,6 +891,20 @@ __global__ __launch_bounds__(WAVES * 64, R == 1 ? 2 : 1) void bnn_fwd_f16r_kerne
 #define BNN_F16Q_DEFER 1
 #endif
 
+#ifndef BNN_RING_HEAD_MERGE
+#define BNN_RING_HEAD_MERGE 1   // the head's weight parts of a k-group in one ring slice (bnn_fwd_ring_kernel)
+#endif
+
+#ifndef BNN_RING_PF
+#define BNN_RING_PF 3   // ring kernel: fragment reads in flight ahead of the MFMAs (P = 1, 2)
+#endif
+#ifndef BNN_RING_PF_X6
+#define BNN_RING_PF_X6 3   // the same for bf16x6 (5 and more spill at its 168-VGPR cap)
+#endif
+#ifndef BNN_RING_PIN
+#define BNN_RING_PIN 1
+#endif
+
 #ifndef BNN_RING_WAVES
 #define BNN_RING_WAVES 4  // waves per workgroup (16 rows each) sharing one ring
 #endif
@@ -907,10 +921,13 @@ __global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_
   static_assert(P == 1 || P == 2 || P == 3, "1: bf16, 2: f16x3, 3: bf16x6 (the exact 3-part bf16 split)");
   static_assert(DEPTH >= 3, "ring of at least 3 slots");
   constexpr bool F16 = P == 2;
-  constexpr int KG = NB2 / 2, NS = P + 4 * KG * P;
+  // the head's slices carry HPS weight parts each: all P of a k-group where they fit a hidden layer's slot
+  // (its P NBO fragments are contiguous in the packing), so the narrow head runs behind KG barriers, not P KG
+  constexpr int HPS = BNN_RING_HEAD_MERGE && Stage<P * NBO, WAVES>::SLOTS <= Stage<NB2, WAVES>::SLOTS ? P : 1;
+  constexpr int KG = NB2 / 2, NS = P + 3 * KG * P + KG * (P / HPS);
   constexpr int JHEAD = P + 3 * KG * P;  // the head's first slice
   constexpr bool KH = NBU < NB2;
-  constexpr int SLOT = Stage<(NB2 > NBO ? NB2 : NBO), WAVES>::SLOTS * 256;
+  constexpr int SLOT = Stage<(NB2 > HPS * NBO ? NB2 : HPS * NBO), WAVES>::SLOTS * 256;
   constexpr int BIAS_LDS = (NB2 * 4 + 63) / 64 * 256;
   // two bias slots: layer L's bias (slot L & 1) goes out at the top of layer L - 1's first slice, so it
   // has a whole layer of slice waits behind it whatever the depth
@@ -943,7 +960,7 @@ __global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_
     constexpr int J = decltype(jc)::value;
     if constexpr (J < NS) {
       constexpr int L = J < P ? 0 : 1 + (J - P) / (P * KG);
-      constexpr int NF = L == 4 ? NBO : NB2;
+      constexpr int NF = L == 4 ? HPS * NBO : NB2;
       constexpr int s = J - (L == 0 ? 0 : P + P * KG * (L - 1));
       stage_slice<NF, WAVES>(src[L] + s * NF * 256, lds + (J % DEPTH) * SLOT, wv, lane);
     }
@@ -1036,11 +1053,16 @@ __global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_
     }
   };
   // the operand parts of k-group kg of `in`: f16x3 the two scaled fp16 parts, bf16 the RN bf16 values
-  auto parts = [&](const float (&v)[8], auto prescaled) {
+  // half: only values 0..3 feed the half-K MFMA of a layer's last k-group (KH); the rest are not split
+  auto parts = [&](const float (&v)[8], auto prescaled, auto half) {
     if constexpr (F16) {
       u32x4v h4, l4;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        if (decltype(half)::value && q >= 2) {
+          h4[q] = l4[q] = 0u;
+          continue;
+        }
         const F16Pair pr = decltype(prescaled)::value ? split_f16_pair_prescaled(v[2 * q], v[2 * q + 1])
                                                       : split_f16_pair(v[2 * q], v[2 * q + 1], s_in);
         h4[q] = pr.hi;
@@ -1052,6 +1074,11 @@ __global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_
       u32x4v p4[3];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        if (decltype(half)::value && q >= 2) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) p4[k][q] = 0u;
+          continue;
+        }
         uint32_t pr[3];
         split_bf16_pair<3>(v[2 * q], v[2 * q + 1], pr);
 #pragma unroll
@@ -1071,21 +1098,23 @@ __global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_
     constexpr bool KHL = L > 0 && KH;
     constexpr bool DEFER = DEF && L > 0;   // `in` holds u; y' made one k-group ahead
     constexpr int J0 = L == 0 ? 0 : P + P * KG * (L - 1);
+    constexpr int PPS = L == 4 ? HPS : 1, SPK = P / PPS;   // weight parts per slice, slices per k-group
 #pragma unroll
     for (int nb = 0; nb < NBL; ++nb) acc[nb] = zero4();
     if constexpr (DEFER) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) act(0, j);
     }
-    RingRun<J0, J0 + P * KGL>::run([&](auto jc) {
-      constexpr int J = decltype(jc)::value, s = J - J0, kg = s / P, p = s % P;
+    RingRun<J0, J0 + SPK * KGL>::run([&](auto jc) {
+      constexpr int J = decltype(jc)::value, s = J - J0, kg = s / SPK, p0 = (s % SPK) * PPS;
       // made when the k-group is first consumed (layers > 0 under FOLD hold y' s already)
-      if constexpr (p == 0) parts(in[kg], std::integral_constant<bool, FOLD && (L > 0)>{});
+      if constexpr (p0 == 0)
+        parts(in[kg], std::integral_constant<bool, FOLD && (L > 0)>{}, std::integral_constant<bool, KHL && kg + 1 == KGL>{});
       // slice J landed (every later slice still in flight may stay so) ... for every wave, and every wave
       // is done with the buffer slice J + DEPTH - 1 goes into (slice J - 1's)
       constexpr int N = [] {
         int n = 0;
-        for (int i = 1; i <= DEPTH - 2; ++i) n += (J + i >= NS ? 0 : (((J + i >= JHEAD) ? NBO : NB2) + WAVES - 1) / WAVES);
+        for (int i = 1; i <= DEPTH - 2; ++i) n += (J + i >= NS ? 0 : (((J + i >= JHEAD) ? HPS * NBO : NB2) + WAVES - 1) / WAVES);
         return n;
       }();
       wait_vm_lgkm0<N>();
@@ -1097,11 +1126,21 @@ __global__ __launch_bounds__(WAVES * 64, ((P == 3 ? BNN_RING_MINB_X6 : BNN_RING_
       issue(std::integral_constant<int, J + DEPTH - 1>{});
       __builtin_amdgcn_sched_barrier(0);
       const float* b = lds + (J % DEPTH) * SLOT;
-      bf16x8 fr_next = *reinterpret_cast<const bf16x8*>(b + lane * 4);
+      // fragment i = pp NBL + nb of the slice: weight part p0 + pp, output block nb
+      auto frag = [&](int i) { return *reinterpret_cast<const bf16x8*>(b + (((i / NBUL) * NBL + i % NBUL) * 64 + lane) * 4); };
+      // fragments read BNN_RING_PF ahead of their MFMAs, each read pinned ahead of the MFMAs that follow it
+      // (left to itself the scheduler sinks it to just before its use: an exposed LDS latency per pair)
+      constexpr int PF = P == 3 ? BNN_RING_PF_X6 : BNN_RING_PF, NFR = PPS * NBUL;
+      bf16x8 fq[PF];
 #pragma unroll
-      for (int nb = 0; nb < NBUL; ++nb) {
-        const bf16x8 fr = fr_next;
-        if (nb + 1 < NBUL) fr_next = *reinterpret_cast<const bf16x8*>(b + ((nb + 1) * 64 + lane) * 4);
+      for (int k = 0; k < PF; ++k)
+        if (k < NFR) fq[k] = frag(k);
+#pragma unroll
+      for (int i = 0; i < NFR; ++i) {
+        const int p = p0 + i / NBUL, nb = i % NBUL;
+        const bf16x8 fr = fq[i % PF];
+        if (i + PF < NFR) fq[i % PF] = frag(i + PF);
+        if constexpr (BNN_RING_PIN) __builtin_amdgcn_sched_barrier(0x0406);   // VALU, SALU, transcendentals may cross
         // part p of W meets the activation parts q < P - p, the lowest first (the product order of
         // layer_lds_split_f32; bf16x6 with x0 first measured the same: 91.4-91.6 vs 91.2-91.6M/s)
 #pragma unroll

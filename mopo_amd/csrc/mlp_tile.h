@@ -422,6 +422,9 @@ __device__ __forceinline__ void row_scale(float mx, float& s, float& inv) {
 #ifndef MOPO_SPLIT_PF
 #define MOPO_SPLIT_PF 1  // LDS fragment reads in flight in layer_lds_split_f32
 #endif
+#ifndef MOPO_SPLIT_PIN
+#define MOPO_SPLIT_PIN 1
+#endif
 // layer_lds_split with f32 activations held (8 VGPRs per k-group instead of 4 * P): each k-group's P
 // bf16 parts are split when its first slice is consumed, so only one k-group's parts are live.
 // F16: the 2 fp16 parts of in * s (split_f16_scaled; s = the row scale) on the f16 MFMA.
@@ -504,6 +507,8 @@ __device__ __forceinline__ void layer_lds_split_f32(const float* __restrict__ wf
       const int pp = i / NB, nb = i % NB, p = (s % SPK) * PS + pp;
       const bf16x8 fr = ring[u % D];
       if (u + D < NU) ring[u % D] = *reinterpret_cast<const bf16x8*>(b + (frag_at(u + D) * 64 + lane) * 4);
+      // the read stays ahead of the MFMAs that follow it (bnn_fwd_ring_kernel's BNN_RING_PIN)
+      if constexpr (MOPO_SPLIT_PIN) __builtin_amdgcn_sched_barrier(0x0406);
 #pragma unroll
       for (int q = P - 1 - p; q >= 0; --q)
         acc[nb] = (KH && kg + 1 == KG) ? mfma_16x16x16_lo<F16>(fr, cur[q], acc[nb])
