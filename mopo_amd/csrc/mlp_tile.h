@@ -235,6 +235,9 @@ __host__ __device__ __forceinline__ int bf16_kperm(int g, int j) { return j < 4 
 
 __device__ __forceinline__ short to_bf16(float x) { return __builtin_bit_cast(short, (__bf16)x); }
 
+#ifndef MOPO_BF16_PF
+#define MOPO_BF16_PF 4   // layer_lds_bf16: fragment reads in flight
+#endif
 template <int KG, int NB, int WAVES, int SLOT, int NBU = NB, bool KH = false>
 __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, const bf16x8 (&in)[KG], f32x4 (&acc)[NB],
                                                float* lds, int w, int lane, const float* __restrict__ bias = nullptr,
@@ -257,9 +260,17 @@ __device__ __forceinline__ void layer_lds_bf16(const float* __restrict__ wf, con
     if (kg + 1 < KG) stage_slice<NB, WAVES>(wf + (kg + 1) * NB * 256, lds + ((kg + 1) & 1) * SLOT, w, lane);
 #endif
     const float* b = lds + (kg & 1) * SLOT;
+    // fragments read MOPO_BF16_PF ahead, each read pinned ahead of the MFMAs that follow it (one MFMA per
+    // fragment: left to the scheduler, every read sits right before its use)
+    constexpr int PF = MOPO_BF16_PF < NBU ? MOPO_BF16_PF : NBU;
+    bf16x8 fq[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) fq[k] = *reinterpret_cast<const bf16x8*>(b + (k * 64 + lane) * 4);
 #pragma unroll
     for (int nb = 0; nb < NBU; ++nb) {  // blocks >= NBU: padding output block, skipped
-      const bf16x8 fr = *reinterpret_cast<const bf16x8*>(b + (nb * 64 + lane) * 4);
+      const bf16x8 fr = fq[nb % PF];
+      if (nb + PF < NBU) fq[nb % PF] = *reinterpret_cast<const bf16x8*>(b + ((nb + PF) * 64 + lane) * 4);
+      if constexpr (MOPO_BF16_PF > 1) __builtin_amdgcn_sched_barrier(0x0406);
 #ifndef BNN_KNOB_NOMFMA
       // KH: the last k-group's upper 16 are padding (odd input-block count), so a 16-deep MFMA
       if (KH && kg + 1 == KG) acc[nb] = mfma_16x16x16_lo<false>(fr, in[kg], acc[nb]);
@@ -420,7 +431,7 @@ __device__ __forceinline__ void row_scale(float mx, float& s, float& inv) {
 }
 
 #ifndef MOPO_SPLIT_PF
-#define MOPO_SPLIT_PF 1  // LDS fragment reads in flight in layer_lds_split_f32
+#define MOPO_SPLIT_PF 3  // LDS fragment reads in flight in layer_lds_split_f32 (pinned: MOPO_SPLIT_PIN)
 #endif
 #ifndef MOPO_SPLIT_PIN
 #define MOPO_SPLIT_PIN 1
