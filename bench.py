@@ -307,19 +307,24 @@ def ensemble_bytes(rows, spec, dtype):
     return rows * (32 * 4 + 2 * D * 4 + 4 + 4) + wbytes
 
 
-def roofline_of(dtype, rows, ms, flop_row=FLOP_BNN_ROW):
+def roofline_of(dtype, rows, ms, flop_row=FLOP_BNN_ROW, hidden=200):
     """Roofline of the ensemble-forward launch: f32 MFMA for fp32; executed bf16 MFMA flops (products x
-    the algorithmic f32 flops) against the bf16 dense peak for the split / bf16 kernels."""
+    the algorithmic f32 flops) against the bf16 dense peak for the split / bf16 kernels.  ``hidden`` picks the
+    kernel name the library dispatches at that width (csrc/bnn.hip launch_bnn_fwd: the ring at H <= 256)."""
     alg = rows * flop_row / (ms * 1e-3) / 1e12
+    wide = hidden > 256
     if dtype == 'fp32':
         return {'bound': 'mfma', 'kernel': 'bnn_fwd_kernel (ensemble forward, f32 MFMA 16x16x4)',
                 'achieved': alg, 'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': alg / MFMA_F32_PEAK_TFLOPS,
                 'flop_per_launch': rows * flop_row, 'avg_launch_ms': ms}
     parts, prods = SPLIT[dtype]
-    if dtype == 'f16x3':
+    if dtype == 'f16x3' and wide:
+        kern = ('bnn_fwd_f16h_kernel (ensemble forward in column halves, f16 MFMA 16x16x32, 3 products per f32 '
+                'product)')
+    elif dtype == 'f16x3':
         kern = ('bnn_fwd_ring_kernel<P=2> (ensemble forward on a 3-slot LDS ring, f16 MFMA 16x16x32, 3 products per f32 '
-                'product; bnn_fwd_f16h_kernel at H > 256)')
-    elif dtype == 'bf16x6':
+                'product)')
+    elif dtype == 'bf16x6' and not wide:
         kern = ('bnn_fwd_ring_kernel<P=3> (ensemble forward on a 3-slot LDS ring, exact 3-part bf16 split, bf16 MFMA '
                 '16x16x32, 6 products per f32 product)')
     else:
@@ -359,7 +364,7 @@ def leg_roofline(args, kms):
     these workloads: halfcheetah never terminates, walker2d legs have horizon 1) priced per dtype, with
     the PMC HBM bytes of the same workload when they were collected."""
     spec = CONFIGS[args.config]
-    r = roofline_of(args.ensemble_dtype, args.batch, kms['ensemble_fwd'], spec_flop_row(spec))
+    r = roofline_of(args.ensemble_dtype, args.batch, kms['ensemble_fwd'], spec_flop_row(spec), spec['H'])
     r['traffic'] = pmc_traffic(args)
     r['traffic_note'] = ('HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction, MI355X_MICROARCH.md '
                          'HBM) from the committed --pmc passes of this workload, ' + os.path.relpath(PMC_SUMMARY, ROOT)
