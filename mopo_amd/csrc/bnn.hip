@@ -345,9 +345,12 @@ __global__ __launch_bounds__(WAVES * 64, P > 1 ? (NB2 > 16 ? 1 : BNN_SPLIT_MINB 
   // per XCD) 19.3M (same box, profiles/r06_c5_bf16_order_ab.txt)
   int e, grp;
   if (a.xcd_members) {   // member-major within the XCD: each owned member's weights are fetched into ONE L2
-    const int j = blockIdx.x >> 3;
-    e = (blockIdx.x & 7) + 8 * (j / groups);
-    grp = j % groups;
+    // a.xcd_members = IW > 1: the XCD's members run IW at a time, interleaved per row group (its inputs read
+    // once per IW members instead of once per member)
+    const int j = blockIdx.x >> 3, iw = a.xcd_members;
+    const int ph = j / (iw * groups), r = j % (iw * groups);
+    e = (blockIdx.x & 7) + 8 * (iw * ph + r % iw);
+    grp = r / iw;
   } else {
     e = blockIdx.x / groups;
     grp = blockIdx.x % groups;
@@ -614,7 +617,7 @@ __global__ __launch_bounds__(WAVES * 64, NB2 > 16 ? BNN_F16_MINB_WIDE : BNN_F16_
 #define BNN_F16H_MINB 2
 #endif
 #ifndef BNN_BF16_XCDMEM
-#define BNN_BF16_XCDMEM 1  // bnn_fwd_bf16_kernel, E % 8 == 0: XCD-owned members (member-major within the XCD)
+#define BNN_BF16_XCDMEM 1  // bnn_fwd_bf16_kernel, E % 8 == 0: XCD-owned members (member-major within the XCD; > 1: that many interleaved)
 #endif
 #ifndef BNN_F16H_XCDMEM
 #define BNN_F16H_XCDMEM 1  // E % 8 == 0: each XCD owns E / 8 members (their weights fetched into one L2)
@@ -1271,7 +1274,7 @@ static int launch_bf16_p(const Bnn* h, int mode, FwdArgs a, hipStream_t s) {
   a.ntiles = (int)ceil_div((int)a.B, 16);
   if (a.ntiles == 0) return 0;
   dim3 grid(ceil_div(a.ntiles, WV) * h->E), block(64 * WV);   // = 8 groups (E / 8) when the XCDs own members
-  a.xcd_members = (BNN_BF16_XCDMEM && h->E % 8 == 0) ? 1 : 0;
+  a.xcd_members = (BNN_BF16_XCDMEM && h->E % (8 * BNN_BF16_XCDMEM) == 0) ? BNN_BF16_XCDMEM : 0;
   // odd hidden-block count (e.g. H = 200): the last block is padding and is skipped (NBU = NB2 - 1); not at
   // H = 400 (25 of 26), where the skipping variant takes 256 VGPRs and spills
   // NB2 = 14: H = 200 only (13 blocks used); the whole-block form is not instantiated (it spilled 8-12 B)
