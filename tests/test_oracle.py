@@ -91,6 +91,14 @@ def test_termination_more_domains_vs_reference():
         ref_like = type('StaticFns', (), {'__module__': 'ref_static_' + d})
         assert term_kind_of(ref_like) == static_fns[d].term_kind
     assert z['done_ant'].any() and z['done_humanoid'].any() and not z['done_ant'].all()
+    # the host StaticFns on torch tensors returns the same mask as a tensor
+    import torch
+    t = torch.from_numpy(nobs)
+    for d in ('ant', 'humanoid', 'walker2d', 'hopper', 'pendulum'):
+        got = static_fns[d].termination_fn(torch.zeros(len(nobs), 17), torch.zeros(len(nobs), 6), t)
+        assert isinstance(got, torch.Tensor) and got.dtype == torch.bool and tuple(got.shape) == (len(nobs), 1)
+        with np.errstate(invalid='ignore'):
+            np.testing.assert_array_equal(got.numpy(), ofe.TERMINATION[d](dummy[0], dummy[1], nobs))
 
 
 def test_pool_vs_reference():
