@@ -44,3 +44,18 @@ def test_cpu_baseline_median_of_five_after_warmup():
     run = bench.cpu_rollout_leg(64, 2, 'walker2d', 5.0, env_rows=500)   # the oracle rollout leg, tiny
     n, dt = run()
     assert 0 < n <= 128 and dt > 0
+
+
+def test_roofline_names_the_dispatched_ensemble_kernel():
+    """The roofline's kernel is the one csrc/bnn.hip launch_bnn_fwd dispatches at the config's width: the LDS ring
+    at H <= 256 (bf16x6: P = 3, f16x3: P = 2), the column-half f16h kernel for f16x3 at H = 400, the split bf16
+    kernel for bf16x6 at H = 400; the executed-flop fraction counts every MFMA product."""
+    import bench
+    ms, rows = 0.5, 50000
+    r = bench.roofline_of('bf16x6', rows, ms, bench.FLOP_BNN_ROW, 200)
+    assert r['kernel'].startswith('bnn_fwd_ring_kernel<P=3>')
+    assert abs(r['frac'] - 6 * rows * bench.FLOP_BNN_ROW / (ms * 1e-3) / 1e12 / bench.BF16_PEAK_TFLOPS) < 1e-12
+    assert bench.roofline_of('f16x3', rows, ms, bench.FLOP_BNN_ROW, 200)['kernel'].startswith('bnn_fwd_ring_kernel<P=2>')
+    assert bench.roofline_of('f16x3', rows, ms, bench.FLOP_BNN_ROW, 400)['kernel'].startswith('bnn_fwd_f16h_kernel')
+    assert bench.roofline_of('bf16x6', rows, ms, bench.FLOP_BNN_ROW, 400)['kernel'].startswith('bnn_fwd_bf16_kernel<P=3>')
+    assert bench.roofline_of('fp32', rows, ms)['kernel'].startswith('bnn_fwd_kernel')
