@@ -513,8 +513,10 @@ static int run_impl(Rollout* h, const mopo_rollout_args* a, const mopo_pool_desc
     for (int k = 1; k < nsplit; ++k)
       if (!h->sp[k]) {
         MOPO_HIP(hipStreamCreateWithFlags(&h->sp[k], hipStreamNonBlocking));
-        MOPO_HIP(hipEventCreateWithFlags(&h->ev_fork[k], hipEventDisableTiming));
-        MOPO_HIP(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
+        // device-scope events (no system-scope cache write-back / invalidate at each record: the parts only
+        // hand device memory to each other)
+        MOPO_HIP(hipEventCreateWithFlags(&h->ev_fork[k], hipEventDisableTiming | hipEventDisableSystemFence));
+        MOPO_HIP(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming | hipEventDisableSystemFence));
       }
     // part k starts once part k - 1's first actor is done: the chains run offset by about one actor
     // launch instead of in lockstep, so their ensemble tails do not coincide
